@@ -1,0 +1,165 @@
+"""Headline benchmark: frames/s of the full FCD height-map pipeline
+(fcd.compute_height_map: FFT, disk band-pass, inverse FFTs, phase, unwrap,
+displacement solve, spectral integration) on 1024x1024 checkerboard frames,
+with the HBM roofline of the demodulation stage and the CPU oracle timed on
+the same host.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--size 1024] [--batch 256]
+
+For N > 1 the driver launches one process per GPU with torch.distributed.run;
+each rank processes its own `--batch` frames (weak scaling, SURVEY.md §8e:
+frames are independent, no collective in the compute), the step time is the
+max over ranks, and rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for p in (ROOT, os.path.join(ROOT, "trapped-modes-ltg_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+METRIC = "frames/sec @1024×1024 checkerboard batch + HBM GB/s vs peak, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def cpu_baseline(size, frames, seconds_cap=25.0):
+    """The CPU oracle (numpy/scipy FFTs + C Herraez unwrap), 1 core, bounded sample."""
+    import numpy as np
+    from bench_data import make_frames_numpy
+    from oracle import fcd_oracle as O
+    ref, fr = make_frames_numpy(size, frames, seed=0)
+    carriers = O.compute_carriers(ref, 0.001)  # once per reference, like the GPU run
+    t0 = time.perf_counter()
+    done = 0
+    for f in fr:
+        O.compute_height_map(ref, f, 0.001, height=1.0, carriers=carriers)
+        done += 1
+        if time.perf_counter() - t0 > seconds_cap:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": f"{done} frames of {size}x{size} (same synthetic recipe), oracle/fcd_oracle.compute_height_map "
+                      f"with carriers cached, scipy.fft workers=1, {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--size", type=int, default=1024)
+    ap.add_argument("--batch", type=int, default=256, help="frames per GPU per step")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-frames", type=int, default=12)
+    ap.add_argument("--gather", action="store_true", help="also time an RCCL gather of the heights to rank 0")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from pyfcd import _lib
+    from pyfcd.dist import dist_env, gather_stack, max_over_ranks
+    from bench_data import make_frames_torch, SQUARE_SIZE
+
+    rank, world, local = dist_env()
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    n, B = args.size, args.batch
+
+    # synthetic batch, generated in HBM; rank r owns frames [r*B, (r+1)*B)
+    ref_t, frames = make_frames_torch(n, B, seed=rank * B, device=dev)
+    heights = torch.empty((B, n, n), dtype=torch.float32, device=dev)
+    eng = _lib.Engine((n, n), device=local)
+    eng.set_reference(ref_t.cpu().numpy(), SQUARE_SIZE)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def step():
+        eng.process_device(frames.data_ptr(), B, 1.0, True, heights.data_ptr(), stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    eng.profile(True)
+    torch.cuda.synchronize(dev)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(args.steps):
+        step()
+    ev1.record()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    stages, nframes = eng.stage_times()
+    eng.profile(False)
+    wall_max = max_over_ranks(wall, device=dev)
+    ms_per_step = wall_max / args.steps * 1e3
+    total_frames = B * world * args.steps
+    value = total_frames / wall_max
+
+    gather_ms = None
+    if args.gather and world > 1:
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        g0 = time.perf_counter()
+        gather_stack(heights, B * world)
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        gather_ms = max_over_ranks((time.perf_counter() - g0) * 1e3, device=dev)
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    # roofline of the demodulation stage: frame f32 in -> 2 wrapped phases f32 out = 12 N^2 bytes/frame
+    demod_bytes = 12.0 * n * n
+    demod_ms_per_frame = stages["demod"] / max(nframes, 1)
+    achieved = demod_bytes / (demod_ms_per_frame * 1e-3) / 1e9
+    per_frame = {k: v / max(nframes, 1) * 1e3 for k, v in stages.items()}  # us per frame
+    out = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic: pattern.py geometry (10-px binary checkerboard, 0/65535) warped by seeded Gaussian bumps, "
+                "generated on device (bench_data.py)",
+        "config": {"workload": f"c2: {n}x{n} frames, {B} per GPU per step, full compute_height_map pipeline "
+                               f"(demod + unwrap + integration), reference state cached",
+                   "frame": n, "batch_per_gpu": B, "global_batch": B * world,
+                   "parallelism": f"frame-sharded x{world}, no collective in the compute"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "kernel": "demod stage (fwd FFT + disk band-pass + 2x inverse FFT + phase), 12*N^2 B/frame",
+                     "stage_us_per_frame": {k: round(v, 2) for k, v in per_frame.items()}},
+        "event_ms_per_step": round(ev0.elapsed_time(ev1) / args.steps, 3),
+    }
+    if gather_ms is not None:
+        out["gather_ms"] = round(gather_ms, 3)
+    if world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(n, args.cpu_frames)
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

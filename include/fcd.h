@@ -1,0 +1,125 @@
+/*
+ * fcd.h — C ABI of the MI355X fast-checkerboard-demodulation engine.
+ *
+ * This is the drop-in boundary for the reference's hot path
+ * (/root/reference/pyfcd/).  The reference is pure Python and
+ * has no FFI of its own; each entry point below replaces the Python-level
+ * interface cited next to it, and the ctypes binding in
+ * trapped-modes-ltg_amd/pyfcd/_lib.py (shown in INTEGRATION.md) keeps the
+ * reference's classmethod signatures on top of it.
+ *
+ * Conventions
+ *   - Every function returns FCD_OK (0) or a negative FCD_E_* code; the
+ *     message is available from fcd_last_error() (per host thread).
+ *   - Buffers are caller-owned.  flags = FCD_HOST_PTRS: all array arguments
+ *     are host pointers (the call copies and synchronises); FCD_DEVICE_PTRS:
+ *     all array arguments are device pointers on the context's device and the
+ *     call is asynchronous on `stream` (NULL = the context's own stream),
+ *     except where a function says it synchronises.
+ *   - Images are row-major float32 [rows][cols]; complex arrays are
+ *     interleaved complex64.  rows and cols must be powers of two in
+ *     [64, 4096].
+ *   - A context belongs to one device and one host thread at a time.
+ */
+#ifndef FCD_H
+#define FCD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FCD_ABI_VERSION 1
+
+enum {
+    FCD_OK = 0,
+    FCD_E_INVALID = -1,      /* bad argument (null pointer, size mismatch, ...) */
+    FCD_E_UNSUPPORTED = -2,  /* shape not supported (non power of two, > 4096) */
+    FCD_E_HIP = -3,          /* HIP runtime / launch failure */
+    FCD_E_STATE = -4,        /* no reference set */
+    FCD_E_NOPEAKS = -5,      /* < 2 carrier peaks: the reference raises ValueError/IndexError */
+    FCD_E_INTERNAL = -6
+};
+
+enum { FCD_HOST_PTRS = 0, FCD_DEVICE_PTRS = 1 };
+
+typedef struct fcd_ctx fcd_ctx;
+
+/* Reference-derived state (fcd.compute_carriers, fcd.py:53-70). */
+typedef struct {
+    int64_t peaks[2][2];        /* fftshifted (row, col): [0] rightmost, [1] perpendicular (fourier.py:38-39) */
+    double radius;              /* |p0 - p1| / 2 (fcd.py:68) */
+    double calibration_factor;  /* fcd.compute_calibration_factor (fcd.py:87-101) */
+    double frequencies[2][2];   /* Carrier.frequencies, (k_row, k_col) (carriers.py:12) */
+    int32_t mask_count[2];      /* pixels inside each disk band-pass (carriers.py:17-20) */
+    int32_t n_blobs;            /* blobs kept by find_peak_locations (<= 4, fourier.py:166-168) */
+    int64_t blob_peaks[4][2];   /* their peak pixels, ascending intensity */
+    float threshold;            /* 0.5 * max |F| after the high-pass (fourier.py:35) */
+} fcd_ref_info;
+
+int fcd_abi_version(void);
+const char* fcd_last_error(void);
+
+/* Allocate a context for `rows` x `cols` frames on HIP device `device`. */
+int fcd_create(int device, int rows, int cols, fcd_ctx** out);
+int fcd_destroy(fcd_ctx* ctx);
+int fcd_synchronize(fcd_ctx* ctx);
+
+/* Replaces fcd.compute_carriers(reference, square_size) (fcd.py:53-70) and,
+ * inside it, fcd.compute_calibration_factor (fcd.py:72-101), fourier.find_peaks
+ * (fourier.py:7-41) and Carrier.__init__ (carriers.py:10-24).  Synchronises. */
+int fcd_set_reference(fcd_ctx* ctx, const float* reference, int flags, double square_size, fcd_ref_info* info);
+
+/* Carrier arrays for the Python mirror: ccsgn complex64 [2][rows][cols]
+ * (carriers.py:22-24, normalised like scipy ifft2) and the ifftshifted disk
+ * masks uint8 [2][rows][cols] (carriers.py:17-20).  Host pointers, either may
+ * be NULL.  Synchronises. */
+int fcd_get_carriers(fcd_ctx* ctx, float* ccsgn, uint8_t* mask);
+
+/* Replaces fcd.compute_height_map(reference, displaced, square_size, layers,
+ * height, unwrap) (fcd.py:13-35) for a batch of n_frames frames against the
+ * reference set by fcd_set_reference.  `height` is the effective height
+ * (fcd.py:16-25; the caller folds layers via fcd.height_from_layers).
+ * Outputs (any may be NULL):
+ *   height_out  float32 [n][rows][cols]
+ *   wrapped_out float32 [n][2][rows][cols]  -angle(ifft2(D*mask)*ccsgn) (fcd.py:118)
+ *   k_out       int32   [n][2][rows][cols]  2*pi multiples: phases = wrapped + 2*pi*k (fcd.py:119)
+ * With unwrap == 0 the phases are the wrapped angles (k_out is zero-filled).
+ * Synchronises once per internal chunk when unwrap != 0 (residue census). */
+int fcd_process(fcd_ctx* ctx, const float* frames, int n_frames, int flags, double height, int unwrap,
+                float* height_out, float* wrapped_out, int32_t* k_out, void* stream);
+
+/* Replaces fcd.compute_phases(displaced_fft, carriers, unwrap) (fcd.py:103-120)
+ * for n spectra (complex64 [n][rows][cols], unshifted fft2 output). */
+int fcd_phases_from_spectrum(fcd_ctx* ctx, const float* spectrum, int n, int flags, int unwrap, float* wrapped_out,
+                             int32_t* k_out, void* stream);
+
+/* Replaces skimage.restoration.unwrap_phase as called at fcd.py:119, for
+ * n_maps float32 maps.  k_out int32 [n][rows][cols]; residues_out (nullable)
+ * int32 [n] residue count per map.  Synchronises. */
+int fcd_unwrap(fcd_ctx* ctx, const float* wrapped, int n_maps, int flags, int32_t* k_out, int32_t* residues_out,
+               void* stream);
+
+/* Replaces fourier.integrate_in_fourier(gx, gy, calibration_factor)
+ * (fourier.py:115-137) for n gradient pairs (float32, result float32). */
+int fcd_integrate(fcd_ctx* ctx, const float* gx, const float* gy, int n, double calibration_factor, int flags,
+                  float* h_out, void* stream);
+
+/* scipy.fft.fft2 of n real float32 images -> complex64 (as fcd.py:28). */
+int fcd_fft2(fcd_ctx* ctx, const float* in, int n, int flags, float* out, void* stream);
+
+/* Stage timing (no reference counterpart; measurement only).  With enable != 0,
+ * fcd_process records HIP events on its stream around each stage of every
+ * chunk.  fcd_stage_times synchronises and returns the accumulated device
+ * milliseconds since the last call: out[0] demodulation (forward FFT, disk
+ * band-pass, inverse FFTs, phase), out[1] unwrap, out[2] displacement +
+ * integration, out[3] whole chunks; *frames = frames covered. */
+int fcd_profile(fcd_ctx* ctx, int enable);
+int fcd_stage_times(fcd_ctx* ctx, double* out4, int64_t* frames);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FCD_H */

@@ -1,0 +1,154 @@
+"""CPU-only checks of the product's host side: the C-ABI library loads and
+exports every symbol include/fcd.h declares (no compute calls without a GPU),
+the Python mirror keeps the reference's API surface, its host table helpers
+match the oracle, and the multi-rank sharding path works over gloo."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "fcd.h")
+
+
+def header_symbols():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"^(?:int|const char\*)\s+(fcd_\w+)\s*\(", text, flags=re.M)))
+
+
+def test_header_lists_bound_symbols():
+    from pyfcd import _lib
+    assert header_symbols() == sorted(_lib.EXPORTED)
+
+
+def test_library_exports_every_header_symbol():
+    from pyfcd import _lib
+    lib = _lib.load_library()
+    for name in header_symbols():
+        assert hasattr(lib, name), name
+    assert lib.fcd_abi_version() == 1
+
+
+def test_library_is_gfx950_code_object():
+    from pyfcd import _lib
+    blob = open(_lib.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob
+
+
+def test_no_silent_fallback_without_device():
+    """Without a HIP device the engine must fail loudly, never compute on the CPU."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    from pyfcd import _lib
+    with pytest.raises(_lib.FcdError):
+        _lib.Engine((64, 64))
+
+
+def test_api_surface_matches_reference():
+    from pyfcd.fcd import fcd, fourier  # val.py:36 imports exactly this
+    from pyfcd.carriers import Carrier  # noqa: F401
+    for name in ("compute_height_map", "height_from_layers", "effective_height", "compute_carriers",
+                 "compute_calibration_factor", "compute_phases", "compute_displacement_field", "fft_peaks"):
+        assert callable(getattr(fcd, name)), name
+    for name in ("find_peaks", "wavenumber", "wavenumber_meshgrid", "remove_degeneracy", "pixel_to_wavenumber",
+                 "integrate_in_fourier", "find_peak_locations"):
+        assert callable(getattr(fourier, name)), name
+    with pytest.raises(TypeError):
+        fcd()
+    with pytest.raises(Warning):
+        fcd.compute_height_map(np.zeros((64, 64)), np.zeros((64, 64)), 1.0, layers=[[1, 1]] * 4, height=1.0)
+
+
+def test_host_tables_match_oracle(golden):
+    from oracle import fcd_oracle as O
+    from pyfcd.fourier import fourier
+    for n in (64, 100, 1024):
+        for cf in (1.0, 0.37, 0.0003158203125):
+            for sh in (False, True):
+                assert np.array_equal(fourier.wavenumber(n, cf, sh), O.wavenumber(n, cf, sh))
+    g = golden("real_pair")
+    from pyfcd.fcd import fcd
+    assert fcd.height_from_layers(g["layers"].tolist()) == float(g["eff_height"])
+    kx = np.arange(64.0)[None].repeat(8, 0)
+    ky = np.arange(8.0)[:, None].repeat(64, 1)
+    fourier.remove_degeneracy(kx, ky, (8, 64))
+    assert (kx[:, 33] == 0).all() and (ky[5] == 0).all()
+
+
+def test_displacement_field_matches_oracle():
+    from oracle import fcd_oracle as O
+    from pyfcd.fcd import fcd
+
+    class C:
+        def __init__(self, f):
+            self.frequencies = np.array(f)
+    cs = [C([0.3, 1.2]), C([-1.1, 0.25])]
+    ph = np.random.default_rng(0).standard_normal((2, 16, 16))
+    assert np.array_equal(fcd.compute_displacement_field(ph, cs), O.displacement_field(ph, cs))
+
+
+def test_find_peak_locations_host_helper(golden):
+    from oracle import fcd_oracle as O
+    from pyfcd.fourier import fourier
+    rng = np.random.default_rng(3)
+    img = rng.random((64, 64)).astype(np.float32)
+    img[10:13, 20:23] += 5
+    img[40, 40] += 4
+    img[50:52, 5:9] += 6
+    a = fourier.find_peak_locations(img, 1.5, 4)
+    b = O.find_peak_locations(img, 1.5, 4)
+    assert [p.tolist() for p in a] == [p.tolist() for p in b]
+
+
+@pytest.mark.parametrize("total,world", [(256, 1), (256, 2), (8192, 8), (10, 4), (3, 8)])
+def test_shard_range_partitions(total, world):
+    from pyfcd.dist import shard_range
+    spans = [shard_range(total, r, world) for r in range(world)]
+    assert spans[0][0] == 0 and spans[-1][1] == total
+    for (a, b), (c, d) in zip(spans, spans[1:]):
+        assert b == c
+    sizes = [b - a for a, b in spans]
+    assert max(sizes) - min(sizes) <= 1
+
+
+def _gloo_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from pyfcd.dist import gather_stack, max_over_ranks, shard_range, sum_over_ranks
+        total = 7
+        a, b = shard_range(total, rank, world)
+        local = torch.arange(a, b, dtype=torch.float32)[:, None, None].expand(b - a, 2, 3).contiguous()
+        out = gather_stack(local, total)
+        t = max_over_ranks(float(rank + 1))
+        n = sum_over_ranks(float(b - a))
+        if rank == 0:
+            q.put((out[:, 0, 0].tolist(), t, n))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_two_rank_shard_gather():
+    import multiprocessing as mp
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_gloo_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    frames, tmax, total = res
+    assert frames == [float(i) for i in range(7)]
+    assert tmax == 2.0 and total == 7.0

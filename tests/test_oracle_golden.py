@@ -1,0 +1,136 @@
+"""Pin the CPU oracle (oracle/) to the reference's own outputs (tests/golden).
+
+The oracle is the checker of every GPU parity test, so it must itself match
+the golden vectors the reference produced (tests/golden/make_golden.py):
+bit-exact peaks / calibration factor / unwrap k-fields, and float32-FFT
+tolerance on phases and heights.
+"""
+import numpy as np
+import pytest
+
+from conftest import border_ring
+from oracle import fcd_oracle as O
+
+LAYERS = [[5.7e-2, 1.0003], [1.2e-2, 1.48899], [4.3e-2, 1.34], [80e-2, 1.0003]]
+
+
+def test_height_from_layers(golden):
+    g = golden("real_pair")
+    assert O.height_from_layers(g["layers"].tolist()) == float(g["eff_height"])
+
+
+def test_wavenumber_tables(golden):
+    g = golden("integrate")
+    for key in ("64x64", "128x64", "256x256"):
+        h, w = (int(v) for v in key.split("x"))
+        kr, kc = O.wavenumber_meshgrid((h, w), float(g[f"cf_{key}"]))
+        assert np.array_equal(kr[:, 0], g[f"krow_{key}"])
+        assert np.array_equal(kc[0, :], g[f"kcol_{key}"])
+
+
+def test_integrate_in_fourier(golden):
+    g = golden("integrate")
+    for key in ("64x64", "128x64", "256x256"):
+        h = O.integrate_in_fourier(g[f"gx_{key}"], g[f"gy_{key}"], float(g[f"cf_{key}"]))
+        np.testing.assert_allclose(h, g[f"h_{key}"], rtol=0, atol=1e-12 * np.abs(g[f"h_{key}"]).max())
+
+
+def test_integrate_symmetrised_tables_equivalence(golden):
+    """The device form (odd-symmetrised kx/ky, real spectrum) equals the reference's real(ifft2(...))."""
+    g = golden("integrate")
+    for key in ("64x64", "128x64"):
+        gx, gy, cf = g[f"gx_{key}"], g[f"gy_{key}"], float(g[f"cf_{key}"])
+        H, W = gx.shape
+        ky, kx = O.wavenumber_meshgrid((H, W), cf)
+        k2 = kx ** 2 + ky ** 2
+        k2[0, 0] = 1
+        kxm, kym = kx.copy(), ky.copy()
+        kxm[:, W // 2 + 1] = 0
+        kym[H // 2 + 1, :] = 0
+        kxe = (kxm - kxm[:, (-np.arange(W)) % W]) / 2
+        kye = (kym - kym[(-np.arange(H)) % H, :]) / 2
+        hat = (-1j * kxe * np.fft.fft2(gx) - 1j * kye * np.fft.fft2(gy)) / k2
+        h = np.fft.ifft2(hat)
+        assert np.abs(h.imag).max() < 1e-12 * np.abs(h.real).max()
+        np.testing.assert_allclose(h.real, g[f"h_{key}"], atol=1e-12 * np.abs(g[f"h_{key}"]).max())
+
+
+def test_real_pair_setup(golden):
+    g = golden("real_pair")
+    ref = g["ref_u8"].astype(np.float32)
+    carriers, cf = O.compute_carriers(ref, float(g["square_size"]))
+    assert cf == float(g["cf"])
+    assert np.array_equal(np.array([np.asarray(c.pixels) for c in carriers]), g["peaks"])
+    assert carriers[0].radius == float(g["radius"])
+    assert np.array_equal(np.array([c.frequencies for c in carriers]), g["freqs"])
+    assert [int(c.mask.sum()) for c in carriers] == list(g["mask_count"])
+
+
+def test_real_df_committed_calibration(golden):
+    d = golden("real_df")
+    cf, peaks = O.calibration_factor(float(d["square_size"]), d["ref_u16"].astype(np.float32))
+    assert cf == float(d["committed_cf"][0])  # examples/Pictures/mask/maps/calibration_factor.npy
+    assert np.array_equal(np.array([np.asarray(p) for p in peaks]), d["peaks"])
+
+
+def test_real_pair_end_to_end(golden):
+    g = golden("real_pair")
+    ref, disp = g["ref_u8"].astype(np.float32), g["disp_u8"].astype(np.float32)
+    h, ph, cf, ex = O.compute_height_map(ref, disp, float(g["square_size"]), layers=g["layers"].tolist())
+    assert np.array_equal(ex["wrapped"][:, ::8, ::8], g["wrapped_sub"])
+    # k-fields: the reference draws border reliabilities from rand(); only border pixels may differ
+    for i in range(2):
+        bad = ex["k"][i] != g["k"][i]
+        assert not bad[~border_ring(bad.shape)].any()
+        assert bad.sum() <= 2
+    rel = np.linalg.norm(h[::4, ::4] - g["height_sub"]) / np.linalg.norm(g["height_sub"])
+    assert rel < 1e-4
+
+
+def test_synthetic_bit_exact(golden):
+    s = golden("synthetic")
+    for c in s["cases"]:
+        h, ph, cf, ex = O.compute_height_map(s[f"{c}_ref"], s[f"{c}_disp"], float(s[f"{c}_sq"]), height=1.0)
+        assert cf == float(s[f"{c}_cf"])
+        assert np.array_equal(ex["wrapped"], s[f"{c}_wrapped"]), c
+        assert np.array_equal(ph, s[f"{c}_phases"]), c
+        np.testing.assert_allclose(h, s[f"{c}_height"], rtol=0, atol=1e-12 * np.abs(s[f"{c}_height"]).max())
+
+
+def test_unwrap_crops_exact(golden):
+    u = golden("unwrap_crops")
+    for w, k in zip(u["crops"], u["k_crops"]):
+        _, ko = O.unwrap(w)
+        bad = ko != k
+        assert not bad[~border_ring(bad.shape)].any()
+        assert bad.sum() <= 2
+    _, ko = O.unwrap(u["rect"])
+    assert (ko != u["k_rect"]).sum() <= 2
+
+
+@pytest.mark.parametrize("which", [0])
+def test_unwrap_full_map_exact(golden, which):
+    u = golden("unwrap_crops")
+    _, ko = O.unwrap(u["full"])
+    bad = ko != u["k_full"]
+    assert not bad[~border_ring(bad.shape)].any()
+    assert bad.sum() <= 2
+
+
+def test_val_accuracy_threshold(golden):
+    """pyval.val(0, gauss_sin) (examples/val_example.py) — README's "< 0.52 %"."""
+    v = golden("val")
+    assert float(v["err_percent"]) < 0.52
+    assert float(v["cf"]) == 1.0
+
+
+def test_residue_counter_matches_definition():
+    rng = np.random.default_rng(1)
+    w = np.angle(np.exp(1j * rng.normal(0, 2.0, (40, 50)))).astype(np.float32)
+    a = w[:-1, :-1].astype(np.float64)
+    b, c, d = w[:-1, 1:], w[1:, 1:], w[1:, :-1]
+
+    def fw(p, q):
+        x = p - np.asarray(q, np.float64)
+        return np.where(x > np.pi, -1, np.where(x < -np.pi, 1, 0))
+    assert O.count_residues(w) == int(((fw(a, b) + fw(b, c) + fw(c, d) + fw(d, a)) != 0).sum())

@@ -1,0 +1,845 @@
+// Host runtime of the MI355X FCD engine: context, device buffers, the
+// per-reference setup and the batched per-frame pipeline behind the C ABI of
+// include/fcd.h.  All numerics run in the HIP kernels (kernels_*.hip); the
+// host only computes the reference's scalar tables (wavenumbers, calibration
+// factor, disk raster) and labels the handful of above-threshold spectrum
+// pixels that find_peak_locations turns into carrier peaks.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <memory>
+#include <numeric>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/fcd.h"
+#include "kernels.hpp"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+struct FcdError : std::runtime_error {
+    int code;
+    FcdError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define HIPCHK(x)                                                                                  \
+    do {                                                                                           \
+        hipError_t e_ = (x);                                                                       \
+        if (e_ != hipSuccess) throw FcdError(FCD_E_HIP, std::string(#x ": ") + hipGetErrorString(e_)); \
+    } while (0)
+
+// Owning device allocation.
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    ~DevBuf() { release(); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    void ensure(size_t n) {
+        if (n <= bytes) return;
+        release();
+        HIPCHK(hipMalloc(&p, n));
+        bytes = n;
+    }
+    template <class T>
+    T* as() const { return static_cast<T*>(p); }
+};
+
+constexpr double kPi = 3.141592653589793;  // numpy.pi
+
+// fourier.wavenumber (fourier.py:43-56): fftfreq(n, cf / (2 pi)), optionally fftshifted.
+std::vector<double> wavenumber(int n, double cf, bool shifted) {
+    const double d = cf / (2 * kPi);
+    const double val = 1.0 / (n * d);
+    std::vector<double> k(n);
+    const int npos = (n - 1) / 2 + 1;
+    for (int i = 0; i < n; ++i) {
+        const long m = i < npos ? i : (long)i - n;
+        k[i] = (double)m * val;
+    }
+    if (shifted) std::rotate(k.begin(), k.begin() + (n - n / 2), k.end());  // fftshift
+    return k;
+}
+
+void upload(void* dst, const void* src, size_t bytes, hipStream_t s) {
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
+}
+
+std::vector<float2> twiddles(int n) {
+    std::vector<float2> t(n);
+    for (int m = 0; m < n; ++m) {
+        const double a = -2.0 * kPi * (double)m / (double)n;
+        t[m] = make_float2((float)std::cos(a), (float)std::sin(a));
+    }
+    return t;
+}
+
+struct Blob {
+    int first;     // raster index of its first pixel (skimage label order)
+    int peak;      // raster index of its max pixel (first in row-major on ties)
+    float value;
+};
+
+}  // namespace
+
+struct fcd_ctx {
+    int device = 0, H = 0, W = 0;
+    hipStream_t own = nullptr;
+    DevBuf tw_row, tw_col;
+
+    // reference state
+    bool has_ref = false;
+    fcd_ref_info info{};
+    DevBuf theta;          // float [2][H][W] angle of ifft2(F_ref * mask)
+    DevBuf refsig;         // float2 [2][H][W] ifft2(F_ref * mask), unnormalised
+    DevBuf disk_rows;      // int [2][2W]
+    std::vector<int> disk_rows_host;
+    DevBuf integ_tab;      // float kxe[W], kye[H], kx2[W], ky2[H]
+    double integ_cf = -1;
+
+    // workspace
+    int chunk = 1;
+    DevBuf spec, work, wrapped, kbuf, colk, rescnt, frames_in, out_h, scalar;
+    DevBuf cand_idx, cand_val;
+    // MST workspace
+    DevBuf mst_comp, mst_off, mst_rel, mst_cw, mst_ce, mst_bw, mst_be, mst_link, mst_hooks, mst_ids;
+    size_t mst_cap = 0;
+
+    // stage timing: 4 events per chunk (start, after demod, after unwrap, after integrate)
+    bool profiling = false;
+    std::vector<hipEvent_t> ev_pool;
+    size_t ev_used = 0;
+    long prof_frames = 0;
+
+    hipStream_t pick(void* s) const { return s ? static_cast<hipStream_t>(s) : own; }
+    hipEvent_t next_event() {
+        if (ev_used == ev_pool.size()) {
+            hipEvent_t e;
+            if (hipEventCreate(&e) != hipSuccess) throw std::runtime_error("hipEventCreate failed");
+            ev_pool.push_back(e);
+        }
+        return ev_pool[ev_used++];
+    }
+    long hw() const { return (long)H * W; }
+};
+
+namespace {
+
+void ensure_chunk_buffers(fcd_ctx* c) {
+    const long hw = c->hw();
+    const size_t n = (size_t)c->chunk;
+    c->spec.ensure(n * hw * sizeof(float2));
+    c->work.ensure(n * hw * sizeof(float2));
+    c->wrapped.ensure(n * 2 * hw * sizeof(float));
+    c->kbuf.ensure(n * 2 * hw * sizeof(int32_t));
+    c->colk.ensure(n * 2 * c->H * sizeof(int));
+    c->rescnt.ensure(n * 2 * sizeof(int));
+}
+
+void ensure_mst(fcd_ctx* c, int nact) {
+    const size_t nv = (size_t)nact * c->hw();
+    if (nv <= c->mst_cap) return;
+    c->mst_comp.ensure(nv * 4);
+    c->mst_off.ensure(nv * 4);
+    c->mst_rel.ensure(nv * 8);
+    c->mst_cw.ensure(nv * 8);
+    c->mst_ce.ensure(nv * 4);
+    c->mst_bw.ensure(nv * 8);
+    c->mst_be.ensure(nv * 4);
+    c->mst_link.ensure(nv * 8);
+    c->mst_hooks.ensure(sizeof(int));
+    c->mst_ids.ensure(sizeof(int) * 2 * (size_t)c->chunk + 64);
+    c->mst_cap = nv;
+}
+
+fcdk::MstWork mst_work(fcd_ctx* c) {
+    fcdk::MstWork m;
+    m.comp = c->mst_comp.as<int>();
+    m.off = c->mst_off.as<int>();
+    m.rel = c->mst_rel.as<double>();
+    m.cand_w = c->mst_cw.as<double>();
+    m.cand_e = c->mst_ce.as<int>();
+    m.best_w = c->mst_bw.as<unsigned long long>();
+    m.best_e = c->mst_be.as<int>();
+    m.link = c->mst_link.as<unsigned long long>();
+    m.nhooks = c->mst_hooks.as<int>();
+    return m;
+}
+
+// 2-D forward FFT of nb real images (row pass from real input) into `out`.
+void fft2_real(fcd_ctx* c, const float* in, float2* out, int nb, float sub, hipStream_t s) {
+    fcdk::row_fft(c->W, false, fcdk::ROW_IN_REAL, fcdk::ROW_OUT_COMPLEX, in, out, (long)nb * c->H, c->H, sub,
+                  c->tw_row.as<float2>(), nullptr, s);
+    fcdk::col_fft(c->H, c->W, false, out, nb, c->tw_col.as<float2>(), s);
+}
+
+// Wrapped phases of nb spectra (in `spec`) for both carriers, fcd.py:116-118.
+void demod_phases(fcd_ctx* c, const float2* spec, int nb, float* wrapped, hipStream_t s) {
+    float2* A = c->work.as<float2>();
+    for (int car = 0; car < 2; ++car) {
+        fcdk::DiskTable t{c->disk_rows.as<int>() + (size_t)car * 2 * c->W};
+        fcdk::disk_mask(spec, A, nb, c->H, c->W, t, s);
+        fcdk::col_fft(c->H, c->W, true, A, nb, c->tw_col.as<float2>(), s);
+        fcdk::PhaseOut ph{c->theta.as<float>() + (size_t)car * c->hw(), wrapped, car};
+        fcdk::row_fft(c->W, true, fcdk::ROW_IN_COMPLEX, fcdk::ROW_OUT_PHASE, A, nullptr, (long)nb * c->H, c->H, 0.f,
+                      c->tw_row.as<float2>(), &ph, s);
+    }
+}
+
+// k-fields of nmaps wrapped maps (skimage unwrap_phase, fcd.py:119).  Synchronises.
+void unwrap_maps(fcd_ctx* c, const float* w, int nmaps, int32_t* k, int* res_host, hipStream_t s) {
+    int* res = c->rescnt.as<int>();
+    fcdk::residues(w, nmaps, c->H, c->W, res, s);
+    fcdk::unwrap_scan(w, nmaps, c->H, c->W, c->colk.as<int>(), k, s);
+    std::vector<int> counts(nmaps);
+    HIPCHK(hipMemcpyAsync(counts.data(), res, sizeof(int) * nmaps, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (res_host) std::copy(counts.begin(), counts.end(), res_host);
+    std::vector<int> active;
+    for (int i = 0; i < nmaps; ++i)
+        if (counts[i] > 0) active.push_back(i);
+    if (active.empty()) return;
+    ensure_mst(c, (int)active.size());
+    fcdk::MstWork m = mst_work(c);
+    const int nact = (int)active.size();
+    upload(c->mst_ids.p, active.data(), sizeof(int) * nact, s);
+    fcdk::mst_init(w, c->mst_ids.as<int>(), nact, c->H, c->W, m, s);
+    const int max_rounds = 64;
+    int rounds = 0;
+    for (; rounds < max_rounds; ++rounds) {
+        fcdk::mst_round(w, c->mst_ids.as<int>(), nact, c->H, c->W, m, s);
+        int hooks = 0;
+        HIPCHK(hipMemcpyAsync(&hooks, m.nhooks, sizeof(int), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        if (hooks == 0) break;
+    }
+    if (rounds == max_rounds) throw FcdError(FCD_E_INTERNAL, "unwrap: Boruvka did not converge");
+    fcdk::mst_finalize(c->mst_ids.as<int>(), nact, c->H, c->W, m, k, s);
+}
+
+// Integration tables for calibration factor cf (fourier.py:128-131, 75-92).
+void ensure_integ_tables(fcd_ctx* c, double cf, hipStream_t s) {
+    if (c->integ_cf == cf) return;
+    const int H = c->H, W = c->W;
+    std::vector<double> kx = wavenumber(W, cf, false), ky = wavenumber(H, cf, false);
+    std::vector<double> kxm = kx, kym = ky;
+    if (W % 2 == 0) kxm[W / 2 + 1] = 0;  // remove_degeneracy, literally N/2+1 (fourier.py:88-92)
+    if (H % 2 == 0) kym[H / 2 + 1] = 0;
+    std::vector<float> tab(2 * (size_t)(W + H));
+    float* kxe = tab.data();
+    float* kye = kxe + W;
+    float* kx2 = kye + H;
+    float* ky2 = kx2 + W;
+    for (int j = 0; j < W; ++j) {
+        kxe[j] = (float)((kxm[j] - kxm[(W - j) % W]) / 2);
+        kx2[j] = (float)(kx[j] * kx[j]);
+    }
+    for (int i = 0; i < H; ++i) {
+        kye[i] = (float)((kym[i] - kym[(H - i) % H]) / 2);
+        ky2[i] = (float)(ky[i] * ky[i]);
+    }
+    c->integ_tab.ensure(tab.size() * sizeof(float));
+    upload(c->integ_tab.p, tab.data(), tab.size() * sizeof(float), s);
+    HIPCHK(hipStreamSynchronize(s));  // tab is a host temporary
+    c->integ_cf = cf;
+}
+
+fcdk::IntegCoef integ_coef(fcd_ctx* c, double a0, double b0, double a1, double b1) {
+    fcdk::IntegCoef k;
+    const float* t = c->integ_tab.as<float>();
+    k.kxe = t;
+    k.kye = t + c->W;
+    k.kx2 = t + c->W + c->H;
+    k.ky2 = t + 2 * c->W + c->H;
+    k.a0 = (float)a0;
+    k.b0 = (float)b0;
+    k.a1 = (float)a1;
+    k.b1 = (float)b1;
+    k.norm = (float)(1.0 / ((double)c->H * (double)c->W));
+    return k;
+}
+
+// h = real(ifft2(multiplier * fft2(z)))  for nb fields z (in c->spec).
+void integrate_z(fcd_ctx* c, int nb, const fcdk::IntegCoef& k, float* h_out, hipStream_t s) {
+    float2* Z = c->spec.as<float2>();
+    float2* Hh = c->work.as<float2>();
+    fcdk::row_fft(c->W, false, fcdk::ROW_IN_COMPLEX, fcdk::ROW_OUT_COMPLEX, Z, Z, (long)nb * c->H, c->H, 0.f,
+                  c->tw_row.as<float2>(), nullptr, s);
+    fcdk::col_fft(c->H, c->W, false, Z, nb, c->tw_col.as<float2>(), s);
+    fcdk::integ_multiply(Z, Hh, nb, c->H, c->W, k, s);
+    fcdk::col_fft(c->H, c->W, true, Hh, nb, c->tw_col.as<float2>(), s);
+    fcdk::row_fft(c->W, true, fcdk::ROW_IN_COMPLEX, fcdk::ROW_OUT_REAL, Hh, h_out, (long)nb * c->H, c->H, 0.f,
+                  c->tw_row.as<float2>(), nullptr, s);
+}
+
+void check_ctx(fcd_ctx* c) {
+    if (!c) throw FcdError(FCD_E_INVALID, "null context");
+    HIPCHK(hipSetDevice(c->device));
+}
+
+void find_carriers_host(fcd_ctx* c, const std::vector<int>& idx_in, const std::vector<float>& val_in, float thr,
+                        double square_size) {
+    const int H = c->H, W = c->W;
+    const size_t n = idx_in.size();
+    std::vector<size_t> order(n);
+    std::iota(order.begin(), order.end(), 0);
+    std::sort(order.begin(), order.end(), [&](size_t a, size_t b) { return idx_in[a] < idx_in[b]; });
+    std::vector<int> idx(n);
+    std::vector<float> val(n);
+    for (size_t i = 0; i < n; ++i) {
+        idx[i] = idx_in[order[i]];
+        val[i] = val_in[order[i]];
+    }
+    // 8-connected labelling of the sparse set (skimage.measure.label, connectivity 2)
+    std::vector<int> parent(n);
+    std::iota(parent.begin(), parent.end(), 0);
+    auto find = [&](int x) {
+        while (parent[x] != x) {
+            parent[x] = parent[parent[x]];
+            x = parent[x];
+        }
+        return x;
+    };
+    auto lookup = [&](int r, int col) -> int {
+        if (r < 0 || col < 0 || r >= H || col >= W) return -1;
+        const int key = r * W + col;
+        auto it = std::lower_bound(idx.begin(), idx.end(), key);
+        return (it != idx.end() && *it == key) ? (int)(it - idx.begin()) : -1;
+    };
+    for (size_t i = 0; i < n; ++i) {
+        const int r = idx[i] / W, col = idx[i] % W;
+        const int nb[4][2] = {{r - 1, col - 1}, {r - 1, col}, {r - 1, col + 1}, {r, col - 1}};
+        for (auto& q : nb) {
+            const int j = lookup(q[0], q[1]);
+            if (j >= 0) {
+                const int a = find((int)i), b = find(j);
+                if (a != b) parent[std::max(a, b)] = std::min(a, b);
+            }
+        }
+    }
+    // blobs in raster order of their first pixel; per blob the max (first on ties)
+    std::vector<Blob> blobs;
+    std::vector<int> blob_of(n, -1);
+    for (size_t i = 0; i < n; ++i) {
+        const int root = find((int)i);
+        if (blob_of[root] < 0) {
+            blob_of[root] = (int)blobs.size();
+            blobs.push_back(Blob{idx[i], idx[i], val[i]});
+        } else {
+            Blob& b = blobs[blob_of[root]];
+            if (val[i] > b.value) {
+                b.value = val[i];
+                b.peak = idx[i];
+            }
+        }
+    }
+    std::stable_sort(blobs.begin(), blobs.end(), [](const Blob& a, const Blob& b) { return a.value < b.value; });
+    if (blobs.size() > 4) blobs.resize(4);
+    if (blobs.size() < 1) throw FcdError(FCD_E_NOPEAKS, "find_peaks: no spectral peaks above threshold");
+
+    const std::vector<double> kr = wavenumber(H, 1.0, true), kc = wavenumber(W, 1.0, true);
+    auto kvec = [&](int p) { return std::pair<double, double>(kr[p / W], kc[p % W]); };
+    // rightmost = min |atan2(k_row, k_col)|; perpendicular = min |k_right . k| (fourier.py:38-39)
+    size_t ir = 0;
+    double best = INFINITY;
+    for (size_t i = 0; i < blobs.size(); ++i) {
+        auto k = kvec(blobs[i].peak);
+        const double a = std::fabs(std::atan2(k.first, k.second));
+        if (a < best) {
+            best = a;
+            ir = i;
+        }
+    }
+    const auto k0 = kvec(blobs[ir].peak);
+    size_t ip = 0;
+    best = INFINITY;
+    for (size_t i = 0; i < blobs.size(); ++i) {
+        auto k = kvec(blobs[i].peak);
+        const double d = std::fabs(k0.first * k.first + k0.second * k.second);
+        if (d < best) {
+            best = d;
+            ip = i;
+        }
+    }
+    fcd_ref_info& info = c->info;
+    std::memset(&info, 0, sizeof(info));
+    info.n_blobs = (int)blobs.size();
+    for (size_t i = 0; i < blobs.size(); ++i) {
+        info.blob_peaks[i][0] = blobs[i].peak / W;
+        info.blob_peaks[i][1] = blobs[i].peak % W;
+    }
+    info.threshold = thr;
+    const int pk[2] = {blobs[ir].peak, blobs[ip].peak};
+    for (int q = 0; q < 2; ++q) {
+        info.peaks[q][0] = pk[q] / W;
+        info.peaks[q][1] = pk[q] % W;
+    }
+    // calibration factor (fcd.py:85-101): 2*sq / (2*pi / mean(|k_pix|))
+    const double ak[4] = {std::fabs(kr[pk[0] / W]), std::fabs(kc[pk[0] % W]), std::fabs(kr[pk[1] / W]),
+                          std::fabs(kc[pk[1] % W])};
+    const double mean = (((ak[0] + ak[1]) + ak[2]) + ak[3]) / 4.0;
+    const double pixel_wavelength = (2 * kPi) / mean;
+    const double cf = (2 * square_size) / pixel_wavelength;
+    info.calibration_factor = cf;
+    const double dr = (double)(info.peaks[0][0] - info.peaks[1][0]);
+    const double dc = (double)(info.peaks[0][1] - info.peaks[1][1]);
+    info.radius = std::sqrt(dr * dr + dc * dc) / 2;
+    const std::vector<double> krc = wavenumber(H, cf, true), kcc = wavenumber(W, cf, true);
+    for (int q = 0; q < 2; ++q) {
+        info.frequencies[q][0] = krc[info.peaks[q][0]];
+        info.frequencies[q][1] = kcc[info.peaks[q][1]];
+    }
+    // disk raster (skimage.draw.disk -> ellipse, rotation 0), per shifted column the row range
+    c->disk_rows_host.assign((size_t)4 * W, 0);
+    const double R = info.radius;
+    for (int q = 0; q < 2; ++q) {
+        int* rows = c->disk_rows_host.data() + (size_t)q * 2 * W;
+        for (int j = 0; j < W; ++j) {
+            rows[2 * j] = 1;
+            rows[2 * j + 1] = 0;
+        }
+        const long pr = info.peaks[q][0], pc = info.peaks[q][1];
+        const long lo_r = std::max<long>((long)std::ceil((double)pr - R), 0);
+        const long hi_r = std::min<long>((long)std::floor((double)pr + R), H - 1);
+        const long lo_c = std::max<long>((long)std::ceil((double)pc - R), 0);
+        const long hi_c = std::min<long>((long)std::floor((double)pc + R), W - 1);
+        int count = 0;
+        for (long sc = lo_c; sc <= hi_c; ++sc) {
+            const double cc = (double)(sc - lo_c) - (double)(pc - lo_c);
+            const double cq = cc / R;
+            const double c2 = cq * cq;
+            int first = -1, last = -2;
+            for (long sr = lo_r; sr <= hi_r; ++sr) {
+                const double rr = (double)(sr - lo_r) - (double)(pr - lo_r);
+                const double rq = rr / R;
+                const double d = rq * rq + c2;
+                if (d < 1.0) {
+                    if (first < 0) first = (int)sr;
+                    last = (int)sr;
+                    ++count;
+                }
+            }
+            if (first >= 0) {
+                rows[2 * sc] = first;
+                rows[2 * sc + 1] = last;
+            }
+        }
+        info.mask_count[q] = count;
+    }
+}
+
+}  // namespace
+
+// ====================================================================== C ABI
+#define FCD_API extern "C" __attribute__((visibility("default")))
+
+#define FCD_TRY(...)                                                            \
+    try {                                                                       \
+        __VA_ARGS__;                                                            \
+        return FCD_OK;                                                          \
+    } catch (const FcdError& e) {                                               \
+        g_last_error = e.what();                                                \
+        return e.code;                                                          \
+    } catch (const std::exception& e) {                                         \
+        g_last_error = e.what();                                                \
+        return FCD_E_INTERNAL;                                                  \
+    } catch (...) {                                                             \
+        g_last_error = "unknown error";                                         \
+        return FCD_E_INTERNAL;                                                  \
+    }
+
+FCD_API int fcd_abi_version(void) { return FCD_ABI_VERSION; }
+
+FCD_API const char* fcd_last_error(void) { return g_last_error.c_str(); }
+
+FCD_API int fcd_create(int device, int rows, int cols, fcd_ctx** out) {
+    FCD_TRY({
+        if (!out) throw FcdError(FCD_E_INVALID, "out is null");
+        *out = nullptr;
+        if (!fcdk::fft_size_supported(rows) || !fcdk::fft_size_supported(cols))
+            throw FcdError(FCD_E_UNSUPPORTED, "rows and cols must be powers of two in [64, 4096], got " +
+                                                  std::to_string(rows) + "x" + std::to_string(cols));
+        int ndev = 0;
+        HIPCHK(hipGetDeviceCount(&ndev));
+        if (device < 0 || device >= ndev) throw FcdError(FCD_E_INVALID, "bad device ordinal");
+        HIPCHK(hipSetDevice(device));
+        std::unique_ptr<fcd_ctx> c(new fcd_ctx());
+        c->device = device;
+        c->H = rows;
+        c->W = cols;
+        HIPCHK(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking));
+        const std::vector<float2> tr = twiddles(cols), tc = twiddles(rows);
+        c->tw_row.ensure(tr.size() * sizeof(float2));
+        c->tw_col.ensure(tc.size() * sizeof(float2));
+        HIPCHK(hipMemcpy(c->tw_row.p, tr.data(), tr.size() * sizeof(float2), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(c->tw_col.p, tc.data(), tc.size() * sizeof(float2), hipMemcpyHostToDevice));
+        // chunk: ~48 B of workspace per pixel per frame; keep the working set near the 256 MiB MALL
+        const long per_frame = 48L * rows * cols;
+        c->chunk = (int)std::max(1L, std::min(64L, (256L << 20) / per_frame));
+        ensure_chunk_buffers(c.get());
+        c->scalar.ensure(64);
+        *out = c.release();
+    })
+}
+
+FCD_API int fcd_destroy(fcd_ctx* ctx) {
+    FCD_TRY({
+        if (!ctx) return FCD_OK;
+        (void)hipSetDevice(ctx->device);
+        (void)hipStreamSynchronize(ctx->own);
+        (void)hipStreamDestroy(ctx->own);
+        delete ctx;
+    })
+}
+
+FCD_API int fcd_synchronize(fcd_ctx* ctx) {
+    FCD_TRY({
+        check_ctx(ctx);
+        HIPCHK(hipStreamSynchronize(ctx->own));
+    })
+}
+
+FCD_API int fcd_set_reference(fcd_ctx* c, const float* reference, int flags, double square_size,
+                              fcd_ref_info* info) {
+    FCD_TRY({
+        check_ctx(c);
+        if (!reference) throw FcdError(FCD_E_INVALID, "reference is null");
+        hipStream_t s = c->own;
+        const long hw = c->hw();
+        c->has_ref = false;
+        const float* dref = reference;
+        if (flags != FCD_DEVICE_PTRS) {
+            c->frames_in.ensure(hw * sizeof(float));
+            upload(c->frames_in.p, reference, hw * sizeof(float), s);
+            dref = c->frames_in.as<float>();
+        }
+        // fourier.find_peaks: |fftshift(fft2(ref - mean))| * highpass  (fourier.py:18-34)
+        double* dmean = c->scalar.as<double>();
+        fcdk::mean_f64(dref, hw, dmean, s);
+        double mean = 0;
+        HIPCHK(hipMemcpyAsync(&mean, dmean, sizeof(double), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        const float meanf = (float)(mean / (double)hw);
+        float2* F = c->spec.as<float2>();
+        fft2_real(c, dref, F, 1, meanf, s);
+        const std::vector<double> krs = wavenumber(c->H, 1.0, true), kcs = wavenumber(c->W, 1.0, true);
+        DevBuf ktab;
+        ktab.ensure((c->H + c->W) * sizeof(double));
+        upload(ktab.p, krs.data(), c->H * sizeof(double), s);
+        upload(ktab.as<double>() + c->H, kcs.data(), c->W * sizeof(double), s);
+        const double kmin = 4 * kPi / (double)std::min(c->H, c->W);
+        float* mag = c->wrapped.as<float>();
+        unsigned* maxbits = reinterpret_cast<unsigned*>(c->scalar.as<char>() + 16);
+        int* count = reinterpret_cast<int*>(c->scalar.as<char>() + 32);
+        fcdk::spectrum_mag(F, mag, maxbits, c->H, c->W, ktab.as<double>(), ktab.as<double>() + c->H, kmin * kmin, s);
+        const int cap = 1 << 16;
+        c->cand_idx.ensure(cap * sizeof(int));
+        c->cand_val.ensure(cap * sizeof(float));
+        fcdk::spectrum_candidates(mag, maxbits, c->H, c->W, count, c->cand_idx.as<int>(), c->cand_val.as<float>(),
+                                  cap, s);
+        int ncand = 0;
+        unsigned mb = 0;
+        HIPCHK(hipMemcpyAsync(&ncand, count, sizeof(int), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(&mb, maxbits, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        if (ncand > cap) throw FcdError(FCD_E_UNSUPPORTED, "find_peaks: too many pixels above threshold");
+        std::vector<int> cidx(ncand);
+        std::vector<float> cval(ncand);
+        if (ncand) {
+            HIPCHK(hipMemcpy(cidx.data(), c->cand_idx.p, ncand * sizeof(int), hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(cval.data(), c->cand_val.p, ncand * sizeof(float), hipMemcpyDeviceToHost));
+        }
+        float mx;
+        std::memcpy(&mx, &mb, 4);
+        find_carriers_host(c, cidx, cval, 0.5f * mx, square_size);
+        c->disk_rows.ensure(c->disk_rows_host.size() * sizeof(int));
+        upload(c->disk_rows.p, c->disk_rows_host.data(), c->disk_rows_host.size() * sizeof(int), s);
+        // Carrier.ccsgn = conj(ifft2(fft2(ref) * mask))  (carriers.py:22-24); we keep its angle.
+        fft2_real(c, dref, F, 1, 0.f, s);
+        c->refsig.ensure(2 * hw * sizeof(float2));
+        c->theta.ensure(2 * hw * sizeof(float));
+        for (int q = 0; q < 2; ++q) {
+            float2* R = c->refsig.as<float2>() + q * hw;
+            fcdk::DiskTable t{c->disk_rows.as<int>() + (size_t)q * 2 * c->W};
+            fcdk::disk_mask(F, R, 1, c->H, c->W, t, s);
+            fcdk::col_fft(c->H, c->W, true, R, 1, c->tw_col.as<float2>(), s);
+            fcdk::row_fft(c->W, true, fcdk::ROW_IN_COMPLEX, fcdk::ROW_OUT_COMPLEX, R, R, c->H, c->H, 0.f,
+                          c->tw_row.as<float2>(), nullptr, s);
+            fcdk::angle(R, c->theta.as<float>() + q * hw, hw, s);
+        }
+        HIPCHK(hipStreamSynchronize(s));
+        c->has_ref = true;
+        if (info) *info = c->info;
+    })
+}
+
+FCD_API int fcd_get_carriers(fcd_ctx* c, float* ccsgn, uint8_t* mask) {
+    FCD_TRY({
+        check_ctx(c);
+        if (!c->has_ref) throw FcdError(FCD_E_STATE, "no reference set");
+        const long hw = c->hw();
+        if (ccsgn) {
+            HIPCHK(hipMemcpy(ccsgn, c->refsig.p, 2 * hw * sizeof(float2), hipMemcpyDeviceToHost));
+            const float sc = (float)(1.0 / (double)hw);
+            for (long i = 0; i < 2 * hw; ++i) {
+                ccsgn[2 * i] *= sc;
+                ccsgn[2 * i + 1] *= -sc;  // conj
+            }
+        }
+        if (mask) {
+            for (int q = 0; q < 2; ++q) {
+                const int* rows = c->disk_rows_host.data() + (size_t)q * 2 * c->W;
+                for (int i = 0; i < c->H; ++i)
+                    for (int j = 0; j < c->W; ++j) {
+                        const int si = (i + c->H / 2) % c->H, sj = (j + c->W / 2) % c->W;
+                        mask[(size_t)q * hw + (size_t)i * c->W + j] = si >= rows[2 * sj] && si <= rows[2 * sj + 1];
+                    }
+            }
+        }
+    })
+}
+
+FCD_API int fcd_process(fcd_ctx* c, const float* frames, int n_frames, int flags, double height, int unwrap,
+                        float* height_out, float* wrapped_out, int32_t* k_out, void* stream) {
+    FCD_TRY({
+        check_ctx(c);
+        if (!c->has_ref) throw FcdError(FCD_E_STATE, "no reference set");
+        if (!frames || n_frames < 0) throw FcdError(FCD_E_INVALID, "bad frames");
+        if (!(height != 0.0)) throw FcdError(FCD_E_INVALID, "height must be non-zero");
+        hipStream_t s = c->pick(stream);
+        const long hw = c->hw();
+        const bool dev = flags == FCD_DEVICE_PTRS;
+        const fcd_ref_info& in = c->info;
+        const double det = in.frequencies[0][1] * in.frequencies[1][0] - in.frequencies[0][0] * in.frequencies[1][1];
+        const double sc = 1.0 / (det * height);
+        ensure_integ_tables(c, in.calibration_factor, s);
+        // h_hat = i/k^2 [(kx f1[0] - ky f1[1]) Phi0 + (ky f0[1] - kx f0[0]) Phi1] / (det * height)
+        const fcdk::IntegCoef coef = integ_coef(c, in.frequencies[1][0] * sc, -in.frequencies[1][1] * sc,
+                                                -in.frequencies[0][0] * sc, in.frequencies[0][1] * sc);
+        if (!dev) {
+            c->frames_in.ensure((size_t)c->chunk * hw * sizeof(float));
+            c->out_h.ensure((size_t)c->chunk * hw * sizeof(float));
+        }
+        for (int f0 = 0; f0 < n_frames; f0 += c->chunk) {
+            const int nb = std::min(c->chunk, n_frames - f0);
+            const float* fr = frames + (size_t)f0 * hw;
+            if (!dev) {
+                upload(c->frames_in.p, fr, (size_t)nb * hw * sizeof(float), s);
+                fr = c->frames_in.as<float>();
+            }
+            if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
+            fft2_real(c, fr, c->spec.as<float2>(), nb, 0.f, s);
+            float* w = c->wrapped.as<float>();
+            demod_phases(c, c->spec.as<float2>(), nb, w, s);
+            if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
+            int32_t* k = nullptr;
+            if (unwrap) {
+                k = c->kbuf.as<int32_t>();
+                unwrap_maps(c, w, 2 * nb, k, nullptr, s);
+            }
+            if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
+            fcdk::make_z(w, k, c->spec.as<float2>(), nb, c->H, c->W, s);
+            float* hdst = height_out ? (dev ? height_out + (size_t)f0 * hw : c->out_h.as<float>()) : nullptr;
+            if (hdst) integrate_z(c, nb, coef, hdst, s);
+            if (c->profiling) {
+                HIPCHK(hipEventRecord(c->next_event(), s));
+                c->prof_frames += nb;
+            }
+            if (dev) {
+                if (wrapped_out)
+                    HIPCHK(hipMemcpyAsync(wrapped_out + (size_t)f0 * 2 * hw, w, (size_t)nb * 2 * hw * 4,
+                                          hipMemcpyDeviceToDevice, s));
+                if (k_out) {
+                    if (k)
+                        HIPCHK(hipMemcpyAsync(k_out + (size_t)f0 * 2 * hw, k, (size_t)nb * 2 * hw * 4,
+                                              hipMemcpyDeviceToDevice, s));
+                    else
+                        HIPCHK(hipMemsetAsync(k_out + (size_t)f0 * 2 * hw, 0, (size_t)nb * 2 * hw * 4, s));
+                }
+            } else {
+                if (hdst)
+                    HIPCHK(hipMemcpyAsync(height_out + (size_t)f0 * hw, hdst, (size_t)nb * hw * 4,
+                                          hipMemcpyDeviceToHost, s));
+                if (wrapped_out)
+                    HIPCHK(hipMemcpyAsync(wrapped_out + (size_t)f0 * 2 * hw, w, (size_t)nb * 2 * hw * 4,
+                                          hipMemcpyDeviceToHost, s));
+                if (k_out) {
+                    if (k)
+                        HIPCHK(hipMemcpyAsync(k_out + (size_t)f0 * 2 * hw, k, (size_t)nb * 2 * hw * 4,
+                                              hipMemcpyDeviceToHost, s));
+                    else
+                        std::memset(k_out + (size_t)f0 * 2 * hw, 0, (size_t)nb * 2 * hw * 4);
+                }
+                HIPCHK(hipStreamSynchronize(s));
+            }
+        }
+    })
+}
+
+FCD_API int fcd_phases_from_spectrum(fcd_ctx* c, const float* spectrum, int n, int flags, int unwrap,
+                                     float* wrapped_out, int32_t* k_out, void* stream) {
+    FCD_TRY({
+        check_ctx(c);
+        if (!c->has_ref) throw FcdError(FCD_E_STATE, "no reference set");
+        if (!spectrum || n < 0) throw FcdError(FCD_E_INVALID, "bad spectrum");
+        hipStream_t s = c->pick(stream);
+        const long hw = c->hw();
+        const bool dev = flags == FCD_DEVICE_PTRS;
+        for (int f0 = 0; f0 < n; f0 += c->chunk) {
+            const int nb = std::min(c->chunk, n - f0);
+            const float2* sp = reinterpret_cast<const float2*>(spectrum) + (size_t)f0 * hw;
+            if (!dev) {
+                upload(c->spec.p, sp, (size_t)nb * hw * sizeof(float2), s);
+                sp = c->spec.as<float2>();
+            }
+            float* w = c->wrapped.as<float>();
+            demod_phases(c, sp, nb, w, s);
+            int32_t* k = nullptr;
+            if (unwrap) {
+                k = c->kbuf.as<int32_t>();
+                unwrap_maps(c, w, 2 * nb, k, nullptr, s);
+            }
+            const hipMemcpyKind kind = dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+            if (wrapped_out)
+                HIPCHK(hipMemcpyAsync(wrapped_out + (size_t)f0 * 2 * hw, w, (size_t)nb * 2 * hw * 4, kind, s));
+            if (k_out && k)
+                HIPCHK(hipMemcpyAsync(k_out + (size_t)f0 * 2 * hw, k, (size_t)nb * 2 * hw * 4, kind, s));
+            else if (k_out && dev)
+                HIPCHK(hipMemsetAsync(k_out + (size_t)f0 * 2 * hw, 0, (size_t)nb * 2 * hw * 4, s));
+            else if (k_out)
+                std::memset(k_out + (size_t)f0 * 2 * hw, 0, (size_t)nb * 2 * hw * 4);
+            if (!dev) HIPCHK(hipStreamSynchronize(s));
+        }
+    })
+}
+
+FCD_API int fcd_unwrap(fcd_ctx* c, const float* wrapped, int n_maps, int flags, int32_t* k_out,
+                       int32_t* residues_out, void* stream) {
+    FCD_TRY({
+        check_ctx(c);
+        if (!wrapped || !k_out || n_maps < 0) throw FcdError(FCD_E_INVALID, "bad arguments");
+        hipStream_t s = c->pick(stream);
+        const long hw = c->hw();
+        const bool dev = flags == FCD_DEVICE_PTRS;
+        const int per = 2 * c->chunk;
+        for (int m0 = 0; m0 < n_maps; m0 += per) {
+            const int nm = std::min(per, n_maps - m0);
+            const float* w = wrapped + (size_t)m0 * hw;
+            if (!dev) {
+                upload(c->wrapped.p, w, (size_t)nm * hw * 4, s);
+                w = c->wrapped.as<float>();
+            }
+            int32_t* k = dev ? k_out + (size_t)m0 * hw : c->kbuf.as<int32_t>();
+            std::vector<int> res(nm);
+            unwrap_maps(c, w, nm, k, res.data(), s);
+            if (residues_out) std::copy(res.begin(), res.end(), residues_out + m0);
+            if (!dev) {
+                HIPCHK(hipMemcpyAsync(k_out + (size_t)m0 * hw, k, (size_t)nm * hw * 4, hipMemcpyDeviceToHost, s));
+                HIPCHK(hipStreamSynchronize(s));
+            }
+        }
+        HIPCHK(hipStreamSynchronize(s));
+    })
+}
+
+FCD_API int fcd_integrate(fcd_ctx* c, const float* gx, const float* gy, int n, double cf, int flags, float* h_out,
+                          void* stream) {
+    FCD_TRY({
+        check_ctx(c);
+        if (!gx || !gy || !h_out || n < 0) throw FcdError(FCD_E_INVALID, "bad arguments");
+        hipStream_t s = c->pick(stream);
+        const long hw = c->hw();
+        const bool dev = flags == FCD_DEVICE_PTRS;
+        ensure_integ_tables(c, cf, s);
+        // h_hat = (-i kx gx_hat - i ky gy_hat) / k^2  ->  a0 = -1, b1 = -1
+        const fcdk::IntegCoef coef = integ_coef(c, -1.0, 0.0, 0.0, -1.0);
+        if (!dev) {
+            c->frames_in.ensure((size_t)c->chunk * hw * 4 * 2);
+            c->out_h.ensure((size_t)c->chunk * hw * 4);
+        }
+        for (int f0 = 0; f0 < n; f0 += c->chunk) {
+            const int nb = std::min(c->chunk, n - f0);
+            const float* x = gx + (size_t)f0 * hw;
+            const float* y = gy + (size_t)f0 * hw;
+            if (!dev) {
+                float* st = c->frames_in.as<float>();
+                upload(st, x, (size_t)nb * hw * 4, s);
+                upload(st + (size_t)nb * hw, y, (size_t)nb * hw * 4, s);
+                x = st;
+                y = st + (size_t)nb * hw;
+            }
+            fcdk::pack_z(x, y, c->spec.as<float2>(), (long)nb * hw, s);
+            float* dst = dev ? h_out + (size_t)f0 * hw : c->out_h.as<float>();
+            integrate_z(c, nb, coef, dst, s);
+            if (!dev) {
+                HIPCHK(hipMemcpyAsync(h_out + (size_t)f0 * hw, dst, (size_t)nb * hw * 4, hipMemcpyDeviceToHost, s));
+                HIPCHK(hipStreamSynchronize(s));
+            }
+        }
+    })
+}
+
+FCD_API int fcd_fft2(fcd_ctx* c, const float* in, int n, int flags, float* out, void* stream) {
+    FCD_TRY({
+        check_ctx(c);
+        if (!in || !out || n < 0) throw FcdError(FCD_E_INVALID, "bad arguments");
+        hipStream_t s = c->pick(stream);
+        const long hw = c->hw();
+        const bool dev = flags == FCD_DEVICE_PTRS;
+        if (!dev) c->frames_in.ensure((size_t)c->chunk * hw * 4);
+        for (int f0 = 0; f0 < n; f0 += c->chunk) {
+            const int nb = std::min(c->chunk, n - f0);
+            const float* x = in + (size_t)f0 * hw;
+            if (!dev) {
+                upload(c->frames_in.p, x, (size_t)nb * hw * 4, s);
+                x = c->frames_in.as<float>();
+            }
+            float2* dst = dev ? reinterpret_cast<float2*>(out) + (size_t)f0 * hw : c->spec.as<float2>();
+            fft2_real(c, x, dst, nb, 0.f, s);
+            if (!dev) {
+                HIPCHK(hipMemcpyAsync(out + (size_t)f0 * hw * 2, dst, (size_t)nb * hw * 8, hipMemcpyDeviceToHost, s));
+                HIPCHK(hipStreamSynchronize(s));
+            }
+        }
+    })
+}
+
+FCD_API int fcd_profile(fcd_ctx* c, int enable) {
+    FCD_TRY({
+        check_ctx(c);
+        HIPCHK(hipStreamSynchronize(c->own));
+        c->profiling = enable != 0;
+        c->ev_used = 0;
+        c->prof_frames = 0;
+    })
+}
+
+FCD_API int fcd_stage_times(fcd_ctx* c, double* out4, int64_t* frames) {
+    FCD_TRY({
+        check_ctx(c);
+        if (!out4) throw FcdError(FCD_E_INVALID, "out4 is null");
+        for (int i = 0; i < 4; ++i) out4[i] = 0;
+        if (c->ev_used) HIPCHK(hipEventSynchronize(c->ev_pool[c->ev_used - 1]));
+        for (size_t q = 0; q + 3 < c->ev_used; q += 4) {
+            float ms[3];
+            for (int i = 0; i < 3; ++i) HIPCHK(hipEventElapsedTime(&ms[i], c->ev_pool[q + i], c->ev_pool[q + i + 1]));
+            for (int i = 0; i < 3; ++i) out4[i] += ms[i];
+            out4[3] += (double)ms[0] + ms[1] + ms[2];
+        }
+        if (frames) *frames = c->prof_frames;
+        c->ev_used = 0;
+        c->prof_frames = 0;
+    })
+}

@@ -1,0 +1,153 @@
+// Device FFT core for gfx950: LDS-staged Stockham autosort FFT with
+// in-register radix-2/4/8/16 codelets and compile-time radix schedules.
+//
+// A "team" of TT = N / E threads computes one N-point complex FFT; each thread
+// holds E complex values per pass (E = 16 for N >= 1024, so a 1024-point FFT
+// is one wave64: radix 16 -> 16 -> 4).  Several teams share a workgroup; the
+// workgroup barrier separates passes.  LDS rows are padded by one complex per
+// 32 (pad()) so the stride-R writes of the first Stockham pass do not pile on
+// one bank (MI355X_MICROARCH.md §LDS: 64 banks, ds_read_b64 in 32-lane groups).
+//
+// Twiddles come from a per-size global table tw[m] = exp(-2*pi*i*m/N) computed
+// on the host in double precision and rounded once to float; tables are a few
+// KiB and stay L1/L2-resident across the grid.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace fcdk {
+
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+    return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ float2 cconj(float2 a) { return make_float2(a.x, -a.y); }
+__device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
+
+__host__ __device__ constexpr int ilog2c(int n) { return n <= 1 ? 0 : 1 + ilog2c(n / 2); }
+
+// Elements per thread for an N-point transform.
+__host__ __device__ constexpr int fft_elems(int n) { return n >= 1024 ? 16 : (n >= 512 ? 8 : 4); }
+// Threads per team.
+__host__ __device__ constexpr int fft_team(int n) { return n / fft_elems(n); }
+// Padded LDS index: one spare complex per 32.
+__device__ __forceinline__ int pad(int i) { return i + (i >> 5); }
+__host__ __device__ constexpr int padded_len(int n) { return n + (n >> 5); }
+
+// cos / sin of 2*pi*m/16, m = 0..15.
+__device__ constexpr float kC16[16] = {
+    1.0f, 0.923879532511286756f, 0.707106781186547524f, 0.382683432365089772f,
+    0.0f, -0.382683432365089772f, -0.707106781186547524f, -0.923879532511286756f,
+    -1.0f, -0.923879532511286756f, -0.707106781186547524f, -0.382683432365089772f,
+    0.0f, 0.382683432365089772f, 0.707106781186547524f, 0.923879532511286756f};
+__device__ constexpr float kS16[16] = {
+    0.0f, 0.382683432365089772f, 0.707106781186547524f, 0.923879532511286756f,
+    1.0f, 0.923879532511286756f, 0.707106781186547524f, 0.382683432365089772f,
+    0.0f, -0.382683432365089772f, -0.707106781186547524f, -0.923879532511286756f,
+    -1.0f, -0.923879532511286756f, -0.707106781186547524f, -0.382683432365089772f};
+
+// v * W_R^K with W_R = exp(-2*pi*i/R) (forward) or its conjugate (inverse).
+template <int R, int K, bool INV>
+__device__ __forceinline__ float2 twc(float2 v) {
+    constexpr int m = (K * (16 / R)) & 15;
+    if constexpr (m == 0) {
+        return v;
+    } else if constexpr (m == 4) {
+        return INV ? make_float2(-v.y, v.x) : make_float2(v.y, -v.x);
+    } else if constexpr (m == 8) {
+        return make_float2(-v.x, -v.y);
+    } else if constexpr (m == 12) {
+        return INV ? make_float2(v.y, -v.x) : make_float2(-v.y, v.x);
+    } else {
+        const float c = kC16[m];
+        const float s = INV ? kS16[m] : -kS16[m];
+        return make_float2(v.x * c - v.y * s, v.x * s + v.y * c);
+    }
+}
+
+template <int R, int K, bool INV>
+__device__ __forceinline__ void dft_combine(float2* a, const float2* e, const float2* o) {
+    if constexpr (K < R / 2) {
+        const float2 t = twc<R, K, INV>(o[K]);
+        a[K] = cadd(e[K], t);
+        a[K + R / 2] = csub(e[K], t);
+        dft_combine<R, K + 1, INV>(a, e, o);
+    }
+}
+
+// In-register R-point DFT, natural order in and out (R <= 16).
+template <int R, bool INV>
+__device__ __forceinline__ void dft_reg(float2* a) {
+    if constexpr (R == 2) {
+        const float2 t = a[0];
+        a[0] = cadd(t, a[1]);
+        a[1] = csub(t, a[1]);
+    } else if constexpr (R > 2) {
+        float2 e[R / 2], o[R / 2];
+#pragma unroll
+        for (int i = 0; i < R / 2; ++i) {
+            e[i] = a[2 * i];
+            o[i] = a[2 * i + 1];
+        }
+        dft_reg<R / 2, INV>(e);
+        dft_reg<R / 2, INV>(o);
+        dft_combine<R, 0, INV>(a, e, o);
+    }
+}
+
+// One Stockham pass over an N-point sequence held (padded) in LDS buffer s.
+// L = product of the radices already applied.  Thread t of the team.
+template <int N, int R, int L, bool INV>
+__device__ __forceinline__ void stockham_pass(float2* s, const float2* __restrict__ tw, int t) {
+    constexpr int TT = fft_team(N);
+    constexpr int NB = N / R;        // butterflies in this pass
+    constexpr int BPT = NB / TT;     // butterflies per thread
+    static_assert(BPT >= 1 && NB % TT == 0, "bad radix schedule");
+    float2 a[BPT][R];
+#pragma unroll
+    for (int b = 0; b < BPT; ++b) {
+        const int j = t + b * TT;
+        const int k = j % L;
+#pragma unroll
+        for (int r = 0; r < R; ++r) a[b][r] = s[pad(j + r * NB)];
+        if constexpr (L > 1) {
+            constexpr int step = N / (L * R);
+#pragma unroll
+            for (int r = 1; r < R; ++r) {
+                float2 w = tw[r * k * step];
+                if (INV) w.y = -w.y;
+                a[b][r] = cmul(a[b][r], w);
+            }
+        }
+        dft_reg<R, INV>(a[b]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int b = 0; b < BPT; ++b) {
+        const int j = t + b * TT;
+        const int k = j % L;
+        const int base = (j - k) * R + k;
+#pragma unroll
+        for (int r = 0; r < R; ++r) s[pad(base + r * L)] = a[b][r];
+    }
+    __syncthreads();
+}
+
+template <int N, int L, bool INV>
+__device__ __forceinline__ void stockham_passes(float2* s, const float2* __restrict__ tw, int t) {
+    if constexpr (L < N) {
+        constexpr int E = fft_elems(N);
+        constexpr int R = (N / L) >= E ? E : (N / L);
+        stockham_pass<N, R, L, INV>(s, tw, t);
+        stockham_passes<N, L * R, INV>(s, tw, t);
+    }
+}
+
+// In-place N-point FFT of the team's padded LDS row s (natural order in/out,
+// unnormalised).  Must be called by every thread of the workgroup (barriers).
+template <int N, bool INV>
+__device__ __forceinline__ void fft_team_lds(float2* s, const float2* __restrict__ tw, int t) {
+    stockham_passes<N, 1, INV>(s, tw, t);
+}
+
+}  // namespace fcdk

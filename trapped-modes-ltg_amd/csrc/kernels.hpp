@@ -1,0 +1,79 @@
+// Launch wrappers for the FCD HIP kernels (gfx950).  Host-callable; every
+// wrapper is asynchronous on the given stream and dispatches on the
+// power-of-two transform length at run time.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace fcdk {
+
+// Row-FFT input / output modes.
+enum RowIn { ROW_IN_COMPLEX = 0, ROW_IN_REAL = 1 };
+enum RowOut { ROW_OUT_COMPLEX = 0, ROW_OUT_REAL = 1, ROW_OUT_PHASE = 2 };
+
+struct PhaseOut {          // ROW_OUT_PHASE: w = wrap(theta - atan2(A))
+    const float* theta;    // [H][W] reference angle of this carrier
+    float* wrapped;        // output base; row r of batch b -> wrapped + ((b*2 + carrier)*H + r)*W
+    int carrier;
+};
+
+// Disk band-pass of one carrier (skimage.draw.disk raster in fftshifted
+// coordinates): per shifted column sc the inclusive shifted-row range
+// [rows[2*sc], rows[2*sc+1]] inside the disk (empty when lo > hi).
+struct DiskTable {
+    const int* rows;       // device, length 2*W
+};
+
+// Integration multipliers: h_hat = i*((kxe*a0 + kye*b0)*Phi0 + (kxe*a1 + kye*b1)*Phi1)/k2 * norm
+struct IntegCoef {
+    const float* kxe;      // [W] odd-symmetrised column wavenumbers
+    const float* kye;      // [H] odd-symmetrised row wavenumbers
+    const float* kx2;      // [W] unmodified column wavenumber squared
+    const float* ky2;      // [H]
+    float a0, b0, a1, b1, norm;
+};
+
+bool fft_size_supported(int n);
+
+// In-place or out-of-place batched row FFT over nrows rows of length W.
+void row_fft(int W, bool inverse, RowIn in_mode, RowOut out_mode, const void* in, void* out, long nrows,
+             int H, float sub, const float2* tw, const PhaseOut* ph, hipStream_t s);
+// In-place batched column FFT of nbatch [H][W] complex arrays.
+void col_fft(int H, int W, bool inverse, float2* data, int nbatch, const float2* tw, hipStream_t s);
+
+// out[b] = in[b] * disk (unshifted spectrum index)
+void disk_mask(const float2* in, float2* out, int nbatch, int H, int W, DiskTable t, hipStream_t s);
+// theta = atan2(R)  (reference carrier angle)
+void angle(const float2* in, float* out, long n, hipStream_t s);
+// Mean of an image (f64 accumulation) into *out_d (device double).
+void mean_f64(const float* img, long n, double* out_d, hipStream_t s);
+// Masked |F| in shifted layout + max (as uint bits) for peak finding.
+void spectrum_mag(const float2* F, float* mag, unsigned* maxbits, int H, int W, const double* krow_s,
+                  const double* kcol_s, double kmin2, hipStream_t s);
+// Candidate pixels of the thresholded spectrum (border excluded).
+void spectrum_candidates(const float* mag, const unsigned* maxbits, int H, int W, int* count, int* idx,
+                         float* val, int cap, hipStream_t s);
+
+// ---- unwrap ----
+void residues(const float* w, int nmaps, int H, int W, int* counts, hipStream_t s);
+void unwrap_scan(const float* w, int nmaps, int H, int W, int* colk, int32_t* k, hipStream_t s);
+
+struct MstWork {
+    int* comp; int* off; double* rel; double* cand_w; int* cand_e;
+    unsigned long long* best_w; int* best_e; unsigned long long* link; int* nhooks;
+};
+// Maps listed in map_ids (device int[nact]) of the wrapped stack w.
+void mst_init(const float* w, const int* map_ids, int nact, int H, int W, MstWork m, hipStream_t s);
+void mst_round(const float* w, const int* map_ids, int nact, int H, int W, MstWork m, hipStream_t s);
+void mst_finalize(const int* map_ids, int nact, int H, int W, MstWork m, int32_t* k, hipStream_t s);
+
+// ---- integration ----
+// z = (w0 + 2pi k0) + i (w1 + 2pi k1)   (k may be null)
+void make_z(const float* w, const int32_t* k, float2* z, int nbatch, int H, int W, hipStream_t s);
+// z = gx + i gy
+void pack_z(const float* gx, const float* gy, float2* z, long n, hipStream_t s);
+void integ_multiply(const float2* Z, float2* Hh, int nbatch, int H, int W, IntegCoef c, hipStream_t s);
+// phases f32 = w + 2pi k
+void compose_phase(const float* w, const int32_t* k, float* out, long n, hipStream_t s);
+
+}  // namespace fcdk

@@ -1,0 +1,336 @@
+// Batched 2-D FFT building blocks and the demodulation band kernels.
+//
+// Replaces, on the device, the scipy.fft calls of the reference hot path:
+//   fft2(displaced)                       /root/reference/pyfcd/fcd.py:28
+//   ifft2(displaced_fft * carrier.mask)   /root/reference/pyfcd/fcd.py:118
+//   fft2(reference), ifft2(... * mask)    /root/reference/pyfcd/carriers.py:22-24
+//   fft2(image - mean) for peak finding   /root/reference/pyfcd/fourier.py:18
+// and the disk band-pass of carriers.py:17-20 (skimage.draw.disk raster).
+#include <hip/hip_runtime.h>
+
+#include <stdexcept>
+#include <string>
+
+#include "fft_lds.hpp"
+#include "kernels.hpp"
+
+namespace fcdk {
+
+#define FCD_HIPCHK(x)                                                               \
+    do {                                                                            \
+        hipError_t e_ = (x);                                                        \
+        if (e_ != hipSuccess) throw std::runtime_error(std::string(#x ": ") + hipGetErrorString(e_)); \
+    } while (0)
+#define FCD_CHECK_LAUNCH()                                                          \
+    do {                                                                            \
+        hipError_t e_ = hipGetLastError();                                          \
+        if (e_ != hipSuccess) throw std::runtime_error(std::string("kernel launch: ") + hipGetErrorString(e_)); \
+    } while (0)
+
+bool fft_size_supported(int n) { return n >= 64 && n <= 4096 && (n & (n - 1)) == 0; }
+
+constexpr float kPiF = 3.14159265358979f;
+constexpr float kTwoPiF = 6.28318530717959f;
+
+// ------------------------------------------------------------------ row FFT
+// One team per row; 256-thread workgroups (a 1024-point row is one wave).
+template <int N>
+struct RowCfg {
+    static constexpr int TT = fft_team(N);
+    static constexpr int BLOCK = TT >= 256 ? TT : 256;
+    static constexpr int TEAMS = BLOCK / TT;
+};
+
+template <int N, bool INV, int IN, int OUT>
+__global__ __launch_bounds__(RowCfg<N>::BLOCK) void k_row_fft(const void* __restrict__ in, void* __restrict__ out,
+                                                               long nrows, int H, float sub,
+                                                               const float2* __restrict__ tw, PhaseOut ph) {
+    using C = RowCfg<N>;
+    constexpr int E = fft_elems(N);
+    __shared__ __attribute__((aligned(16))) float2 lds[C::TEAMS][padded_len(N)];
+    const int team = threadIdx.x / C::TT;
+    const int t = threadIdx.x % C::TT;
+    const long row = (long)blockIdx.x * C::TEAMS + team;
+    const bool valid = row < nrows;
+    float2* s = lds[team];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int i = t + e * C::TT;
+        float2 v = make_float2(0.f, 0.f);
+        if (valid) {
+            if constexpr (IN == ROW_IN_REAL) {
+                v.x = static_cast<const float*>(in)[row * N + i] - sub;
+            } else {
+                v = static_cast<const float2*>(in)[row * N + i];
+            }
+        }
+        s[pad(i)] = v;
+    }
+    __syncthreads();
+    fft_team_lds<N, INV>(s, tw, t);
+    if (!valid) return;
+    if constexpr (OUT == ROW_OUT_COMPLEX) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const int i = t + e * C::TT;
+            static_cast<float2*>(out)[row * N + i] = s[pad(i)];
+        }
+    } else if constexpr (OUT == ROW_OUT_REAL) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const int i = t + e * C::TT;
+            static_cast<float*>(out)[row * N + i] = s[pad(i)].x;
+        }
+    } else {
+        // w = wrap(theta - angle(A)) == -angle(A * conj(R)) of fcd.py:118
+        const long b = row / H, r = row % H;
+        const float* th = ph.theta + r * N;
+        float* wo = ph.wrapped + ((b * 2 + ph.carrier) * H + r) * (long)N;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const int i = t + e * C::TT;
+            const float2 a = s[pad(i)];
+            float d = th[i] - atan2f(a.y, a.x);
+            if (d > kPiF) d -= kTwoPiF;
+            else if (d < -kPiF) d += kTwoPiF;
+            wo[i] = d;
+        }
+    }
+}
+
+template <int N, bool INV, int IN, int OUT>
+static void launch_row(const void* in, void* out, long nrows, int H, float sub, const float2* tw, const PhaseOut* ph,
+                       hipStream_t s) {
+    using C = RowCfg<N>;
+    PhaseOut p{};
+    if (ph) p = *ph;
+    const long blocks = (nrows + C::TEAMS - 1) / C::TEAMS;
+    hipLaunchKernelGGL((k_row_fft<N, INV, IN, OUT>), dim3((unsigned)blocks), dim3(C::BLOCK), 0, s, in, out, nrows, H,
+                       sub, tw, p);
+    FCD_CHECK_LAUNCH();
+}
+
+template <int N>
+static void row_dispatch_n(bool inv, RowIn im, RowOut om, const void* in, void* out, long nrows, int H, float sub,
+                           const float2* tw, const PhaseOut* ph, hipStream_t s) {
+    if (!inv && im == ROW_IN_REAL && om == ROW_OUT_COMPLEX)
+        launch_row<N, false, ROW_IN_REAL, ROW_OUT_COMPLEX>(in, out, nrows, H, sub, tw, ph, s);
+    else if (!inv && im == ROW_IN_COMPLEX && om == ROW_OUT_COMPLEX)
+        launch_row<N, false, ROW_IN_COMPLEX, ROW_OUT_COMPLEX>(in, out, nrows, H, sub, tw, ph, s);
+    else if (inv && im == ROW_IN_COMPLEX && om == ROW_OUT_COMPLEX)
+        launch_row<N, true, ROW_IN_COMPLEX, ROW_OUT_COMPLEX>(in, out, nrows, H, sub, tw, ph, s);
+    else if (inv && im == ROW_IN_COMPLEX && om == ROW_OUT_REAL)
+        launch_row<N, true, ROW_IN_COMPLEX, ROW_OUT_REAL>(in, out, nrows, H, sub, tw, ph, s);
+    else if (inv && im == ROW_IN_COMPLEX && om == ROW_OUT_PHASE)
+        launch_row<N, true, ROW_IN_COMPLEX, ROW_OUT_PHASE>(in, out, nrows, H, sub, tw, ph, s);
+    else
+        throw std::runtime_error("row_fft: unsupported mode combination");
+}
+
+void row_fft(int W, bool inverse, RowIn im, RowOut om, const void* in, void* out, long nrows, int H, float sub,
+             const float2* tw, const PhaseOut* ph, hipStream_t s) {
+    if (nrows <= 0) return;
+    switch (W) {
+        case 64: row_dispatch_n<64>(inverse, im, om, in, out, nrows, H, sub, tw, ph, s); break;
+        case 128: row_dispatch_n<128>(inverse, im, om, in, out, nrows, H, sub, tw, ph, s); break;
+        case 256: row_dispatch_n<256>(inverse, im, om, in, out, nrows, H, sub, tw, ph, s); break;
+        case 512: row_dispatch_n<512>(inverse, im, om, in, out, nrows, H, sub, tw, ph, s); break;
+        case 1024: row_dispatch_n<1024>(inverse, im, om, in, out, nrows, H, sub, tw, ph, s); break;
+        case 2048: row_dispatch_n<2048>(inverse, im, om, in, out, nrows, H, sub, tw, ph, s); break;
+        case 4096: row_dispatch_n<4096>(inverse, im, om, in, out, nrows, H, sub, tw, ph, s); break;
+        default: throw std::runtime_error("row_fft: unsupported length " + std::to_string(W));
+    }
+}
+
+// ------------------------------------------------------------------ column FFT
+// A workgroup loads G adjacent columns (G*8-byte row segments), one team
+// transforms each column in LDS.  Column stride padded_len(H)+1 (odd) keeps
+// the transposing loads/stores bank-conflict free.
+template <int N>
+struct ColCfg {
+    static constexpr int TT = fft_team(N);
+    static constexpr int BLOCK = TT >= 512 ? TT : 512;
+    static constexpr int G = BLOCK / TT;
+    static constexpr int STRIDE = padded_len(N) + 1;
+};
+
+template <int N, bool INV>
+__global__ __launch_bounds__(ColCfg<N>::BLOCK) void k_col_fft(float2* __restrict__ data, int W, int g_used,
+                                                              const float2* __restrict__ tw) {
+    using C = ColCfg<N>;
+    extern __shared__ __attribute__((aligned(16))) float2 lds_dyn[];
+    const int team = threadIdx.x / C::TT;
+    const int t = threadIdx.x % C::TT;
+    const int colblocks = W / g_used;
+    const long b = blockIdx.x / colblocks;
+    const int c0 = (blockIdx.x % colblocks) * g_used;
+    float2* base = data + b * (long)N * W + c0;
+    for (int idx = threadIdx.x; idx < N * g_used; idx += C::BLOCK) {
+        const int r = idx / g_used, g = idx % g_used;
+        lds_dyn[g * C::STRIDE + pad(r)] = base[(long)r * W + g];
+    }
+    __syncthreads();
+    fft_team_lds<N, INV>(lds_dyn + team * C::STRIDE, tw, t);
+    for (int idx = threadIdx.x; idx < N * g_used; idx += C::BLOCK) {
+        const int r = idx / g_used, g = idx % g_used;
+        base[(long)r * W + g] = lds_dyn[g * C::STRIDE + pad(r)];
+    }
+}
+
+template <int N>
+static void launch_col(int W, bool inv, float2* data, int nbatch, const float2* tw, hipStream_t s) {
+    using C = ColCfg<N>;
+    // Teams beyond the used columns transform zeros (keeps every barrier uniform).
+    const int g_used = W < C::G ? W : C::G;
+    const size_t lds = (size_t)C::G * C::STRIDE * sizeof(float2);
+    const unsigned blocks = (unsigned)((long)nbatch * (W / g_used));
+    static bool attr_set = false;  // per instantiation: allow > 64 KiB dynamic LDS (gfx950 has 160 KiB)
+    if (!attr_set) {
+        FCD_HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_col_fft<N, true>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        FCD_HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_col_fft<N, false>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        attr_set = true;
+    }
+    if (inv)
+        hipLaunchKernelGGL((k_col_fft<N, true>), dim3(blocks), dim3(C::BLOCK), lds, s, data, W, g_used, tw);
+    else
+        hipLaunchKernelGGL((k_col_fft<N, false>), dim3(blocks), dim3(C::BLOCK), lds, s, data, W, g_used, tw);
+    FCD_CHECK_LAUNCH();
+}
+
+void col_fft(int H, int W, bool inverse, float2* data, int nbatch, const float2* tw, hipStream_t s) {
+    if (nbatch <= 0) return;
+    switch (H) {
+        case 64: launch_col<64>(W, inverse, data, nbatch, tw, s); break;
+        case 128: launch_col<128>(W, inverse, data, nbatch, tw, s); break;
+        case 256: launch_col<256>(W, inverse, data, nbatch, tw, s); break;
+        case 512: launch_col<512>(W, inverse, data, nbatch, tw, s); break;
+        case 1024: launch_col<1024>(W, inverse, data, nbatch, tw, s); break;
+        case 2048: launch_col<2048>(W, inverse, data, nbatch, tw, s); break;
+        case 4096: launch_col<4096>(W, inverse, data, nbatch, tw, s); break;
+        default: throw std::runtime_error("col_fft: unsupported length " + std::to_string(H));
+    }
+}
+
+// ------------------------------------------------------------------ band-pass
+// mask = ifftshift(disk(peak, R)): unshifted (i, j) is inside iff the shifted
+// (i+H/2, j+W/2) lies in the skimage disk raster (carriers.py:17-20).
+__global__ void k_disk_mask(const float2* __restrict__ in, float2* __restrict__ out, long n, int H, int W,
+                            DiskTable t) {
+    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= n) return;
+    const long p = idx % ((long)H * W);
+    const int i = (int)(p / W), j = (int)(p % W);
+    const int si = (i + H / 2) & (H - 1), sj = (j + W / 2) & (W - 1);
+    const int2 rr = reinterpret_cast<const int2*>(t.rows)[sj];
+    const bool inside = si >= rr.x && si <= rr.y;
+    out[idx] = inside ? in[idx] : make_float2(0.f, 0.f);
+}
+
+void disk_mask(const float2* in, float2* out, int nbatch, int H, int W, DiskTable t, hipStream_t s) {
+    const long n = (long)nbatch * H * W;
+    hipLaunchKernelGGL(k_disk_mask, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, in, out, n, H, W, t);
+    FCD_CHECK_LAUNCH();
+}
+
+__global__ void k_angle(const float2* __restrict__ in, float* __restrict__ out, long n) {
+    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx < n) out[idx] = atan2f(in[idx].y, in[idx].x);
+}
+
+void angle(const float2* in, float* out, long n, hipStream_t s) {
+    hipLaunchKernelGGL(k_angle, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, in, out, n);
+    FCD_CHECK_LAUNCH();
+}
+
+// ------------------------------------------------------------------ peak finding support
+// fourier.find_peaks (fourier.py:18-35): |fftshift(F)| * highpass, max, threshold.
+__global__ void k_mean(const float* __restrict__ img, long n, double* out) {
+    __shared__ double part[256];
+    double acc = 0.0;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+        acc += (double)img[i];
+    part[threadIdx.x] = acc;
+    __syncthreads();
+    for (int st = 128; st > 0; st >>= 1) {
+        if ((int)threadIdx.x < st) part[threadIdx.x] += part[threadIdx.x + st];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) atomicAdd(out, part[0]);
+}
+
+void mean_f64(const float* img, long n, double* out_d, hipStream_t s) {
+    FCD_HIPCHK(hipMemsetAsync(out_d, 0, sizeof(double), s));
+    hipLaunchKernelGGL(k_mean, dim3(256), dim3(256), 0, s, img, n, out_d);
+    FCD_CHECK_LAUNCH();
+}
+
+__global__ void k_spectrum_mag(const float2* __restrict__ F, float* __restrict__ mag, unsigned* maxbits, int H, int W,
+                               const double* __restrict__ krow_s, const double* __restrict__ kcol_s, double kmin2) {
+    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    float m = 0.f;
+    if (idx < (long)H * W) {
+        const int si = (int)(idx / W), sj = (int)(idx % W);           // shifted coordinates
+        int i = (si + H / 2) & (H - 1), j = (sj + W / 2) & (W - 1);  // unshifted source
+        // Read the Hermitian pair (k, -k) from ONE canonical bin so |F(k)| == |F(-k)|
+        // bit-for-bit, as the reference's real-input pocketfft guarantees; its peak
+        // picks rely on that tie (SURVEY.md §8a parity fact 1).
+        const int mi = (H - i) & (H - 1), mj = (W - j) & (W - 1);
+        if (mi < i || (mi == i && mj < j)) {
+            i = mi;
+            j = mj;
+        }
+        const float2 f = F[(long)i * W + j];
+        m = hypotf(f.x, f.y);
+        const double kr = krow_s[si], kc = kcol_s[sj];
+        const double k2 = __dadd_rn(__dmul_rn(kr, kr), __dmul_rn(kc, kc));
+        if (!(k2 > kmin2)) m = 0.f;
+        mag[idx] = m;
+    }
+    // wave max then one atomic per wave (non-negative floats order as uints)
+    unsigned u = __float_as_uint(m);
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned v = __shfl_xor(u, o, 64);
+        u = v > u ? v : u;
+    }
+    if ((threadIdx.x & 63) == 0) atomicMax(maxbits, u);
+}
+
+void spectrum_mag(const float2* F, float* mag, unsigned* maxbits, int H, int W, const double* krow_s,
+                  const double* kcol_s, double kmin2, hipStream_t s) {
+    const long n = (long)H * W;
+    FCD_HIPCHK(hipMemsetAsync(maxbits, 0, sizeof(unsigned), s));
+    hipLaunchKernelGGL(k_spectrum_mag, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, F, mag, maxbits, H, W,
+                       krow_s, kcol_s, kmin2);
+    FCD_CHECK_LAUNCH();
+}
+
+// find_peak_locations (fourier.py:152-158): pixels > threshold, 1-px border zeroed.
+__global__ void k_candidates(const float* __restrict__ mag, const unsigned* __restrict__ maxbits, int H, int W,
+                             int* count, int* idx_out, float* val_out, int cap) {
+    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (long)H * W) return;
+    const int si = (int)(idx / W), sj = (int)(idx % W);
+    if (si == 0 || sj == 0 || si == H - 1 || sj == W - 1) return;
+    const float thr = 0.5f * __uint_as_float(*maxbits);
+    const float m = mag[idx];
+    if (m > thr) {
+        const int slot = atomicAdd(count, 1);
+        if (slot < cap) {
+            idx_out[slot] = (int)idx;
+            val_out[slot] = m;
+        }
+    }
+}
+
+void spectrum_candidates(const float* mag, const unsigned* maxbits, int H, int W, int* count, int* idx, float* val,
+                         int cap, hipStream_t s) {
+    const long n = (long)H * W;
+    FCD_HIPCHK(hipMemsetAsync(count, 0, sizeof(int), s));
+    hipLaunchKernelGGL(k_candidates, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, mag, maxbits, H, W, count,
+                       idx, val, cap);
+    FCD_CHECK_LAUNCH();
+}
+
+}  // namespace fcdk

@@ -1,0 +1,348 @@
+// Phase unwrapping on the device: the reference's
+//   phases[i] = unwrap_phase(phase_angles)        /root/reference/pyfcd/fcd.py:119
+// (scikit-image 0.18.3, Herraez et al. 2002; restated in oracle/herraez_unwrap.c).
+//
+// Herraez's greedy merge over edges sorted by reliability accepts exactly the
+// edges of the unique minimum spanning tree under the total order
+// (reliability, edge index), and the result is w + 2*pi*k with k integrated
+// along that tree (k2 - k1 = -find_wrap(w1, w2) across every tree edge),
+// up to one global constant.  Two device paths produce that k-field:
+//
+//  * residue-free maps (no plaquette with non-zero wrap-count circulation):
+//    every path integrates to the same k, so a column-0 prefix scan plus a
+//    per-row prefix scan (one wave per row) gives it exactly;
+//  * maps with residues: Boruvka MST on the 4-connected pixel grid with the
+//    reference's f64 reliabilities and edge-index tie-break, carrying each
+//    vertex's k-offset to its component root through every hook and pointer
+//    jump, so the tree integration falls out of the MST construction itself.
+//
+// Both normalise k(0, 0) = 0 (the reference's constant depends on its merge
+// history).
+#include <hip/hip_runtime.h>
+
+#include <stdexcept>
+#include <string>
+
+#include "kernels.hpp"
+
+namespace fcdk {
+
+#define FCD_HIPCHK(x)                                                               \
+    do {                                                                            \
+        hipError_t e_ = (x);                                                        \
+        if (e_ != hipSuccess) throw std::runtime_error(std::string(#x ": ") + hipGetErrorString(e_)); \
+    } while (0)
+#define FCD_CHECK_LAUNCH()                                                          \
+    do {                                                                            \
+        hipError_t e_ = hipGetLastError();                                          \
+        if (e_ != hipSuccess) throw std::runtime_error(std::string("kernel launch: ") + hipGetErrorString(e_)); \
+    } while (0)
+
+constexpr double kPi = 3.141592653589793;      // skimage unwrap's PI (probed: double M_PI)
+constexpr double kTwoPi = 6.283185307179586;
+constexpr double kBorderRel = 9999999.0;
+
+// find_wrap of the reference unwrapper: -1 if w1 - w2 > pi, +1 if < -pi.
+__device__ __forceinline__ int find_wrap(float a, float b) {
+    const double d = (double)a - (double)b;  // exact in f64
+    return d > kPi ? -1 : (d < -kPi ? 1 : 0);
+}
+
+__device__ __forceinline__ double wrapd(double x) {
+    return x > kPi ? __dsub_rn(x, kTwoPi) : (x < -kPi ? __dadd_rn(x, kTwoPi) : x);
+}
+
+// ------------------------------------------------------------------ residues
+__global__ void k_residues(const float* __restrict__ w, int nmaps, int H, int W, int* counts) {
+    const long hw = (long)H * W;
+    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    int r = 0;
+    int map = -1;
+    if (idx < nmaps * hw) {
+        map = (int)(idx / hw);
+        const long p = idx % hw;
+        const int i = (int)(p / W), j = (int)(p % W);
+        if (i < H - 1 && j < W - 1) {
+            const float* m = w + map * hw;
+            const float a = m[p], b = m[p + 1], c = m[p + W + 1], d = m[p + W];
+            r = (find_wrap(a, b) + find_wrap(b, c) + find_wrap(c, d) + find_wrap(d, a)) != 0;
+        }
+    }
+    // blocks never straddle maps when H*W % 256 == 0 (H, W >= 64 powers of two)
+    unsigned long long bal = __ballot(r);
+    const int wave_cnt = __popcll(bal);
+    if ((threadIdx.x & 63) == 0 && wave_cnt && map >= 0) atomicAdd(counts + map, wave_cnt);
+}
+
+void residues(const float* w, int nmaps, int H, int W, int* counts, hipStream_t s) {
+    const long n = (long)nmaps * H * W;
+    FCD_HIPCHK(hipMemsetAsync(counts, 0, sizeof(int) * nmaps, s));
+    hipLaunchKernelGGL(k_residues, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, w, nmaps, H, W, counts);
+    FCD_CHECK_LAUNCH();
+}
+
+// ------------------------------------------------------------------ residue-free scan path
+// colk[map][i] = k(i, 0) = -sum_{i' < i} find_wrap(w[i'][0], w[i'+1][0])
+__global__ __launch_bounds__(256) void k_colk(const float* __restrict__ w, int H, int W, int* __restrict__ colk) {
+    __shared__ int part[256];
+    const int map = blockIdx.x;
+    const float* m = w + (long)map * H * W;
+    const int per = (H + 255) / 256;
+    const int i0 = threadIdx.x * per;
+    int loc[16];
+    int sum = 0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int i = i0 + q;
+        loc[q] = 0;
+        if (q < per && i + 1 < H) {
+            sum -= find_wrap(m[(long)i * W], m[(long)(i + 1) * W]);
+        }
+        loc[q] = sum;  // inclusive within the thread: k(i+1,0) - base
+    }
+    part[threadIdx.x] = sum;
+    __syncthreads();
+    // exclusive scan of part (256 entries)
+    for (int off = 1; off < 256; off <<= 1) {
+        const int v = (int)threadIdx.x >= off ? part[threadIdx.x - off] : 0;
+        __syncthreads();
+        part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    const int base = threadIdx.x ? part[threadIdx.x - 1] : 0;
+    int* out = colk + (long)map * H;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int i = i0 + q;
+        if (q < per && i < H) out[i] = base + (q ? loc[q - 1] : 0);
+    }
+}
+
+// One wave per row: k(i, j) = colk[i] - sum_{j' < j} find_wrap(w[i][j'], w[i][j'+1]).
+__global__ __launch_bounds__(256) void k_rowscan(const float* __restrict__ w, long nrows, int H, int W,
+                                                 const int* __restrict__ colk, int32_t* __restrict__ k) {
+    const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (row >= nrows) return;
+    const float* r = w + row * W;
+    const int per = W / 64;  // W >= 64
+    const int j0 = lane * per;
+    int run = 0;
+    for (int q = 0; q < per; ++q) {
+        const int j = j0 + q;
+        if (j + 1 < W) run -= find_wrap(r[j], r[j + 1]);
+    }
+    // exclusive wave scan of per-lane totals
+    int incl = run;
+    for (int off = 1; off < 64; off <<= 1) {
+        const int v = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += v;
+    }
+    int acc = colk[row] + incl - run;  // row index == map*H + i == colk layout
+    int32_t* ko = k + row * W;
+    for (int q = 0; q < per; ++q) {
+        const int j = j0 + q;
+        ko[j] = acc;
+        if (j + 1 < W) acc -= find_wrap(r[j], r[j + 1]);
+    }
+}
+
+void unwrap_scan(const float* w, int nmaps, int H, int W, int* colk, int32_t* k, hipStream_t s) {
+    if (H > 4096) throw std::runtime_error("unwrap_scan: H too large");
+    hipLaunchKernelGGL(k_colk, dim3(nmaps), dim3(256), 0, s, w, H, W, colk);
+    FCD_CHECK_LAUNCH();
+    const long nrows = (long)nmaps * H;
+    hipLaunchKernelGGL(k_rowscan, dim3((unsigned)((nrows + 3) / 4)), dim3(256), 0, s, w, nrows, H, W, colk, k);
+    FCD_CHECK_LAUNCH();
+}
+
+// ------------------------------------------------------------------ Boruvka MST path
+// Vertex ids are slot*H*W + pixel for the nact active maps (slot -> map_ids[slot]).
+__device__ __forceinline__ unsigned long long pack_link(int parent, int off) {
+    return ((unsigned long long)(unsigned)parent << 32) | (unsigned)off;
+}
+__device__ __forceinline__ int link_parent(unsigned long long l) { return (int)(l >> 32); }
+__device__ __forceinline__ int link_off(unsigned long long l) { return (int)(unsigned)(l & 0xffffffffull); }
+
+__global__ void k_mst_rel(const float* __restrict__ w, const int* __restrict__ map_ids, int nact, int H, int W,
+                          double* __restrict__ rel, int* comp, int* off) {
+    const long hw = (long)H * W;
+    const long v = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= nact * hw) return;
+    const int slot = (int)(v / hw);
+    const long p = v % hw;
+    const int i = (int)(p / W), j = (int)(p % W);
+    const float* m = w + (long)map_ids[slot] * hw;
+    double r = kBorderRel;
+    if (i > 0 && j > 0 && i < H - 1 && j < W - 1) {
+        const double c = m[p];
+        const double h = __dsub_rn(wrapd(__dsub_rn((double)m[p - 1], c)), wrapd(__dsub_rn(c, (double)m[p + 1])));
+        const double vv = __dsub_rn(wrapd(__dsub_rn((double)m[p - W], c)), wrapd(__dsub_rn(c, (double)m[p + W])));
+        const double d1 =
+            __dsub_rn(wrapd(__dsub_rn((double)m[p - W - 1], c)), wrapd(__dsub_rn(c, (double)m[p + W + 1])));
+        const double d2 =
+            __dsub_rn(wrapd(__dsub_rn((double)m[p - W + 1], c)), wrapd(__dsub_rn(c, (double)m[p + W - 1])));
+        double s = __dadd_rn(__dmul_rn(h, h), __dmul_rn(vv, vv));
+        s = __dadd_rn(s, __dmul_rn(d1, d1));
+        s = __dadd_rn(s, __dmul_rn(d2, d2));
+        r = s;
+    }
+    rel[v] = r;
+    comp[v] = (int)v;
+    off[v] = 0;
+}
+
+// Candidate: the lightest (rel_e, edge index) edge of v leaving its component.
+__global__ void k_mst_cand(const int* __restrict__ map_ids, int nact, int H, int W, MstWork m) {
+    const long hw = (long)H * W;
+    const long v = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= nact * hw) return;
+    (void)map_ids;
+    const long base = (v / hw) * hw;
+    const long p = v - base;
+    const int i = (int)(p / W), j = (int)(p % W);
+    const int cv = m.comp[v];
+    const double rv = m.rel[v];
+    const int nh = H * (W - 1);
+    double bw = __longlong_as_double(0x7ff0000000000000ll);  // +inf
+    int be = 0x7fffffff;
+    auto consider = [&](long u, int eidx) {
+        if (m.comp[u] == cv) return;
+        const double we = (u > v) ? __dadd_rn(rv, m.rel[u]) : __dadd_rn(m.rel[u], rv);  // rel(p1) + rel(p2)
+        if (we < bw || (we == bw && eidx < be)) {
+            bw = we;
+            be = eidx;
+        }
+    };
+    if (j + 1 < W) consider(v + 1, i * (W - 1) + j);
+    if (j > 0) consider(v - 1, i * (W - 1) + j - 1);
+    if (i + 1 < H) consider(v + W, nh + i * W + j);
+    if (i > 0) consider(v - W, nh + (i - 1) * W + j);
+    m.cand_w[v] = bw;
+    m.cand_e[v] = be;
+    m.link[v] = pack_link((int)v, 0);
+    if (be != 0x7fffffff) atomicMin(m.best_w + cv, (unsigned long long)__double_as_longlong(bw));
+}
+
+__global__ void k_mst_cand2(int nact, int H, int W, MstWork m) {
+    const long v = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= nact * (long)H * W) return;
+    const int be = m.cand_e[v];
+    if (be == 0x7fffffff) return;
+    const int cv = m.comp[v];
+    if ((unsigned long long)__double_as_longlong(m.cand_w[v]) == m.best_w[cv]) atomicMin(m.best_e + cv, be);
+}
+
+__global__ void k_mst_hook(const float* __restrict__ w, const int* __restrict__ map_ids, int nact, int H, int W,
+                           MstWork m) {
+    const long hw = (long)H * W;
+    const long c = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= nact * hw) return;
+    if (m.comp[c] != (int)c) return;
+    const int e = m.best_e[c];
+    if (e == 0x7fffffff) return;
+    const long base = (c / hw) * hw;
+    const int nh = H * (W - 1);
+    long p1, p2;
+    if (e < nh) {
+        p1 = base + (long)(e / (W - 1)) * W + (e % (W - 1));
+        p2 = p1 + 1;
+    } else {
+        p1 = base + (e - nh);
+        p2 = p1 + W;
+    }
+    const float* mw = w + (long)map_ids[c / hw] * hw;
+    const int inc = find_wrap(mw[p1 - base], mw[p2 - base]);
+    long x, y;
+    int delta;  // k(y) - k(x) across the edge
+    if (m.comp[p1] == (int)c) {
+        x = p1; y = p2; delta = -inc;
+    } else {
+        x = p2; y = p1; delta = inc;
+    }
+    const int d = m.comp[y];
+    if (m.best_e[d] == e && c < d) return;  // mutual pair: the smaller root stays a root
+    const int poff = m.off[y] - m.off[x] - delta;  // K_c - K_d
+    m.link[c] = pack_link(d, poff);
+    atomicAdd(m.nhooks, 1);
+}
+
+__global__ void k_mst_jump(int nact, int H, int W, MstWork m) {
+    const long c = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= nact * (long)H * W) return;
+    if (m.comp[c] != (int)c) return;
+    unsigned long long l = __hip_atomic_load(m.link + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int p = link_parent(l), o = link_off(l);
+    if (p == (int)c) return;
+    for (;;) {
+        const unsigned long long l2 = __hip_atomic_load(m.link + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int pp = link_parent(l2);
+        if (pp == p) break;
+        o += link_off(l2);
+        p = pp;
+        __hip_atomic_store(m.link + c, pack_link(p, o), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+__global__ void k_mst_update(int nact, int H, int W, MstWork m) {
+    const long v = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= nact * (long)H * W) return;
+    const int c = m.comp[v];
+    const unsigned long long l = __hip_atomic_load(m.link + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int r = link_parent(l);
+    if (r != c) {
+        m.comp[v] = r;
+        m.off[v] += link_off(l);
+    }
+    m.best_w[v] = 0x7ff0000000000000ull;  // bits of +inf (positive doubles order as uints)
+    m.best_e[v] = 0x7fffffff;
+}
+
+__global__ void k_mst_reset(int nact, int H, int W, MstWork m) {
+    const long v = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= nact * (long)H * W) return;
+    m.best_w[v] = 0x7ff0000000000000ull;
+    m.best_e[v] = 0x7fffffff;
+}
+
+static inline unsigned nblk(long n) { return (unsigned)((n + 255) / 256); }
+
+void mst_init(const float* w, const int* map_ids, int nact, int H, int W, MstWork m, hipStream_t s) {
+    const long n = (long)nact * H * W;
+    hipLaunchKernelGGL(k_mst_rel, dim3(nblk(n)), dim3(256), 0, s, w, map_ids, nact, H, W, m.rel, m.comp, m.off);
+    FCD_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_mst_reset, dim3(nblk(n)), dim3(256), 0, s, nact, H, W, m);
+    FCD_CHECK_LAUNCH();
+}
+
+void mst_round(const float* w, const int* map_ids, int nact, int H, int W, MstWork m, hipStream_t s) {
+    const long n = (long)nact * H * W;
+    FCD_HIPCHK(hipMemsetAsync(m.nhooks, 0, sizeof(int), s));
+    hipLaunchKernelGGL(k_mst_cand, dim3(nblk(n)), dim3(256), 0, s, map_ids, nact, H, W, m);
+    FCD_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_mst_cand2, dim3(nblk(n)), dim3(256), 0, s, nact, H, W, m);
+    FCD_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_mst_hook, dim3(nblk(n)), dim3(256), 0, s, w, map_ids, nact, H, W, m);
+    FCD_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_mst_jump, dim3(nblk(n)), dim3(256), 0, s, nact, H, W, m);
+    FCD_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_mst_update, dim3(nblk(n)), dim3(256), 0, s, nact, H, W, m);
+    FCD_CHECK_LAUNCH();
+}
+
+__global__ void k_mst_finalize(const int* __restrict__ map_ids, int nact, int H, int W, MstWork m, int32_t* k) {
+    const long hw = (long)H * W;
+    const long v = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= nact * hw) return;
+    const int slot = (int)(v / hw);
+    const long base = slot * hw;
+    k[(long)map_ids[slot] * hw + (v - base)] = m.off[v] - m.off[base];
+}
+
+void mst_finalize(const int* map_ids, int nact, int H, int W, MstWork m, int32_t* k, hipStream_t s) {
+    const long n = (long)nact * H * W;
+    hipLaunchKernelGGL(k_mst_finalize, dim3(nblk(n)), dim3(256), 0, s, map_ids, nact, H, W, m, k);
+    FCD_CHECK_LAUNCH();
+}
+
+}  // namespace fcdk

@@ -1,0 +1,252 @@
+"""ctypes binding of the MI355X FCD engine (include/fcd.h).
+
+The engine is the in-tree shared library lib/libfcd_mi355x.so built from
+csrc/ (HIP kernels for gfx950).  There is no fallback: if the library or a
+HIP device is missing every entry point raises.
+"""
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+_PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get("FCD_LIB", os.path.join(_PKG_ROOT, "lib", "libfcd_mi355x.so"))
+
+FCD_OK = 0
+FCD_E_INVALID = -1
+FCD_E_UNSUPPORTED = -2
+FCD_E_HIP = -3
+FCD_E_STATE = -4
+FCD_E_NOPEAKS = -5
+FCD_E_INTERNAL = -6
+FCD_HOST_PTRS = 0
+FCD_DEVICE_PTRS = 1
+
+# Every symbol include/fcd.h declares (checked by tests/test_abi.py).
+EXPORTED = (
+    "fcd_abi_version", "fcd_last_error", "fcd_create", "fcd_destroy", "fcd_synchronize",
+    "fcd_set_reference", "fcd_get_carriers", "fcd_process", "fcd_phases_from_spectrum",
+    "fcd_unwrap", "fcd_integrate", "fcd_fft2", "fcd_profile", "fcd_stage_times",
+)
+
+
+class FcdRefInfo(ctypes.Structure):
+    _fields_ = [
+        ("peaks", (ctypes.c_int64 * 2) * 2),
+        ("radius", ctypes.c_double),
+        ("calibration_factor", ctypes.c_double),
+        ("frequencies", (ctypes.c_double * 2) * 2),
+        ("mask_count", ctypes.c_int32 * 2),
+        ("n_blobs", ctypes.c_int32),
+        ("blob_peaks", (ctypes.c_int64 * 2) * 4),
+        ("threshold", ctypes.c_float),
+    ]
+
+
+class FcdError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"fcd error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def load_library(path=None):
+    """Load libfcd_mi355x.so and declare the ABI.  Raises OSError if absent."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise OSError(f"MI355X FCD engine not built: {p} is missing (run __graft_entry__.build() or "
+                          f"`make -C trapped-modes-ltg_amd`)")
+        lib = ctypes.CDLL(p)
+        vp, i32, f64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_double
+        sig = {
+            "fcd_abi_version": ([], i32),
+            "fcd_last_error": ([], ctypes.c_char_p),
+            "fcd_create": ([i32, i32, i32, ctypes.POINTER(vp)], i32),
+            "fcd_destroy": ([vp], i32),
+            "fcd_synchronize": ([vp], i32),
+            "fcd_set_reference": ([vp, vp, i32, f64, ctypes.POINTER(FcdRefInfo)], i32),
+            "fcd_get_carriers": ([vp, vp, vp], i32),
+            "fcd_process": ([vp, vp, i32, i32, f64, i32, vp, vp, vp, vp], i32),
+            "fcd_phases_from_spectrum": ([vp, vp, i32, i32, i32, vp, vp, vp], i32),
+            "fcd_unwrap": ([vp, vp, i32, i32, vp, vp, vp], i32),
+            "fcd_integrate": ([vp, vp, vp, i32, f64, i32, vp, vp], i32),
+            "fcd_fft2": ([vp, vp, i32, i32, vp, vp], i32),
+            "fcd_profile": ([vp, i32], i32),
+            "fcd_stage_times": ([vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)], i32),
+        }
+        for name, (args, res) in sig.items():
+            fn = getattr(lib, name)
+            fn.argtypes = args
+            fn.restype = res
+        if path is None:
+            _lib = lib
+        return lib
+
+
+def _check(rc):
+    if rc != FCD_OK:
+        raise FcdError(rc, load_library().fcd_last_error().decode(errors="replace"))
+
+
+def _f32(a):
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data
+
+
+class Engine:
+    """One engine context: a device, a frame shape, and (once set) a reference."""
+
+    def __init__(self, shape, device=None):
+        lib = load_library()
+        if device is None:
+            device = int(os.environ.get("FCD_DEVICE", "0"))
+        self.shape = (int(shape[0]), int(shape[1]))
+        self.device = device
+        h = ctypes.c_void_p()
+        _check(lib.fcd_create(device, self.shape[0], self.shape[1], ctypes.byref(h)))
+        self._h = h
+        self._lib = lib
+        self.info = None
+        self.ref_copy = None
+        self.ref_square_size = None
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.fcd_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    # ------------------------------------------------------------ reference
+    def set_reference(self, reference, square_size):
+        ref = _f32(reference)
+        if ref.shape != self.shape:
+            raise ValueError(f"reference shape {ref.shape} != engine shape {self.shape}")
+        info = FcdRefInfo()
+        _check(self._lib.fcd_set_reference(self._h, ref.ctypes.data, FCD_HOST_PTRS, float(square_size),
+                                           ctypes.byref(info)))
+        self.info = info
+        self.ref_copy = ref.copy()
+        self.ref_square_size = float(square_size)
+        return info
+
+    def matches(self, reference, square_size):
+        if self.ref_copy is None or self.ref_square_size != float(square_size):
+            return False
+        ref = np.asarray(reference)
+        return ref.shape == self.ref_copy.shape and np.array_equal(_f32(ref), self.ref_copy)
+
+    def carriers_arrays(self):
+        h, w = self.shape
+        cc = np.empty((2, h, w), np.complex64)
+        mask = np.empty((2, h, w), np.uint8)
+        _check(self._lib.fcd_get_carriers(self._h, cc.ctypes.data, mask.ctypes.data))
+        return cc, mask.astype(bool)
+
+    # ------------------------------------------------------------ per frame
+    def process(self, frames, height, unwrap=True, want_phases=True):
+        fr = _f32(frames)
+        if fr.ndim == 2:
+            fr = fr[None]
+        n = fr.shape[0]
+        if fr.shape[1:] != self.shape:
+            raise ValueError(f"frame shape {fr.shape[1:]} != engine shape {self.shape}")
+        hmap = np.empty((n,) + self.shape, np.float32)
+        wrapped = np.empty((n, 2) + self.shape, np.float32) if want_phases else None
+        k = np.empty((n, 2) + self.shape, np.int32) if want_phases else None
+        _check(self._lib.fcd_process(self._h, fr.ctypes.data, n, FCD_HOST_PTRS, float(height), int(bool(unwrap)),
+                                     hmap.ctypes.data, _ptr(wrapped), _ptr(k), None))
+        return hmap, wrapped, k
+
+    def process_device(self, frames_ptr, n, height, unwrap, height_ptr, wrapped_ptr=None, k_ptr=None,
+                       stream=None):
+        """Device-pointer variant (e.g. torch tensors' data_ptr()); asynchronous on `stream`."""
+        _check(self._lib.fcd_process(self._h, ctypes.c_void_p(frames_ptr), int(n), FCD_DEVICE_PTRS, float(height),
+                                     int(bool(unwrap)), ctypes.c_void_p(height_ptr) if height_ptr else None,
+                                     ctypes.c_void_p(wrapped_ptr) if wrapped_ptr else None,
+                                     ctypes.c_void_p(k_ptr) if k_ptr else None,
+                                     ctypes.c_void_p(stream) if stream else None))
+
+    def profile(self, enable=True):
+        _check(self._lib.fcd_profile(self._h, int(bool(enable))))
+
+    def stage_times(self):
+        """(ms dict {demod, unwrap, integrate, total}, frames) accumulated since the last call."""
+        out = (ctypes.c_double * 4)()
+        nf = ctypes.c_int64()
+        _check(self._lib.fcd_stage_times(self._h, out, ctypes.byref(nf)))
+        return dict(zip(("demod", "unwrap", "integrate", "total"), list(out))), nf.value
+
+    def phases_from_spectrum(self, spectrum, unwrap=True):
+        sp = np.ascontiguousarray(spectrum, dtype=np.complex64)
+        if sp.ndim == 2:
+            sp = sp[None]
+        n = sp.shape[0]
+        wrapped = np.empty((n, 2) + self.shape, np.float32)
+        k = np.empty((n, 2) + self.shape, np.int32)
+        _check(self._lib.fcd_phases_from_spectrum(self._h, sp.ctypes.data, n, FCD_HOST_PTRS, int(bool(unwrap)),
+                                                  wrapped.ctypes.data, k.ctypes.data, None))
+        return wrapped, k
+
+    def unwrap(self, maps):
+        m = _f32(maps)
+        if m.ndim == 2:
+            m = m[None]
+        n = m.shape[0]
+        k = np.empty(m.shape, np.int32)
+        res = np.empty(n, np.int32)
+        _check(self._lib.fcd_unwrap(self._h, m.ctypes.data, n, FCD_HOST_PTRS, k.ctypes.data, res.ctypes.data, None))
+        return k, res
+
+    def integrate(self, gx, gy, calibration_factor=1.0):
+        x, y = _f32(gx), _f32(gy)
+        squeeze = x.ndim == 2
+        if squeeze:
+            x, y = x[None], y[None]
+        h = np.empty(x.shape, np.float32)
+        _check(self._lib.fcd_integrate(self._h, x.ctypes.data, y.ctypes.data, x.shape[0], float(calibration_factor),
+                                       FCD_HOST_PTRS, h.ctypes.data, None))
+        return h[0] if squeeze else h
+
+    def fft2(self, images):
+        x = _f32(images)
+        squeeze = x.ndim == 2
+        if squeeze:
+            x = x[None]
+        out = np.empty(x.shape, np.complex64)
+        _check(self._lib.fcd_fft2(self._h, x.ctypes.data, x.shape[0], FCD_HOST_PTRS, out.ctypes.data, None))
+        return out[0] if squeeze else out
+
+
+_engines = {}
+_engines_lock = threading.Lock()
+
+
+def engine_for(shape, device=None):
+    """Process-wide engine cache, one per (shape, device, thread)."""
+    key = (tuple(int(s) for s in shape), device, threading.get_ident())
+    with _engines_lock:
+        e = _engines.get(key)
+        if e is None:
+            e = Engine(shape, device)
+            _engines[key] = e
+        return e
