@@ -109,6 +109,13 @@ struct fcd_ctx {
     DevBuf integ_tab;      // float kxe[W], kye[H], kx2[W], ky2[H]
     double integ_cf = -1;
 
+    // band-pruned demodulation tables (DemodTables) and the fast path's workspace
+    DevBuf dt_hc, dt_outs, dt_outrows, dt_nouts, dt_colslot;
+    int NC = 0, NCc[2] = {0, 0}, NCA = 0;
+    int fchunk = 1;                  // frames per fast-path chunk
+    DevBuf Xb, Ab, Zt, Ht, fk, fres; // per-chunk intermediates; fk: k-fields for the fix-up pass
+    size_t fres_cap = 0;
+
     // workspace
     int chunk = 1;
     DevBuf spec, work, wrapped, kbuf, colk, rescnt, frames_in, out_h, scalar;
@@ -160,7 +167,7 @@ void ensure_mst(fcd_ctx* c, int nact) {
     c->mst_be.ensure(nv * 4);
     c->mst_link.ensure(nv * 8);
     c->mst_hooks.ensure(sizeof(int));
-    c->mst_ids.ensure(sizeof(int) * 2 * (size_t)c->chunk + 64);
+    c->mst_ids.ensure(sizeof(int) * 2 * (size_t)std::max(c->chunk, c->fchunk) + 64);
     c->mst_cap = nv;
 }
 
@@ -440,6 +447,100 @@ void find_carriers_host(fcd_ctx* c, const std::vector<int>& idx_in, const std::v
     }
 }
 
+// Band-pruned demodulation tables: which unshifted columns each carrier disk
+// covers, the half-spectrum column each one is read from (directly, or as the
+// conjugate mirror of column W - uc of the real input's spectrum), and the
+// per-carrier column slots of the inverse-transform planes.
+void build_demod_tables(fcd_ctx* c, hipStream_t s) {
+    const int H = c->H, W = c->W;
+    std::vector<int> colslot(2 * (size_t)W, -1);
+    struct Out { int carrier, cslot, mirror, uc, lo, hi; };
+    std::vector<std::vector<Out>> per_hc(W / 2 + 1);
+    for (int q = 0; q < 2; ++q) {
+        const int* rows = c->disk_rows_host.data() + (size_t)q * 2 * W;
+        int n = 0;
+        for (int sc = 0; sc < W; ++sc) {
+            if (rows[2 * sc] > rows[2 * sc + 1]) continue;
+            const int uc = (sc + W / 2) % W;  // ifftshift: shifted column -> unshifted
+            colslot[(size_t)q * W + uc] = n;
+            const int hc = uc <= W / 2 ? uc : W - uc;
+            per_hc[hc].push_back(Out{q, n, uc > W / 2 ? 1 : 0, uc, rows[2 * sc], rows[2 * sc + 1]});
+            ++n;
+        }
+        c->NCc[q] = n;
+    }
+    (void)H;
+    std::vector<int> hc_list, nouts;
+    std::vector<int4> outs;
+    std::vector<int2> outrows;
+    for (int hc = 0; hc <= W / 2; ++hc) {
+        if (per_hc[hc].empty()) continue;
+        if (per_hc[hc].size() > 4) throw FcdError(FCD_E_INTERNAL, "demod tables: > 4 outputs per column");
+        hc_list.push_back(hc);
+        nouts.push_back((int)per_hc[hc].size());
+        for (int e = 0; e < 4; ++e) {
+            if (e < (int)per_hc[hc].size()) {
+                const Out& o = per_hc[hc][e];
+                outs.push_back(make_int4(o.carrier, o.cslot, o.mirror, o.uc));
+                outrows.push_back(make_int2(o.lo, o.hi));
+            } else {
+                outs.push_back(make_int4(0, 0, 0, 0));
+                outrows.push_back(make_int2(1, 0));
+            }
+        }
+    }
+    c->NC = (int)hc_list.size();
+    c->NCA = std::max(std::max(c->NCc[0], c->NCc[1]), 1);
+    if (c->NC == 0) throw FcdError(FCD_E_NOPEAKS, "carrier disks are empty");
+    c->dt_hc.ensure(hc_list.size() * sizeof(int));
+    c->dt_nouts.ensure(nouts.size() * sizeof(int));
+    c->dt_outs.ensure(outs.size() * sizeof(int4));
+    c->dt_outrows.ensure(outrows.size() * sizeof(int2));
+    c->dt_colslot.ensure(colslot.size() * sizeof(int));
+    upload(c->dt_hc.p, hc_list.data(), hc_list.size() * sizeof(int), s);
+    upload(c->dt_nouts.p, nouts.data(), nouts.size() * sizeof(int), s);
+    upload(c->dt_outs.p, outs.data(), outs.size() * sizeof(int4), s);
+    upload(c->dt_outrows.p, outrows.data(), outrows.size() * sizeof(int2), s);
+    upload(c->dt_colslot.p, colslot.data(), colslot.size() * sizeof(int), s);
+    HIPCHK(hipStreamSynchronize(s));  // host vectors die here
+    // workspace per frame: Xb + Ab + wrapped + Zt + Ht (+ k for the fix-up path)
+    const long hw = c->hw();
+    const long per_frame = 8L * H * c->NC + 16L * H * c->NCA + 8L * hw + 8L * hw + 8L * H * (W / 2 + 1);
+    c->fchunk = (int)std::max(1L, std::min(32L, (192L << 20) / per_frame));
+    const size_t nb = (size_t)c->fchunk;
+    c->Xb.ensure(nb * H * c->NC * sizeof(float2));
+    c->Ab.ensure(nb * 2 * H * c->NCA * sizeof(float2));
+    c->Zt.ensure(nb * hw * sizeof(float2));
+    c->Ht.ensure(nb * H * (W / 2 + 1) * sizeof(float2));
+    c->wrapped.ensure(std::max(nb, (size_t)c->chunk) * 2 * hw * sizeof(float));
+    c->colk.ensure(std::max(nb, (size_t)c->chunk) * 2 * H * sizeof(int));
+    c->fk.ensure(nb * 2 * hw * sizeof(int32_t));
+    c->rescnt.ensure(std::max(nb, (size_t)c->chunk) * 2 * sizeof(int));
+    c->mst_cap = 0;  // re-size the MST workspace for the new chunk on next use
+}
+
+fcdk::DemodTables demod_tables(fcd_ctx* c) {
+    fcdk::DemodTables t;
+    t.hc = c->dt_hc.as<int>();
+    t.outs = c->dt_outs.as<int4>();
+    t.outrows = c->dt_outrows.as<int2>();
+    t.nouts = c->dt_nouts.as<int>();
+    t.colslot = c->dt_colslot.as<int>();
+    t.NC = c->NC;
+    t.NCc[0] = c->NCc[0];
+    t.NCc[1] = c->NCc[1];
+    return t;
+}
+
+// Fast path for nb frames (device pointer): band-pruned demod -> wrapped (c->wrapped).
+void fast_demod(fcd_ctx* c, const float* frames, int nb, hipStream_t s) {
+    const fcdk::DemodTables T = demod_tables(c);
+    fcdk::demod_rows(c->W, frames, c->H, nb, T, c->Xb.as<float2>(), c->tw_row.as<float2>(), s);
+    fcdk::demod_cols(c->H, c->Xb.as<float2>(), nb, T, c->Ab.as<float2>(), c->NCA, c->tw_col.as<float2>(), s);
+    fcdk::demod_phase(c->W, c->Ab.as<float2>(), c->H, nb, c->NCA, T, c->theta.as<float>(), c->wrapped.as<float>(),
+                      c->tw_row.as<float2>(), s);
+}
+
 }  // namespace
 
 // ====================================================================== C ABI
@@ -566,6 +667,7 @@ FCD_API int fcd_set_reference(fcd_ctx* c, const float* reference, int flags, dou
         find_carriers_host(c, cidx, cval, 0.5f * mx, square_size);
         c->disk_rows.ensure(c->disk_rows_host.size() * sizeof(int));
         upload(c->disk_rows.p, c->disk_rows_host.data(), c->disk_rows_host.size() * sizeof(int), s);
+        build_demod_tables(c, s);
         // Carrier.ccsgn = conj(ifft2(fft2(ref) * mask))  (carriers.py:22-24); we keep its angle.
         fft2_real(c, dref, F, 1, 0.f, s);
         c->refsig.ensure(2 * hw * sizeof(float2));
@@ -628,62 +730,84 @@ FCD_API int fcd_process(fcd_ctx* c, const float* frames, int n_frames, int flags
         // h_hat = i/k^2 [(kx f1[0] - ky f1[1]) Phi0 + (ky f0[1] - kx f0[0]) Phi1] / (det * height)
         const fcdk::IntegCoef coef = integ_coef(c, in.frequencies[1][0] * sc, -in.frequencies[1][1] * sc,
                                                 -in.frequencies[0][0] * sc, in.frequencies[0][1] * sc);
-        if (!dev) {
-            c->frames_in.ensure((size_t)c->chunk * hw * sizeof(float));
-            c->out_h.ensure((size_t)c->chunk * hw * sizeof(float));
+        const int nbmax = c->fchunk;
+        c->frames_in.ensure((size_t)nbmax * hw * sizeof(float));
+        c->out_h.ensure((size_t)nbmax * hw * sizeof(float));
+        const hipMemcpyKind out_kind = dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+        int* res = nullptr;
+        if (unwrap) {  // residue census of every map of the call
+            c->fres.ensure((size_t)n_frames * 2 * sizeof(int) + 16);
+            res = c->fres.as<int>();
+            HIPCHK(hipMemsetAsync(res, 0, (size_t)n_frames * 2 * sizeof(int), s));
         }
-        for (int f0 = 0; f0 < n_frames; f0 += c->chunk) {
-            const int nb = std::min(c->chunk, n_frames - f0);
+        // ---- pass 1: every frame through the band-pruned pipeline with the residue-free unwrap
+        for (int f0 = 0; f0 < n_frames; f0 += nbmax) {
+            const int nb = std::min(nbmax, n_frames - f0);
             const float* fr = frames + (size_t)f0 * hw;
             if (!dev) {
                 upload(c->frames_in.p, fr, (size_t)nb * hw * sizeof(float), s);
                 fr = c->frames_in.as<float>();
             }
             if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
-            fft2_real(c, fr, c->spec.as<float2>(), nb, 0.f, s);
-            float* w = c->wrapped.as<float>();
-            demod_phases(c, c->spec.as<float2>(), nb, w, s);
+            fast_demod(c, fr, nb, s);
             if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
-            int32_t* k = nullptr;
-            if (unwrap) {
-                k = c->kbuf.as<int32_t>();
-                unwrap_maps(c, w, 2 * nb, k, nullptr, s);
-            }
+            if (unwrap) fcdk::unwrap_colk(c->wrapped.as<float>(), 2 * nb, c->H, c->W, c->colk.as<int>(), s);
             if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
-            fcdk::make_z(w, k, c->spec.as<float2>(), nb, c->H, c->W, s);
-            float* hdst = height_out ? (dev ? height_out + (size_t)f0 * hw : c->out_h.as<float>()) : nullptr;
-            if (hdst) integrate_z(c, nb, coef, hdst, s);
+            float* hdst = (dev && height_out) ? height_out + (size_t)f0 * hw : c->out_h.as<float>();
+            int32_t* kdst = k_out && unwrap ? (dev ? k_out + (size_t)f0 * 2 * hw : c->fk.as<int32_t>()) : nullptr;
+            fcdk::int_rows(c->W, unwrap ? 1 : 0, c->wrapped.as<float>(), c->colk.as<int>(), nullptr, kdst,
+                           res ? res + (size_t)f0 * 2 : nullptr, c->H, nb, c->Zt.as<float2>(),
+                           c->tw_row.as<float2>(), s);
+            fcdk::int_cols(c->H, c->Zt.as<float2>(), c->W, nb, coef, c->Ht.as<float2>(), c->tw_col.as<float2>(), s);
+            fcdk::int_c2r(c->W, c->Ht.as<float2>(), c->H, nb, hdst, c->tw_row.as<float2>(), s);
             if (c->profiling) {
                 HIPCHK(hipEventRecord(c->next_event(), s));
                 c->prof_frames += nb;
             }
-            if (dev) {
-                if (wrapped_out)
-                    HIPCHK(hipMemcpyAsync(wrapped_out + (size_t)f0 * 2 * hw, w, (size_t)nb * 2 * hw * 4,
-                                          hipMemcpyDeviceToDevice, s));
-                if (k_out) {
-                    if (k)
-                        HIPCHK(hipMemcpyAsync(k_out + (size_t)f0 * 2 * hw, k, (size_t)nb * 2 * hw * 4,
-                                              hipMemcpyDeviceToDevice, s));
-                    else
-                        HIPCHK(hipMemsetAsync(k_out + (size_t)f0 * 2 * hw, 0, (size_t)nb * 2 * hw * 4, s));
-                }
-            } else {
-                if (hdst)
-                    HIPCHK(hipMemcpyAsync(height_out + (size_t)f0 * hw, hdst, (size_t)nb * hw * 4,
-                                          hipMemcpyDeviceToHost, s));
-                if (wrapped_out)
-                    HIPCHK(hipMemcpyAsync(wrapped_out + (size_t)f0 * 2 * hw, w, (size_t)nb * 2 * hw * 4,
-                                          hipMemcpyDeviceToHost, s));
-                if (k_out) {
-                    if (k)
-                        HIPCHK(hipMemcpyAsync(k_out + (size_t)f0 * 2 * hw, k, (size_t)nb * 2 * hw * 4,
-                                              hipMemcpyDeviceToHost, s));
-                    else
-                        std::memset(k_out + (size_t)f0 * 2 * hw, 0, (size_t)nb * 2 * hw * 4);
-                }
-                HIPCHK(hipStreamSynchronize(s));
+            if (height_out && !dev)
+                HIPCHK(hipMemcpyAsync(height_out + (size_t)f0 * hw, hdst, (size_t)nb * hw * 4, out_kind, s));
+            if (wrapped_out)
+                HIPCHK(hipMemcpyAsync(wrapped_out + (size_t)f0 * 2 * hw, c->wrapped.p, (size_t)nb * 2 * hw * 4,
+                                      out_kind, s));
+            if (k_out && unwrap && !dev)
+                HIPCHK(hipMemcpyAsync(k_out + (size_t)f0 * 2 * hw, kdst, (size_t)nb * 2 * hw * 4, out_kind, s));
+            if (k_out && !unwrap) {
+                if (dev)
+                    HIPCHK(hipMemsetAsync(k_out + (size_t)f0 * 2 * hw, 0, (size_t)nb * 2 * hw * 4, s));
+                else
+                    std::memset(k_out + (size_t)f0 * 2 * hw, 0, (size_t)nb * 2 * hw * 4);
             }
+            if (!dev) HIPCHK(hipStreamSynchronize(s));
+        }
+        if (!unwrap) return FCD_OK;
+        // ---- pass 2: frames whose maps have residues are redone with the Boruvka (MST) unwrap
+        std::vector<int> counts((size_t)n_frames * 2);
+        HIPCHK(hipMemcpyAsync(counts.data(), res, counts.size() * sizeof(int), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        std::vector<int> redo;
+        for (int f = 0; f < n_frames; ++f)
+            if (counts[2 * (size_t)f] || counts[2 * (size_t)f + 1]) redo.push_back(f);
+        for (size_t g0 = 0; g0 < redo.size(); g0 += nbmax) {
+            const int ng = (int)std::min<size_t>(nbmax, redo.size() - g0);
+            for (int i = 0; i < ng; ++i)
+                HIPCHK(hipMemcpyAsync(c->frames_in.as<float>() + (size_t)i * hw, frames + (size_t)redo[g0 + i] * hw,
+                                      hw * sizeof(float), dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
+            fast_demod(c, c->frames_in.as<float>(), ng, s);
+            int32_t* kf = c->fk.as<int32_t>();
+            unwrap_maps(c, c->wrapped.as<float>(), 2 * ng, kf, nullptr, s);
+            fcdk::int_rows(c->W, 2, c->wrapped.as<float>(), nullptr, kf, nullptr, nullptr, c->H, ng,
+                           c->Zt.as<float2>(), c->tw_row.as<float2>(), s);
+            fcdk::int_cols(c->H, c->Zt.as<float2>(), c->W, ng, coef, c->Ht.as<float2>(), c->tw_col.as<float2>(), s);
+            fcdk::int_c2r(c->W, c->Ht.as<float2>(), c->H, ng, c->out_h.as<float>(), c->tw_row.as<float2>(), s);
+            for (int i = 0; i < ng; ++i) {
+                const size_t f = (size_t)redo[g0 + i];
+                if (height_out)
+                    HIPCHK(hipMemcpyAsync(height_out + f * hw, c->out_h.as<float>() + (size_t)i * hw, hw * 4,
+                                          out_kind, s));
+                if (k_out)
+                    HIPCHK(hipMemcpyAsync(k_out + f * 2 * hw, kf + (size_t)i * 2 * hw, 2 * hw * 4, out_kind, s));
+            }
+            HIPCHK(hipStreamSynchronize(s));
         }
     })
 }

@@ -33,7 +33,35 @@ struct IntegCoef {
     float a0, b0, a1, b1, norm;
 };
 
+// Band-pruned demodulation tables (built once per reference on the host).
+struct DemodTables {
+    const int* hc;         // [NC] half-spectrum columns (0..W/2) the carrier disks need
+    const int4* outs;      // [NC][4] (carrier, cslot, mirror, unshifted column) per output column
+    const int2* outrows;   // [NC][4] shifted-row range [lo, hi] of the disk in that column
+    const int* nouts;      // [NC] outputs per half column (<= 4)
+    const int* colslot;    // [2][W] carrier column slot of each unshifted column, or -1
+    int NC;
+    int NCc[2];
+};
+
 bool fft_size_supported(int n);
+
+// ---- band-pruned per-frame pipeline (kernels_fast.hip) ----
+void demod_rows(int W, const float* frames, int H, int nb, const DemodTables& T, float2* Xb, const float2* tw,
+                hipStream_t s);
+void demod_cols(int H, const float2* Xb, int nb, const DemodTables& T, float2* Ab, int NCA, const float2* tw,
+                hipStream_t s);
+void demod_phase(int W, const float2* Ab, int H, int nb, int NCA, const DemodTables& T, const float* theta,
+                 float* wrapped, const float2* tw, hipStream_t s);
+void int_rows(int W, int kmode, const float* w, const int* colk, const int32_t* kin, int32_t* kout, int* rescount,
+              int H, int nb, float2* Zt, const float2* tw, hipStream_t s);
+struct IntegCoef;
+void int_cols(int H, const float2* Zt, int W, int nb, const IntegCoef& c, float2* Ht, const float2* tw,
+              hipStream_t s);
+void int_c2r(int W, const float2* Ht, int H, int nb, float* h, const float2* tw, hipStream_t s);
+int c2r_rows_per_block(int W);
+// column-0 prefix of the residue-free unwrap (kernels_unwrap.hip)
+void unwrap_colk(const float* w, int nmaps, int H, int W, int* colk, hipStream_t s);
 
 // In-place or out-of-place batched row FFT over nrows rows of length W.
 void row_fft(int W, bool inverse, RowIn in_mode, RowOut out_mode, const void* in, void* out, long nrows,

@@ -1,0 +1,640 @@
+// Batched, band-pruned per-frame pipeline (the throughput path of fcd_process).
+//
+//   K1 demod_rows   frame rows -> packed-pair R2C row FFT -> only the spectrum
+//                   columns the two carrier disks touch (fcd.py:28)
+//   K2 demod_cols   per such column: column FFT, disk band-pass (carriers.py:17-20),
+//                   inverse column FFT (fcd.py:118, first half of ifft2)
+//   K3 demod_phase  per row and carrier: inverse row FFT of the band, phase
+//                   -angle(A * ccsgn) = wrap(theta_ref - atan2(A)) (fcd.py:118)
+//   I1 int_rows     residue census + residue-free unwrap (column-0 scan + row
+//                   scan, fcd.py:119) + phi0 + i*phi1 + forward row FFT
+//   I2 int_cols     per column pair (c, -c): forward column FFTs, Phi0/Phi1
+//                   split, displacement solve + integration multiplier
+//                   (fcd.py:122-138, fourier.py:115-137), inverse column FFT
+//   I3 int_c2r      packed-pair C2R row FFT -> height (fcd.py:33)
+//
+// Row <-> column hand-offs use a 16-row tiled layout [row/16][col][row%16]:
+// a column kernel reads/writes whole 128-byte lines (16 rows of one column),
+// a row-block workgroup covers whole tiles.  All FFT data stays in registers
+// (regfft.hpp); LDS carries only pass exchanges and small staging blocks.
+#include <hip/hip_runtime.h>
+
+#include <stdexcept>
+#include <string>
+
+#include "kernels.hpp"
+#include "regfft.hpp"
+
+namespace fcdk {
+
+#define FCD_CHECK_LAUNCH()                                                          \
+    do {                                                                            \
+        hipError_t e_ = hipGetLastError();                                          \
+        if (e_ != hipSuccess) throw std::runtime_error(std::string("kernel launch: ") + hipGetErrorString(e_)); \
+    } while (0)
+#define FCD_HIPCHK(x)                                                               \
+    do {                                                                            \
+        hipError_t e_ = (x);                                                        \
+        if (e_ != hipSuccess) throw std::runtime_error(std::string(#x ": ") + hipGetErrorString(e_)); \
+    } while (0)
+
+constexpr int TILE = 16;
+constexpr int BLOCK = 256;
+constexpr float kPiF = 3.14159265358979f;
+constexpr float kTwoPiF = 6.28318530717959f;
+
+__device__ __forceinline__ long tix(int row, int col, int ncols) {
+    return ((long)(row >> 4) * ncols + col) * TILE + (row & 15);
+}
+
+template <int N>
+struct KCfg {
+    static constexpr int TT = Sched<N>::TT;
+    static constexpr int E = Sched<N>::E;
+    static constexpr int TEAMS = TT >= BLOCK ? 1 : BLOCK / TT;
+    static constexpr int THREADS = TEAMS * TT;
+    static constexpr int ROW = padded_len(N);  // float2 per team row
+};
+
+// find_wrap(a, b) of the reference unwrapper with an f32 fast path:
+// fl(a - b) > fl(pi) only if a - b > M_PI; equality needs the exact f64 test.
+__device__ __forceinline__ int fw_fast(float a, float b) {
+    const float d = a - b;
+    constexpr float P = 3.14159274f;  // nearest float to M_PI (above it)
+    if (d > P) return -1;
+    if (d < -P) return 1;
+    if (d == P || d == -P) {
+        const double e = (double)a - (double)b;
+        return e > 3.141592653589793 ? -1 : (e < -3.141592653589793 ? 1 : 0);
+    }
+    return 0;
+}
+
+// ------------------------------------------------------------------ K1
+template <int W>
+__global__ __launch_bounds__(BLOCK) void k_demod_rows(const float* __restrict__ frames, int H, int nb,
+                                                      DemodTables T, float2* __restrict__ Xb,
+                                                      const float2* __restrict__ tw) {
+    using C = KCfg<W>;
+    constexpr int TT = C::TT, E = C::E, TEAMS = C::TEAMS;
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    const int team = threadIdx.x / TT, t = threadIdx.x % TT;
+    float2* s = lds + team * C::ROW;
+    float2* stage = lds + TEAMS * C::ROW;  // [NC][TILE + 1]
+    RegFFT<W> fft;
+    fft.init(tw, t);
+    const int NC = T.NC;
+    const int rbs = H / TILE;
+    for (int blk = blockIdx.x; blk < nb * rbs; blk += gridDim.x) {
+        const int f = blk / rbs, rb = blk % rbs;
+        for (int pr = team; pr < TILE / 2; pr += TEAMS) {
+            const int r = rb * TILE + 2 * pr;
+            const float* ra = frames + ((long)f * H + r) * W;
+            float2 x[E];
+#pragma unroll
+            for (int q = 0; q < E; ++q) x[q] = make_float2(ra[t + TT * q], ra[W + t + TT * q]);
+            fft.template run<false>(x, s, t);
+            if constexpr (!Sched<W>::WAVE_LOCAL) __syncthreads();
+#pragma unroll
+            for (int q = 0; q < E; ++q) s[pad(t + TT * q)] = x[q];
+            team_sync<W>();
+            for (int i = t; i < NC; i += TT) {
+                const int hc = T.hc[i];
+                const float2 zk = s[pad(hc)], zm = s[pad((W - hc) & (W - 1))];
+                // X_a = (Z(k) + conj Z(-k)) / 2 ; X_b = (Z(k) - conj Z(-k)) / 2i
+                stage[i * (TILE + 1) + 2 * pr] = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y));
+                stage[i * (TILE + 1) + 2 * pr + 1] = make_float2(0.5f * (zk.y + zm.y), -0.5f * (zk.x - zm.x));
+            }
+        }
+        __syncthreads();
+        float2* dst = Xb + (long)f * H * NC + (long)rb * NC * TILE;
+        for (int idx = threadIdx.x; idx < NC * TILE; idx += C::THREADS)
+            dst[idx] = stage[(idx / TILE) * (TILE + 1) + (idx % TILE)];
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------ K2
+template <int H>
+__global__ __launch_bounds__(BLOCK) void k_demod_cols(const float2* __restrict__ Xb, int nb, DemodTables T,
+                                                      float2* __restrict__ Ab, int NCA,
+                                                      const float2* __restrict__ tw) {
+    using C = KCfg<H>;
+    constexpr int TT = C::TT, E = C::E, TEAMS = C::TEAMS;
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    const int team = threadIdx.x / TT, t = threadIdx.x % TT;
+    float2* s = lds + team * C::ROW;            // holds the forward column spectrum
+    float2* s2 = lds + (TEAMS + team) * C::ROW;  // exchanges of the inverse FFTs
+    RegFFT<H> fft;
+    fft.init(tw, t);
+    const int NC = T.NC;
+    const int items = nb * NC;
+    for (int base = blockIdx.x * TEAMS; base < items; base += gridDim.x * TEAMS) {
+        const int item = base + team;
+        const bool valid = item < items;
+        const int f = valid ? item / NC : 0, i = valid ? item % NC : 0;
+        float2 x[E];
+        const float2* src = Xb + (long)f * H * NC;
+#pragma unroll
+        for (int q = 0; q < E; ++q) x[q] = src[tix(t + TT * q, i, NC)];
+        fft.template run<false>(x, s, t);
+        if constexpr (!Sched<H>::WAVE_LOCAL) __syncthreads();
+#pragma unroll
+        for (int q = 0; q < E; ++q) s[pad(t + TT * q)] = x[q];
+        team_sync<H>();
+        const int nout = valid ? T.nouts[i] : 0;
+        // teams spanning waves share the workgroup barrier: keep their loop counts equal
+        const int nmax = (Sched<H>::WAVE_LOCAL || TEAMS == 1) ? nout : 4;
+        for (int e = 0; e < nmax; ++e) {
+            const bool live = e < nout;
+            const int4 o = live ? T.outs[i * 4 + e] : make_int4(0, 0, 0, 0);  // carrier, cslot, mirror, uc
+            const int2 rr = live ? T.outrows[i * 4 + e] : make_int2(1, 0);   // shifted rows [lo, hi]
+            float2 y[E];
+#pragma unroll
+            for (int q = 0; q < E; ++q) {
+                const int u = t + TT * q;
+                const int sr = (u + H / 2) & (H - 1);
+                float2 v = make_float2(0.f, 0.f);
+                if (sr >= rr.x && sr <= rr.y) {
+                    if (o.z) {
+                        v = s[pad((H - u) & (H - 1))];
+                        v.y = -v.y;
+                    } else {
+                        v = s[pad(u)];
+                    }
+                }
+                y[q] = v;
+            }
+            fft.template run<true>(y, s2, t);
+            if (live) {
+                float2* dst = Ab + ((long)f * 2 + o.x) * H * NCA;
+#pragma unroll
+                for (int q = 0; q < E; ++q) dst[tix(t + TT * q, o.y, NCA)] = y[q];
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------ K3
+template <int W>
+__global__ __launch_bounds__(BLOCK) void k_demod_phase(const float2* __restrict__ Ab, int H, int nb, int NCA,
+                                                       DemodTables T, const float* __restrict__ theta,
+                                                       float* __restrict__ wrapped, const float2* __restrict__ tw) {
+    using C = KCfg<W>;
+    constexpr int TT = C::TT, E = C::E, TEAMS = C::TEAMS;
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    const int team = threadIdx.x / TT, t = threadIdx.x % TT;
+    float2* s = lds + team * C::ROW;
+    float2* stage = lds + TEAMS * C::ROW;  // [NCc][TILE + 1]
+    RegFFT<W> fft;
+    fft.init(tw, t);
+    const int rbs = H / TILE;
+    const int items = nb * 2 * rbs;
+    for (int blk = blockIdx.x; blk < items; blk += gridDim.x) {
+        const int f = blk / (2 * rbs), c = (blk / rbs) % 2, rb = blk % rbs;
+        const int ncc = T.NCc[c];
+        const float2* src = Ab + ((long)f * 2 + c) * H * NCA + (long)rb * NCA * TILE;
+        for (int idx = threadIdx.x; idx < ncc * TILE; idx += C::THREADS)
+            stage[(idx / TILE) * (TILE + 1) + (idx % TILE)] = src[idx];
+        int cs[E];
+#pragma unroll
+        for (int q = 0; q < E; ++q) cs[q] = T.colslot[c * W + t + TT * q];
+        __syncthreads();
+        for (int rl = team; rl < TILE; rl += TEAMS) {
+            const int r = rb * TILE + rl;
+            float2 x[E];
+#pragma unroll
+            for (int q = 0; q < E; ++q)
+                x[q] = cs[q] >= 0 ? stage[cs[q] * (TILE + 1) + rl] : make_float2(0.f, 0.f);
+            fft.template run<true>(x, s, t);
+            const float* th = theta + ((long)c * H + r) * W;
+            float* wo = wrapped + (((long)f * 2 + c) * H + r) * W;
+#pragma unroll
+            for (int q = 0; q < E; ++q) {
+                const int i = t + TT * q;
+                float d = th[i] - atan2f(x[q].y, x[q].x);
+                if (d > kPiF) d -= kTwoPiF;
+                else if (d < -kPiF) d += kTwoPiF;
+                wo[i] = d;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------ team scan
+// Exclusive add-scan of v across the team; returns (exclusive, total).
+template <int TT>
+__device__ __forceinline__ int2 team_scan_excl(int v, int t, int* scratch) {
+    if constexpr (TT <= 64) {
+        const int incl = team_scan_incl_dpp<TT>(v);
+        const int total = __shfl(incl, TT - 1, TT);
+        return make_int2(incl - v, total);
+    } else {
+        constexpr int NW = TT / 64;
+        const int incl = team_scan_incl_dpp<64>(v);
+        const int wv = t >> 6;
+        if ((t & 63) == 63) scratch[wv] = incl;
+        __syncthreads();
+        int before = 0, total = 0;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) {
+            const int tk = scratch[k];
+            before += k < wv ? tk : 0;
+            total += tk;
+        }
+        __syncthreads();
+        return make_int2(before + incl - v, total);
+    }
+}
+
+// ------------------------------------------------------------------ I1
+// KMODE 0: phases = wrapped (unwrap=False); 1: residue-free scan unwrap + residue
+// census; 2: k-field from kin (Boruvka path for maps with residues).
+template <int W, int KMODE>
+__global__ __launch_bounds__(BLOCK) void k_int_rows(const float* __restrict__ wrapped, const int* __restrict__ colk,
+                                                    const int32_t* __restrict__ kin, int32_t* __restrict__ kout,
+                                                    int* __restrict__ rescount, int H, int nb,
+                                                    float2* __restrict__ Zt, const float2* __restrict__ tw) {
+    using C = KCfg<W>;
+    constexpr int TT = C::TT, E = C::E, TEAMS = C::TEAMS;
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    const int team = threadIdx.x / TT, t = threadIdx.x % TT;
+    float2* s = lds + team * C::ROW;
+    int* scratch = reinterpret_cast<int*>(lds + TEAMS * C::ROW) + team * 8;
+    RegFFT<W> fft;
+    fft.init(tw, t);
+    const int rbs = H / TILE;
+    const int j0 = t * E;  // this thread's blocked segment [j0, j0 + E)
+    for (int blk = blockIdx.x; blk < nb * rbs; blk += gridDim.x) {
+        const int f = blk / rbs, rb = blk % rbs;
+        int res[2] = {0, 0};
+        for (int rl = team; rl < TILE; rl += TEAMS) {
+            const int r = rb * TILE + rl;
+            float ph[2][E];
+#pragma unroll
+            for (int m = 0; m < 2; ++m) {
+                const float* wr = wrapped + (((long)f * 2 + m) * H + r) * W + j0;
+#pragma unroll
+                for (int j = 0; j < E; j += 4) {
+                    const float4 v = *reinterpret_cast<const float4*>(wr + j);
+                    ph[m][j] = v.x; ph[m][j + 1] = v.y; ph[m][j + 2] = v.z; ph[m][j + 3] = v.w;
+                }
+            }
+            if constexpr (KMODE == 1) {
+                float nxt[2];
+                int packed[E];
+#pragma unroll
+                for (int m = 0; m < 2; ++m) {
+                    const float* wr = wrapped + (((long)f * 2 + m) * H + r) * W;
+                    nxt[m] = (j0 + E < W) ? wr[j0 + E] : 0.f;
+                }
+                // d(j) = -find_wrap(w(j), w(j+1)), biased +1 and packed (map0 low, map1 high)
+                int run = 0;
+#pragma unroll
+                for (int j = 0; j < E; ++j) {
+                    int dd[2];
+#pragma unroll
+                    for (int m = 0; m < 2; ++m) {
+                        const float b = j + 1 < E ? ph[m][j + 1] : nxt[m];
+                        dd[m] = (j0 + j + 1 < W) ? -fw_fast(ph[m][j], b) : 0;
+                    }
+                    packed[j] = run;  // exclusive within the segment
+                    run += (dd[0] + 1) | ((dd[1] + 1) << 16);
+                }
+                const int2 sc = team_scan_excl<TT>(run, t, scratch);
+                int kk[2][E];
+#pragma unroll
+                for (int j = 0; j < E; ++j) {
+                    const int p = sc.x + packed[j];
+                    const int cnt = j0 + j;  // biased items before element j0 + j
+                    kk[0][j] = (p & 0xffff) - cnt;
+                    kk[1][j] = (p >> 16) - cnt;
+                }
+#pragma unroll
+                for (int m = 0; m < 2; ++m) {
+                    const int base = colk[((long)f * 2 + m) * H + r];
+#pragma unroll
+                    for (int j = 0; j < E; ++j) kk[m][j] += base;
+                }
+                // residue census on the plaquettes (r, j)..(r+1, j+1)
+                if (r + 1 < H) {
+#pragma unroll
+                    for (int m = 0; m < 2; ++m) {
+                        const float* w0 = wrapped + (((long)f * 2 + m) * H + r) * W;
+                        const float* w1 = w0 + W;
+                        float lo[E + 1];
+#pragma unroll
+                        for (int j = 0; j < E; j += 4) {
+                            const float4 v = *reinterpret_cast<const float4*>(w1 + j0 + j);
+                            lo[j] = v.x; lo[j + 1] = v.y; lo[j + 2] = v.z; lo[j + 3] = v.w;
+                        }
+                        lo[E] = (j0 + E < W) ? w1[j0 + E] : 0.f;
+                        int cnt = 0;
+#pragma unroll
+                        for (int j = 0; j < E; ++j) {
+                            if (j0 + j + 1 < W) {
+                                const float a = ph[m][j], b = j + 1 < E ? ph[m][j + 1] : nxt[m];
+                                const float cc = lo[j + 1], d = lo[j];
+                                cnt += (fw_fast(a, b) + fw_fast(b, cc) + fw_fast(cc, d) + fw_fast(d, a)) != 0;
+                            }
+                        }
+                        res[m] += cnt;
+                    }
+                }
+                if (kout) {
+#pragma unroll
+                    for (int m = 0; m < 2; ++m) {
+                        int32_t* ko = kout + (((long)f * 2 + m) * H + r) * W + j0;
+#pragma unroll
+                        for (int j = 0; j < E; j += 4)
+                            *reinterpret_cast<int4*>(ko + j) = make_int4(kk[m][j], kk[m][j + 1], kk[m][j + 2], kk[m][j + 3]);
+                    }
+                }
+#pragma unroll
+                for (int m = 0; m < 2; ++m)
+#pragma unroll
+                    for (int j = 0; j < E; ++j) ph[m][j] = fmaf((float)kk[m][j], kTwoPiF, ph[m][j]);
+            } else if constexpr (KMODE == 2) {
+#pragma unroll
+                for (int m = 0; m < 2; ++m) {
+                    const int32_t* ki = kin + (((long)f * 2 + m) * H + r) * W + j0;
+#pragma unroll
+                    for (int j = 0; j < E; ++j) ph[m][j] = (float)((double)ph[m][j] + 6.283185307179586 * (double)ki[j]);
+                }
+            }
+            // blocked (phi0, phi1) -> LDS -> natural layout -> forward row FFT
+            if constexpr (!Sched<W>::WAVE_LOCAL) __syncthreads();
+#pragma unroll
+            for (int j = 0; j < E; ++j) s[pad(j0 + j)] = make_float2(ph[0][j], ph[1][j]);
+            team_sync<W>();
+            float2 x[E];
+#pragma unroll
+            for (int q = 0; q < E; ++q) x[q] = s[pad(t + TT * q)];
+            fft.template run<false>(x, s, t);
+            float2* dst = Zt + (long)f * H * W;
+#pragma unroll
+            for (int q = 0; q < E; ++q) dst[tix(r, t + TT * q, W)] = x[q];
+        }
+        if constexpr (KMODE == 1) {
+#pragma unroll
+            for (int m = 0; m < 2; ++m) {
+                int v = res[m];
+                for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+                if ((threadIdx.x & 63) == 0 && v) atomicAdd(rescount + f * 2 + m, v);
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------ I2
+template <int H>
+__global__ __launch_bounds__(BLOCK) void k_int_cols(const float2* __restrict__ Zt, int W, int nb, IntegCoef c,
+                                                    float2* __restrict__ Ht, const float2* __restrict__ tw) {
+    using C = KCfg<H>;
+    constexpr int TT = C::TT, E = C::E, TEAMS = C::TEAMS;
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    const int team = threadIdx.x / TT, t = threadIdx.x % TT;
+    float2* s = lds + team * C::ROW;
+    RegFFT<H> fft;
+    fft.init(tw, t);
+    const int NCH = W / 2 + 1;
+    const int items = nb * NCH;
+    for (int base = blockIdx.x * TEAMS; base < items; base += gridDim.x * TEAMS) {
+        const int item = base + team;
+        const bool valid = item < items;
+        const int f = valid ? item / NCH : 0, col = valid ? item % NCH : 0;
+        const int colm = (W - col) & (W - 1);
+        const float2* src = Zt + (long)f * H * W;
+        float2 x[E], y[E];
+#pragma unroll
+        for (int q = 0; q < E; ++q) {
+            x[q] = src[tix(t + TT * q, col, W)];
+            y[q] = src[tix(t + TT * q, colm, W)];
+        }
+        fft.template run<false>(x, s, t);
+        fft.template run<false>(y, s, t);
+        if constexpr (!Sched<H>::WAVE_LOCAL) __syncthreads();
+#pragma unroll
+        for (int q = 0; q < E; ++q) s[pad(t + TT * q)] = y[q];
+        team_sync<H>();
+        const float kx = c.kxe[col], kx2 = c.kx2[col];
+#pragma unroll
+        for (int q = 0; q < E; ++q) {
+            const int i = t + TT * q;
+            const float2 z = x[q];
+            const float2 zm = s[pad((H - i) & (H - 1))];
+            const float2 f0 = make_float2(0.5f * (z.x + zm.x), 0.5f * (z.y - zm.y));
+            const float2 f1 = make_float2(0.5f * (z.y + zm.y), -0.5f * (z.x - zm.x));
+            const float ky = c.kye[i];
+            float k2 = kx2 + c.ky2[i];
+            if (i == 0 && col == 0) k2 = 1.f;
+            const float sc = c.norm / k2;
+            const float m0 = (kx * c.a0 + ky * c.b0) * sc;
+            const float m1 = (kx * c.a1 + ky * c.b1) * sc;
+            const float re = m0 * f0.x + m1 * f1.x;
+            const float im = m0 * f0.y + m1 * f1.y;
+            x[q] = make_float2(-im, re);
+        }
+        fft.template run<true>(x, s, t);
+        if (valid) {
+            float2* dst = Ht + (long)f * H * NCH;
+#pragma unroll
+            for (int q = 0; q < E; ++q) dst[tix(t + TT * q, col, NCH)] = x[q];
+        }
+    }
+}
+
+// ------------------------------------------------------------------ I3
+template <int W>
+__global__ __launch_bounds__(BLOCK) void k_int_c2r(const float2* __restrict__ Ht, int H, int nb, int rpw,
+                                                   float* __restrict__ hout, const float2* __restrict__ tw) {
+    using C = KCfg<W>;
+    constexpr int TT = C::TT, E = C::E, TEAMS = C::TEAMS;
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    const int team = threadIdx.x / TT, t = threadIdx.x % TT;
+    float2* s = lds + team * C::ROW;
+    float2* stage = lds + TEAMS * C::ROW;  // [NCH][rpw + 1]
+    RegFFT<W> fft;
+    fft.init(tw, t);
+    const int NCH = W / 2 + 1;
+    const int nblk = H / rpw;
+    for (int blk = blockIdx.x; blk < nb * nblk; blk += gridDim.x) {
+        const int f = blk / nblk, r0 = (blk % nblk) * rpw;
+        const float2* src = Ht + (long)f * H * NCH;
+        for (int idx = threadIdx.x; idx < NCH * rpw; idx += C::THREADS) {
+            const int col = idx / rpw, rl = idx % rpw;
+            stage[col * (rpw + 1) + rl] = src[tix(r0 + rl, col, NCH)];
+        }
+        __syncthreads();
+        for (int pr = team; pr < rpw / 2; pr += TEAMS) {
+            float2 x[E];
+#pragma unroll
+            for (int q = 0; q < E; ++q) {
+                const int col = t + TT * q;
+                float2 g1, g2;
+                if (col <= W / 2) {
+                    g1 = stage[col * (rpw + 1) + 2 * pr];
+                    g2 = stage[col * (rpw + 1) + 2 * pr + 1];
+                } else {  // row-wise Hermitian: G(y, W - c) = conj G(y, c)
+                    g1 = stage[(W - col) * (rpw + 1) + 2 * pr];
+                    g2 = stage[(W - col) * (rpw + 1) + 2 * pr + 1];
+                    g1.y = -g1.y;
+                    g2.y = -g2.y;
+                }
+                x[q] = make_float2(g1.x - g2.y, g1.y + g2.x);
+            }
+            fft.template run<true>(x, s, t);
+            float* h1 = hout + ((long)f * H + r0 + 2 * pr) * W;
+#pragma unroll
+            for (int q = 0; q < E; ++q) {
+                h1[t + TT * q] = x[q].x;
+                h1[W + t + TT * q] = x[q].y;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------ launchers
+static int g_num_cu = 0;
+static int grid_for(long work_items, int per_cu) {
+    if (!g_num_cu) {
+        int dev = 0;
+        hipDeviceProp_t p;
+        if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&p, dev) == hipSuccess)
+            g_num_cu = p.multiProcessorCount;
+        if (!g_num_cu) g_num_cu = 256;
+    }
+    const long cap = (long)g_num_cu * per_cu;
+    return (int)(work_items < cap ? (work_items > 0 ? work_items : 1) : cap);
+}
+
+template <class K>
+static void set_lds(K kernel, size_t bytes) {
+    if (bytes > 64 * 1024)
+        FCD_HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+}
+
+#define FCD_SIZE_SWITCH(n, FN, ...)                                   \
+    switch (n) {                                                      \
+        case 64: FN<64>(__VA_ARGS__); break;                          \
+        case 128: FN<128>(__VA_ARGS__); break;                        \
+        case 256: FN<256>(__VA_ARGS__); break;                        \
+        case 512: FN<512>(__VA_ARGS__); break;                        \
+        case 1024: FN<1024>(__VA_ARGS__); break;                      \
+        case 2048: FN<2048>(__VA_ARGS__); break;                      \
+        case 4096: FN<4096>(__VA_ARGS__); break;                      \
+        default: throw std::runtime_error("unsupported FFT length " + std::to_string(n)); \
+    }
+
+template <int W>
+static void launch_demod_rows(const float* frames, int H, int nb, const DemodTables& T, float2* Xb, const float2* tw,
+                              hipStream_t s) {
+    using C = KCfg<W>;
+    const size_t lds = (size_t)C::TEAMS * C::ROW * 8 + (size_t)T.NC * (TILE + 1) * 8;
+    set_lds(k_demod_rows<W>, lds);
+    const int grid = grid_for((long)nb * (H / TILE), 4);
+    hipLaunchKernelGGL(k_demod_rows<W>, dim3(grid), dim3(C::THREADS), lds, s, frames, H, nb, T, Xb, tw);
+    FCD_CHECK_LAUNCH();
+}
+
+template <int H>
+static void launch_demod_cols(const float2* Xb, int nb, const DemodTables& T, float2* Ab, int NCA, const float2* tw,
+                              hipStream_t s) {
+    using C = KCfg<H>;
+    const size_t lds = (size_t)2 * C::TEAMS * C::ROW * 8;
+    set_lds(k_demod_cols<H>, lds);
+    const int grid = grid_for(((long)nb * T.NC + C::TEAMS - 1) / C::TEAMS, 4);
+    hipLaunchKernelGGL(k_demod_cols<H>, dim3(grid), dim3(C::THREADS), lds, s, Xb, nb, T, Ab, NCA, tw);
+    FCD_CHECK_LAUNCH();
+}
+
+template <int W>
+static void launch_demod_phase(const float2* Ab, int H, int nb, int NCA, const DemodTables& T, const float* theta,
+                               float* wrapped, const float2* tw, hipStream_t s) {
+    using C = KCfg<W>;
+    const size_t lds = (size_t)C::TEAMS * C::ROW * 8 + (size_t)NCA * (TILE + 1) * 8;
+    set_lds(k_demod_phase<W>, lds);
+    const int grid = grid_for((long)nb * 2 * (H / TILE), 4);
+    hipLaunchKernelGGL(k_demod_phase<W>, dim3(grid), dim3(C::THREADS), lds, s, Ab, H, nb, NCA, T, theta, wrapped, tw);
+    FCD_CHECK_LAUNCH();
+}
+
+template <int W>
+static void launch_int_rows(int kmode, const float* w, const int* colk, const int32_t* kin, int32_t* kout,
+                            int* rescount, int H, int nb, float2* Zt, const float2* tw, hipStream_t s) {
+    using C = KCfg<W>;
+    const size_t lds = (size_t)C::TEAMS * C::ROW * 8 + (size_t)C::TEAMS * 8 * 4;
+    const int grid = grid_for((long)nb * (H / TILE), 4);
+    if (kmode == 0) {
+        set_lds(k_int_rows<W, 0>, lds);
+        hipLaunchKernelGGL((k_int_rows<W, 0>), dim3(grid), dim3(C::THREADS), lds, s, w, colk, kin, kout, rescount, H,
+                           nb, Zt, tw);
+    } else if (kmode == 1) {
+        set_lds(k_int_rows<W, 1>, lds);
+        hipLaunchKernelGGL((k_int_rows<W, 1>), dim3(grid), dim3(C::THREADS), lds, s, w, colk, kin, kout, rescount, H,
+                           nb, Zt, tw);
+    } else {
+        set_lds(k_int_rows<W, 2>, lds);
+        hipLaunchKernelGGL((k_int_rows<W, 2>), dim3(grid), dim3(C::THREADS), lds, s, w, colk, kin, kout, rescount, H,
+                           nb, Zt, tw);
+    }
+    FCD_CHECK_LAUNCH();
+}
+
+template <int H>
+static void launch_int_cols(const float2* Zt, int W, int nb, const IntegCoef& c, float2* Ht, const float2* tw,
+                            hipStream_t s) {
+    using C = KCfg<H>;
+    const size_t lds = (size_t)C::TEAMS * C::ROW * 8;
+    set_lds(k_int_cols<H>, lds);
+    const int grid = grid_for(((long)nb * (W / 2 + 1) + C::TEAMS - 1) / C::TEAMS, 4);
+    hipLaunchKernelGGL(k_int_cols<H>, dim3(grid), dim3(C::THREADS), lds, s, Zt, W, nb, c, Ht, tw);
+    FCD_CHECK_LAUNCH();
+}
+
+int c2r_rows_per_block(int W) {
+    const long per_row = (long)(W / 2 + 1) * 8;
+    int rpw = 16;
+    while (rpw > 2 && per_row * (rpw + 1) > 72 * 1024) rpw /= 2;
+    return rpw;
+}
+
+template <int W>
+static void launch_int_c2r(const float2* Ht, int H, int nb, float* h, const float2* tw, hipStream_t s) {
+    using C = KCfg<W>;
+    const int rpw = c2r_rows_per_block(W);
+    const size_t lds = (size_t)C::TEAMS * C::ROW * 8 + (size_t)(W / 2 + 1) * (rpw + 1) * 8;
+    set_lds(k_int_c2r<W>, lds);
+    const int grid = grid_for((long)nb * (H / rpw), 4);
+    hipLaunchKernelGGL(k_int_c2r<W>, dim3(grid), dim3(C::THREADS), lds, s, Ht, H, nb, rpw, h, tw);
+    FCD_CHECK_LAUNCH();
+}
+
+void demod_rows(int W, const float* frames, int H, int nb, const DemodTables& T, float2* Xb, const float2* tw,
+                hipStream_t s) {
+    FCD_SIZE_SWITCH(W, launch_demod_rows, frames, H, nb, T, Xb, tw, s);
+}
+void demod_cols(int H, const float2* Xb, int nb, const DemodTables& T, float2* Ab, int NCA, const float2* tw,
+                hipStream_t s) {
+    FCD_SIZE_SWITCH(H, launch_demod_cols, Xb, nb, T, Ab, NCA, tw, s);
+}
+void demod_phase(int W, const float2* Ab, int H, int nb, int NCA, const DemodTables& T, const float* theta,
+                 float* wrapped, const float2* tw, hipStream_t s) {
+    FCD_SIZE_SWITCH(W, launch_demod_phase, Ab, H, nb, NCA, T, theta, wrapped, tw, s);
+}
+void int_rows(int W, int kmode, const float* w, const int* colk, const int32_t* kin, int32_t* kout, int* rescount,
+              int H, int nb, float2* Zt, const float2* tw, hipStream_t s) {
+    FCD_SIZE_SWITCH(W, launch_int_rows, kmode, w, colk, kin, kout, rescount, H, nb, Zt, tw, s);
+}
+void int_cols(int H, const float2* Zt, int W, int nb, const IntegCoef& c, float2* Ht, const float2* tw,
+              hipStream_t s) {
+    FCD_SIZE_SWITCH(H, launch_int_cols, Zt, W, nb, c, Ht, tw, s);
+}
+void int_c2r(int W, const float2* Ht, int H, int nb, float* h, const float2* tw, hipStream_t s) {
+    FCD_SIZE_SWITCH(W, launch_int_c2r, Ht, H, nb, h, tw, s);
+}
+
+}  // namespace fcdk

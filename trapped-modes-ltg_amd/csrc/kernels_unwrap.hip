@@ -147,6 +147,11 @@ __global__ __launch_bounds__(256) void k_rowscan(const float* __restrict__ w, lo
     }
 }
 
+void unwrap_colk(const float* w, int nmaps, int H, int W, int* colk, hipStream_t s) {
+    hipLaunchKernelGGL(k_colk, dim3(nmaps), dim3(256), 0, s, w, H, W, colk);
+    FCD_CHECK_LAUNCH();
+}
+
 void unwrap_scan(const float* w, int nmaps, int H, int W, int* colk, int32_t* k, hipStream_t s) {
     if (H > 4096) throw std::runtime_error("unwrap_scan: H too large");
     hipLaunchKernelGGL(k_colk, dim3(nmaps), dim3(256), 0, s, w, H, W, colk);
