@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "../../include/fcd.h"
+#include "fft_lds.hpp"
 #include "kernels.hpp"
 
 namespace {
@@ -86,6 +87,28 @@ std::vector<float2> twiddles(int n) {
     return t;
 }
 
+// Pass-major twiddles of the register FFT (regfft.hpp): the schedule of
+// fcdk::Sched<n> (radix E = fft_elems(n) passes, a smaller last one), and for
+// each pass p >= 1, k < L_p, r = 1..R_p-1: exp(-2 pi i r k / (L_p R_p)).
+std::vector<float2> pass_twiddles(int n) {
+    const int E = fcdk::fft_elems(n);
+    std::vector<float2> t;
+    int L = 1, p = 0;
+    while (L < n) {
+        const int R = std::min(E, n / L);
+        if (p > 0)
+            for (int k = 0; k < L; ++k)
+                for (int r = 1; r < R; ++r) {
+                    const double a = -2.0 * kPi * (double)r * (double)k / ((double)L * (double)R);
+                    t.push_back(make_float2((float)std::cos(a), (float)std::sin(a)));
+                }
+        L *= R;
+        ++p;
+    }
+    t.resize(std::max<size_t>(t.size(), (size_t)n), make_float2(0.f, 0.f));  // kernels copy n entries
+    return t;
+}
+
 struct Blob {
     int first;     // raster index of its first pixel (skimage label order)
     int peak;      // raster index of its max pixel (first in row-major on ties)
@@ -97,7 +120,8 @@ struct Blob {
 struct fcd_ctx {
     int device = 0, H = 0, W = 0;
     hipStream_t own = nullptr;
-    DevBuf tw_row, tw_col;
+    DevBuf tw_row, tw_col;        // plain tables exp(-2 pi i m / n) (generic LDS FFT kernels)
+    DevBuf twp_row, twp_col;      // pass-major tables (register FFT kernels)
 
     // reference state
     bool has_ref = false;
@@ -535,10 +559,10 @@ fcdk::DemodTables demod_tables(fcd_ctx* c) {
 // Fast path for nb frames (device pointer): band-pruned demod -> wrapped (c->wrapped).
 void fast_demod(fcd_ctx* c, const float* frames, int nb, hipStream_t s) {
     const fcdk::DemodTables T = demod_tables(c);
-    fcdk::demod_rows(c->W, frames, c->H, nb, T, c->Xb.as<float2>(), c->tw_row.as<float2>(), s);
-    fcdk::demod_cols(c->H, c->Xb.as<float2>(), nb, T, c->Ab.as<float2>(), c->NCA, c->tw_col.as<float2>(), s);
+    fcdk::demod_rows(c->W, frames, c->H, nb, T, c->Xb.as<float2>(), c->twp_row.as<float2>(), s);
+    fcdk::demod_cols(c->H, c->Xb.as<float2>(), nb, T, c->Ab.as<float2>(), c->NCA, c->twp_col.as<float2>(), s);
     fcdk::demod_phase(c->W, c->Ab.as<float2>(), c->H, nb, c->NCA, T, c->theta.as<float>(), c->wrapped.as<float>(),
-                      c->tw_row.as<float2>(), s);
+                      c->twp_row.as<float2>(), s);
 }
 
 }  // namespace
@@ -586,6 +610,11 @@ FCD_API int fcd_create(int device, int rows, int cols, fcd_ctx** out) {
         c->tw_col.ensure(tc.size() * sizeof(float2));
         HIPCHK(hipMemcpy(c->tw_row.p, tr.data(), tr.size() * sizeof(float2), hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(c->tw_col.p, tc.data(), tc.size() * sizeof(float2), hipMemcpyHostToDevice));
+        const std::vector<float2> pr = pass_twiddles(cols), pc = pass_twiddles(rows);
+        c->twp_row.ensure(pr.size() * sizeof(float2));
+        c->twp_col.ensure(pc.size() * sizeof(float2));
+        HIPCHK(hipMemcpy(c->twp_row.p, pr.data(), pr.size() * sizeof(float2), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(c->twp_col.p, pc.data(), pc.size() * sizeof(float2), hipMemcpyHostToDevice));
         // chunk: ~48 B of workspace per pixel per frame; keep the working set near the 256 MiB MALL
         const long per_frame = 48L * rows * cols;
         c->chunk = (int)std::max(1L, std::min(64L, (256L << 20) / per_frame));
@@ -757,9 +786,9 @@ FCD_API int fcd_process(fcd_ctx* c, const float* frames, int n_frames, int flags
             int32_t* kdst = k_out && unwrap ? (dev ? k_out + (size_t)f0 * 2 * hw : c->fk.as<int32_t>()) : nullptr;
             fcdk::int_rows(c->W, unwrap ? 1 : 0, c->wrapped.as<float>(), c->colk.as<int>(), nullptr, kdst,
                            res ? res + (size_t)f0 * 2 : nullptr, c->H, nb, c->Zt.as<float2>(),
-                           c->tw_row.as<float2>(), s);
-            fcdk::int_cols(c->H, c->Zt.as<float2>(), c->W, nb, coef, c->Ht.as<float2>(), c->tw_col.as<float2>(), s);
-            fcdk::int_c2r(c->W, c->Ht.as<float2>(), c->H, nb, hdst, c->tw_row.as<float2>(), s);
+                           c->twp_row.as<float2>(), s);
+            fcdk::int_cols(c->H, c->Zt.as<float2>(), c->W, nb, coef, c->Ht.as<float2>(), c->twp_col.as<float2>(), s);
+            fcdk::int_c2r(c->W, c->Ht.as<float2>(), c->H, nb, hdst, c->twp_row.as<float2>(), s);
             if (c->profiling) {
                 HIPCHK(hipEventRecord(c->next_event(), s));
                 c->prof_frames += nb;
@@ -796,9 +825,9 @@ FCD_API int fcd_process(fcd_ctx* c, const float* frames, int n_frames, int flags
             int32_t* kf = c->fk.as<int32_t>();
             unwrap_maps(c, c->wrapped.as<float>(), 2 * ng, kf, nullptr, s);
             fcdk::int_rows(c->W, 2, c->wrapped.as<float>(), nullptr, kf, nullptr, nullptr, c->H, ng,
-                           c->Zt.as<float2>(), c->tw_row.as<float2>(), s);
-            fcdk::int_cols(c->H, c->Zt.as<float2>(), c->W, ng, coef, c->Ht.as<float2>(), c->tw_col.as<float2>(), s);
-            fcdk::int_c2r(c->W, c->Ht.as<float2>(), c->H, ng, c->out_h.as<float>(), c->tw_row.as<float2>(), s);
+                           c->Zt.as<float2>(), c->twp_row.as<float2>(), s);
+            fcdk::int_cols(c->H, c->Zt.as<float2>(), c->W, ng, coef, c->Ht.as<float2>(), c->twp_col.as<float2>(), s);
+            fcdk::int_c2r(c->W, c->Ht.as<float2>(), c->H, ng, c->out_h.as<float>(), c->twp_row.as<float2>(), s);
             for (int i = 0; i < ng; ++i) {
                 const size_t f = (size_t)redo[g0 + i];
                 if (height_out)

@@ -27,12 +27,17 @@ __device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2
 __host__ __device__ constexpr int ilog2c(int n) { return n <= 1 ? 0 : 1 + ilog2c(n / 2); }
 
 // Elements per thread for an N-point transform.
-__host__ __device__ constexpr int fft_elems(int n) { return n >= 1024 ? 16 : (n >= 512 ? 8 : 4); }
+// 8 complex per thread for N >= 512 keeps a register FFT near 70 VGPRs
+// (7 waves/SIMD); 16 per thread measured 130+ VGPRs (<= 2 waves/SIMD).
+__host__ __device__ constexpr int fft_elems(int n) { return n >= 512 ? 8 : 4; }
 // Threads per team.
 __host__ __device__ constexpr int fft_team(int n) { return n / fft_elems(n); }
-// Padded LDS index: one spare complex per 32.
-__device__ __forceinline__ int pad(int i) { return i + (i >> 5); }
-__host__ __device__ constexpr int padded_len(int n) { return n + (n >> 5); }
+// Padded LDS index: one spare complex per 16.  With this padding every
+// exchange pattern of the register FFT (16t + r, t + 64q, base + 16r) is affine
+// in the compile-time index (one address register + immediate offsets) and
+// conflict-free for ds_*_b64 within each 32-lane group.
+__device__ __forceinline__ int pad(int i) { return i + (i >> 4); }
+__host__ __device__ constexpr int padded_len(int n) { return n + (n >> 4); }
 
 // cos / sin of 2*pi*m/16, m = 0..15.
 __device__ constexpr float kC16[16] = {
@@ -75,13 +80,65 @@ __device__ __forceinline__ void dft_combine(float2* a, const float2* e, const fl
     }
 }
 
+template <bool INV>
+__device__ __forceinline__ void bfly4(float2& a0, float2& a1, float2& a2, float2& a3) {
+    const float2 t0 = cadd(a0, a2), t1 = csub(a0, a2), t2 = cadd(a1, a3), t3 = csub(a1, a3);
+    const float2 u3 = INV ? make_float2(-t3.y, t3.x) : make_float2(t3.y, -t3.x);  // (+/-i) * t3
+    a0 = cadd(t0, t2);
+    a2 = csub(t0, t2);
+    a1 = cadd(t1, u3);
+    a3 = csub(t1, u3);
+}
+
+template <int R, int R1, int N1, int K2, bool INV>
+__device__ __forceinline__ void dft_twiddle_step(float2* a) {
+    // a[n1 + R1*k2] *= W_R^(n1*k2) for the compile-time (n1, k2) grid
+    if constexpr (N1 < R1) {
+        if constexpr (K2 < R / R1) {
+            a[N1 + R1 * K2] = twc<R, N1 * K2, INV>(a[N1 + R1 * K2]);
+            dft_twiddle_step<R, R1, N1, K2 + 1, INV>(a);
+        } else {
+            dft_twiddle_step<R, R1, N1 + 1, 0, INV>(a);
+        }
+    }
+}
+
 // In-register R-point DFT, natural order in and out (R <= 16).
+// R = 16 and 8 are factored as R1 x R2 (4 x 4, 2 x 4): R2-point DFTs over
+// n = n1 + R1*n2, twiddles W_R^(n1*k2), R1-point DFTs, and a compile-time
+// output permutation (pure register renaming).
 template <int R, bool INV>
 __device__ __forceinline__ void dft_reg(float2* a) {
     if constexpr (R == 2) {
         const float2 t = a[0];
         a[0] = cadd(t, a[1]);
         a[1] = csub(t, a[1]);
+    } else if constexpr (R == 4) {
+        bfly4<INV>(a[0], a[1], a[2], a[3]);
+    } else if constexpr (R == 8 || R == 16) {
+        constexpr int R1 = R == 16 ? 4 : 2, R2 = R / R1;
+#pragma unroll
+        for (int n1 = 0; n1 < R1; ++n1) {
+            float2 b[R2];
+#pragma unroll
+            for (int n2 = 0; n2 < R2; ++n2) b[n2] = a[n1 + R1 * n2];
+            dft_reg<R2, INV>(b);
+#pragma unroll
+            for (int k2 = 0; k2 < R2; ++k2) a[n1 + R1 * k2] = b[k2];
+        }
+        dft_twiddle_step<R, R1, 1, 1, INV>(a);
+        float2 out[R];
+#pragma unroll
+        for (int k2 = 0; k2 < R2; ++k2) {
+            float2 c[R1];
+#pragma unroll
+            for (int n1 = 0; n1 < R1; ++n1) c[n1] = a[n1 + R1 * k2];
+            dft_reg<R1, INV>(c);
+#pragma unroll
+            for (int k1 = 0; k1 < R1; ++k1) out[k2 + R2 * k1] = c[k1];
+        }
+#pragma unroll
+        for (int k = 0; k < R; ++k) a[k] = out[k];
     } else if constexpr (R > 2) {
         float2 e[R / 2], o[R / 2];
 #pragma unroll

@@ -40,6 +40,17 @@ namespace fcdk {
 
 constexpr int TILE = 16;
 constexpr int BLOCK = 256;
+// Minimum waves per SIMD for every fast-path kernel (launch-bounds 2nd argument):
+// 4 caps the allocation at 128 VGPRs, i.e. 16 waves per CU to hide HBM latency.
+#ifndef FCD_MIN_WAVES
+#define FCD_MIN_WAVES 4
+#endif
+// The column kernels hold two transforms' worth of state (130-186 VGPRs
+// unconstrained): 3 waves/SIMD (168 VGPRs) up to 2048 points, 2 at 4096.
+template <int N>
+struct ColWaves {
+    static constexpr int V = N >= 4096 ? 2 : 3;
+};
 constexpr float kPiF = 3.14159265358979f;
 constexpr float kTwoPiF = 6.28318530717959f;
 
@@ -51,9 +62,10 @@ template <int N>
 struct KCfg {
     static constexpr int TT = Sched<N>::TT;
     static constexpr int E = Sched<N>::E;
-    static constexpr int TEAMS = TT >= BLOCK ? 1 : BLOCK / TT;
-    static constexpr int THREADS = TEAMS * TT;
+    static constexpr int THREADS = TT > BLOCK ? TT : BLOCK;  // 4096-point teams span 8 waves
+    static constexpr int TEAMS = THREADS / TT;
     static constexpr int ROW = padded_len(N);  // float2 per team row
+    static constexpr int NLEN = N;             // twiddle table entries (float2) at the LDS base
 };
 
 // find_wrap(a, b) of the reference unwrapper with an f32 fast path:
@@ -72,17 +84,19 @@ __device__ __forceinline__ int fw_fast(float a, float b) {
 
 // ------------------------------------------------------------------ K1
 template <int W>
-__global__ __launch_bounds__(BLOCK) void k_demod_rows(const float* __restrict__ frames, int H, int nb,
+__global__ __launch_bounds__(KCfg<W>::THREADS, FCD_MIN_WAVES) void k_demod_rows(const float* __restrict__ frames, int H, int nb,
                                                       DemodTables T, float2* __restrict__ Xb,
                                                       const float2* __restrict__ tw) {
     using C = KCfg<W>;
     constexpr int TT = C::TT, E = C::E, TEAMS = C::TEAMS;
-    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    extern __shared__ __attribute__((aligned(16))) float2 lds_raw[];
+    float2* const lds = lds_raw + C::NLEN;  // lds_raw[0, NLEN): the twiddle table
     const int team = threadIdx.x / TT, t = threadIdx.x % TT;
     float2* s = lds + team * C::ROW;
     float2* stage = lds + TEAMS * C::ROW;  // [NC][TILE + 1]
     RegFFT<W> fft;
-    fft.init(tw, t);
+    fft.init(tw, lds_raw, threadIdx.x, C::THREADS);
+    __syncthreads();
     const int NC = T.NC;
     const int rbs = H / TILE;
     for (int blk = blockIdx.x; blk < nb * rbs; blk += gridDim.x) {
@@ -116,17 +130,19 @@ __global__ __launch_bounds__(BLOCK) void k_demod_rows(const float* __restrict__ 
 
 // ------------------------------------------------------------------ K2
 template <int H>
-__global__ __launch_bounds__(BLOCK) void k_demod_cols(const float2* __restrict__ Xb, int nb, DemodTables T,
+__global__ __launch_bounds__(KCfg<H>::THREADS, ColWaves<H>::V) void k_demod_cols(const float2* __restrict__ Xb, int nb, DemodTables T,
                                                       float2* __restrict__ Ab, int NCA,
                                                       const float2* __restrict__ tw) {
     using C = KCfg<H>;
     constexpr int TT = C::TT, E = C::E, TEAMS = C::TEAMS;
-    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    extern __shared__ __attribute__((aligned(16))) float2 lds_raw[];
+    float2* const lds = lds_raw + C::NLEN;  // lds_raw[0, NLEN): the twiddle table
     const int team = threadIdx.x / TT, t = threadIdx.x % TT;
     float2* s = lds + team * C::ROW;            // holds the forward column spectrum
     float2* s2 = lds + (TEAMS + team) * C::ROW;  // exchanges of the inverse FFTs
     RegFFT<H> fft;
-    fft.init(tw, t);
+    fft.init(tw, lds_raw, threadIdx.x, C::THREADS);
+    __syncthreads();
     const int NC = T.NC;
     const int items = nb * NC;
     for (int base = blockIdx.x * TEAMS; base < items; base += gridDim.x * TEAMS) {
@@ -143,8 +159,18 @@ __global__ __launch_bounds__(BLOCK) void k_demod_cols(const float2* __restrict__
         for (int q = 0; q < E; ++q) s[pad(t + TT * q)] = x[q];
         team_sync<H>();
         const int nout = valid ? T.nouts[i] : 0;
-        // teams spanning waves share the workgroup barrier: keep their loop counts equal
-        const int nmax = (Sched<H>::WAVE_LOCAL || TEAMS == 1) ? nout : 4;
+        // teams spanning waves share the workgroup barrier: every team loops to
+        // the largest output count among the workgroup's items
+        int nmax = nout;
+        if constexpr (!Sched<H>::WAVE_LOCAL && TEAMS > 1) {
+            nmax = 0;
+#pragma unroll
+            for (int tm = 0; tm < TEAMS; ++tm) {
+                const int it = base + tm;
+                nmax = max(nmax, it < items ? T.nouts[it % NC] : 0);
+            }
+        }
+#pragma unroll 1
         for (int e = 0; e < nmax; ++e) {
             const bool live = e < nout;
             const int4 o = live ? T.outs[i * 4 + e] : make_int4(0, 0, 0, 0);  // carrier, cslot, mirror, uc
@@ -177,17 +203,19 @@ __global__ __launch_bounds__(BLOCK) void k_demod_cols(const float2* __restrict__
 
 // ------------------------------------------------------------------ K3
 template <int W>
-__global__ __launch_bounds__(BLOCK) void k_demod_phase(const float2* __restrict__ Ab, int H, int nb, int NCA,
+__global__ __launch_bounds__(KCfg<W>::THREADS, FCD_MIN_WAVES) void k_demod_phase(const float2* __restrict__ Ab, int H, int nb, int NCA,
                                                        DemodTables T, const float* __restrict__ theta,
                                                        float* __restrict__ wrapped, const float2* __restrict__ tw) {
     using C = KCfg<W>;
     constexpr int TT = C::TT, E = C::E, TEAMS = C::TEAMS;
-    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    extern __shared__ __attribute__((aligned(16))) float2 lds_raw[];
+    float2* const lds = lds_raw + C::NLEN;  // lds_raw[0, NLEN): the twiddle table
     const int team = threadIdx.x / TT, t = threadIdx.x % TT;
     float2* s = lds + team * C::ROW;
     float2* stage = lds + TEAMS * C::ROW;  // [NCc][TILE + 1]
     RegFFT<W> fft;
-    fft.init(tw, t);
+    fft.init(tw, lds_raw, threadIdx.x, C::THREADS);
+    __syncthreads();
     const int rbs = H / TILE;
     const int items = nb * 2 * rbs;
     for (int blk = blockIdx.x; blk < items; blk += gridDim.x) {
@@ -252,18 +280,20 @@ __device__ __forceinline__ int2 team_scan_excl(int v, int t, int* scratch) {
 // KMODE 0: phases = wrapped (unwrap=False); 1: residue-free scan unwrap + residue
 // census; 2: k-field from kin (Boruvka path for maps with residues).
 template <int W, int KMODE>
-__global__ __launch_bounds__(BLOCK) void k_int_rows(const float* __restrict__ wrapped, const int* __restrict__ colk,
+__global__ __launch_bounds__(KCfg<W>::THREADS, FCD_MIN_WAVES) void k_int_rows(const float* __restrict__ wrapped, const int* __restrict__ colk,
                                                     const int32_t* __restrict__ kin, int32_t* __restrict__ kout,
                                                     int* __restrict__ rescount, int H, int nb,
                                                     float2* __restrict__ Zt, const float2* __restrict__ tw) {
     using C = KCfg<W>;
     constexpr int TT = C::TT, E = C::E, TEAMS = C::TEAMS;
-    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    extern __shared__ __attribute__((aligned(16))) float2 lds_raw[];
+    float2* const lds = lds_raw + C::NLEN;  // lds_raw[0, NLEN): the twiddle table
     const int team = threadIdx.x / TT, t = threadIdx.x % TT;
     float2* s = lds + team * C::ROW;
     int* scratch = reinterpret_cast<int*>(lds + TEAMS * C::ROW) + team * 8;
     RegFFT<W> fft;
-    fft.init(tw, t);
+    fft.init(tw, lds_raw, threadIdx.x, C::THREADS);
+    __syncthreads();
     const int rbs = H / TILE;
     const int j0 = t * E;  // this thread's blocked segment [j0, j0 + E)
     for (int blk = blockIdx.x; blk < nb * rbs; blk += gridDim.x) {
@@ -288,6 +318,31 @@ __global__ __launch_bounds__(BLOCK) void k_int_rows(const float* __restrict__ wr
                 for (int m = 0; m < 2; ++m) {
                     const float* wr = wrapped + (((long)f * 2 + m) * H + r) * W;
                     nxt[m] = (j0 + E < W) ? wr[j0 + E] : 0.f;
+                }
+                // residue census on the plaquettes (r, j)..(r+1, j+1)  (before the scan:
+                // keeps the k-field registers dead while the next row is in flight)
+                if (r + 1 < H) {
+#pragma unroll
+                    for (int m = 0; m < 2; ++m) {
+                        const float* w1 = wrapped + (((long)f * 2 + m) * H + r + 1) * W;
+                        float lo[E + 1];
+#pragma unroll
+                        for (int j = 0; j < E; j += 4) {
+                            const float4 v = *reinterpret_cast<const float4*>(w1 + j0 + j);
+                            lo[j] = v.x; lo[j + 1] = v.y; lo[j + 2] = v.z; lo[j + 3] = v.w;
+                        }
+                        lo[E] = (j0 + E < W) ? w1[j0 + E] : 0.f;
+                        int cnt = 0;
+#pragma unroll
+                        for (int j = 0; j < E; ++j) {
+                            if (j0 + j + 1 < W) {
+                                const float a = ph[m][j], b = j + 1 < E ? ph[m][j + 1] : nxt[m];
+                                const float cc = lo[j + 1], d = lo[j];
+                                cnt += (fw_fast(a, b) + fw_fast(b, cc) + fw_fast(cc, d) + fw_fast(d, a)) != 0;
+                            }
+                        }
+                        res[m] += cnt;
+                    }
                 }
                 // d(j) = -find_wrap(w(j), w(j+1)), biased +1 and packed (map0 low, map1 high)
                 int run = 0;
@@ -316,31 +371,6 @@ __global__ __launch_bounds__(BLOCK) void k_int_rows(const float* __restrict__ wr
                     const int base = colk[((long)f * 2 + m) * H + r];
 #pragma unroll
                     for (int j = 0; j < E; ++j) kk[m][j] += base;
-                }
-                // residue census on the plaquettes (r, j)..(r+1, j+1)
-                if (r + 1 < H) {
-#pragma unroll
-                    for (int m = 0; m < 2; ++m) {
-                        const float* w0 = wrapped + (((long)f * 2 + m) * H + r) * W;
-                        const float* w1 = w0 + W;
-                        float lo[E + 1];
-#pragma unroll
-                        for (int j = 0; j < E; j += 4) {
-                            const float4 v = *reinterpret_cast<const float4*>(w1 + j0 + j);
-                            lo[j] = v.x; lo[j + 1] = v.y; lo[j + 2] = v.z; lo[j + 3] = v.w;
-                        }
-                        lo[E] = (j0 + E < W) ? w1[j0 + E] : 0.f;
-                        int cnt = 0;
-#pragma unroll
-                        for (int j = 0; j < E; ++j) {
-                            if (j0 + j + 1 < W) {
-                                const float a = ph[m][j], b = j + 1 < E ? ph[m][j + 1] : nxt[m];
-                                const float cc = lo[j + 1], d = lo[j];
-                                cnt += (fw_fast(a, b) + fw_fast(b, cc) + fw_fast(cc, d) + fw_fast(d, a)) != 0;
-                            }
-                        }
-                        res[m] += cnt;
-                    }
                 }
                 if (kout) {
 #pragma unroll
@@ -389,15 +419,18 @@ __global__ __launch_bounds__(BLOCK) void k_int_rows(const float* __restrict__ wr
 
 // ------------------------------------------------------------------ I2
 template <int H>
-__global__ __launch_bounds__(BLOCK) void k_int_cols(const float2* __restrict__ Zt, int W, int nb, IntegCoef c,
+__global__ __launch_bounds__(KCfg<H>::THREADS, ColWaves<H>::V) void k_int_cols(const float2* __restrict__ Zt, int W, int nb, IntegCoef c,
                                                     float2* __restrict__ Ht, const float2* __restrict__ tw) {
     using C = KCfg<H>;
     constexpr int TT = C::TT, E = C::E, TEAMS = C::TEAMS;
-    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    extern __shared__ __attribute__((aligned(16))) float2 lds_raw[];
+    float2* const lds = lds_raw + C::NLEN;  // lds_raw[0, NLEN): the twiddle table
     const int team = threadIdx.x / TT, t = threadIdx.x % TT;
     float2* s = lds + team * C::ROW;
+    float2* s2 = lds + (TEAMS + team) * C::ROW;
     RegFFT<H> fft;
-    fft.init(tw, t);
+    fft.init(tw, lds_raw, threadIdx.x, C::THREADS);
+    __syncthreads();
     const int NCH = W / 2 + 1;
     const int items = nb * NCH;
     for (int base = blockIdx.x * TEAMS; base < items; base += gridDim.x * TEAMS) {
@@ -406,24 +439,25 @@ __global__ __launch_bounds__(BLOCK) void k_int_cols(const float2* __restrict__ Z
         const int f = valid ? item / NCH : 0, col = valid ? item % NCH : 0;
         const int colm = (W - col) & (W - 1);
         const float2* src = Zt + (long)f * H * W;
-        float2 x[E], y[E];
+        {   // Z(:, -c) first, parked in s2 so only one column is live in registers
+            float2 y[E];
 #pragma unroll
-        for (int q = 0; q < E; ++q) {
-            x[q] = src[tix(t + TT * q, col, W)];
-            y[q] = src[tix(t + TT * q, colm, W)];
+            for (int q = 0; q < E; ++q) y[q] = src[tix(t + TT * q, colm, W)];
+            fft.template run<false>(y, s, t);
+            if constexpr (!Sched<H>::WAVE_LOCAL) __syncthreads();
+#pragma unroll
+            for (int q = 0; q < E; ++q) s2[pad(t + TT * q)] = y[q];
         }
-        fft.template run<false>(x, s, t);
-        fft.template run<false>(y, s, t);
-        if constexpr (!Sched<H>::WAVE_LOCAL) __syncthreads();
+        float2 x[E];
 #pragma unroll
-        for (int q = 0; q < E; ++q) s[pad(t + TT * q)] = y[q];
-        team_sync<H>();
+        for (int q = 0; q < E; ++q) x[q] = src[tix(t + TT * q, col, W)];
+        fft.template run<false>(x, s, t);  // its exchange barriers also publish s2
         const float kx = c.kxe[col], kx2 = c.kx2[col];
 #pragma unroll
         for (int q = 0; q < E; ++q) {
             const int i = t + TT * q;
             const float2 z = x[q];
-            const float2 zm = s[pad((H - i) & (H - 1))];
+            const float2 zm = s2[pad((H - i) & (H - 1))];
             const float2 f0 = make_float2(0.5f * (z.x + zm.x), 0.5f * (z.y - zm.y));
             const float2 f1 = make_float2(0.5f * (z.y + zm.y), -0.5f * (z.x - zm.x));
             const float ky = c.kye[i];
@@ -447,16 +481,18 @@ __global__ __launch_bounds__(BLOCK) void k_int_cols(const float2* __restrict__ Z
 
 // ------------------------------------------------------------------ I3
 template <int W>
-__global__ __launch_bounds__(BLOCK) void k_int_c2r(const float2* __restrict__ Ht, int H, int nb, int rpw,
+__global__ __launch_bounds__(KCfg<W>::THREADS, FCD_MIN_WAVES) void k_int_c2r(const float2* __restrict__ Ht, int H, int nb, int rpw,
                                                    float* __restrict__ hout, const float2* __restrict__ tw) {
     using C = KCfg<W>;
     constexpr int TT = C::TT, E = C::E, TEAMS = C::TEAMS;
-    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    extern __shared__ __attribute__((aligned(16))) float2 lds_raw[];
+    float2* const lds = lds_raw + C::NLEN;  // lds_raw[0, NLEN): the twiddle table
     const int team = threadIdx.x / TT, t = threadIdx.x % TT;
     float2* s = lds + team * C::ROW;
     float2* stage = lds + TEAMS * C::ROW;  // [NCH][rpw + 1]
     RegFFT<W> fft;
-    fft.init(tw, t);
+    fft.init(tw, lds_raw, threadIdx.x, C::THREADS);
+    __syncthreads();
     const int NCH = W / 2 + 1;
     const int nblk = H / rpw;
     for (int blk = blockIdx.x; blk < nb * nblk; blk += gridDim.x) {
@@ -533,7 +569,7 @@ template <int W>
 static void launch_demod_rows(const float* frames, int H, int nb, const DemodTables& T, float2* Xb, const float2* tw,
                               hipStream_t s) {
     using C = KCfg<W>;
-    const size_t lds = (size_t)C::TEAMS * C::ROW * 8 + (size_t)T.NC * (TILE + 1) * 8;
+    const size_t lds = (size_t)C::NLEN * 8 + (size_t)C::TEAMS * C::ROW * 8 + (size_t)T.NC * (TILE + 1) * 8;
     set_lds(k_demod_rows<W>, lds);
     const int grid = grid_for((long)nb * (H / TILE), 4);
     hipLaunchKernelGGL(k_demod_rows<W>, dim3(grid), dim3(C::THREADS), lds, s, frames, H, nb, T, Xb, tw);
@@ -544,7 +580,7 @@ template <int H>
 static void launch_demod_cols(const float2* Xb, int nb, const DemodTables& T, float2* Ab, int NCA, const float2* tw,
                               hipStream_t s) {
     using C = KCfg<H>;
-    const size_t lds = (size_t)2 * C::TEAMS * C::ROW * 8;
+    const size_t lds = (size_t)C::NLEN * 8 + (size_t)2 * C::TEAMS * C::ROW * 8;
     set_lds(k_demod_cols<H>, lds);
     const int grid = grid_for(((long)nb * T.NC + C::TEAMS - 1) / C::TEAMS, 4);
     hipLaunchKernelGGL(k_demod_cols<H>, dim3(grid), dim3(C::THREADS), lds, s, Xb, nb, T, Ab, NCA, tw);
@@ -555,7 +591,7 @@ template <int W>
 static void launch_demod_phase(const float2* Ab, int H, int nb, int NCA, const DemodTables& T, const float* theta,
                                float* wrapped, const float2* tw, hipStream_t s) {
     using C = KCfg<W>;
-    const size_t lds = (size_t)C::TEAMS * C::ROW * 8 + (size_t)NCA * (TILE + 1) * 8;
+    const size_t lds = (size_t)C::NLEN * 8 + (size_t)C::TEAMS * C::ROW * 8 + (size_t)NCA * (TILE + 1) * 8;
     set_lds(k_demod_phase<W>, lds);
     const int grid = grid_for((long)nb * 2 * (H / TILE), 4);
     hipLaunchKernelGGL(k_demod_phase<W>, dim3(grid), dim3(C::THREADS), lds, s, Ab, H, nb, NCA, T, theta, wrapped, tw);
@@ -566,7 +602,7 @@ template <int W>
 static void launch_int_rows(int kmode, const float* w, const int* colk, const int32_t* kin, int32_t* kout,
                             int* rescount, int H, int nb, float2* Zt, const float2* tw, hipStream_t s) {
     using C = KCfg<W>;
-    const size_t lds = (size_t)C::TEAMS * C::ROW * 8 + (size_t)C::TEAMS * 8 * 4;
+    const size_t lds = (size_t)C::NLEN * 8 + (size_t)C::TEAMS * C::ROW * 8 + (size_t)C::TEAMS * 8 * 4;
     const int grid = grid_for((long)nb * (H / TILE), 4);
     if (kmode == 0) {
         set_lds(k_int_rows<W, 0>, lds);
@@ -588,7 +624,7 @@ template <int H>
 static void launch_int_cols(const float2* Zt, int W, int nb, const IntegCoef& c, float2* Ht, const float2* tw,
                             hipStream_t s) {
     using C = KCfg<H>;
-    const size_t lds = (size_t)C::TEAMS * C::ROW * 8;
+    const size_t lds = (size_t)C::NLEN * 8 + (size_t)2 * C::TEAMS * C::ROW * 8;
     set_lds(k_int_cols<H>, lds);
     const int grid = grid_for(((long)nb * (W / 2 + 1) + C::TEAMS - 1) / C::TEAMS, 4);
     hipLaunchKernelGGL(k_int_cols<H>, dim3(grid), dim3(C::THREADS), lds, s, Zt, W, nb, c, Ht, tw);
@@ -606,7 +642,7 @@ template <int W>
 static void launch_int_c2r(const float2* Ht, int H, int nb, float* h, const float2* tw, hipStream_t s) {
     using C = KCfg<W>;
     const int rpw = c2r_rows_per_block(W);
-    const size_t lds = (size_t)C::TEAMS * C::ROW * 8 + (size_t)(W / 2 + 1) * (rpw + 1) * 8;
+    const size_t lds = (size_t)C::NLEN * 8 + (size_t)C::TEAMS * C::ROW * 8 + (size_t)(W / 2 + 1) * (rpw + 1) * 8;
     set_lds(k_int_c2r<W>, lds);
     const int grid = grid_for((long)nb * (H / rpw), 4);
     hipLaunchKernelGGL(k_int_c2r<W>, dim3(grid), dim3(C::THREADS), lds, s, Ht, H, nb, rpw, h, tw);

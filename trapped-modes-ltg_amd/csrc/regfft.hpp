@@ -68,26 +68,26 @@ __device__ __forceinline__ void team_sync() {
         __syncthreads();
 }
 
+// Pass-major twiddle table, built on the host in double precision
+// (pass_twiddle_table in fcd_engine.cpp): for passes P = 1..NP-1, for
+// k < L_P, for r = 1..R_P-1: exp(-2 pi i r k / (L_P R_P)).  A butterfly reads
+// its R-1 twiddles contiguously: one address + immediate offsets.
 template <int N>
 struct RegFFT {
     using S = Sched<N>;
     static constexpr int E = S::E, TT = S::TT, NP = S::NP;
-    float2 tw[S::NTW > 0 ? S::NTW : 1];
+    const float2* tw;  // the workgroup's LDS copy of the pass-major table (< N entries)
 
-    __device__ __forceinline__ void init(const float2* __restrict__ table, int t) { init_pass<1>(table, t); }
+    static constexpr int passoff(int p) {
+        int o = 0;
+        for (int i = 1; i < p; ++i) o += S::ell(i) * (S::radix(i) - 1);
+        return o;
+    }
 
-    template <int P>
-    __device__ __forceinline__ void init_pass(const float2* __restrict__ table, int t) {
-        if constexpr (P < NP) {
-            constexpr int R = S::radix(P), L = S::ell(P), BPT = E / R, OFF = S::twoff(P);
-#pragma unroll
-            for (int b = 0; b < BPT; ++b) {
-                const int k = (t + b * TT) & (L - 1);
-#pragma unroll
-                for (int r = 1; r < R; ++r) tw[OFF + b * (R - 1) + r - 1] = table[r * k * (N / (L * R))];
-            }
-            init_pass<P + 1>(table, t);
-        }
+    // Cooperative copy of the host's twiddle table into LDS (caller syncs after).
+    __device__ __forceinline__ void init(const float2* __restrict__ table, float2* lds_tw, int tid, int nthreads) {
+        for (int i = tid; i < N; i += nthreads) lds_tw[i] = table[i];
+        tw = lds_tw;
     }
 
     // x: natural strided layout in and out.  s: the team's LDS row (padded_len(N)).
@@ -97,16 +97,18 @@ struct RegFFT {
 
     template <int P, bool INV>
     __device__ __forceinline__ void run_pass(float2 (&x)[E], float2* s, int t) const {
-        constexpr int R = S::radix(P), L = S::ell(P), BPT = E / R, OFF = S::twoff(P);
+        constexpr int R = S::radix(P), L = S::ell(P), BPT = E / R;
         float2 a[BPT][R];
 #pragma unroll
         for (int b = 0; b < BPT; ++b) {
 #pragma unroll
             for (int r = 0; r < R; ++r) a[b][r] = x[b + BPT * r];
             if constexpr (P > 0) {
+                const int k = (t + b * TT) & (L - 1);
+                const float2* twk = tw + passoff(P) + k * (R - 1) - 1;
 #pragma unroll
                 for (int r = 1; r < R; ++r) {
-                    const float2 w = tw[OFF + b * (R - 1) + r - 1];
+                    const float2 w = twk[r];
                     a[b][r] = INV ? cmul(a[b][r], make_float2(w.x, -w.y)) : cmul(a[b][r], w);
                 }
             }
