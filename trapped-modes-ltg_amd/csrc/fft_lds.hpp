@@ -29,7 +29,10 @@ __host__ __device__ constexpr int ilog2c(int n) { return n <= 1 ? 0 : 1 + ilog2c
 // Elements per thread for an N-point transform.
 // 8 complex per thread for N >= 512 keeps a register FFT near 70 VGPRs
 // (7 waves/SIMD); 16 per thread measured 130+ VGPRs (<= 2 waves/SIMD).
-__host__ __device__ constexpr int fft_elems(int n) { return n >= 512 ? 8 : 4; }
+#ifndef FCD_ELEMS_1024
+#define FCD_ELEMS_1024 8
+#endif
+__host__ __device__ constexpr int fft_elems(int n) { return n >= 1024 ? FCD_ELEMS_1024 : (n >= 512 ? 8 : 4); }
 // Threads per team.
 __host__ __device__ constexpr int fft_team(int n) { return n / fft_elems(n); }
 // Padded LDS index: one spare complex per 16.  With this padding every

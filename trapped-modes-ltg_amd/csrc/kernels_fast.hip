@@ -321,7 +321,11 @@ __global__ __launch_bounds__(KCfg<W>::THREADS, FCD_MIN_WAVES) void k_int_rows(co
                 }
                 // residue census on the plaquettes (r, j)..(r+1, j+1)  (before the scan:
                 // keeps the k-field registers dead while the next row is in flight)
+#ifdef FCD_EXP_NO_RESIDUE
+                if (false) {
+#else
                 if (r + 1 < H) {
+#endif
 #pragma unroll
                     for (int m = 0; m < 2; ++m) {
                         const float* w1 = wrapped + (((long)f * 2 + m) * H + r + 1) * W;
@@ -404,7 +408,13 @@ __global__ __launch_bounds__(KCfg<W>::THREADS, FCD_MIN_WAVES) void k_int_rows(co
             fft.template run<false>(x, s, t);
             float2* dst = Zt + (long)f * H * W;
 #pragma unroll
-            for (int q = 0; q < E; ++q) dst[tix(r, t + TT * q, W)] = x[q];
+            for (int q = 0; q < E; ++q) {
+#ifdef FCD_EXP_ZT_ROWMAJOR
+                dst[(long)r * W + t + TT * q] = x[q];  // timing experiment only (wrong layout)
+#else
+                dst[tix(r, t + TT * q, W)] = x[q];
+#endif
+            }
         }
         if constexpr (KMODE == 1) {
 #pragma unroll
@@ -420,7 +430,7 @@ __global__ __launch_bounds__(KCfg<W>::THREADS, FCD_MIN_WAVES) void k_int_rows(co
 // ------------------------------------------------------------------ I2
 template <int H>
 __global__ __launch_bounds__(KCfg<H>::THREADS, ColWaves<H>::V) void k_int_cols(const float2* __restrict__ Zt, int W, int nb, IntegCoef c,
-                                                    float2* __restrict__ Ht, const float2* __restrict__ tw) {
+                                                    float2* __restrict__ Ht, const float2* __restrict__ tw, int zts) {
     using C = KCfg<H>;
     constexpr int TT = C::TT, E = C::E, TEAMS = C::TEAMS;
     extern __shared__ __attribute__((aligned(16))) float2 lds_raw[];
@@ -442,7 +452,14 @@ __global__ __launch_bounds__(KCfg<H>::THREADS, ColWaves<H>::V) void k_int_cols(c
         {   // Z(:, -c) first, parked in s2 so only one column is live in registers
             float2 y[E];
 #pragma unroll
-            for (int q = 0; q < E; ++q) y[q] = src[tix(t + TT * q, colm, W)];
+            for (int q = 0; q < E; ++q) {
+#ifdef FCD_EXP_ZT_ROWMAJOR
+                y[q] = src[(long)(t + TT * q) * W + colm];
+#else
+                const int rr = t + TT * q;
+                y[q] = src[((long)(rr >> zts) * W + colm) * (1 << zts) + (rr & ((1 << zts) - 1))];
+#endif
+            }
             fft.template run<false>(y, s, t);
             if constexpr (!Sched<H>::WAVE_LOCAL) __syncthreads();
 #pragma unroll
@@ -450,7 +467,14 @@ __global__ __launch_bounds__(KCfg<H>::THREADS, ColWaves<H>::V) void k_int_cols(c
         }
         float2 x[E];
 #pragma unroll
-        for (int q = 0; q < E; ++q) x[q] = src[tix(t + TT * q, col, W)];
+        for (int q = 0; q < E; ++q) {
+#ifdef FCD_EXP_ZT_ROWMAJOR
+            x[q] = src[(long)(t + TT * q) * W + col];
+#else
+            const int rr = t + TT * q;
+            x[q] = src[((long)(rr >> zts) * W + col) * (1 << zts) + (rr & ((1 << zts) - 1))];
+#endif
+        }
         fft.template run<false>(x, s, t);  // its exchange barriers also publish s2
         const float kx = c.kxe[col], kx2 = c.kx2[col];
 #pragma unroll
@@ -532,6 +556,8 @@ __global__ __launch_bounds__(KCfg<W>::THREADS, FCD_MIN_WAVES) void k_int_c2r(con
     }
 }
 
+#include "int_rows.inc"
+
 // ------------------------------------------------------------------ launchers
 static int g_num_cu = 0;
 static int grid_for(long work_items, int per_cu) {
@@ -601,20 +627,20 @@ static void launch_demod_phase(const float2* Ab, int H, int nb, int NCA, const D
 template <int W>
 static void launch_int_rows(int kmode, const float* w, const int* colk, const int32_t* kin, int32_t* kout,
                             int* rescount, int H, int nb, float2* Zt, const float2* tw, hipStream_t s) {
-    using C = KCfg<W>;
-    const size_t lds = (size_t)C::NLEN * 8 + (size_t)C::TEAMS * C::ROW * 8 + (size_t)C::TEAMS * 8 * 4;
-    const int grid = grid_for((long)nb * (H / TILE), 4);
+    using C = IRCfg<W>;
+    const size_t lds = C::LDS_BYTES;
+    const int grid = grid_for((long)nb * (H / C::ZT), 1);
     if (kmode == 0) {
-        set_lds(k_int_rows<W, 0>, lds);
-        hipLaunchKernelGGL((k_int_rows<W, 0>), dim3(grid), dim3(C::THREADS), lds, s, w, colk, kin, kout, rescount, H,
+        set_lds(k_int_rows2<W, 0>, lds);
+        hipLaunchKernelGGL((k_int_rows2<W, 0>), dim3(grid), dim3(C::THREADS), lds, s, w, colk, kin, kout, rescount, H,
                            nb, Zt, tw);
     } else if (kmode == 1) {
-        set_lds(k_int_rows<W, 1>, lds);
-        hipLaunchKernelGGL((k_int_rows<W, 1>), dim3(grid), dim3(C::THREADS), lds, s, w, colk, kin, kout, rescount, H,
+        set_lds(k_int_rows2<W, 1>, lds);
+        hipLaunchKernelGGL((k_int_rows2<W, 1>), dim3(grid), dim3(C::THREADS), lds, s, w, colk, kin, kout, rescount, H,
                            nb, Zt, tw);
     } else {
-        set_lds(k_int_rows<W, 2>, lds);
-        hipLaunchKernelGGL((k_int_rows<W, 2>), dim3(grid), dim3(C::THREADS), lds, s, w, colk, kin, kout, rescount, H,
+        set_lds(k_int_rows2<W, 2>, lds);
+        hipLaunchKernelGGL((k_int_rows2<W, 2>), dim3(grid), dim3(C::THREADS), lds, s, w, colk, kin, kout, rescount, H,
                            nb, Zt, tw);
     }
     FCD_CHECK_LAUNCH();
@@ -627,7 +653,9 @@ static void launch_int_cols(const float2* Zt, int W, int nb, const IntegCoef& c,
     const size_t lds = (size_t)C::NLEN * 8 + (size_t)2 * C::TEAMS * C::ROW * 8;
     set_lds(k_int_cols<H>, lds);
     const int grid = grid_for(((long)nb * (W / 2 + 1) + C::TEAMS - 1) / C::TEAMS, 4);
-    hipLaunchKernelGGL(k_int_cols<H>, dim3(grid), dim3(C::THREADS), lds, s, Zt, W, nb, c, Ht, tw);
+    const int zt = zt_rows(W);
+    const int zts = zt == 16 ? 4 : (zt == 8 ? 3 : 2);
+    hipLaunchKernelGGL(k_int_cols<H>, dim3(grid), dim3(C::THREADS), lds, s, Zt, W, nb, c, Ht, tw, zts);
     FCD_CHECK_LAUNCH();
 }
 

@@ -1,0 +1,139 @@
+// Kernel micro-benchmark for the band-pruned fast path (tuning tool, not part
+// of the product ABI).  Times each stage kernel with HIP events on synthetic
+// data shaped like the 1024^2 bench workload: nb frames per launch, a carrier
+// pair of radius 51 (the pattern.py board's disks), 103 half-spectrum columns.
+//
+//   kbench [N=1024] [nb=8] [iters=20]
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "../csrc/kernels.hpp"
+
+#define CK(x)                                                                 \
+    do {                                                                      \
+        hipError_t e = (x);                                                   \
+        if (e != hipSuccess) {                                                \
+            std::fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e));      \
+            std::exit(1);                                                     \
+        }                                                                     \
+    } while (0)
+
+template <class T>
+static T* dalloc(size_t n) {
+    T* p = nullptr;
+    CK(hipMalloc(&p, n * sizeof(T)));
+    CK(hipMemset(p, 0, n * sizeof(T)));
+    return p;
+}
+
+int main(int argc, char** argv) {
+    const int N = argc > 1 ? std::atoi(argv[1]) : 1024;
+    const int nb = argc > 2 ? std::atoi(argv[2]) : 8;
+    const int iters = argc > 3 ? std::atoi(argv[3]) : 20;
+    const int H = N, W = N;
+    const long hw = (long)H * W;
+    const int R = N / 20;  // disk radius ~ |p0 - p1| / 2 of the 10-px board
+    hipStream_t s;
+    CK(hipStreamCreate(&s));
+
+    // tables: carrier 0 disk centred at unshifted column R, carrier 1 at W - R (mirror of hc)
+    std::vector<int> hc, nouts, colslot(2 * (size_t)W, -1);
+    std::vector<int4> outs;
+    std::vector<int2> outrows;
+    const int NCc = 2 * R + 1;
+    for (int j = 0; j < NCc; ++j) {
+        colslot[j] = j;                              // carrier 0: uc = j
+        colslot[(size_t)W + (W - j) % W] = j;       // carrier 1: uc = -j
+    }
+    for (int h = 0; h < NCc; ++h) {
+        hc.push_back(h);
+        nouts.push_back(2);
+        outs.push_back(make_int4(0, h, 0, h));
+        outs.push_back(make_int4(1, h, h ? 1 : 0, (W - h) % W));
+        outs.push_back(make_int4(0, 0, 0, 0));
+        outs.push_back(make_int4(0, 0, 0, 0));
+        for (int e = 0; e < 2; ++e) outrows.push_back(make_int2(H / 2 - R, H / 2 + R));
+        outrows.push_back(make_int2(1, 0));
+        outrows.push_back(make_int2(1, 0));
+    }
+    fcdk::DemodTables T;
+    int* d_hc = dalloc<int>(hc.size());
+    int* d_nouts = dalloc<int>(nouts.size());
+    int4* d_outs = dalloc<int4>(outs.size());
+    int2* d_outrows = dalloc<int2>(outrows.size());
+    int* d_colslot = dalloc<int>(colslot.size());
+    CK(hipMemcpy(d_hc, hc.data(), hc.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_nouts, nouts.data(), nouts.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_outs, outs.data(), outs.size() * 16, hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_outrows, outrows.data(), outrows.size() * 8, hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_colslot, colslot.data(), colslot.size() * 4, hipMemcpyHostToDevice));
+    T.hc = d_hc;
+    T.nouts = d_nouts;
+    T.outs = d_outs;
+    T.outrows = d_outrows;
+    T.colslot = d_colslot;
+    T.NC = NCc;
+    T.NCc[0] = T.NCc[1] = NCc;
+    const int NCA = NCc;
+
+    std::vector<float2> twh(N);
+    for (int i = 0; i < N; ++i) twh[i] = make_float2(1.f, 0.f);
+    float2* tw = dalloc<float2>(N);
+    CK(hipMemcpy(tw, twh.data(), N * 8, hipMemcpyHostToDevice));
+
+    std::vector<float> fr(nb * hw);
+    for (size_t i = 0; i < fr.size(); ++i) fr[i] = (float)((i * 2654435761u) % 1000) * 0.001f;
+    float* frames = dalloc<float>(nb * hw);
+    CK(hipMemcpy(frames, fr.data(), fr.size() * 4, hipMemcpyHostToDevice));
+    float2* Xb = dalloc<float2>((size_t)nb * H * T.NC);
+    float2* Ab = dalloc<float2>((size_t)nb * 2 * H * NCA);
+    float* theta = dalloc<float>(2 * hw);
+    float* wrapped = dalloc<float>((size_t)nb * 2 * hw);
+    CK(hipMemcpy(wrapped, fr.data(), fr.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(wrapped + nb * hw, fr.data(), fr.size() * 4, hipMemcpyHostToDevice));
+    int* colk = dalloc<int>((size_t)nb * 2 * H);
+    int* res = dalloc<int>((size_t)nb * 2);
+    int32_t* kbuf = dalloc<int32_t>((size_t)nb * 2 * hw);
+    float2* Zt = dalloc<float2>((size_t)nb * hw);
+    float2* Ht = dalloc<float2>((size_t)nb * H * (W / 2 + 1));
+    float* hout = dalloc<float>((size_t)nb * hw);
+    float* ktab = dalloc<float>(2 * (W + H));
+    fcdk::IntegCoef coef{ktab, ktab + W, ktab + W + H, ktab + 2 * W + H, 1.f, 0.5f, -0.5f, 1.f, 1e-6f};
+
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    auto timeit = [&](const char* name, double bytes_per_frame, auto fn) {
+        for (int i = 0; i < 3; ++i) fn();
+        CK(hipStreamSynchronize(s));
+        CK(hipEventRecord(e0, s));
+        for (int i = 0; i < iters; ++i) fn();
+        CK(hipEventRecord(e1, s));
+        CK(hipEventSynchronize(e1));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        const double us = ms * 1e3 / iters;
+        std::printf("%-22s %9.1f us/launch %8.2f us/frame %8.1f GB/s\n", name, us, us / nb,
+                    bytes_per_frame * nb / (us * 1e-6) / 1e9);
+    };
+    const double f = 4.0 * hw;
+    timeit("demod_rows", f + 8.0 * H * T.NC, [&] { fcdk::demod_rows(W, frames, H, nb, T, Xb, tw, s); });
+    timeit("demod_cols", 8.0 * H * T.NC + 16.0 * H * NCA, [&] { fcdk::demod_cols(H, Xb, nb, T, Ab, NCA, tw, s); });
+    timeit("demod_phase", 16.0 * H * NCA + 8 * f, [&] {
+        fcdk::demod_phase(W, Ab, H, nb, NCA, T, theta, wrapped, tw, s);
+    });
+    timeit("colk", 8.0 * H, [&] { fcdk::unwrap_colk(wrapped, 2 * nb, H, W, colk, s); });
+    timeit("int_rows k0", 2 * f + 2 * f, [&] {
+        fcdk::int_rows(W, 0, wrapped, colk, nullptr, nullptr, nullptr, H, nb, Zt, tw, s);
+    });
+    timeit("int_rows k1", 2 * f + 2 * f, [&] {
+        fcdk::int_rows(W, 1, wrapped, colk, nullptr, nullptr, res, H, nb, Zt, tw, s);
+    });
+    timeit("int_cols", 2 * f + 8.0 * H * (W / 2 + 1),
+           [&] { fcdk::int_cols(H, Zt, W, nb, coef, Ht, tw, s); });
+    timeit("int_c2r", 8.0 * H * (W / 2 + 1) + f, [&] { fcdk::int_c2r(W, Ht, H, nb, hout, tw, s); });
+    return 0;
+}
