@@ -127,7 +127,9 @@ def main():
     demod_bytes = 12.0 * n * n
     demod_ms_per_frame = stages["demod"] / max(nframes, 1)
     achieved = demod_bytes / (demod_ms_per_frame * 1e-3) / 1e9
+    fix_frames = int(stages.pop("fixup_frames"))
     per_frame = {k: v / max(nframes, 1) * 1e3 for k, v in stages.items()}  # us per frame
+    per_frame["fixup_frames_per_step"] = fix_frames / args.steps
     out = {
         "metric": METRIC,
         "value": round(value, 2),

@@ -5,7 +5,7 @@ of 10-pixel squares, 0 / 65535 (uint16 -> float32), optionally rotated (the
 survey's strict-parity variant uses 5 degrees).  Frame b is the reference
 sampled bilinearly at r + grad(h_b) (the warp of pyval/val.py:100-106), with
 h_b a sum of 6 Gaussian bumps seeded by b: centres U(0.2N, 0.8N), sigma
-U(0.05N, 0.15N), amplitude +-0.25 sigma^2 (peak strain ~0.25: the phase spans
+U(0.05N, 0.15N), amplitude +-0.2 sigma^2 (peak strain ~0.2: the phase spans
 several 2*pi); the displacement is tapered to zero over the outer 10 % of the
 frame (sin^2 window) so the non-periodic image border adds no residues: the wrapped maps are
 residue-free, as SURVEY.md §8d asks of the throughput configs.
@@ -17,6 +17,7 @@ import numpy as np
 
 SQUARE_PX = 10
 SQUARE_SIZE = 0.001  # physical square side for calibration (any value; only scales cf)
+AMP = 0.2  # bump amplitude / sigma^2 (peak strain)
 
 
 def checkerboard(n, rotate_deg=0.0, dtype=np.float32):
@@ -33,7 +34,7 @@ def bumps(n, seed, count=6):
     cy = rng.uniform(0.2 * n, 0.8 * n, count)
     cx = rng.uniform(0.2 * n, 0.8 * n, count)
     sg = rng.uniform(0.05 * n, 0.15 * n, count)
-    amp = rng.choice([-1.0, 1.0], count) * 0.25 * sg * sg
+    amp = rng.choice([-1.0, 1.0], count) * AMP * sg * sg
     return cy, cx, sg, amp
 
 

@@ -113,10 +113,12 @@ int fcd_fft2(fcd_ctx* ctx, const float* in, int n, int flags, float* out, void* 
  * fcd_process records HIP events on its stream around each stage of every
  * chunk.  fcd_stage_times synchronises and returns the accumulated device
  * milliseconds since the last call: out[0] demodulation (forward FFT, disk
- * band-pass, inverse FFTs, phase), out[1] unwrap, out[2] displacement +
- * integration, out[3] whole chunks; *frames = frames covered. */
+ * band-pass, inverse FFTs, phase), out[1] unwrap pre-pass, out[2] unwrap scan
+ * + displacement + integration, out[3] whole first pass, out[4] the exact
+ * (Boruvka) fix-up pass, out[5] frames that needed it; *frames = frames
+ * covered by the first pass. */
 int fcd_profile(fcd_ctx* ctx, int enable);
-int fcd_stage_times(fcd_ctx* ctx, double* out4, int64_t* frames);
+int fcd_stage_times(fcd_ctx* ctx, double* out6, int64_t* frames);
 
 #ifdef __cplusplus
 }

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -153,6 +154,8 @@ struct fcd_ctx {
     std::vector<hipEvent_t> ev_pool;
     size_t ev_used = 0;
     long prof_frames = 0;
+    double prof_fix_ms = 0;   // host wall time of the exact fix-up pass (it synchronises)
+    long prof_fix_frames = 0;
 
     hipStream_t pick(void* s) const { return s ? static_cast<hipStream_t>(s) : own; }
     hipEvent_t next_event() {
@@ -249,8 +252,10 @@ void unwrap_maps(fcd_ctx* c, const float* w, int nmaps, int32_t* k, int* res_hos
     fcdk::mst_init(w, c->mst_ids.as<int>(), nact, c->H, c->W, m, s);
     const int max_rounds = 64;
     int rounds = 0;
-    for (; rounds < max_rounds; ++rounds) {
-        fcdk::mst_round(w, c->mst_ids.as<int>(), nact, c->H, c->W, m, s);
+    // Boruvka halves the component count every round; check convergence every
+    // third round (a round after convergence hooks nothing and changes nothing).
+    for (; rounds < max_rounds; rounds += 3) {
+        for (int g = 0; g < 3; ++g) fcdk::mst_round(w, c->mst_ids.as<int>(), nact, c->H, c->W, m, s);
         int hooks = 0;
         HIPCHK(hipMemcpyAsync(&hooks, m.nhooks, sizeof(int), hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
@@ -816,6 +821,19 @@ FCD_API int fcd_process(fcd_ctx* c, const float* frames, int n_frames, int flags
         std::vector<int> redo;
         for (int f = 0; f < n_frames; ++f)
             if (counts[2 * (size_t)f] || counts[2 * (size_t)f + 1]) redo.push_back(f);
+        const auto fix_t0 = std::chrono::steady_clock::now();
+        struct FixTimer {
+            fcd_ctx* c;
+            std::chrono::steady_clock::time_point t0;
+            size_t n;
+            ~FixTimer() {
+                if (c->profiling) {
+                    c->prof_fix_ms +=
+                        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+                    c->prof_fix_frames += (long)n;
+                }
+            }
+        } fix_timer{c, fix_t0, redo.size()};
         for (size_t g0 = 0; g0 < redo.size(); g0 += nbmax) {
             const int ng = (int)std::min<size_t>(nbmax, redo.size() - g0);
             for (int i = 0; i < ng; ++i)
@@ -982,8 +1000,12 @@ FCD_API int fcd_profile(fcd_ctx* c, int enable) {
 FCD_API int fcd_stage_times(fcd_ctx* c, double* out4, int64_t* frames) {
     FCD_TRY({
         check_ctx(c);
-        if (!out4) throw FcdError(FCD_E_INVALID, "out4 is null");
+        if (!out4) throw FcdError(FCD_E_INVALID, "out6 is null");
         for (int i = 0; i < 4; ++i) out4[i] = 0;
+        out4[4] = c->prof_fix_ms;
+        out4[5] = (double)c->prof_fix_frames;
+        c->prof_fix_ms = 0;
+        c->prof_fix_frames = 0;
         if (c->ev_used) HIPCHK(hipEventSynchronize(c->ev_pool[c->ev_used - 1]));
         for (size_t q = 0; q + 3 < c->ev_used; q += 4) {
             float ms[3];

@@ -504,10 +504,26 @@ __global__ __launch_bounds__(KCfg<H>::THREADS, ColWaves<H>::V) void k_int_cols(c
 }
 
 // ------------------------------------------------------------------ I3
+// Rows per workgroup: the staged block of the half spectrum (W/2+1 columns x
+// RPW rows) plus one exchange row per team stays under ~156 KiB of LDS; one
+// team per row pair, so W = 1024 runs 16 waves per CU from one workgroup.
+__host__ __device__ constexpr int c2r_rpw(int W) { return W <= 1024 ? 16 : (W == 2048 ? 4 : 2); }
+
 template <int W>
-__global__ __launch_bounds__(KCfg<W>::THREADS, FCD_MIN_WAVES) void k_int_c2r(const float2* __restrict__ Ht, int H, int nb, int rpw,
+struct C2RCfg {
+    static constexpr int TT = Sched<W>::TT;
+    static constexpr int E = Sched<W>::E;
+    static constexpr int RPW = c2r_rpw(W);
+    static constexpr int THREADS = (RPW / 2) * TT < 1024 ? ((RPW / 2) * TT > TT ? (RPW / 2) * TT : TT) : 1024;
+    static constexpr int TEAMS = THREADS / TT;
+    static constexpr int ROW = padded_len(W);
+    static constexpr int NLEN = W;
+};
+
+template <int W>
+__global__ __launch_bounds__(C2RCfg<W>::THREADS) void k_int_c2r(const float2* __restrict__ Ht, int H, int nb, int rpw,
                                                    float* __restrict__ hout, const float2* __restrict__ tw) {
-    using C = KCfg<W>;
+    using C = C2RCfg<W>;
     constexpr int TT = C::TT, E = C::E, TEAMS = C::TEAMS;
     extern __shared__ __attribute__((aligned(16))) float2 lds_raw[];
     float2* const lds = lds_raw + C::NLEN;  // lds_raw[0, NLEN): the twiddle table
@@ -659,20 +675,15 @@ static void launch_int_cols(const float2* Zt, int W, int nb, const IntegCoef& c,
     FCD_CHECK_LAUNCH();
 }
 
-int c2r_rows_per_block(int W) {
-    const long per_row = (long)(W / 2 + 1) * 8;
-    int rpw = 16;
-    while (rpw > 2 && per_row * (rpw + 1) > 72 * 1024) rpw /= 2;
-    return rpw;
-}
+int c2r_rows_per_block(int W) { return c2r_rpw(W); }
 
 template <int W>
 static void launch_int_c2r(const float2* Ht, int H, int nb, float* h, const float2* tw, hipStream_t s) {
-    using C = KCfg<W>;
-    const int rpw = c2r_rows_per_block(W);
+    using C = C2RCfg<W>;
+    const int rpw = C::RPW;
     const size_t lds = (size_t)C::NLEN * 8 + (size_t)C::TEAMS * C::ROW * 8 + (size_t)(W / 2 + 1) * (rpw + 1) * 8;
     set_lds(k_int_c2r<W>, lds);
-    const int grid = grid_for((long)nb * (H / rpw), 4);
+    const int grid = grid_for((long)nb * (H / rpw), 2);
     hipLaunchKernelGGL(k_int_c2r<W>, dim3(grid), dim3(C::THREADS), lds, s, Ht, H, nb, rpw, h, tw);
     FCD_CHECK_LAUNCH();
 }

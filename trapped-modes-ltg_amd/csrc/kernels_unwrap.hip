@@ -238,14 +238,29 @@ __global__ void k_mst_cand2(int nact, int H, int W, MstWork m) {
     if ((unsigned long long)__double_as_longlong(m.cand_w[v]) == m.best_w[cv]) atomicMin(m.best_e + cv, be);
 }
 
+__device__ __forceinline__ bool mst_hook_one(const float* __restrict__ w, const int* __restrict__ map_ids, int H, int W,
+                                             MstWork& m, long c);
+
+__device__ __forceinline__ void count_hook(bool hooked, int* nhooks) {
+    // one atomic per wave: a per-thread add on one word serialised ~1M times in round 1
+    const unsigned long long b = __ballot(hooked);
+    if ((threadIdx.x & 63) == 0 && b) atomicAdd(nhooks, __popcll(b));
+}
+
 __global__ void k_mst_hook(const float* __restrict__ w, const int* __restrict__ map_ids, int nact, int H, int W,
                            MstWork m) {
     const long hw = (long)H * W;
     const long c = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= nact * hw) return;
-    if (m.comp[c] != (int)c) return;
+    bool hooked = false;
+    if (c < nact * hw && m.comp[c] == (int)c) hooked = mst_hook_one(w, map_ids, H, W, m, c);
+    count_hook(hooked, m.nhooks);
+}
+
+__device__ __forceinline__ bool mst_hook_one(const float* __restrict__ w, const int* __restrict__ map_ids, int H, int W,
+                                             MstWork& m, long c) {
+    const long hw = (long)H * W;
     const int e = m.best_e[c];
-    if (e == 0x7fffffff) return;
+    if (e == 0x7fffffff) return false;
     const long base = (c / hw) * hw;
     const int nh = H * (W - 1);
     long p1, p2;
@@ -266,10 +281,10 @@ __global__ void k_mst_hook(const float* __restrict__ w, const int* __restrict__ 
         x = p2; y = p1; delta = inc;
     }
     const int d = m.comp[y];
-    if (m.best_e[d] == e && c < d) return;  // mutual pair: the smaller root stays a root
+    if (m.best_e[d] == e && c < d) return false;  // mutual pair: the smaller root stays a root
     const int poff = m.off[y] - m.off[x] - delta;  // K_c - K_d
     m.link[c] = pack_link(d, poff);
-    atomicAdd(m.nhooks, 1);
+    return true;
 }
 
 __global__ void k_mst_jump(int nact, int H, int W, MstWork m) {

@@ -190,11 +190,12 @@ class Engine:
         _check(self._lib.fcd_profile(self._h, int(bool(enable))))
 
     def stage_times(self):
-        """(ms dict {demod, unwrap, integrate, total}, frames) accumulated since the last call."""
-        out = (ctypes.c_double * 4)()
+        """(ms dict {demod, unwrap, integrate, total, fixup, fixup_frames}, frames) since the last call."""
+        out = (ctypes.c_double * 6)()
         nf = ctypes.c_int64()
         _check(self._lib.fcd_stage_times(self._h, out, ctypes.byref(nf)))
-        return dict(zip(("demod", "unwrap", "integrate", "total"), list(out))), nf.value
+        keys = ("demod", "unwrap", "integrate", "total", "fixup", "fixup_frames")
+        return dict(zip(keys, list(out))), nf.value
 
     def phases_from_spectrum(self, spectrum, unwrap=True):
         sp = np.ascontiguousarray(spectrum, dtype=np.complex64)
