@@ -1,0 +1,16 @@
+#!/bin/bash
+# One GPU-box pass: parity tests, smoke, bench, rocprofv3 kernel stats.
+# Usage (from the repo root on the box): bash tools/gpu_check.sh [tag]
+set -o pipefail
+tag=${1:-r1}
+out=gpurun_out/$tag
+mkdir -p $out
+export TMPDIR=/tmp
+timeout -k 10 900 python -m pytest tests -m gpu -x -q > $out/pytest_gpu.log 2>&1 || { echo "pytest gpu failed"; tail -40 $out/pytest_gpu.log; exit 1; }
+tail -3 $out/pytest_gpu.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1 || { echo "smoke failed"; tail -40 $out/smoke.log; exit 1; }
+tail -2 $out/smoke.log
+timeout -k 10 400 python bench.py > $out/bench.log 2>&1 || { echo "bench failed"; tail -40 $out/bench.log; exit 1; }
+tail -1 $out/bench.log
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $out/prof -o run -- python3 bench.py --no-cpu-baseline --steps 5 --warmup 2 > $out/prof.log 2>&1 || { echo "rocprof failed"; tail -40 $out/prof.log; exit 1; }
+find $out/prof -name '*kernel_stats.csv' | head -5
