@@ -39,6 +39,27 @@ def const_offset(ours, ref):
     return d - c * TWOPI, int(c)
 
 
+def band_amplitude(img, carrier_masks, step=8):
+    """|ifft2(fft2(img) * mask)| per carrier on the golden sub-grid (the demodulated
+    signal whose angle is the wrapped phase), from numpy in float64."""
+    F = np.fft.fft2(np.asarray(img, np.float64))
+    return np.stack([np.abs(np.fft.ifft2(F * m))[::step, ::step] for m in carrier_masks])
+
+
+def assert_phase_close(ours, ref, amp, tol=1e-3):
+    """Wrapped phases within `tol` rad wherever the band amplitude is >= 1 % of its
+    median.  Below that the phase is ill-conditioned: float32 FFT rounding moves it by
+    ~eps * median / |A| rad (measured on real_df frame 1: |A|/median = 2.5e-4, the
+    reference's own float32 phase is 6.8e-4 rad off the float64 one there, ours
+    4.3e-4 on the other side), so there the absolute error of the complex signal is
+    checked instead: err * |A| / median < tol * 1e-2."""
+    e = wrap_diff(ours, ref)
+    rel = amp / np.median(amp, axis=(-2, -1), keepdims=True)
+    well = rel >= 1e-2
+    assert e[well].max() < tol, e[well].max()
+    assert (e * np.minimum(rel, 1.0)).max() < tol * 1e-2
+
+
 def rel_l2(a, b):
     a = np.asarray(a)
     a = a.astype(np.complex128) if np.iscomplexobj(a) else a.astype(np.float64)
@@ -225,9 +246,10 @@ def test_real_df_frames(lib, golden):
                                                         [80e-2, 1.0003]], return_phases=True)
     assert cf == float(d["committed_cf"][0])
     from oracle import fcd_oracle as O
+    masks = [c.mask for c in O.compute_carriers(ref, float(d["square_size"]))[0]]
     for f in range(hmaps.shape[0]):
         w = np.angle(np.exp(1j * phases[f]))[:, ::8, ::8]
-        assert wrap_diff(w, d["wrapped_sub"][f]).max() < 1e-3
+        assert_phase_close(w, d["wrapped_sub"][f], band_amplitude(d["frames_u16"][f], masks))
         # These frames carry 7..1611 residues per map.  Where residues sit, the
         # Herraez tree depends on reliabilities that the float32 FFT rounding
         # moves by ~1e-6, so the k-field may branch differently from the

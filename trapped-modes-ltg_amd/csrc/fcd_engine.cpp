@@ -110,6 +110,43 @@ std::vector<float2> pass_twiddles(int n) {
     return t;
 }
 
+// Pass-major twiddles of the group FFT (gfft.hpp, GSched<B>): radix min(16, B/L)
+// passes; for each pass p >= 1, k < L_p, r = 1..R_p-1: exp(-2 pi i r k / (L_p R_p)).
+std::vector<float2> group_twiddles(int B) {
+    std::vector<float2> t;
+    int L = 1, p = 0;
+    while (L < B) {
+        const int R = std::min(16, B / L);
+        if (p > 0)
+            for (int k = 0; k < L; ++k)
+                for (int r = 1; r < R; ++r) {
+                    const double a = -2.0 * kPi * (double)r * (double)k / ((double)L * (double)R);
+                    t.push_back(make_float2((float)std::cos(a), (float)std::sin(a)));
+                }
+        L *= R;
+        ++p;
+    }
+    if (t.empty()) t.push_back(make_float2(1.f, 0.f));
+    return t;
+}
+
+// Pre-twiddles of the band-pruned inverse (kernels_band.hip): lane l of a row
+// (group g = l / G, lane t = l % G, G = B / 16) multiplies band slot
+// j = t + G q by exp(+2 pi i j g / W).
+std::vector<float2> band_pretwiddles(int W, int B) {
+    const int G = B / 16, RL = W / 16;
+    std::vector<float2> t((size_t)RL * 16);
+    for (int l = 0; l < RL; ++l) {
+        const int g = l / G, tt = l % G;
+        for (int q = 0; q < 16; ++q) {
+            const long j = tt + (long)G * q;
+            const double a = 2.0 * kPi * (double)((j * g) % W) / (double)W;
+            t[(size_t)l * 16 + q] = make_float2((float)std::cos(a), (float)std::sin(a));
+        }
+    }
+    return t;
+}
+
 struct Blob {
     int first;     // raster index of its first pixel (skimage label order)
     int peak;      // raster index of its max pixel (first in row-major on ties)
@@ -139,6 +176,8 @@ struct fcd_ctx {
     int NC = 0, NCc[2] = {0, 0}, NCA = 0;
     int fchunk = 1;                  // frames per fast-path chunk
     DevBuf Xb, Ab, Zt, Ht, fk, fres; // per-chunk intermediates; fk: k-fields for the fix-up pass
+    int band_B = 0;                  // band window of the pruned inverse (0: full-length k_demod_phase)
+    DevBuf band_pre, band_ptw, theta_b;  // its pre-twiddles, pass twiddles, reference angle of the band
     size_t fres_cap = 0;
 
     // workspace
@@ -531,6 +570,20 @@ void build_demod_tables(fcd_ctx* c, hipStream_t s) {
     upload(c->dt_outs.p, outs.data(), outs.size() * sizeof(int4), s);
     upload(c->dt_outrows.p, outrows.data(), outrows.size() * sizeof(int2), s);
     upload(c->dt_colslot.p, colslot.data(), colslot.size() * sizeof(int), s);
+    // band-pruned inverse: smallest power-of-two window >= 16 holding either carrier's band
+    int B = 16;
+    while (B < std::max(c->NCc[0], c->NCc[1])) B *= 2;
+    c->band_B = fcdk::band_supported(W, B) ? B : 0;
+    std::vector<float2> pre, ptw;
+    if (c->band_B) {
+        pre = band_pretwiddles(W, B);
+        ptw = group_twiddles(B);
+        c->band_pre.ensure(pre.size() * sizeof(float2));
+        c->band_ptw.ensure(ptw.size() * sizeof(float2));
+        upload(c->band_pre.p, pre.data(), pre.size() * sizeof(float2), s);
+        upload(c->band_ptw.p, ptw.data(), ptw.size() * sizeof(float2), s);
+        c->theta_b.ensure(2 * (size_t)c->hw() * sizeof(float));
+    }
     HIPCHK(hipStreamSynchronize(s));  // host vectors die here
     // workspace per frame: Xb + Ab + wrapped + Zt + Ht (+ k for the fix-up path)
     const long hw = c->hw();
@@ -566,8 +619,24 @@ void fast_demod(fcd_ctx* c, const float* frames, int nb, hipStream_t s) {
     const fcdk::DemodTables T = demod_tables(c);
     fcdk::demod_rows(c->W, frames, c->H, nb, T, c->Xb.as<float2>(), c->twp_row.as<float2>(), s);
     fcdk::demod_cols(c->H, c->Xb.as<float2>(), nb, T, c->Ab.as<float2>(), c->NCA, c->twp_col.as<float2>(), s);
-    fcdk::demod_phase(c->W, c->Ab.as<float2>(), c->H, nb, c->NCA, T, c->theta.as<float>(), c->wrapped.as<float>(),
-                      c->twp_row.as<float2>(), s);
+    if (c->band_B)
+        fcdk::band_phase(c->W, c->band_B, false, c->Ab.as<float2>(), c->H, nb, c->NCA, c->NCc[0], c->NCc[1],
+                         c->theta_b.as<float>(), c->wrapped.as<float>(), c->band_pre.as<float2>(),
+                         c->band_ptw.as<float2>(), s);
+    else
+        fcdk::demod_phase(c->W, c->Ab.as<float2>(), c->H, nb, c->NCA, T, c->theta.as<float>(), c->wrapped.as<float>(),
+                          c->twp_row.as<float2>(), s);
+}
+
+// Reference angle of the band-pruned inverse: the same band pipeline run on
+// the reference image, angle(y_ref) (kernels_band.hip REF mode).
+void band_reference(fcd_ctx* c, const float* dref, hipStream_t s) {
+    if (!c->band_B) return;
+    const fcdk::DemodTables T = demod_tables(c);
+    fcdk::demod_rows(c->W, dref, c->H, 1, T, c->Xb.as<float2>(), c->twp_row.as<float2>(), s);
+    fcdk::demod_cols(c->H, c->Xb.as<float2>(), 1, T, c->Ab.as<float2>(), c->NCA, c->twp_col.as<float2>(), s);
+    fcdk::band_phase(c->W, c->band_B, true, c->Ab.as<float2>(), c->H, 1, c->NCA, c->NCc[0], c->NCc[1], nullptr,
+                     c->theta_b.as<float>(), c->band_pre.as<float2>(), c->band_ptw.as<float2>(), s);
 }
 
 }  // namespace
@@ -702,6 +771,7 @@ FCD_API int fcd_set_reference(fcd_ctx* c, const float* reference, int flags, dou
         c->disk_rows.ensure(c->disk_rows_host.size() * sizeof(int));
         upload(c->disk_rows.p, c->disk_rows_host.data(), c->disk_rows_host.size() * sizeof(int), s);
         build_demod_tables(c, s);
+        band_reference(c, dref, s);
         // Carrier.ccsgn = conj(ifft2(fft2(ref) * mask))  (carriers.py:22-24); we keep its angle.
         fft2_real(c, dref, F, 1, 0.f, s);
         c->refsig.ensure(2 * hw * sizeof(float2));

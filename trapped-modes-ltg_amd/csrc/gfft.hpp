@@ -1,0 +1,164 @@
+// Group FFT for gfx950: a B-point complex FFT held by G = B/16 lanes of ONE
+// wave, 16 complex values per lane, radix-16 first pass, so B <= 256 needs at
+// most one exchange (B = 128: 16 x 8, B = 256: 16 x 16).  Several groups share
+// a wave (64/G of them) and exchange through their own padded LDS regions with
+// wave-level synchronisation only: no workgroup barrier inside a transform.
+//
+// Layout ("natural strided"): lane t of the group holds element t + G*q in
+// slot q, both on input and on output (Stockham autosort), which is what
+// coalesced loads/stores produce when consecutive groups/lanes cover
+// consecutive addresses.
+//
+// Per-lane twiddles of the passes after the first depend only on the lane,
+// so a kernel that runs many transforms loads them once into registers.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "fft_lds.hpp"
+#include "regfft.hpp"
+
+namespace fcdk {
+
+template <int B>
+struct GSched {
+    static_assert(B >= 16 && (B & (B - 1)) == 0, "group FFT length must be a power of two >= 16");
+    static constexpr int E = 16;
+    static constexpr int G = B / E;  // lanes per transform
+    static constexpr int radix(int p) {
+        int L = 1;
+        for (int i = 0; i < p; ++i) L *= (B / L >= E ? E : B / L);
+        return B / L >= E ? E : B / L;
+    }
+    static constexpr int ell(int p) {
+        int L = 1;
+        for (int i = 0; i < p; ++i) L *= radix(i);
+        return L;
+    }
+    static constexpr int npass() {
+        int p = 0, L = 1;
+        while (L < B) {
+            L *= radix(p);
+            ++p;
+        }
+        return p;
+    }
+    static constexpr int NP = npass();
+    // offset of pass p's twiddles in the pass-major table: sum over passes 1..p-1 of ell*(radix-1)
+    static constexpr int passoff(int p) {
+        int o = 0;
+        for (int i = 1; i < p; ++i) o += ell(i) * (radix(i) - 1);
+        return o;
+    }
+    static constexpr int TABLE = passoff(NP);  // table entries (complex)
+    // per-lane register twiddles: sum over passes >= 1 of (E/radix)*(radix-1)
+    static constexpr int nreg() {
+        int o = 0;
+        for (int i = 1; i < NP; ++i) o += (E / radix(i)) * (radix(i) - 1);
+        return o;
+    }
+    static constexpr int NREG = nreg();
+    static constexpr int REGOFF(int p) {
+        int o = 0;
+        for (int i = 1; i < p; ++i) o += (E / radix(i)) * (radix(i) - 1);
+        return o;
+    }
+    // padded LDS region of one transform; pad() keeps the radix-16 write
+    // (16t + r) and the strided read (t + G q) conflict-free
+    static constexpr int REGION = padded_len(B) > 16 ? padded_len(B) : 16;
+};
+
+template <int B>
+struct GroupFFT {
+    using S = GSched<B>;
+    static constexpr int E = S::E, G = S::G, NP = S::NP;
+    float2 tw[S::NREG > 0 ? S::NREG : 1];
+
+    // table: pass-major forward twiddles exp(-2 pi i r k / (L_p R_p)), k < L_p, r = 1..R_p-1
+    __device__ __forceinline__ void load(const float2* __restrict__ table, int t) {
+        load_pass<1>(table, t);
+    }
+    template <int P>
+    __device__ __forceinline__ void load_pass(const float2* __restrict__ table, int t) {
+        if constexpr (P < NP) {
+            constexpr int R = S::radix(P), L = S::ell(P), BPT = E / R;
+#pragma unroll
+            for (int b = 0; b < BPT; ++b) {
+                const int k = (t + b * G) & (L - 1);
+#pragma unroll
+                for (int r = 1; r < R; ++r)
+                    tw[S::REGOFF(P) + b * (R - 1) + r - 1] = table[S::passoff(P) + k * (R - 1) + r - 1];
+            }
+            load_pass<P + 1>(table, t);
+        }
+    }
+
+    // x: natural strided in and out; s: this transform's LDS region.
+    template <bool INV>
+    __device__ __forceinline__ void run(float2 (&x)[E], float2* s, int t) const {
+        pass<0, INV>(x, s, t);
+    }
+
+    template <int P, bool INV>
+    __device__ __forceinline__ void pass(float2 (&x)[E], float2* s, int t) const {
+        constexpr int R = S::radix(P), L = S::ell(P), BPT = E / R;
+        float2 a[BPT][R];
+#pragma unroll
+        for (int b = 0; b < BPT; ++b) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) a[b][r] = x[b + BPT * r];
+            if constexpr (P > 0) {
+#pragma unroll
+                for (int r = 1; r < R; ++r) {
+                    const float2 w = tw[S::REGOFF(P) + b * (R - 1) + r - 1];
+                    a[b][r] = INV ? cmul(a[b][r], make_float2(w.x, -w.y)) : cmul(a[b][r], w);
+                }
+            }
+            dft_reg<R, INV>(a[b]);
+        }
+        if constexpr (P + 1 == NP) {
+#pragma unroll
+            for (int b = 0; b < BPT; ++b)
+#pragma unroll
+                for (int r = 0; r < R; ++r) x[b + BPT * r] = a[b][r];
+        } else {
+            wave_sync();  // earlier readers of s (previous transform) are done
+#pragma unroll
+            for (int b = 0; b < BPT; ++b) {
+                const int j = t + b * G;
+                const int k = j & (L - 1);
+                const int base = (j - k) * R + k;
+#pragma unroll
+                for (int r = 0; r < R; ++r) s[pad(base + r * L)] = a[b][r];
+            }
+            wave_sync();
+#pragma unroll
+            for (int q = 0; q < E; ++q) x[q] = s[pad(t + G * q)];
+            pass<P + 1, INV>(x, s, t);
+        }
+    }
+};
+
+// atan2(y, x) in f32: |error| <= ~2.5e-7 rad (degree-8 odd minimax-fit
+// polynomial on [0, 1] after the octant reduction, v_rcp_f32 division);
+// atan2(0, 0) = 0, like atan2f.  About 20 VALU operations.
+__device__ __forceinline__ float fast_atan2(float y, float x) {
+    const float ax = fabsf(x), ay = fabsf(y);
+    const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+    const float r = mx > 0.f ? mn * __builtin_amdgcn_rcpf(mx) : 0.f;
+    const float s = r * r;
+    float p = 0.0024567286018282175f;
+    p = fmaf(p, s, -0.014401371590793133f);
+    p = fmaf(p, s, 0.03978124260902405f);
+    p = fmaf(p, s, -0.07234858721494675f);
+    p = fmaf(p, s, 0.10498946160078049f);
+    p = fmaf(p, s, -0.14161229133605957f);
+    p = fmaf(p, s, 0.19985906779766083f);
+    p = fmaf(p, s, -0.33332598209381104f);
+    p = fmaf(p, s, 0.9999998807907104f);
+    float a = r * p;
+    a = ay > ax ? 1.57079632679489662f - a : a;
+    a = x < 0.f ? 3.14159265358979324f - a : a;
+    return copysignf(a, y);
+}
+
+}  // namespace fcdk

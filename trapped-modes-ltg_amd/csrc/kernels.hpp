@@ -60,6 +60,11 @@ void int_cols(int H, const float2* Zt, int W, int nb, const IntegCoef& c, float2
               hipStream_t s);
 void int_c2r(int W, const float2* Ht, int H, int nb, float* h, const float2* tw, hipStream_t s);
 int c2r_rows_per_block(int W);
+// band-pruned inverse row transform + phase (kernels_band.hip): B-point window
+// of the carrier band, W/B pre-twiddled group transforms per row.
+bool band_supported(int W, int B);
+void band_phase(int W, int B, bool ref, const float2* Ab, int H, int nb, int NCA, int ncc0, int ncc1,
+                const float* theta, float* out, const float2* pre, const float2* ptw, hipStream_t s);
 // column-0 prefix of the residue-free unwrap (kernels_unwrap.hip)
 void unwrap_colk(const float* w, int nmaps, int H, int W, int* colk, hipStream_t s);
 

@@ -1,0 +1,206 @@
+// K3b band_phase: band-pruned inverse row transform + phase extraction
+// (the second half of ifft2(D * mask) and -angle(. * ccsgn), fcd.py:118).
+//
+// After the inverse column FFT (k_demod_cols) every row of carrier c holds
+// non-zeros only in its disk's columns, a contiguous (mod W) run of
+// NCc <= B slots starting at unshifted column lo_c.  With n = g + L*n2
+// (g < L = W/B, n2 < B):
+//
+//   x[n] = sum_j A[j] e^{2 pi i (lo_c + j) n / W}
+//        = e^{2 pi i lo_c n / W} * IDFT_B( A[j] e^{2 pi i j g / W} )[n2]
+//
+// so one W-point inverse becomes L pre-twiddled B-point inverses (transform
+// decomposition), 16 complex per lane, one wave per 1024-point row
+// (L = 8 groups of 8 lanes at B = 128), no workgroup barrier inside a
+// transform.  The carrier ramp e^{2 pi i lo_c n / W} cancels in the phase:
+// the reference angle theta_b is produced by this same kernel from the
+// reference's band (REF = true), so
+//
+//   wrapped = wrap(theta_b - angle(y)) = -angle(x_frame * conj(x_ref))
+//
+// exactly as fcd.py:118 up to float rounding.
+#include <hip/hip_runtime.h>
+
+#include <stdexcept>
+#include <string>
+
+#include "gfft.hpp"
+#include "kernels.hpp"
+
+namespace fcdk {
+
+namespace {
+
+#ifndef FCD_BAND_WAVES
+#define FCD_BAND_WAVES 2  // min waves per SIMD (launch-bounds): 2 keeps every twiddle in VGPRs
+#endif
+
+constexpr int BTILE = 16;   // rows per Ab tile (k_demod_cols layout)
+constexpr int SROW = 17;    // staged tile row pitch (complex): conflict-free strided reads
+
+template <int W, int B>
+struct BPCfg {
+    static constexpr int G = B / 16;        // lanes per group transform
+    static constexpr int L = W / B;         // groups per row
+    static constexpr int RL = W / 16;       // lanes per row
+    static constexpr int THREADS = (16 * RL) < 256 ? 16 * RL : 256;
+    static constexpr int RP = THREADS / RL; // rows in flight per workgroup
+    static constexpr int REGION = GSched<B>::REGION;
+    static constexpr bool XCH = GSched<B>::NP > 1;
+    static constexpr size_t XOFF = (size_t)B * SROW + (size_t)RL * 16;  // exchange regions after stage + pre-twiddles
+    static constexpr size_t LDS = XOFF * 8 + (XCH ? (size_t)RP * L * REGION * 8 : 0);
+};
+
+}  // namespace
+
+template <int W, int B, bool REF>
+__global__ __launch_bounds__((BPCfg<W, B>::THREADS), FCD_BAND_WAVES) void k_band_phase(
+    const float2* __restrict__ Ab, int H, int nb, int NCA, int ncc0, int ncc1, const float* __restrict__ theta,
+    float* __restrict__ out, const float2* __restrict__ pre, const float2* __restrict__ ptw) {
+    using C = BPCfg<W, B>;
+    constexpr int G = C::G, L = C::L, RL = C::RL, RP = C::RP, E = 16;
+    extern __shared__ __attribute__((aligned(16))) float2 lds_b[];
+    float2* const stage = lds_b;  // [B][SROW]
+    const int team = threadIdx.x / RL, l = threadIdx.x % RL, g = l / G, t = l % G;
+    float2* const ptl = lds_b + (size_t)B * SROW;  // pre-twiddles [q][RL]
+    float2* const s = lds_b + C::XOFF + (size_t)(team * L + g) * C::REGION;
+    GroupFFT<B> fft;
+    fft.load(ptw, t);
+    for (int i = threadIdx.x; i < RL * E; i += C::THREADS) ptl[(i % E) * RL + i / E] = pre[i];
+    const int rbs = H / BTILE;
+    const int items = nb * 2 * rbs;
+    // Tile staging is software-pipelined: the next item's tile is loaded into
+    // registers (SPT values per thread, all loads in flight at once) while
+    // the current item's rows are transformed.
+    constexpr int SPT_ALL = (B * BTILE + C::THREADS - 1) / C::THREADS;
+    constexpr int SPT = SPT_ALL < 8 ? SPT_ALL : 8;  // prefetched per thread (VGPR budget); the rest loads at staging
+    const int tile_n = NCA * BTILE;
+    float2 pf[SPT];
+    auto tile_src = [&](int blk) {
+        const int f = blk / (2 * rbs), c = (blk / rbs) % 2, rb = blk % rbs;
+        return Ab + (((long)f * 2 + c) * rbs + rb) * (long)tile_n;
+    };
+    auto fetch = [&](int blk) {
+        const float2* src = tile_src(blk);
+#pragma unroll
+        for (int i = 0; i < SPT; ++i) pf[i] = src[min((int)threadIdx.x + i * C::THREADS, tile_n - 1)];
+    };
+    if ((int)blockIdx.x < items) fetch(blockIdx.x);
+    for (int blk = blockIdx.x; blk < items; blk += gridDim.x) {
+        const int f = blk / (2 * rbs), c = (blk / rbs) % 2, rb = blk % rbs;
+        const int ncc = c ? ncc1 : ncc0;
+        // slots [ncc, B) are staged as zeros: the transform input needs no select
+        if constexpr (SPT_ALL > SPT) {
+            const float2* src = tile_src(blk);
+            for (int idx = threadIdx.x + SPT * C::THREADS; idx < B * BTILE; idx += C::THREADS)
+                stage[(idx >> 4) * SROW + (idx & 15)] = idx < ncc * BTILE ? src[idx] : make_float2(0.f, 0.f);
+        }
+#pragma unroll
+        for (int i = 0; i < SPT; ++i) {
+            const int idx = threadIdx.x + i * C::THREADS;
+            if (idx < B * BTILE)
+                stage[(idx >> 4) * SROW + (idx & 15)] = idx < ncc * BTILE ? pf[i] : make_float2(0.f, 0.f);
+        }
+        __syncthreads();
+        if (blk + (int)gridDim.x < items) fetch(blk + gridDim.x);
+        for (int rl = team; rl < BTILE; rl += RP) {
+            const int r = rb * BTILE + rl;
+            const long row = ((long)f * 2 + c) * H + r;
+            float th[E];
+            if constexpr (!REF) {  // issued before the transform: its latency hides behind the FFT
+                const float* tr = theta + ((long)c * H + r) * W;
+#pragma unroll
+                for (int q = 0; q < E; ++q) th[q] = tr[g + L * t + RL * q];
+            }
+            float2 x[E];
+#pragma unroll
+            for (int q = 0; q < E; ++q) x[q] = cmul(stage[(t + G * q) * SROW + rl], ptl[q * RL + l]);
+            fft.template run<true>(x, s, t);
+            float* o = out + row * W;
+#pragma unroll
+            for (int q = 0; q < E; ++q) {
+                if (q % 4 == 0) __builtin_amdgcn_sched_barrier(0);  // bound the atan2 chains in flight
+                const int n = g + L * t + RL * q;
+                const float a = fast_atan2(x[q].y, x[q].x);
+                if constexpr (REF) {
+                    o[n] = a;
+                } else {
+                    // wrap to [-pi, pi]: d - 2 pi rint(d / 2 pi), |d| < 2 pi
+                    const float d = th[q] - a;
+                    o[n] = fmaf(-6.28318530717959f, rintf(d * 0.159154943091895f), d);
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------ launchers
+static int band_grid(long items, int per_cu) {
+    static int ncu = 0;
+    if (!ncu) {
+        int dev = 0;
+        hipDeviceProp_t p;
+        if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&p, dev) == hipSuccess) ncu = p.multiProcessorCount;
+        if (!ncu) ncu = 256;
+    }
+    const long cap = (long)ncu * per_cu;
+    return (int)(items < cap ? (items > 0 ? items : 1) : cap);
+}
+
+template <int W, int B>
+static void launch_band(bool ref, const float2* Ab, int H, int nb, int NCA, int ncc0, int ncc1, const float* theta,
+                        float* out, const float2* pre, const float2* ptw, hipStream_t s) {
+    using C = BPCfg<W, B>;
+    const size_t lds = C::LDS;
+    const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(8, (160 * 1024) / lds));
+    const int grid = band_grid((long)nb * 2 * (H / BTILE), per_cu);
+    if (ref) {
+        if (lds > 64 * 1024)
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_band_phase<W, B, true>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL((k_band_phase<W, B, true>), dim3(grid), dim3(C::THREADS), lds, s, Ab, H, nb, NCA, ncc0,
+                           ncc1, theta, out, pre, ptw);
+    } else {
+        if (lds > 64 * 1024)
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_band_phase<W, B, false>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL((k_band_phase<W, B, false>), dim3(grid), dim3(C::THREADS), lds, s, Ab, H, nb, NCA, ncc0,
+                           ncc1, theta, out, pre, ptw);
+    }
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) throw std::runtime_error(std::string("band_phase launch: ") + hipGetErrorString(e));
+}
+
+template <int W>
+static void band_dispatch_b(int B, bool ref, const float2* Ab, int H, int nb, int NCA, int ncc0, int ncc1,
+                            const float* theta, float* out, const float2* pre, const float2* ptw, hipStream_t s) {
+    switch (B) {
+        case 16: if constexpr (W >= 32) { launch_band<W, 16>(ref, Ab, H, nb, NCA, ncc0, ncc1, theta, out, pre, ptw, s); return; } break;
+        case 32: if constexpr (W >= 64) { launch_band<W, 32>(ref, Ab, H, nb, NCA, ncc0, ncc1, theta, out, pre, ptw, s); return; } break;
+        case 64: if constexpr (W >= 128) { launch_band<W, 64>(ref, Ab, H, nb, NCA, ncc0, ncc1, theta, out, pre, ptw, s); return; } break;
+        case 128: if constexpr (W >= 256) { launch_band<W, 128>(ref, Ab, H, nb, NCA, ncc0, ncc1, theta, out, pre, ptw, s); return; } break;
+        case 256: if constexpr (W >= 512) { launch_band<W, 256>(ref, Ab, H, nb, NCA, ncc0, ncc1, theta, out, pre, ptw, s); return; } break;
+        default: break;
+    }
+    throw std::runtime_error("band_phase: unsupported band window " + std::to_string(B) + " for row length " +
+                             std::to_string(W));
+}
+
+bool band_supported(int W, int B) { return B >= 16 && B <= 256 && 2 * B <= W && (B & (B - 1)) == 0; }
+
+void band_phase(int W, int B, bool ref, const float2* Ab, int H, int nb, int NCA, int ncc0, int ncc1,
+                const float* theta, float* out, const float2* pre, const float2* ptw, hipStream_t s) {
+    switch (W) {
+        case 64: band_dispatch_b<64>(B, ref, Ab, H, nb, NCA, ncc0, ncc1, theta, out, pre, ptw, s); break;
+        case 128: band_dispatch_b<128>(B, ref, Ab, H, nb, NCA, ncc0, ncc1, theta, out, pre, ptw, s); break;
+        case 256: band_dispatch_b<256>(B, ref, Ab, H, nb, NCA, ncc0, ncc1, theta, out, pre, ptw, s); break;
+        case 512: band_dispatch_b<512>(B, ref, Ab, H, nb, NCA, ncc0, ncc1, theta, out, pre, ptw, s); break;
+        case 1024: band_dispatch_b<1024>(B, ref, Ab, H, nb, NCA, ncc0, ncc1, theta, out, pre, ptw, s); break;
+        case 2048: band_dispatch_b<2048>(B, ref, Ab, H, nb, NCA, ncc0, ncc1, theta, out, pre, ptw, s); break;
+        case 4096: band_dispatch_b<4096>(B, ref, Ab, H, nb, NCA, ncc0, ncc1, theta, out, pre, ptw, s); break;
+        default: throw std::runtime_error("band_phase: unsupported row length " + std::to_string(W));
+    }
+}
+
+}  // namespace fcdk

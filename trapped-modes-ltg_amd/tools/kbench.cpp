@@ -125,6 +125,19 @@ int main(int argc, char** argv) {
     timeit("demod_phase", 16.0 * H * NCA + 8 * f, [&] {
         fcdk::demod_phase(W, Ab, H, nb, NCA, T, theta, wrapped, tw, s);
     });
+    {
+        int Bw = 16;
+        while (Bw < NCc) Bw *= 2;
+        std::vector<float2> ones(N, make_float2(1.f, 0.f));
+        float2* pre = dalloc<float2>(N);
+        float2* ptw = dalloc<float2>(N);
+        CK(hipMemcpy(pre, ones.data(), N * 8, hipMemcpyHostToDevice));
+        CK(hipMemcpy(ptw, ones.data(), N * 8, hipMemcpyHostToDevice));
+        if (fcdk::band_supported(W, Bw))
+            timeit("band_phase", 16.0 * H * NCA + 8 * f, [&] {
+                fcdk::band_phase(W, Bw, false, Ab, H, nb, NCA, NCc, NCc, theta, wrapped, pre, ptw, s);
+            });
+    }
     timeit("colk", 8.0 * H, [&] { fcdk::unwrap_colk(wrapped, 2 * nb, H, W, colk, s); });
     timeit("int_rows k0", 2 * f + 2 * f, [&] {
         fcdk::int_rows(W, 0, wrapped, colk, nullptr, nullptr, nullptr, H, nb, Zt, tw, s);
