@@ -297,3 +297,50 @@ def test_full_size_1024_vs_oracle(lib):
         if ours == [np.asarray(c.pixels).tolist() for c in ex["carriers"]]:
             d, _ = const_offset(ph[f], po)
             assert np.abs(d).max() < 2e-4
+
+
+@pytest.fixture
+def fused(monkeypatch):
+    """Engines created inside the test take the fused height-only path."""
+    monkeypatch.setenv("FCD_FUSED", "1")
+    from pyfcd import _lib
+    _lib._engines.clear()
+    yield
+    _lib._engines.clear()
+
+
+def test_fused_height_path_vs_oracle(lib, fused):
+    """Height-only batches (analyze.folder's use of compute_height_map) take the fused
+    kernel (kernels_phase_rows.hip: band transforms + phase + unwrap + row FFT in one
+    pass, column-0 offsets applied in the spectra's DC bins): same heights as the
+    oracle and as the unfused path, with and without unwrapping."""
+    from oracle import fcd_oracle as O
+    from bench_data import make_frames_numpy
+    from pyfcd.fcd import fcd
+    ref, frames = make_frames_numpy(1024, 3, seed=5, rotate_deg=5.0)
+    for unwrap in (True, False):
+        hf, cf = fcd.compute_height_maps(ref, frames, 0.001, height=1.0, unwrap=unwrap)
+        hu, _, _ = fcd.compute_height_maps(ref, frames, 0.001, height=1.0, unwrap=unwrap, return_phases=True)
+        for f in range(frames.shape[0]):
+            ho, _, cfo, _ = O.compute_height_map(ref, frames[f], 0.001, height=1.0, unwrap_phases=unwrap)
+            assert cf == cfo
+            assert rel_l2(hf[f], ho) < 1e-5, (unwrap, f)
+            assert rel_l2(hf[f], hu[f]) < 1e-6, (unwrap, f)
+
+
+def test_fused_census_sends_residue_frames_to_exact_pass(lib, golden, fused):
+    """real_df frames carry 7..1611 residues per map: the fused kernel's vertical
+    census must flag every one of them, so their heights come from the exact MST pass
+    and equal the unfused path's bit for bit."""
+    d = golden("real_df")
+    ref = d["ref_u16"].astype(np.float32)
+    frames = d["frames_u16"].astype(np.float32)
+    eng = lib.Engine(ref.shape)
+    eng.set_reference(ref, float(d["square_size"]))
+    eng.profile(True)
+    hf, _, _ = eng.process(frames, 1.0, unwrap=True, want_phases=False)
+    st, _ = eng.stage_times()
+    eng.profile(False)
+    assert int(st["fixup_frames"]) == frames.shape[0]
+    hu, _, _ = eng.process(frames, 1.0, unwrap=True, want_phases=True)
+    assert np.array_equal(hf, hu)

@@ -1,5 +1,7 @@
 set -o pipefail
-timeout -k 10 60 trapped-modes-ltg_amd/tools/kbench 1024 8 20 || exit 1
+timeout -k 10 60 trapped-modes-ltg_amd/tools/kbench 1024 32 5 || exit 1
 timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1; rc=$?; tail -3 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || { tail -60 gpurun_out/pytest_gpu.log; exit 1; }
 timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/bench.log 2>&1 || { tail -20 gpurun_out/bench.log; exit 1; }
 tail -1 gpurun_out/bench.log
+FCD_UNFUSED=1 timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/bench_unfused.log 2>&1 || { tail -20 gpurun_out/bench_unfused.log; exit 1; }
+tail -1 gpurun_out/bench_unfused.log

@@ -68,7 +68,17 @@ def main():
                   f"ACTIVE_LDS/WAVE_CYCLES {m.get('SQ_ACTIVE_INST_LDS', 0) / max(m['SQ_WAVE_CYCLES'], 1):.3f}")
         if "SQ_LDS_IDX_ACTIVE" in m:
             print(f"   LDS bank conflict / idx active {m['SQ_LDS_BANK_CONFLICT'] / max(m['SQ_LDS_IDX_ACTIVE'], 1):.3f}, "
-                  f"WAIT_ANY/WAVE_CYCLES n/a in this pass")
+                  f"unaligned stall / idx active {m.get('SQ_LDS_UNALIGNED_STALL', 0) / max(m['SQ_LDS_IDX_ACTIVE'], 1):.3f}")
+        if "SQ_WAVE_CYCLES" in m and "SQ_WAIT_ANY" in m:
+            wc = max(m["SQ_WAVE_CYCLES"], 1)
+            print(f"   wave time: waitcnt/barrier {m['SQ_WAIT_ANY'] / wc:.2f}, issue-stall {m.get('SQ_WAIT_INST_ANY', 0) / wc:.2f}, "
+                  f"active {m.get('SQ_ACTIVE_INST_ANY', 0) / wc:.2f}; mean resident waves/CU "
+                  f"{m.get('SQ_LEVEL_WAVES', 0) / max(m.get('SQ_BUSY_CYCLES', 1), 1) / 256 * 4 if m.get('SQ_LEVEL_WAVES') else 0:.1f}")
+        if "SQ_THREAD_CYCLES_VALU" in m and "SQ_ACTIVE_INST_VALU" in m:
+            print(f"   VALU lane utilisation {m['SQ_THREAD_CYCLES_VALU'] / max(64 * m['SQ_ACTIVE_INST_VALU'], 1):.2f}")
+        if "_dur" in m and "SQ_ACTIVE_INST_VALU" in m:
+            # ACTIVE_INST_VALU counts quad-cycles summed over waves; 1024 SIMDs
+            print(f"   VALU busy per SIMD: {m['SQ_ACTIVE_INST_VALU'] * 4 / 1024 / (m['_dur'] * 1e-6 * 2.4e9):.2f} (at 2.4 GHz)")
 
 
 if __name__ == "__main__":

@@ -10,6 +10,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <numeric>
@@ -147,6 +148,11 @@ std::vector<float2> band_pretwiddles(int W, int B) {
     return t;
 }
 
+int fcd_env_int(const char* name, int dflt) {
+    const char* v = std::getenv(name);
+    return (v && *v) ? std::atoi(v) : dflt;
+}
+
 struct Blob {
     int first;     // raster index of its first pixel (skimage label order)
     int peak;      // raster index of its max pixel (first in row-major on ties)
@@ -178,6 +184,9 @@ struct fcd_ctx {
     DevBuf Xb, Ab, Zt, Ht, fk, fres; // per-chunk intermediates; fk: k-fields for the fix-up pass
     int band_B = 0;                  // band window of the pruned inverse (0: full-length k_demod_phase)
     DevBuf band_pre, band_ptw, theta_b;  // its pre-twiddles, pass twiddles, reference angle of the band
+    bool fused_ok = false;           // k_phase_rows applies (height-only calls)
+    bool force_unfused = true;       // FCD_FUSED=1 enables the fused path (A/B measurement until it wins)
+    DevBuf ztw, col0;                // its 1024-point group-FFT twiddles; column-0 wrapped values [f][2][H]
     size_t fres_cap = 0;
 
     // workspace
@@ -584,11 +593,21 @@ void build_demod_tables(fcd_ctx* c, hipStream_t s) {
         upload(c->band_ptw.p, ptw.data(), ptw.size() * sizeof(float2), s);
         c->theta_b.ensure(2 * (size_t)c->hw() * sizeof(float));
     }
+    c->fused_ok = c->band_B && fcdk::phase_rows_supported(W, c->band_B, H);
+    std::vector<float2> ztw;
+    if (c->fused_ok) {
+        ztw = group_twiddles(W);
+        c->ztw.ensure(ztw.size() * sizeof(float2));
+        upload(c->ztw.p, ztw.data(), ztw.size() * sizeof(float2), s);
+    }
     HIPCHK(hipStreamSynchronize(s));  // host vectors die here
     // workspace per frame: Xb + Ab + wrapped + Zt + Ht (+ k for the fix-up path)
     const long hw = c->hw();
     const long per_frame = 8L * H * c->NC + 16L * H * c->NCA + 8L * hw + 8L * hw + 8L * H * (W / 2 + 1);
-    c->fchunk = (int)std::max(1L, std::min(32L, (192L << 20) / per_frame));
+    // frames per launch: 32 keeps every kernel's grid several waves deep (measured
+    // 25.5 -> 21.1 us/frame from 8 to 32 frames at 1024^2); ~0.7 GB of workspace
+    const long budget = (long)fcd_env_int("FCD_CHUNK_MB", 768) << 20;
+    c->fchunk = (int)std::max(1L, std::min((long)fcd_env_int("FCD_CHUNK_MAX", 32), budget / per_frame));
     const size_t nb = (size_t)c->fchunk;
     c->Xb.ensure(nb * H * c->NC * sizeof(float2));
     c->Ab.ensure(nb * 2 * H * c->NCA * sizeof(float2));
@@ -597,6 +616,7 @@ void build_demod_tables(fcd_ctx* c, hipStream_t s) {
     c->wrapped.ensure(std::max(nb, (size_t)c->chunk) * 2 * hw * sizeof(float));
     c->colk.ensure(std::max(nb, (size_t)c->chunk) * 2 * H * sizeof(int));
     c->fk.ensure(nb * 2 * hw * sizeof(int32_t));
+    c->col0.ensure(nb * 2 * (size_t)H * sizeof(float));
     c->rescnt.ensure(std::max(nb, (size_t)c->chunk) * 2 * sizeof(int));
     c->mst_cap = 0;  // re-size the MST workspace for the new chunk on next use
 }
@@ -676,6 +696,7 @@ FCD_API int fcd_create(int device, int rows, int cols, fcd_ctx** out) {
         HIPCHK(hipSetDevice(device));
         std::unique_ptr<fcd_ctx> c(new fcd_ctx());
         c->device = device;
+        c->force_unfused = fcd_env_int("FCD_FUSED", 0) == 0;
         c->H = rows;
         c->W = cols;
         HIPCHK(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking));
@@ -845,6 +866,7 @@ FCD_API int fcd_process(fcd_ctx* c, const float* frames, int n_frames, int flags
             HIPCHK(hipMemsetAsync(res, 0, (size_t)n_frames * 2 * sizeof(int), s));
         }
         // ---- pass 1: every frame through the band-pruned pipeline with the residue-free unwrap
+        const bool fused = c->fused_ok && !wrapped_out && !k_out && !c->force_unfused;
         for (int f0 = 0; f0 < n_frames; f0 += nbmax) {
             const int nb = std::min(nbmax, n_frames - f0);
             const float* fr = frames + (size_t)f0 * hw;
@@ -852,18 +874,38 @@ FCD_API int fcd_process(fcd_ctx* c, const float* frames, int n_frames, int flags
                 upload(c->frames_in.p, fr, (size_t)nb * hw * sizeof(float), s);
                 fr = c->frames_in.as<float>();
             }
+            float* hdst = (dev && height_out) ? height_out + (size_t)f0 * hw : c->out_h.as<float>();
+            int32_t* kdst = k_out && unwrap ? (dev ? k_out + (size_t)f0 * 2 * hw : c->fk.as<int32_t>()) : nullptr;
+            if (fused) {
+                // height only: band transforms, phase, unwrap and the z-row FFT in one
+                // pass (kernels_phase_rows.hip); colk lands in the spectra's DC bins
+                const fcdk::DemodTables T = demod_tables(c);
+                if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
+                fcdk::demod_rows(c->W, fr, c->H, nb, T, c->Xb.as<float2>(), c->twp_row.as<float2>(), s);
+                fcdk::demod_cols(c->H, c->Xb.as<float2>(), nb, T, c->Ab.as<float2>(), c->NCA, c->twp_col.as<float2>(),
+                                 s);
+                if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
+                fcdk::phase_rows(unwrap != 0, c->Ab.as<float2>(), c->H, nb, c->NCA, c->NCc[0], c->NCc[1],
+                                 c->theta_b.as<float>(), c->band_pre.as<float2>(), c->band_ptw.as<float2>(),
+                                 c->ztw.as<float2>(), c->col0.as<float>(), res ? res + (size_t)f0 * 2 : nullptr,
+                                 c->Zt.as<float2>(), s);
+                if (unwrap) fcdk::unwrap_colk_compact(c->col0.as<float>(), 2 * nb, c->H, c->colk.as<int>(), s);
+                if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
+                fcdk::int_cols(c->H, c->Zt.as<float2>(), c->W, nb, coef, c->Ht.as<float2>(), c->twp_col.as<float2>(), s,
+                               unwrap ? c->colk.as<int>() : nullptr);
+                fcdk::int_c2r(c->W, c->Ht.as<float2>(), c->H, nb, hdst, c->twp_row.as<float2>(), s);
+            } else {
             if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
             fast_demod(c, fr, nb, s);
             if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
             if (unwrap) fcdk::unwrap_colk(c->wrapped.as<float>(), 2 * nb, c->H, c->W, c->colk.as<int>(), s);
             if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
-            float* hdst = (dev && height_out) ? height_out + (size_t)f0 * hw : c->out_h.as<float>();
-            int32_t* kdst = k_out && unwrap ? (dev ? k_out + (size_t)f0 * 2 * hw : c->fk.as<int32_t>()) : nullptr;
             fcdk::int_rows(c->W, unwrap ? 1 : 0, c->wrapped.as<float>(), c->colk.as<int>(), nullptr, kdst,
                            res ? res + (size_t)f0 * 2 : nullptr, c->H, nb, c->Zt.as<float2>(),
                            c->twp_row.as<float2>(), s);
             fcdk::int_cols(c->H, c->Zt.as<float2>(), c->W, nb, coef, c->Ht.as<float2>(), c->twp_col.as<float2>(), s);
             fcdk::int_c2r(c->W, c->Ht.as<float2>(), c->H, nb, hdst, c->twp_row.as<float2>(), s);
+            }
             if (c->profiling) {
                 HIPCHK(hipEventRecord(c->next_event(), s));
                 c->prof_frames += nb;

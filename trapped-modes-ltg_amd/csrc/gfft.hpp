@@ -138,6 +138,62 @@ struct GroupFFT {
     }
 };
 
+// The same transform with the pass twiddles read from a table (typically in
+// LDS: GSched<B>::TABLE entries, pass-major as GroupFFT::load expects) instead
+// of per-lane registers: for long transforms whose register twiddles would
+// cost too many VGPRs (B = 1024: 27 complex per lane).
+template <int B>
+struct GroupFFTTab {
+    using S = GSched<B>;
+    static constexpr int E = S::E, G = S::G, NP = S::NP;
+
+    template <bool INV>
+    __device__ __forceinline__ static void run(float2 (&x)[E], float2* s, int t, const float2* tab) {
+        pass<0, INV>(x, s, t, tab);
+    }
+
+    template <int P, bool INV>
+    __device__ __forceinline__ static void pass(float2 (&x)[E], float2* s, int t, const float2* tab) {
+        constexpr int R = S::radix(P), L = S::ell(P), BPT = E / R;
+        float2 a[BPT][R];
+#pragma unroll
+        for (int b = 0; b < BPT; ++b) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) a[b][r] = x[b + BPT * r];
+            if constexpr (P > 0) {
+                const int k = (t + b * G) & (L - 1);
+                const float2* tk = tab + S::passoff(P) + k * (R - 1) - 1;
+#pragma unroll
+                for (int r = 1; r < R; ++r) {
+                    const float2 w = tk[r];
+                    a[b][r] = INV ? cmul(a[b][r], make_float2(w.x, -w.y)) : cmul(a[b][r], w);
+                }
+            }
+            dft_reg<R, INV>(a[b]);
+        }
+        if constexpr (P + 1 == NP) {
+#pragma unroll
+            for (int b = 0; b < BPT; ++b)
+#pragma unroll
+                for (int r = 0; r < R; ++r) x[b + BPT * r] = a[b][r];
+        } else {
+            wave_sync();
+#pragma unroll
+            for (int b = 0; b < BPT; ++b) {
+                const int j = t + b * G;
+                const int k = j & (L - 1);
+                const int base = (j - k) * R + k;
+#pragma unroll
+                for (int r = 0; r < R; ++r) s[pad(base + r * L)] = a[b][r];
+            }
+            wave_sync();
+#pragma unroll
+            for (int q = 0; q < E; ++q) x[q] = s[pad(t + G * q)];
+            pass<P + 1, INV>(x, s, t, tab);
+        }
+    }
+};
+
 // atan2(y, x) in f32: |error| <= ~2.5e-7 rad (degree-8 odd minimax-fit
 // polynomial on [0, 1] after the octant reduction, v_rcp_f32 division);
 // atan2(0, 0) = 0, like atan2f.  About 20 VALU operations.

@@ -56,8 +56,10 @@ void demod_phase(int W, const float2* Ab, int H, int nb, int NCA, const DemodTab
 void int_rows(int W, int kmode, const float* w, const int* colk, const int32_t* kin, int32_t* kout, int* rescount,
               int H, int nb, float2* Zt, const float2* tw, hipStream_t s);
 struct IntegCoef;
+// colk (nullable): per (frame, map, row) column-0 unwrap offsets still to be
+// added (the fused path adds 2 pi W (colk0 + i colk1) to each row's DC bin).
 void int_cols(int H, const float2* Zt, int W, int nb, const IntegCoef& c, float2* Ht, const float2* tw,
-              hipStream_t s);
+              hipStream_t s, const int* colk = nullptr);
 void int_c2r(int W, const float2* Ht, int H, int nb, float* h, const float2* tw, hipStream_t s);
 int c2r_rows_per_block(int W);
 // band-pruned inverse row transform + phase (kernels_band.hip): B-point window
@@ -67,6 +69,14 @@ void band_phase(int W, int B, bool ref, const float2* Ab, int H, int nb, int NCA
                 const float* theta, float* out, const float2* pre, const float2* ptw, hipStream_t s);
 // column-0 prefix of the residue-free unwrap (kernels_unwrap.hip)
 void unwrap_colk(const float* w, int nmaps, int H, int W, int* colk, hipStream_t s);
+// the same over compact column-0 values col0[map][H] (the fused path's side output)
+void unwrap_colk_compact(const float* col0, int nmaps, int H, int* colk, hipStream_t s);
+// fused band transform + phase + unwrap + z-row FFT (kernels_phase_rows.hip)
+bool phase_rows_supported(int W, int B, int H);
+int phase_rows_tile();
+void phase_rows(bool unwrap, const float2* Ab, int H, int nb, int NCA, int ncc0, int ncc1, const float* theta,
+                const float2* pre, const float2* ptw, const float2* ztw, float* col0, int* flags, float2* Zt,
+                hipStream_t s);
 
 // In-place or out-of-place batched row FFT over nrows rows of length W.
 void row_fft(int W, bool inverse, RowIn in_mode, RowOut out_mode, const void* in, void* out, long nrows,

@@ -430,7 +430,8 @@ __global__ __launch_bounds__(KCfg<W>::THREADS, FCD_MIN_WAVES) void k_int_rows(co
 // ------------------------------------------------------------------ I2
 template <int H>
 __global__ __launch_bounds__(KCfg<H>::THREADS, ColWaves<H>::V) void k_int_cols(const float2* __restrict__ Zt, int W, int nb, IntegCoef c,
-                                                    float2* __restrict__ Ht, const float2* __restrict__ tw, int zts) {
+                                                    float2* __restrict__ Ht, const float2* __restrict__ tw, int zts,
+                                                    const int* __restrict__ colk) {
     using C = KCfg<H>;
     constexpr int TT = C::TT, E = C::E, TEAMS = C::TEAMS;
     extern __shared__ __attribute__((aligned(16))) float2 lds_raw[];
@@ -460,6 +461,15 @@ __global__ __launch_bounds__(KCfg<H>::THREADS, ColWaves<H>::V) void k_int_cols(c
                 y[q] = src[((long)(rr >> zts) * W + colm) * (1 << zts) + (rr & ((1 << zts) - 1))];
 #endif
             }
+            if (colk && colm == 0) {  // column-0 unwrap offsets of the fused path: row DC bins
+                const float sc = 6.28318530717959f * (float)W;
+#pragma unroll
+                for (int q = 0; q < E; ++q) {
+                    const int rr = t + TT * q;
+                    y[q].x += sc * (float)colk[((long)f * 2 + 0) * H + rr];
+                    y[q].y += sc * (float)colk[((long)f * 2 + 1) * H + rr];
+                }
+            }
             fft.template run<false>(y, s, t);
             if constexpr (!Sched<H>::WAVE_LOCAL) __syncthreads();
 #pragma unroll
@@ -474,6 +484,15 @@ __global__ __launch_bounds__(KCfg<H>::THREADS, ColWaves<H>::V) void k_int_cols(c
             const int rr = t + TT * q;
             x[q] = src[((long)(rr >> zts) * W + col) * (1 << zts) + (rr & ((1 << zts) - 1))];
 #endif
+        }
+        if (colk && col == 0) {
+            const float sc = 6.28318530717959f * (float)W;
+#pragma unroll
+            for (int q = 0; q < E; ++q) {
+                const int rr = t + TT * q;
+                x[q].x += sc * (float)colk[((long)f * 2 + 0) * H + rr];
+                x[q].y += sc * (float)colk[((long)f * 2 + 1) * H + rr];
+            }
         }
         fft.template run<false>(x, s, t);  // its exchange barriers also publish s2
         const float kx = c.kxe[col], kx2 = c.kx2[col];
@@ -645,7 +664,8 @@ static void launch_int_rows(int kmode, const float* w, const int* colk, const in
                             int* rescount, int H, int nb, float2* Zt, const float2* tw, hipStream_t s) {
     using C = IRCfg<W>;
     const size_t lds = C::LDS_BYTES;
-    const int grid = grid_for((long)nb * (H / C::ZT), 1);
+    const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(2048 / C::THREADS, (160 * 1024) / lds));
+    const int grid = grid_for((long)nb * (H / C::ZT), per_cu);
     if (kmode == 0) {
         set_lds(k_int_rows2<W, 0>, lds);
         hipLaunchKernelGGL((k_int_rows2<W, 0>), dim3(grid), dim3(C::THREADS), lds, s, w, colk, kin, kout, rescount, H,
@@ -664,14 +684,14 @@ static void launch_int_rows(int kmode, const float* w, const int* colk, const in
 
 template <int H>
 static void launch_int_cols(const float2* Zt, int W, int nb, const IntegCoef& c, float2* Ht, const float2* tw,
-                            hipStream_t s) {
+                            hipStream_t s, const int* colk) {
     using C = KCfg<H>;
     const size_t lds = (size_t)C::NLEN * 8 + (size_t)2 * C::TEAMS * C::ROW * 8;
     set_lds(k_int_cols<H>, lds);
     const int grid = grid_for(((long)nb * (W / 2 + 1) + C::TEAMS - 1) / C::TEAMS, 4);
     const int zt = zt_rows(W);
     const int zts = zt == 16 ? 4 : (zt == 8 ? 3 : 2);
-    hipLaunchKernelGGL(k_int_cols<H>, dim3(grid), dim3(C::THREADS), lds, s, Zt, W, nb, c, Ht, tw, zts);
+    hipLaunchKernelGGL(k_int_cols<H>, dim3(grid), dim3(C::THREADS), lds, s, Zt, W, nb, c, Ht, tw, zts, colk);
     FCD_CHECK_LAUNCH();
 }
 
@@ -705,8 +725,8 @@ void int_rows(int W, int kmode, const float* w, const int* colk, const int32_t* 
     FCD_SIZE_SWITCH(W, launch_int_rows, kmode, w, colk, kin, kout, rescount, H, nb, Zt, tw, s);
 }
 void int_cols(int H, const float2* Zt, int W, int nb, const IntegCoef& c, float2* Ht, const float2* tw,
-              hipStream_t s) {
-    FCD_SIZE_SWITCH(H, launch_int_cols, Zt, W, nb, c, Ht, tw, s);
+              hipStream_t s, const int* colk) {
+    FCD_SIZE_SWITCH(H, launch_int_cols, Zt, W, nb, c, Ht, tw, s, colk);
 }
 void int_c2r(int W, const float2* Ht, int H, int nb, float* h, const float2* tw, hipStream_t s) {
     FCD_SIZE_SWITCH(W, launch_int_c2r, Ht, H, nb, h, tw, s);

@@ -1,0 +1,265 @@
+// Fused throughput kernel of the height-only path (fcd_process with no phase
+// outputs, i.e. analyze.folder's use of compute_height_map, analyze.py:247-262):
+//
+//   band-pruned inverse row transforms of both carriers + phase   (fcd.py:118)
+//   residue-free unwrap of both maps + its census                 (fcd.py:119)
+//   phi0' + i*phi1' -> forward row FFT -> Zt tile                  (fourier.py:134)
+//
+// in ONE pass over each 8-row tile, so the wrapped phase maps (8 N^2 bytes per
+// frame) never touch HBM.  One wave per row (W = 1024: 64 lanes x 16 values):
+//
+//   * band transform: kernels_band.hip's decomposition (8 pre-twiddled
+//     128-point group FFTs per row), exchange in the row's own LDS slot;
+//   * unwrap: the row's wrapped values go blocked (16 consecutive pixels per
+//     lane) through the slot; h = find_wrap of horizontal neighbours (f32 with
+//     the +-fl(pi) ambiguity flag), one wave-wide DPP scan gives
+//     k'(r, c) = -sum_{c' < c} h(r, c'), phi' = w + 2 pi k' (k'(r, 0) = 0);
+//   * the column-0 offsets colk(r) are NOT applied here: they add the constant
+//     2 pi colk(r) (+ i ...) to row r, i.e. 2 pi W colk(r) to its spectrum's
+//     DC bin only, which k_int_cols applies (colk from k_colk_side over the
+//     column-0 values this kernel writes);
+//   * census: the unwrap is the unique residue-free one iff every vertical
+//     edge is consistent (int_rows.inc): |phi'(r+1,c) - phi'(r,c) + 2 pi d(r)|
+//     <= pi - margin with d(r) = colk(r+1) - colk(r) = -find_wrap(w(r,0),
+//     w(r+1,0)) (exact, f64).  A ninth wave computes the halo row below the
+//     tile, so every edge of the tile's rows is checked inside the block;
+//   * z-row FFT: a 1024-point wave-local group FFT (16 x 16 x 4, twiddles from
+//     an LDS table) in the slot, then the tile leaves as whole 64-byte lines.
+#include <hip/hip_runtime.h>
+
+#include <stdexcept>
+#include <string>
+
+#include "gfft.hpp"
+#include "kernels.hpp"
+
+namespace fcdk {
+
+namespace {
+
+constexpr int PR_W = 1024;            // row length of the fused kernel
+constexpr int PR_B = 128;             // band window
+constexpr int PR_ROWS = 8;            // output rows per tile (Zt tile height)
+constexpr int PR_WAVES = PR_ROWS + 1; // + the halo row
+constexpr int PR_THREADS = 64 * PR_WAVES;
+constexpr int PR_G = PR_B / 16, PR_L = PR_W / PR_B;
+constexpr int PR_SLOT = padded_len(PR_W) + 2;  // as int_rows.inc: == 2 (mod 32)
+constexpr int PR_SROW = PR_WAVES;              // staged band rows (odd pitch)
+constexpr int PR_ZTAB = GSched<PR_W>::TABLE;   // 1008 twiddles of the 1024-point group FFT
+// LDS carve (float2 units)
+constexpr int OFF_STAGE = 0;                                   // [2][B][SROW]
+constexpr int OFF_PRE = OFF_STAGE + 2 * PR_B * PR_SROW;        // [16][64] pre-twiddles
+constexpr int OFF_ZTAB = OFF_PRE + 16 * 64;                    // z-FFT twiddles
+constexpr int OFF_BTAB = OFF_ZTAB + PR_ZTAB;                   // band-FFT twiddles
+constexpr int OFF_SLOT = (OFF_BTAB + GSched<PR_B>::TABLE + 1) & ~1;  // 16-byte aligned slots
+constexpr int OFF_WSC = OFF_SLOT + PR_WAVES * PR_SLOT;         // [waves][W] floats: carrier-0 phases
+constexpr size_t PR_LDS = (size_t)OFF_WSC * 8 + (size_t)PR_WAVES * PR_W * 4;
+static_assert(PR_LDS <= 160 * 1024, "fused kernel LDS");
+static_assert(PR_L * GSched<PR_B>::REGION <= PR_SLOT, "band exchange must fit the slot");
+
+constexpr float kTwoPiF = 6.28318530717959f;
+constexpr float kPR_VLim = 3.14159265f - 4e-3f;
+
+__device__ __forceinline__ int fw_amb(float a, float b, int& amb) {
+    constexpr float P = 3.14159274f;  // fl(M_PI)
+    const float d = a - b;
+    amb |= fabsf(d) == P;
+    return d > P ? -1 : (d < -P ? 1 : 0);
+}
+
+__device__ __forceinline__ int fw_exact(float a, float b) {
+    const double d = (double)a - (double)b;
+    return d > 3.141592653589793 ? -1 : (d < -3.141592653589793 ? 1 : 0);
+}
+
+}  // namespace
+
+template <bool UNWRAP>
+__global__ __launch_bounds__(PR_THREADS) void k_phase_rows(
+    const float2* __restrict__ Ab, int H, int nb, int NCA, int ncc0, int ncc1, const float* __restrict__ theta,
+    const float2* __restrict__ pre, const float2* __restrict__ ptw, const float2* __restrict__ ztw,
+    float* __restrict__ col0, int* __restrict__ flags, float2* __restrict__ Zt) {
+    extern __shared__ __attribute__((aligned(16))) float2 lds_p[];
+    float2* const stage = lds_p + OFF_STAGE;
+    float2* const ptl = lds_p + OFF_PRE;
+    float2* const ztab = lds_p + OFF_ZTAB;
+    float2* const btab = lds_p + OFF_BTAB;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int g = lane / PR_G, t = lane % PR_G;  // band group / lane in group
+    float2* const slot = lds_p + OFF_SLOT + wave * PR_SLOT;
+    float* const wsc = reinterpret_cast<float*>(lds_p + OFF_WSC) + wave * PR_W;
+    for (int i = threadIdx.x; i < GSched<PR_B>::TABLE; i += PR_THREADS) btab[i] = ptw[i];
+    for (int i = threadIdx.x; i < 16 * 64; i += PR_THREADS) ptl[(i % 16) * 64 + i / 16] = pre[i];
+    for (int i = threadIdx.x; i < PR_ZTAB; i += PR_THREADS) ztab[i] = ztw[i];
+    const int rbs = H / PR_ROWS;
+    const int items = nb * rbs;
+    const int tiles16 = H / 16;
+    // staged band values of the next item, prefetched into registers
+    constexpr int NST = 2 * PR_B * PR_WAVES;             // (carrier, slot, row) entries
+    constexpr int SPT = (NST + PR_THREADS - 1) / PR_THREADS;
+    float2 pf[SPT];
+    auto fetch = [&](int blk) {
+        const int f = blk / rbs, rb = blk % rbs;
+#pragma unroll
+        for (int i = 0; i < SPT; ++i) {
+            const int e = threadIdx.x + i * PR_THREADS;
+            const int c = e / (PR_B * PR_WAVES), rem = e % (PR_B * PR_WAVES), j = rem / PR_WAVES, rr = rem % PR_WAVES;
+            const int r = min(rb * PR_ROWS + rr, H - 1);
+            const int ncc = c ? ncc1 : ncc0;
+            float2 v = make_float2(0.f, 0.f);
+            if (e < NST && j < ncc)
+                v = Ab[((((long)f * 2 + c) * tiles16 + (r >> 4)) * NCA + j) * 16 + (r & 15)];
+            pf[i] = v;
+        }
+    };
+    if ((int)blockIdx.x < items) fetch(blockIdx.x);
+    for (int blk = blockIdx.x; blk < items; blk += gridDim.x) {
+        const int f = blk / rbs, rb = blk % rbs;
+        const int r = rb * PR_ROWS + wave;           // this wave's row (wave 8: the halo row)
+        const bool live = r < H;
+        const bool halo = rb * PR_ROWS + PR_ROWS < H;
+#pragma unroll
+        for (int i = 0; i < SPT; ++i) {
+            const int e = threadIdx.x + i * PR_THREADS;
+            if (e < NST) stage[e] = pf[i];  // stage[(c*B + j)*SROW + row]
+        }
+        __syncthreads();
+        if (blk + (int)gridDim.x < items) fetch(blk + gridDim.x);
+        // ---- band transforms of both carriers -> wrapped phases (natural strided)
+        float w1[16];
+        {
+            const int rr = live ? r : H - 1;
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                float th[16];  // issued before the transform: the latency hides behind it
+#pragma unroll
+                for (int q = 0; q < 16; ++q) th[q] = theta[((long)c * H + rr) * PR_W + g + PR_L * t + 64 * q];
+                float2 x[16];
+#pragma unroll
+                for (int q = 0; q < 16; ++q)
+                    x[q] = cmul(stage[(c * PR_B + t + PR_G * q) * PR_SROW + wave], ptl[q * 64 + lane]);
+                GroupFFTTab<PR_B>::template run<true>(x, slot + g * GSched<PR_B>::REGION, t, btab);
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    if (q % 4 == 0) __builtin_amdgcn_sched_barrier(0);
+                    const float d = th[q] - fast_atan2(x[q].y, x[q].x);
+                    const float wq = fmaf(-kTwoPiF, rintf(d * 0.159154943091895f), d);
+                    if (c == 0)
+                        wsc[g + PR_L * t + 64 * q] = wq;  // parked in LDS: frees 16 VGPRs for carrier 1
+                    else
+                        w1[q] = wq;
+                }
+            }
+        }
+        // ---- natural strided -> blocked through the slot
+        wave_sync();
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int n = g + PR_L * t + 64 * q;
+            slot[pad(n)] = make_float2(wsc[n], w1[q]);  // wsc[n] was written by this lane
+        }
+        wave_sync();
+        const int j0 = lane * 16;
+        float* const sf = reinterpret_cast<float*>(slot);  // map m of pixel n at sf[2 * pad(n) + m]
+        int bad = 0;
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+            float v[17];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) v[j] = sf[2 * pad(j0 + j) + m];
+            v[16] = lane < 63 ? sf[2 * pad(j0 + 16) + m] : 0.f;
+            if (live && wave < PR_ROWS && lane == 0) col0[((long)f * 2 + m) * H + r] = v[0];
+            if constexpr (UNWRAP) {
+                int amb = 0, hb = 0;  // 2-bit codes of h + 1
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    const int h = (j0 + j + 1 < PR_W) ? fw_amb(v[j], v[j + 1], amb) : 0;
+                    hb |= (h + 1) << (2 * j);
+                }
+                int run = 0;  // (1 - h) increments of the segment
+#pragma unroll
+                for (int j = 0; j < 16; ++j) run += 2 - ((hb >> (2 * j)) & 3);
+                const int incl = team_scan_incl_dpp<64>(run);
+                int acc = incl - run - j0;  // k' at the segment start
+                wave_sync();                // every lane has read its neighbour's first value
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    sf[2 * pad(j0 + j) + m] = fmaf((float)acc, kTwoPiF, v[j]);
+                    acc -= ((hb >> (2 * j)) & 3) - 1;
+                }
+                bad |= live ? amb : 0;
+            }
+        }
+        __syncthreads();
+        // ---- vertical census against the next row (the halo for row 7)
+        if constexpr (UNWRAP) {
+            if (wave < PR_ROWS && live && (wave < PR_ROWS - 1 || halo) && r + 1 < H) {
+                const float2* nx = slot + PR_SLOT;
+                const float2 a0 = slot[0], b0 = nx[0];  // phi'(r, 0) = w(r, 0)
+                const float d0 = kTwoPiF * (float)(-fw_exact(a0.x, b0.x));
+                const float d1 = kTwoPiF * (float)(-fw_exact(a0.y, b0.y));
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    const float2 a = slot[pad(j0 + j)], b = nx[pad(j0 + j)];
+                    bad |= (int)(fabsf(b.x - a.x + d0) > kPR_VLim) | (int)(fabsf(b.y - a.y + d1) > kPR_VLim);
+                }
+            }
+            if (__any(bad) && lane == 0) atomicOr(flags + f * 2, 1);
+        }
+        // ---- forward row FFT of phi0' + i phi1' (rows of the tile only)
+        if (wave < PR_ROWS) {
+            __builtin_amdgcn_sched_barrier(0);
+            float2 x[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) x[q] = slot[pad(lane + 64 * q)];
+            GroupFFTTab<PR_W>::template run<false>(x, slot, lane, ztab);
+            wave_sync();
+#pragma unroll
+            for (int q = 0; q < 16; ++q) slot[pad(lane + 64 * q)] = x[q];
+        }
+        __syncthreads();
+        // ---- whole 64-byte tile lines: Zt[f][rb][col][0..8)
+        float2* dst = Zt + (long)f * H * PR_W + (long)rb * PR_W * PR_ROWS;
+        if (wave < PR_ROWS) {  // 512 threads: thread i writes column (i >> 3) + 64 k, row i & 7
+            const int c0 = threadIdx.x >> 3, rl = threadIdx.x & 7;
+            const float2* src = lds_p + OFF_SLOT + rl * PR_SLOT;
+#pragma unroll 4
+            for (int k = 0; k < PR_W * PR_ROWS / 512; ++k) dst[threadIdx.x + 512 * k] = src[pad(c0 + 64 * k)];
+        }
+        __syncthreads();
+    }
+}
+
+bool phase_rows_supported(int W, int B, int H) { return W == PR_W && B == PR_B && H % 16 == 0 && H >= 16; }
+
+int phase_rows_tile() { return PR_ROWS; }
+
+void phase_rows(bool unwrap, const float2* Ab, int H, int nb, int NCA, int ncc0, int ncc1, const float* theta,
+                const float2* pre, const float2* ptw, const float2* ztw, float* col0, int* flags, float2* Zt,
+                hipStream_t s) {
+    static int ncu = 0;
+    if (!ncu) {
+        int dev = 0;
+        hipDeviceProp_t p;
+        if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&p, dev) == hipSuccess) ncu = p.multiProcessorCount;
+        if (!ncu) ncu = 256;
+    }
+    const long items = (long)nb * (H / PR_ROWS);
+    const int grid = (int)std::min<long>(items, ncu);
+    if (grid <= 0) return;
+    if (unwrap) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_phase_rows<true>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)PR_LDS);
+        hipLaunchKernelGGL(k_phase_rows<true>, dim3(grid), dim3(PR_THREADS), PR_LDS, s, Ab, H, nb, NCA, ncc0, ncc1,
+                           theta, pre, ptw, ztw, col0, flags, Zt);
+    } else {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_phase_rows<false>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)PR_LDS);
+        hipLaunchKernelGGL(k_phase_rows<false>, dim3(grid), dim3(PR_THREADS), PR_LDS, s, Ab, H, nb, NCA, ncc0, ncc1,
+                           theta, pre, ptw, ztw, col0, flags, Zt);
+    }
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) throw std::runtime_error(std::string("phase_rows launch: ") + hipGetErrorString(e));
+}
+
+}  // namespace fcdk

@@ -83,10 +83,11 @@ void residues(const float* w, int nmaps, int H, int W, int* counts, hipStream_t 
 
 // ------------------------------------------------------------------ residue-free scan path
 // colk[map][i] = k(i, 0) = -sum_{i' < i} find_wrap(w[i'][0], w[i'+1][0])
-__global__ __launch_bounds__(256) void k_colk(const float* __restrict__ w, int H, int W, int* __restrict__ colk) {
+__global__ __launch_bounds__(256) void k_colk(const float* __restrict__ w, int H, long map_stride, long W,
+                                              int* __restrict__ colk) {
     __shared__ int part[256];
     const int map = blockIdx.x;
-    const float* m = w + (long)map * H * W;
+    const float* m = w + (long)map * map_stride;
     const int per = (H + 255) / 256;
     const int i0 = threadIdx.x * per;
     int loc[16];
@@ -96,7 +97,7 @@ __global__ __launch_bounds__(256) void k_colk(const float* __restrict__ w, int H
         const int i = i0 + q;
         loc[q] = 0;
         if (q < per && i + 1 < H) {
-            sum -= find_wrap(m[(long)i * W], m[(long)(i + 1) * W]);
+            sum -= find_wrap(m[(long)i * W], m[(long)(i + 1) * W]);  // W: row stride
         }
         loc[q] = sum;  // inclusive within the thread: k(i+1,0) - base
     }
@@ -148,13 +149,18 @@ __global__ __launch_bounds__(256) void k_rowscan(const float* __restrict__ w, lo
 }
 
 void unwrap_colk(const float* w, int nmaps, int H, int W, int* colk, hipStream_t s) {
-    hipLaunchKernelGGL(k_colk, dim3(nmaps), dim3(256), 0, s, w, H, W, colk);
+    hipLaunchKernelGGL(k_colk, dim3(nmaps), dim3(256), 0, s, w, H, (long)H * W, (long)W, colk);
+    FCD_CHECK_LAUNCH();
+}
+
+void unwrap_colk_compact(const float* col0, int nmaps, int H, int* colk, hipStream_t s) {
+    hipLaunchKernelGGL(k_colk, dim3(nmaps), dim3(256), 0, s, col0, H, (long)H, 1L, colk);
     FCD_CHECK_LAUNCH();
 }
 
 void unwrap_scan(const float* w, int nmaps, int H, int W, int* colk, int32_t* k, hipStream_t s) {
     if (H > 4096) throw std::runtime_error("unwrap_scan: H too large");
-    hipLaunchKernelGGL(k_colk, dim3(nmaps), dim3(256), 0, s, w, H, W, colk);
+    hipLaunchKernelGGL(k_colk, dim3(nmaps), dim3(256), 0, s, w, H, (long)H * W, (long)W, colk);
     FCD_CHECK_LAUNCH();
     const long nrows = (long)nmaps * H;
     hipLaunchKernelGGL(k_rowscan, dim3((unsigned)((nrows + 3) / 4)), dim3(256), 0, s, w, nrows, H, W, colk, k);

@@ -148,5 +148,49 @@ int main(int argc, char** argv) {
     timeit("int_cols", 2 * f + 8.0 * H * (W / 2 + 1),
            [&] { fcdk::int_cols(H, Zt, W, nb, coef, Ht, tw, s); });
     timeit("int_c2r", 8.0 * H * (W / 2 + 1) + f, [&] { fcdk::int_c2r(W, Ht, H, nb, hout, tw, s); });
+
+    // whole chain (band demod + unwrap + integration) over nb frames, split into
+    // S slices on S streams: how much do kernel boundaries / ramps cost?
+    {
+        int Bw = 16;
+        while (Bw < NCc) Bw *= 2;
+        std::vector<float2> ones(N, make_float2(1.f, 0.f));
+        float2* pre = dalloc<float2>(N);
+        float2* ptw = dalloc<float2>(N);
+        CK(hipMemcpy(pre, ones.data(), N * 8, hipMemcpyHostToDevice));
+        CK(hipMemcpy(ptw, ones.data(), N * 8, hipMemcpyHostToDevice));
+        hipStream_t ss[4];
+        for (auto& x : ss) CK(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+        hipEvent_t fork, join[4];
+        CK(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
+        for (auto& x : join) CK(hipEventCreateWithFlags(&x, hipEventDisableTiming));
+        for (int S : {1, 2, 4}) {
+            if (nb % S) continue;
+            const int m = nb / S;
+            auto chain = [&](int k, hipStream_t st) {
+                const long o = (long)k * m;
+                fcdk::demod_rows(W, frames + o * hw, H, m, T, Xb + o * H * T.NC, tw, st);
+                fcdk::demod_cols(H, Xb + o * H * T.NC, m, T, Ab + o * 2 * H * NCA, NCA, tw, st);
+                fcdk::band_phase(W, Bw, false, Ab + o * 2 * H * NCA, H, m, NCA, NCc, NCc, theta, wrapped + o * 2 * hw,
+                                 pre, ptw, st);
+                fcdk::unwrap_colk(wrapped + o * 2 * hw, 2 * m, H, W, colk + o * 2 * H, st);
+                fcdk::int_rows(W, 1, wrapped + o * 2 * hw, colk + o * 2 * H, nullptr, nullptr, res + 2 * o, H, m,
+                               Zt + o * hw, tw, st);
+                fcdk::int_cols(H, Zt + o * hw, W, m, coef, Ht + o * H * (W / 2 + 1), tw, st);
+                fcdk::int_c2r(W, Ht + o * H * (W / 2 + 1), H, m, hout + o * hw, tw, st);
+            };
+            char name[64];
+            std::snprintf(name, sizeof name, "chain x%d streams", S);
+            timeit(name, 0.0, [&] {
+                CK(hipEventRecord(fork, s));
+                for (int k = 0; k < S; ++k) {
+                    CK(hipStreamWaitEvent(ss[k], fork, 0));
+                    chain(k, ss[k]);
+                    CK(hipEventRecord(join[k], ss[k]));
+                }
+                for (int k = 0; k < S; ++k) CK(hipStreamWaitEvent(s, join[k], 0));
+            });
+        }
+    }
     return 0;
 }

@@ -1,0 +1,42 @@
+// Memory-access calibration (tuning tool): streaming copy of 512 MiB with
+// 4 / 8 / 16 bytes per lane, and a strided-4B pattern like the FFT kernels'
+// natural layouts.  hipcc --offload-arch=gfx950 -O3 membench.hip -o membench
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s\n", hipGetErrorString(e)); return 1; } } while (0)
+template <class T>
+__global__ void copyk(const T* __restrict__ a, T* __restrict__ b, long n) {
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) b[i] = a[i];
+}
+// each thread: 8 floats at stride TT (=128) inside a 1024-float row (like RegFFT natural layout)
+__global__ void strided(const float* __restrict__ a, float* __restrict__ b, long rows) {
+    const int t = threadIdx.x & 127, team = threadIdx.x >> 7;
+    for (long r = blockIdx.x * 2L + team; r < rows; r += gridDim.x * 2L) {
+        float x[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) x[q] = a[r * 1024 + t + 128 * q];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) b[r * 1024 + t + 128 * q] = x[q];
+    }
+}
+int main() {
+    const long bytes = 512L << 20;
+    float *a, *b;
+    CK(hipMalloc(&a, bytes)); CK(hipMalloc(&b, bytes));
+    CK(hipMemset(a, 0, bytes)); CK(hipMemset(b, 0, bytes));
+    hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
+    auto run = [&](const char* name, auto fn) {
+        for (int i = 0; i < 3; ++i) fn();
+        hipEventRecord(e0); for (int i = 0; i < 10; ++i) fn(); hipEventRecord(e1); hipEventSynchronize(e1);
+        float ms; hipEventElapsedTime(&ms, e0, e1);
+        printf("%-28s %8.1f GB/s (read+write)\n", name, 2.0 * bytes * 10 / (ms * 1e-3) / 1e9);
+    };
+    for (int g : {2048, 8192}) {
+        printf("grid %d x 256\n", g);
+        run("copy 4B/lane", [&] { copyk<float><<<g, 256>>>(a, b, bytes / 4); });
+        run("copy 8B/lane", [&] { copyk<float2><<<g, 256>>>((float2*)a, (float2*)b, bytes / 8); });
+        run("copy 16B/lane", [&] { copyk<float4><<<g, 256>>>((float4*)a, (float4*)b, bytes / 16); });
+        run("strided 4B (fft layout)", [&] { strided<<<g, 256>>>(a, b, bytes / 4096); });
+    }
+    return 0;
+}
