@@ -98,6 +98,59 @@ struct GroupFFT {
         pass<0, INV>(x, s, t);
     }
 
+    // The same with the exchange through a FLOAT region of REGION entries (real
+    // parts, then imaginary parts): half the LDS per transform for two more
+    // wave syncs, so more workgroups fit a CU.
+    template <bool INV>
+    __device__ __forceinline__ void run_half(float2 (&x)[E], float* s, int t) const {
+        pass_half<0, INV>(x, s, t);
+    }
+
+    template <int P, bool INV>
+    __device__ __forceinline__ void pass_half(float2 (&x)[E], float* s, int t) const {
+        constexpr int R = S::radix(P), L = S::ell(P), BPT = E / R;
+        float2 a[BPT][R];
+#pragma unroll
+        for (int b = 0; b < BPT; ++b) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) a[b][r] = x[b + BPT * r];
+            if constexpr (P > 0) {
+#pragma unroll
+                for (int r = 1; r < R; ++r) {
+                    const float2 w = tw[S::REGOFF(P) + b * (R - 1) + r - 1];
+                    a[b][r] = INV ? cmul(a[b][r], make_float2(w.x, -w.y)) : cmul(a[b][r], w);
+                }
+            }
+            dft_reg<R, INV>(a[b]);
+        }
+        if constexpr (P + 1 == NP) {
+#pragma unroll
+            for (int b = 0; b < BPT; ++b)
+#pragma unroll
+                for (int r = 0; r < R; ++r) x[b + BPT * r] = a[b][r];
+        } else {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                wave_sync();
+#pragma unroll
+                for (int b = 0; b < BPT; ++b) {
+                    const int j = t + b * G;
+                    const int k = j & (L - 1);
+                    const int base = (j - k) * R + k;
+#pragma unroll
+                    for (int r = 0; r < R; ++r) s[pad(base + r * L)] = h ? a[b][r].y : a[b][r].x;
+                }
+                wave_sync();
+#pragma unroll
+                for (int q = 0; q < E; ++q) {
+                    const float v = s[pad(t + G * q)];
+                    if (h) x[q].y = v; else x[q].x = v;
+                }
+            }
+            pass_half<P + 1, INV>(x, s, t);
+        }
+    }
+
     template <int P, bool INV>
     __device__ __forceinline__ void pass(float2 (&x)[E], float2* s, int t) const {
         constexpr int R = S::radix(P), L = S::ell(P), BPT = E / R;

@@ -32,7 +32,11 @@ namespace fcdk {
 namespace {
 
 #ifndef FCD_BAND_WAVES
-#define FCD_BAND_WAVES 2  // min waves per SIMD (launch-bounds): 2 keeps every twiddle in VGPRs
+#define FCD_BAND_WAVES 3  // min waves per SIMD (launch-bounds): 3 blocks of 4 waves per CU (168 VGPRs)
+#endif
+
+#ifndef FCD_ATAN_GROUP
+#define FCD_ATAN_GROUP 4  // atan2 chains interleaved per scheduling group (0: unbounded)
 #endif
 
 constexpr int BTILE = 16;   // rows per Ab tile (k_demod_cols layout)
@@ -48,10 +52,19 @@ struct BPCfg {
     static constexpr int REGION = GSched<B>::REGION;
     static constexpr bool XCH = GSched<B>::NP > 1;
     static constexpr size_t XOFF = (size_t)B * SROW + (size_t)RL * 16;  // exchange regions after stage + pre-twiddles
-    static constexpr size_t LDS = XOFF * 8 + (XCH ? (size_t)RP * L * REGION * 8 : 0);
+    // exchange in float halves (GroupFFT::run_half): 4 B per element per transform
+    static constexpr size_t LDS = XOFF * 8 + (XCH ? (size_t)RP * L * REGION * 4 : 0);
 };
 
 }  // namespace
+
+#ifdef FCD_STAMPS
+// Diagnostic build only: s_memtime stamps of block 0, wave 0 (no output depends on them).
+__device__ unsigned long long g_band_stamps[512];
+#define STAMP(i) do { const int si_ = (i); if (blockIdx.x == 0 && threadIdx.x == 0 && si_ < 512) g_band_stamps[si_] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define STAMP(i) do { } while (0)
+#endif
 
 template <int W, int B, bool REF>
 __global__ __launch_bounds__((BPCfg<W, B>::THREADS), FCD_BAND_WAVES) void k_band_phase(
@@ -63,7 +76,7 @@ __global__ __launch_bounds__((BPCfg<W, B>::THREADS), FCD_BAND_WAVES) void k_band
     float2* const stage = lds_b;  // [B][SROW]
     const int team = threadIdx.x / RL, l = threadIdx.x % RL, g = l / G, t = l % G;
     float2* const ptl = lds_b + (size_t)B * SROW;  // pre-twiddles [q][RL]
-    float2* const s = lds_b + C::XOFF + (size_t)(team * L + g) * C::REGION;
+    float* const s = reinterpret_cast<float*>(lds_b + C::XOFF) + (size_t)(team * L + g) * C::REGION;
     GroupFFT<B> fft;
     fft.load(ptw, t);
     for (int i = threadIdx.x; i < RL * E; i += C::THREADS) ptl[(i % E) * RL + i / E] = pre[i];
@@ -85,10 +98,27 @@ __global__ __launch_bounds__((BPCfg<W, B>::THREADS), FCD_BAND_WAVES) void k_band
 #pragma unroll
         for (int i = 0; i < SPT; ++i) pf[i] = src[min((int)threadIdx.x + i * C::THREADS, tile_n - 1)];
     };
-    if ((int)blockIdx.x < items) fetch(blockIdx.x);
+    // theta of the NEXT row this wave handles is loaded before the current row's
+    // stores: vmcnt counts loads and stores in issue order, so a load issued after
+    // a store batch cannot be waited for without waiting for those stores too.
+    float th[E];
+    auto th_load = [&](int blk, int rl) {
+        if constexpr (!REF) {
+            const int c = (blk / rbs) % 2, rb = blk % rbs;
+            const float* tr = theta + ((long)c * H + rb * BTILE + rl) * W;
+#pragma unroll
+            for (int q = 0; q < E; ++q) th[q] = tr[g + L * t + RL * q];
+        }
+    };
+    if ((int)blockIdx.x < items) {
+        fetch(blockIdx.x);
+        th_load(blockIdx.x, team);
+    }
+    int st = 0;
     for (int blk = blockIdx.x; blk < items; blk += gridDim.x) {
         const int f = blk / (2 * rbs), c = (blk / rbs) % 2, rb = blk % rbs;
         const int ncc = c ? ncc1 : ncc0;
+        STAMP(st++);
         // slots [ncc, B) are staged as zeros: the transform input needs no select
         if constexpr (SPT_ALL > SPT) {
             const float2* src = tile_src(blk);
@@ -102,38 +132,52 @@ __global__ __launch_bounds__((BPCfg<W, B>::THREADS), FCD_BAND_WAVES) void k_band
                 stage[(idx >> 4) * SROW + (idx & 15)] = idx < ncc * BTILE ? pf[i] : make_float2(0.f, 0.f);
         }
         __syncthreads();
-        if (blk + (int)gridDim.x < items) fetch(blk + gridDim.x);
+        STAMP(st++);
+        const int nblk = blk + (int)gridDim.x;
+        if (nblk < items) fetch(nblk);
         for (int rl = team; rl < BTILE; rl += RP) {
+            STAMP(st++);
             const int r = rb * BTILE + rl;
             const long row = ((long)f * 2 + c) * H + r;
-            float th[E];
-            if constexpr (!REF) {  // issued before the transform: its latency hides behind the FFT
-                const float* tr = theta + ((long)c * H + r) * W;
+            float thc[E];
 #pragma unroll
-                for (int q = 0; q < E; ++q) th[q] = tr[g + L * t + RL * q];
-            }
+            for (int q = 0; q < E; ++q) thc[q] = th[q];
+            if (rl + RP < BTILE)
+                th_load(blk, rl + RP);
+            else if (nblk < items)
+                th_load(nblk, team);
             float2 x[E];
 #pragma unroll
             for (int q = 0; q < E; ++q) x[q] = cmul(stage[(t + G * q) * SROW + rl], ptl[q * RL + l]);
-            fft.template run<true>(x, s, t);
+            STAMP(st++);
+            fft.template run_half<true>(x, s, t);
+            STAMP(st++);
             float* o = out + row * W;
 #pragma unroll
             for (int q = 0; q < E; ++q) {
-                if (q % 4 == 0) __builtin_amdgcn_sched_barrier(0);  // bound the atan2 chains in flight
+                if (FCD_ATAN_GROUP && q % FCD_ATAN_GROUP == 0) __builtin_amdgcn_sched_barrier(0);  // bound the atan2 chains in flight
                 const int n = g + L * t + RL * q;
                 const float a = fast_atan2(x[q].y, x[q].x);
                 if constexpr (REF) {
                     o[n] = a;
                 } else {
                     // wrap to [-pi, pi]: d - 2 pi rint(d / 2 pi), |d| < 2 pi
-                    const float d = th[q] - a;
+                    const float d = thc[q] - a;
                     o[n] = fmaf(-6.28318530717959f, rintf(d * 0.159154943091895f), d);
                 }
             }
+            STAMP(st++);
         }
         __syncthreads();
     }
+    STAMP(st++);
 }
+
+#ifdef FCD_STAMPS
+extern "C" int fcd_debug_band_stamps(unsigned long long* out) {
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_band_stamps), sizeof(g_band_stamps));
+}
+#endif
 
 // ------------------------------------------------------------------ launchers
 static int band_grid(long items, int per_cu) {

@@ -137,6 +137,14 @@ int main(int argc, char** argv) {
             timeit("band_phase", 16.0 * H * NCA + 8 * f, [&] {
                 fcdk::band_phase(W, Bw, false, Ab, H, nb, NCA, NCc, NCc, theta, wrapped, pre, ptw, s);
             });
+        if (fcdk::phase_rows_supported(W, Bw, H)) {
+            float2* ztw = dalloc<float2>(N);
+            CK(hipMemcpy(ztw, ones.data(), N * 8, hipMemcpyHostToDevice));
+            float* col0 = dalloc<float>((size_t)nb * 2 * H);
+            timeit("phase_rows (fused)", 16.0 * H * NCA + 2 * f, [&] {
+                fcdk::phase_rows(true, Ab, H, nb, NCA, NCc, NCc, theta, pre, ptw, ztw, col0, res, Zt, s);
+            });
+        }
     }
     timeit("colk", 8.0 * H, [&] { fcdk::unwrap_colk(wrapped, 2 * nb, H, W, colk, s); });
     timeit("int_rows k0", 2 * f + 2 * f, [&] {
