@@ -26,6 +26,22 @@ METRIC = "frames/sec @1024×1024 checkerboard batch + HBM GB/s vs peak, 1/2/4/8 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
+def load_traffic(n, chunk):
+    """HBM bytes per demod launch group from the committed PMC summary
+    (profiles/traffic_latest.json, written by tools/traffic_summary.py from two
+    rocprofv3 --pmc passes, FETCH_SIZE and WRITE_SIZE, over this bench command),
+    if it was measured for the same frame size and chunk."""
+    p = os.path.join(ROOT, "profiles", "traffic_latest.json")
+    try:
+        with open(p) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if t.get("frame") != n or t.get("chunk") != chunk:
+        return None
+    return t
+
+
 def cpu_baseline(size, frames, seconds_cap=25.0):
     """The CPU oracle (numpy/scipy FFTs + C Herraez unwrap), 1 core, bounded sample."""
     import numpy as np
@@ -49,8 +65,8 @@ def cpu_baseline(size, frames, seconds_cap=25.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--size", type=int, default=1024)
     ap.add_argument("--batch", type=int, default=256, help="frames per GPU per step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -84,14 +100,11 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    eng.profile(True)
-    torch.cuda.synchronize(dev)
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
+    torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     ev0.record()
     for _ in range(args.steps):
@@ -101,6 +114,12 @@ def main():
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
+    # per-stage device time from the engine's own HIP events (a separate, profiled
+    # pass, so the headline timing above carries no event overhead)
+    prof_steps = max(2, min(args.steps, 4))
+    eng.profile(True)
+    for _ in range(prof_steps):
+        step()
     stages, nframes = eng.stage_times()
     eng.profile(False)
     wall_max = max_over_ranks(wall, device=dev)
@@ -123,13 +142,20 @@ def main():
             dist.destroy_process_group()
         return
 
-    # roofline of the demodulation stage: frame f32 in -> 2 wrapped phases f32 out = 12 N^2 bytes/frame
+    # Roofline of the demodulation launch group (SURVEY.md §8d unit: frame f32 in ->
+    # two wrapped phase planes f32 out, B_demod = 12 N^2 bytes per frame): one group =
+    # k_demod_rows + k_demod_cols + k_band_phase over one chunk of `chunk` frames,
+    # timed by HIP events the engine records on the launch stream around the group.
+    chunk = int(stages.pop("chunk"))
+    launches = int(stages.pop("launches"))
     demod_bytes = 12.0 * n * n
-    demod_ms_per_frame = stages["demod"] / max(nframes, 1)
-    achieved = demod_bytes / (demod_ms_per_frame * 1e-3) / 1e9
+    demod_us_per_launch = stages["demod"] * 1e3 / max(launches, 1)
+    demod_frames_per_launch = nframes / max(launches, 1)
+    achieved = demod_bytes * demod_frames_per_launch / (demod_us_per_launch * 1e-6) / 1e9
     fix_frames = int(stages.pop("fixup_frames"))
     per_frame = {k: v / max(nframes, 1) * 1e3 for k, v in stages.items()}  # us per frame
-    per_frame["fixup_frames_per_step"] = fix_frames / args.steps
+    per_frame["fixup_frames_per_step"] = fix_frames / prof_steps
+    traffic = load_traffic(n, chunk)
     out = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -149,8 +175,14 @@ def main():
                    "frame": n, "batch_per_gpu": B, "global_batch": B * world,
                    "parallelism": f"frame-sharded x{world}, no collective in the compute"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                     "kernel": "demod stage (fwd FFT + disk band-pass + 2x inverse FFT + phase), 12*N^2 B/frame",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": traffic["demod_group_bytes_per_launch"] if traffic else None,
+                     "kernel": "demod launch group k_demod_rows + k_demod_cols + k_band_phase "
+                               "(frame f32 in -> 2 wrapped phases f32 out), 12*N^2 B/frame",
+                     "frames_per_launch": round(demod_frames_per_launch, 2),
+                     "us_per_launch": round(demod_us_per_launch, 2),
+                     "algorithmic_bytes_per_launch": int(demod_bytes * demod_frames_per_launch),
+                     "traffic_source": traffic["source"] if traffic else None,
                      "stage_us_per_frame": {k: round(v, 2) for k, v in per_frame.items()}},
         "event_ms_per_step": round(ev0.elapsed_time(ev1) / args.steps, 3),
     }

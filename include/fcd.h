@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define FCD_ABI_VERSION 1
+#define FCD_ABI_VERSION 2
 
 enum {
     FCD_OK = 0,
@@ -115,10 +115,11 @@ int fcd_fft2(fcd_ctx* ctx, const float* in, int n, int flags, float* out, void* 
  * milliseconds since the last call: out[0] demodulation (forward FFT, disk
  * band-pass, inverse FFTs, phase), out[1] unwrap pre-pass, out[2] unwrap scan
  * + displacement + integration, out[3] whole first pass, out[4] the exact
- * (Boruvka) fix-up pass, out[5] frames that needed it; *frames = frames
- * covered by the first pass. */
+ * (Boruvka) fix-up pass, out[5] frames that needed it, out[6] launch groups
+ * (chunks) covered, out[7] frames per launch group (the chunk size); *frames =
+ * frames covered by the first pass. */
 int fcd_profile(fcd_ctx* ctx, int enable);
-int fcd_stage_times(fcd_ctx* ctx, double* out6, int64_t* frames);
+int fcd_stage_times(fcd_ctx* ctx, double* out8, int64_t* frames);
 
 #ifdef __cplusplus
 }

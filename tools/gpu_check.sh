@@ -1,5 +1,5 @@
 #!/bin/bash
-# One GPU-box pass: parity tests, smoke, bench, rocprofv3 kernel stats.
+# One GPU-box pass: parity tests, smoke, bench, rocprofv3 kernel stats, PMC traffic.
 # Usage (from the repo root on the box): bash tools/gpu_check.sh [tag]
 set -o pipefail
 tag=${1:-r1}
@@ -12,5 +12,6 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $out/smok
 tail -2 $out/smoke.log
 timeout -k 10 400 python bench.py > $out/bench.log 2>&1 || { echo "bench failed"; tail -40 $out/bench.log; exit 1; }
 tail -1 $out/bench.log
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $out/prof -o run -- python3 bench.py --no-cpu-baseline --steps 5 --warmup 2 > $out/prof.log 2>&1 || { echo "rocprof failed"; tail -40 $out/prof.log; exit 1; }
-find $out/prof -name '*kernel_stats.csv' | head -5
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d $out/prof -o run -- python3 bench.py --no-cpu-baseline > $out/prof.log 2>&1 || { echo "rocprof failed"; tail -40 $out/prof.log; exit 1; }
+grep '^{' $out/prof.log > $out/prof_bench.json
+bash tools/traffic.sh $tag/traffic || exit 1

@@ -1,0 +1,59 @@
+"""Write profiles/<tag>.md from a tools/gpu_check.sh run: the rocprofv3
+--kernel-trace --stats summary (engine kernels), the bench line of the same
+(profiled) command, the unprofiled bench line, and the PMC traffic table.
+
+    python tools/profile_md.py gpurun_out/<tag> profiles/<name>.md
+"""
+import csv
+import json
+import os
+import sys
+
+src, dst = sys.argv[1], sys.argv[2]
+rows = list(csv.DictReader(open(os.path.join(src, "prof", "run_kernel_stats.csv"))))
+prof_bench = json.loads(open(os.path.join(src, "prof_bench.json")).read().strip().splitlines()[-1])
+bench = [l for l in open(os.path.join(src, "bench.log")) if l.startswith("{")][-1]
+chunk = prof_bench["roofline"]["frames_per_launch"]
+
+
+def short(n):
+    n = n.replace("HIP_vector_type<float, 2u>", "float2")
+    n = n[5:] if n.startswith("void ") else n
+    return n[:n.find("(")] if "(" in n else n
+
+
+lines = [f"# {os.path.basename(dst)[:-3]} — rocprofv3 --kernel-trace --stats (MI355X, 1 GPU)", "",
+         "Command: `rocprofv3 --kernel-trace --stats -f csv -- python3 bench.py --no-cpu-baseline` "
+         f"(1024x1024 frames, 256 per step, {chunk:g} frames per launch group). Engine kernels only; the torch "
+         "kernels of the on-device synthetic frame generator are omitted. Source: "
+         f"`{src}/prof/run_kernel_stats.csv`.", "",
+         "| kernel | calls | avg us | min us | max us | us/frame |", "|---|---|---|---|---|---|"]
+demod = 0.0
+for r in rows:
+    if "fcdk::" not in r["Name"]:
+        continue
+    avg = float(r["AverageNs"]) / 1e3
+    k = short(r["Name"])
+    if any(x in k for x in ("k_demod_rows", "k_demod_cols", "k_band_phase")) and int(r["Calls"]) > 50:
+        demod += avg
+    lines.append(f"| `{k}` | {r['Calls']} | {avg:.2f} | {float(r['MinNs']) / 1e3:.2f} | "
+                 f"{float(r['MaxNs']) / 1e3:.2f} | {avg / chunk:.3f} |")
+lines += ["", f"Demod launch group (k_demod_rows + k_demod_cols + k_band_phase) from this table: **{demod:.1f} us per "
+          f"launch**; the bench's HIP-event figure for the same group in this run: "
+          f"**{prof_bench['roofline']['us_per_launch']} us per launch**.", "",
+          "Bench line of the profiled command:", "", "```json", json.dumps(prof_bench), "```", "",
+          "Unprofiled `python bench.py` on the same box:", "", "```json", bench.strip(), "```", ""]
+tp = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles", "traffic_latest.json")
+if os.path.exists(tp):
+    t = json.load(open(tp))
+    lines += ["PMC traffic (rocprofv3 `--pmc FETCH_SIZE` / `--pmc WRITE_SIZE`, separate passes over `bench.py --steps 2`; "
+              "FETCH x2 and WRITE x1 as calibrated on streaming copies of known size, `tools/traffic_summary.py`), "
+              "bytes per launch group:", "",
+              "| kernel | read MB | write MB |", "|---|---|---|"]
+    for k, v in t["per_kernel"].items():
+        lines.append(f"| `{k}` | {v['read_bytes_per_launch'] / 1e6:.1f} | {v['write_bytes_per_launch'] / 1e6:.1f} |")
+    lines += ["", f"Demod group: {t['demod_group_bytes_per_launch'] / 1e6:.1f} MB per launch = "
+              f"{t['demod_group_bytes_per_frame'] / 1e6:.2f} MB per frame against "
+              f"{t['algorithmic_bytes_per_frame'] / 1e6:.2f} MB algorithmic (12 N^2).", ""]
+open(dst, "w").write("\n".join(lines))
+print("\n".join(lines))

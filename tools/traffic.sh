@@ -1,0 +1,15 @@
+#!/bin/bash
+# HBM traffic of the bench command from rocprofv3 PMC counters (MI355X_MICROARCH.md
+# §HBM / rocprofv3): FETCH_SIZE and WRITE_SIZE in separate --pmc passes (kernel
+# trace only), plus a calibration pass over streaming copies of known byte counts
+# at 4 / 8 / 16 B per lane.  Then: python tools/traffic_summary.py gpurun_out/<tag>
+set -o pipefail
+tag=${1:-traffic}
+out=gpurun_out/$tag
+mkdir -p $out
+export TMPDIR=/tmp
+for c in FETCH_SIZE WRITE_SIZE; do
+  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $c -f csv -d $out/$c -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > $out/$c.log 2>&1 || { echo "pmc $c failed"; tail -5 $out/$c.log; exit 1; }
+  timeout -k 10 120 rocprofv3 --kernel-trace --pmc $c -f csv -d $out/cal_$c -o run -- trapped-modes-ltg_amd/tools/membench cal > $out/cal_$c.log 2>&1 || { echo "calibration $c failed"; tail -5 $out/cal_$c.log; exit 1; }
+done
+echo traffic passes done

@@ -1,0 +1,92 @@
+"""HBM bytes per launch from the PMC passes of tools/traffic.sh.
+
+    python tools/traffic_summary.py gpurun_out/<tag> [--frame 1024]
+
+Calibration (MI355X_MICROARCH.md §HBM: FETCH_SIZE reads half the bytes of a wide
+streaming read; other widths uncalibrated): the membench copies move a known
+512 MiB per launch at 4, 8 and 16 B per lane, which gives the FETCH_SIZE and
+WRITE_SIZE scale of each width on this pool.  The engine's kernels are scaled
+with the factor of the width their dominant stream uses (measured, printed).
+Writes profiles/traffic_latest.json for bench.py (roofline.traffic) and prints
+a per-kernel table.
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+import statistics
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DEMOD = ("k_demod_rows", "k_demod_cols", "k_band_phase")
+CHAIN = DEMOD + ("k_colk", "k_int_rows2", "k_int_cols", "k_int_c2r")
+
+
+def per_dispatch(path):
+    rows = defaultdict(dict)
+    for f in glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            d = rows[(f, r["Dispatch_Id"])]
+            d["name"] = r["Kernel_Name"]
+            d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    return list(rows.values())
+
+
+def short(n):
+    for k in CHAIN + ("copyk<float>", "copyk<HIP_vector_type<float, 2u> >", "copyk<HIP_vector_type<float, 4u> >", "strided"):
+        if k in n:
+            return k
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir")
+    ap.add_argument("--frame", type=int, default=1024)
+    a = ap.parse_args()
+    known = 512 << 20
+    cal = {}
+    for c in ("FETCH_SIZE", "WRITE_SIZE"):
+        for d in per_dispatch(os.path.join(a.dir, "cal_" + c)):
+            k = short(d["name"])
+            if k:
+                cal.setdefault(k, {})[c] = known / (d[c] * 1024.0)  # true bytes per counted byte
+    print("calibration (true bytes / counter bytes):", json.dumps(cal, indent=1))
+    fetch_f = cal.get("copyk<float>", {}).get("FETCH_SIZE", 2.0)   # 4 B per lane streams
+    fetch_f8 = cal.get("copyk<HIP_vector_type<float, 2u> >", {}).get("FETCH_SIZE", 2.0)
+    write_f = cal.get("copyk<float>", {}).get("WRITE_SIZE", 1.0)
+    vals = defaultdict(lambda: defaultdict(list))
+    for c in ("FETCH_SIZE", "WRITE_SIZE"):
+        for d in per_dispatch(os.path.join(a.dir, c)):
+            k = short(d["name"])
+            if k in CHAIN:
+                vals[k][c].append(d[c] * 1024.0)
+    # demod_rows / band_phase stream 4-B lanes (frame, theta, phases); demod_cols 8-B tiles
+    factor = {"k_demod_rows": fetch_f, "k_band_phase": fetch_f, "k_demod_cols": fetch_f8}
+    table = {}
+    for k in CHAIN:
+        if k not in vals:
+            continue
+        fr = statistics.mean(vals[k]["FETCH_SIZE"]) * factor.get(k, fetch_f8) if vals[k]["FETCH_SIZE"] else 0.0
+        wr = statistics.mean(vals[k]["WRITE_SIZE"]) * write_f if vals[k]["WRITE_SIZE"] else 0.0
+        table[k] = {"read_bytes_per_launch": fr, "write_bytes_per_launch": wr}
+    group = sum(table[k]["read_bytes_per_launch"] + table[k]["write_bytes_per_launch"] for k in DEMOD if k in table)
+    # chunk size: frames per launch from the bench log line
+    chunk = None
+    for line in open(os.path.join(a.dir, "FETCH_SIZE.log")):
+        if line.startswith("{"):
+            chunk = int(round(json.loads(line)["roofline"]["frames_per_launch"]))
+    res = {"frame": a.frame, "chunk": chunk, "demod_group_bytes_per_launch": int(group),
+           "demod_group_bytes_per_frame": int(group / chunk) if chunk else None,
+           "algorithmic_bytes_per_frame": 12 * a.frame * a.frame,
+           "per_kernel": table, "calibration": cal,
+           "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over bench.py ({os.path.basename(a.dir)}); "
+                     "FETCH scaled by the membench 4/8-B-lane calibration, WRITE by the 4-B-lane one"}
+    print(json.dumps(res, indent=1))
+    with open(os.path.join(ROOT, "profiles", "traffic_latest.json"), "w") as f:
+        json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -1112,10 +1112,12 @@ FCD_API int fcd_profile(fcd_ctx* c, int enable) {
 FCD_API int fcd_stage_times(fcd_ctx* c, double* out4, int64_t* frames) {
     FCD_TRY({
         check_ctx(c);
-        if (!out4) throw FcdError(FCD_E_INVALID, "out6 is null");
+        if (!out4) throw FcdError(FCD_E_INVALID, "out8 is null");
         for (int i = 0; i < 4; ++i) out4[i] = 0;
         out4[4] = c->prof_fix_ms;
         out4[5] = (double)c->prof_fix_frames;
+        out4[6] = (double)(c->ev_used / 4);  // launch groups (chunks) covered
+        out4[7] = (double)c->fchunk;         // frames per launch group
         c->prof_fix_ms = 0;
         c->prof_fix_frames = 0;
         if (c->ev_used) HIPCHK(hipEventSynchronize(c->ev_pool[c->ev_used - 1]));

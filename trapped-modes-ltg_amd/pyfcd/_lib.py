@@ -190,11 +190,11 @@ class Engine:
         _check(self._lib.fcd_profile(self._h, int(bool(enable))))
 
     def stage_times(self):
-        """(ms dict {demod, unwrap, integrate, total, fixup, fixup_frames}, frames) since the last call."""
-        out = (ctypes.c_double * 6)()
+        """(ms dict {demod, unwrap, integrate, total, fixup, fixup_frames, launches, chunk}, frames) since the last call."""
+        out = (ctypes.c_double * 8)()
         nf = ctypes.c_int64()
         _check(self._lib.fcd_stage_times(self._h, out, ctypes.byref(nf)))
-        keys = ("demod", "unwrap", "integrate", "total", "fixup", "fixup_frames")
+        keys = ("demod", "unwrap", "integrate", "total", "fixup", "fixup_frames", "launches", "chunk")
         return dict(zip(keys, list(out))), nf.value
 
     def phases_from_spectrum(self, spectrum, unwrap=True):
