@@ -301,8 +301,9 @@ def test_full_size_1024_vs_oracle(lib):
 
 @pytest.fixture
 def fused(monkeypatch):
-    """Engines created inside the test take the fused height-only path."""
-    monkeypatch.setenv("FCD_FUSED", "1")
+    """Engines created inside the test take the fused height-only path (the default;
+    FCD_UNFUSED=1 selects the unfused chain for A/B measurements)."""
+    monkeypatch.delenv("FCD_UNFUSED", raising=False)
     from pyfcd import _lib
     _lib._engines.clear()
     yield
@@ -326,6 +327,17 @@ def test_fused_height_path_vs_oracle(lib, fused):
             assert cf == cfo
             assert rel_l2(hf[f], ho) < 1e-5, (unwrap, f)
             assert rel_l2(hf[f], hu[f]) < 1e-6, (unwrap, f)
+    # residue-free frames must pass the fused census (tile interiors and seams): none
+    # may fall back to the exact pass
+    assert all(O.count_residues(w) == 0 for f in range(frames.shape[0])
+               for w in O.compute_height_map(ref, frames[f], 0.001, height=1.0)[3]["wrapped"])
+    eng = lib.Engine(ref.shape)
+    eng.set_reference(ref, 0.001)
+    eng.profile(True)
+    eng.process(frames, 1.0, unwrap=True, want_phases=False)
+    st, _ = eng.stage_times()
+    eng.profile(False)
+    assert int(st["fixup_frames"]) == 0
 
 
 def test_fused_census_sends_residue_frames_to_exact_pass(lib, golden, fused):

@@ -185,8 +185,9 @@ struct fcd_ctx {
     int band_B = 0;                  // band window of the pruned inverse (0: full-length k_demod_phase)
     DevBuf band_pre, band_ptw, theta_b;  // its pre-twiddles, pass twiddles, reference angle of the band
     bool fused_ok = false;           // k_phase_rows applies (height-only calls)
-    bool force_unfused = true;       // FCD_FUSED=1 enables the fused path (A/B measurement until it wins)
-    DevBuf ztw, col0;                // its 1024-point group-FFT twiddles; column-0 wrapped values [f][2][H]
+    bool force_unfused = false;      // FCD_UNFUSED=1: take the unfused chain (A/B measurement)
+    DevBuf ztw, col0, seam;          // its 1024-point group-FFT twiddles; column-0 wrapped values [f][2][H];
+                                     // first/last unwrapped rows of every tile [f][H/tile][2][W]
     size_t fres_cap = 0;
 
     // workspace
@@ -617,6 +618,7 @@ void build_demod_tables(fcd_ctx* c, hipStream_t s) {
     c->colk.ensure(std::max(nb, (size_t)c->chunk) * 2 * H * sizeof(int));
     c->fk.ensure(nb * 2 * hw * sizeof(int32_t));
     c->col0.ensure(nb * 2 * (size_t)H * sizeof(float));
+    if (c->fused_ok) c->seam.ensure(nb * (size_t)(H / fcdk::phase_rows_tile()) * 2 * W * sizeof(float2));
     c->rescnt.ensure(std::max(nb, (size_t)c->chunk) * 2 * sizeof(int));
     c->mst_cap = 0;  // re-size the MST workspace for the new chunk on next use
 }
@@ -696,7 +698,7 @@ FCD_API int fcd_create(int device, int rows, int cols, fcd_ctx** out) {
         HIPCHK(hipSetDevice(device));
         std::unique_ptr<fcd_ctx> c(new fcd_ctx());
         c->device = device;
-        c->force_unfused = fcd_env_int("FCD_FUSED", 0) == 0;
+        c->force_unfused = fcd_env_int("FCD_UNFUSED", 0) != 0;
         c->H = rows;
         c->W = cols;
         HIPCHK(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking));
@@ -888,7 +890,7 @@ FCD_API int fcd_process(fcd_ctx* c, const float* frames, int n_frames, int flags
                 fcdk::phase_rows(unwrap != 0, c->Ab.as<float2>(), c->H, nb, c->NCA, c->NCc[0], c->NCc[1],
                                  c->theta_b.as<float>(), c->band_pre.as<float2>(), c->band_ptw.as<float2>(),
                                  c->ztw.as<float2>(), c->col0.as<float>(), res ? res + (size_t)f0 * 2 : nullptr,
-                                 c->Zt.as<float2>(), s);
+                                 c->Zt.as<float2>(), c->seam.as<float2>(), s);
                 if (unwrap) fcdk::unwrap_colk_compact(c->col0.as<float>(), 2 * nb, c->H, c->colk.as<int>(), s);
                 if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
                 fcdk::int_cols(c->H, c->Zt.as<float2>(), c->W, nb, coef, c->Ht.as<float2>(), c->twp_col.as<float2>(), s,

@@ -76,7 +76,7 @@ bool phase_rows_supported(int W, int B, int H);
 int phase_rows_tile();
 void phase_rows(bool unwrap, const float2* Ab, int H, int nb, int NCA, int ncc0, int ncc1, const float* theta,
                 const float2* pre, const float2* ptw, const float2* ztw, float* col0, int* flags, float2* Zt,
-                hipStream_t s);
+                float2* seam, hipStream_t s);
 
 // In-place or out-of-place batched row FFT over nrows rows of length W.
 void row_fft(int W, bool inverse, RowIn in_mode, RowOut out_mode, const void* in, void* out, long nrows,

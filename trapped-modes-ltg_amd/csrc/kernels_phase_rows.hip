@@ -21,8 +21,10 @@
 //   * census: the unwrap is the unique residue-free one iff every vertical
 //     edge is consistent (int_rows.inc): |phi'(r+1,c) - phi'(r,c) + 2 pi d(r)|
 //     <= pi - margin with d(r) = colk(r+1) - colk(r) = -find_wrap(w(r,0),
-//     w(r+1,0)) (exact, f64).  A ninth wave computes the halo row below the
-//     tile, so every edge of the tile's rows is checked inside the block;
+//     w(r+1,0)) (exact, f64).  Edges inside the tile are checked here; the
+//     tile's first and last unwrapped rows go to a seam buffer and
+//     k_seam_check checks the edges between tiles (no halo recompute, and
+//     8 waves = exactly 2 per SIMD);
 //   * z-row FFT: a 1024-point wave-local group FFT (16 x 16 x 4, twiddles from
 //     an LDS table) in the slot, then the tile leaves as whole 64-byte lines.
 #include <hip/hip_runtime.h>
@@ -40,11 +42,11 @@ namespace {
 constexpr int PR_W = 1024;            // row length of the fused kernel
 constexpr int PR_B = 128;             // band window
 constexpr int PR_ROWS = 8;            // output rows per tile (Zt tile height)
-constexpr int PR_WAVES = PR_ROWS + 1; // + the halo row
+constexpr int PR_WAVES = PR_ROWS;     // one wave per row
 constexpr int PR_THREADS = 64 * PR_WAVES;
 constexpr int PR_G = PR_B / 16, PR_L = PR_W / PR_B;
 constexpr int PR_SLOT = padded_len(PR_W) + 2;  // as int_rows.inc: == 2 (mod 32)
-constexpr int PR_SROW = PR_WAVES;              // staged band rows (odd pitch)
+constexpr int PR_SROW = PR_ROWS + 1;           // staged band rows (odd pitch)
 constexpr int PR_ZTAB = GSched<PR_W>::TABLE;   // 1008 twiddles of the 1024-point group FFT
 // LDS carve (float2 units)
 constexpr int OFF_STAGE = 0;                                   // [2][B][SROW]
@@ -52,8 +54,7 @@ constexpr int OFF_PRE = OFF_STAGE + 2 * PR_B * PR_SROW;        // [16][64] pre-t
 constexpr int OFF_ZTAB = OFF_PRE + 16 * 64;                    // z-FFT twiddles
 constexpr int OFF_BTAB = OFF_ZTAB + PR_ZTAB;                   // band-FFT twiddles
 constexpr int OFF_SLOT = (OFF_BTAB + GSched<PR_B>::TABLE + 1) & ~1;  // 16-byte aligned slots
-constexpr int OFF_WSC = OFF_SLOT + PR_WAVES * PR_SLOT;         // [waves][W] floats: carrier-0 phases
-constexpr size_t PR_LDS = (size_t)OFF_WSC * 8 + (size_t)PR_WAVES * PR_W * 4;
+constexpr size_t PR_LDS = (size_t)(OFF_SLOT + PR_WAVES * PR_SLOT) * 8;
 static_assert(PR_LDS <= 160 * 1024, "fused kernel LDS");
 static_assert(PR_L * GSched<PR_B>::REGION <= PR_SLOT, "band exchange must fit the slot");
 
@@ -78,7 +79,7 @@ template <bool UNWRAP>
 __global__ __launch_bounds__(PR_THREADS) void k_phase_rows(
     const float2* __restrict__ Ab, int H, int nb, int NCA, int ncc0, int ncc1, const float* __restrict__ theta,
     const float2* __restrict__ pre, const float2* __restrict__ ptw, const float2* __restrict__ ztw,
-    float* __restrict__ col0, int* __restrict__ flags, float2* __restrict__ Zt) {
+    float* __restrict__ col0, int* __restrict__ flags, float2* __restrict__ Zt, float2* __restrict__ seam) {
     extern __shared__ __attribute__((aligned(16))) float2 lds_p[];
     float2* const stage = lds_p + OFF_STAGE;
     float2* const ptl = lds_p + OFF_PRE;
@@ -87,7 +88,6 @@ __global__ __launch_bounds__(PR_THREADS) void k_phase_rows(
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int g = lane / PR_G, t = lane % PR_G;  // band group / lane in group
     float2* const slot = lds_p + OFF_SLOT + wave * PR_SLOT;
-    float* const wsc = reinterpret_cast<float*>(lds_p + OFF_WSC) + wave * PR_W;
     for (int i = threadIdx.x; i < GSched<PR_B>::TABLE; i += PR_THREADS) btab[i] = ptw[i];
     for (int i = threadIdx.x; i < 16 * 64; i += PR_THREADS) ptl[(i % 16) * 64 + i / 16] = pre[i];
     for (int i = threadIdx.x; i < PR_ZTAB; i += PR_THREADS) ztab[i] = ztw[i];
@@ -95,7 +95,7 @@ __global__ __launch_bounds__(PR_THREADS) void k_phase_rows(
     const int items = nb * rbs;
     const int tiles16 = H / 16;
     // staged band values of the next item, prefetched into registers
-    constexpr int NST = 2 * PR_B * PR_WAVES;             // (carrier, slot, row) entries
+    constexpr int NST = 2 * PR_B * PR_SROW;              // (carrier, slot, row) entries, SROW-pitched
     constexpr int SPT = (NST + PR_THREADS - 1) / PR_THREADS;
     float2 pf[SPT];
     auto fetch = [&](int blk) {
@@ -103,11 +103,11 @@ __global__ __launch_bounds__(PR_THREADS) void k_phase_rows(
 #pragma unroll
         for (int i = 0; i < SPT; ++i) {
             const int e = threadIdx.x + i * PR_THREADS;
-            const int c = e / (PR_B * PR_WAVES), rem = e % (PR_B * PR_WAVES), j = rem / PR_WAVES, rr = rem % PR_WAVES;
+            const int c = e / (PR_B * PR_SROW), rem = e % (PR_B * PR_SROW), j = rem / PR_SROW, rr = rem % PR_SROW;
             const int r = min(rb * PR_ROWS + rr, H - 1);
             const int ncc = c ? ncc1 : ncc0;
             float2 v = make_float2(0.f, 0.f);
-            if (e < NST && j < ncc)
+            if (e < NST && j < ncc && rr < PR_ROWS)
                 v = Ab[((((long)f * 2 + c) * tiles16 + (r >> 4)) * NCA + j) * 16 + (r & 15)];
             pf[i] = v;
         }
@@ -115,9 +115,7 @@ __global__ __launch_bounds__(PR_THREADS) void k_phase_rows(
     if ((int)blockIdx.x < items) fetch(blockIdx.x);
     for (int blk = blockIdx.x; blk < items; blk += gridDim.x) {
         const int f = blk / rbs, rb = blk % rbs;
-        const int r = rb * PR_ROWS + wave;           // this wave's row (wave 8: the halo row)
-        const bool live = r < H;
-        const bool halo = rb * PR_ROWS + PR_ROWS < H;
+        const int r = rb * PR_ROWS + wave;           // this wave's row
 #pragma unroll
         for (int i = 0; i < SPT; ++i) {
             const int e = threadIdx.x + i * PR_THREADS;
@@ -126,9 +124,9 @@ __global__ __launch_bounds__(PR_THREADS) void k_phase_rows(
         __syncthreads();
         if (blk + (int)gridDim.x < items) fetch(blk + gridDim.x);
         // ---- band transforms of both carriers -> wrapped phases (natural strided)
-        float w1[16];
+        float w0[16], w1[16];
         {
-            const int rr = live ? r : H - 1;
+            const int rr = r;
 #pragma unroll
             for (int c = 0; c < 2; ++c) {
                 float th[16];  // issued before the transform: the latency hides behind it
@@ -145,7 +143,7 @@ __global__ __launch_bounds__(PR_THREADS) void k_phase_rows(
                     const float d = th[q] - fast_atan2(x[q].y, x[q].x);
                     const float wq = fmaf(-kTwoPiF, rintf(d * 0.159154943091895f), d);
                     if (c == 0)
-                        wsc[g + PR_L * t + 64 * q] = wq;  // parked in LDS: frees 16 VGPRs for carrier 1
+                        w0[q] = wq;
                     else
                         w1[q] = wq;
                 }
@@ -156,7 +154,7 @@ __global__ __launch_bounds__(PR_THREADS) void k_phase_rows(
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
             const int n = g + PR_L * t + 64 * q;
-            slot[pad(n)] = make_float2(wsc[n], w1[q]);  // wsc[n] was written by this lane
+            slot[pad(n)] = make_float2(w0[q], w1[q]);
         }
         wave_sync();
         const int j0 = lane * 16;
@@ -168,7 +166,7 @@ __global__ __launch_bounds__(PR_THREADS) void k_phase_rows(
 #pragma unroll
             for (int j = 0; j < 16; ++j) v[j] = sf[2 * pad(j0 + j) + m];
             v[16] = lane < 63 ? sf[2 * pad(j0 + 16) + m] : 0.f;
-            if (live && wave < PR_ROWS && lane == 0) col0[((long)f * 2 + m) * H + r] = v[0];
+            if (lane == 0) col0[((long)f * 2 + m) * H + r] = v[0];
             if constexpr (UNWRAP) {
                 int amb = 0, hb = 0;  // 2-bit codes of h + 1
 #pragma unroll
@@ -187,13 +185,24 @@ __global__ __launch_bounds__(PR_THREADS) void k_phase_rows(
                     sf[2 * pad(j0 + j) + m] = fmaf((float)acc, kTwoPiF, v[j]);
                     acc -= ((hb >> (2 * j)) & 3) - 1;
                 }
-                bad |= live ? amb : 0;
+                bad |= amb;
+            }
+        }
+        if constexpr (UNWRAP) {  // first and last unwrapped rows of the tile -> seam buffer (k_seam_check)
+            if (wave == 0 || wave == PR_ROWS - 1) {
+                float4* sd = reinterpret_cast<float4*>(seam + (((long)f * (H / PR_ROWS) + rb) * 2 + (wave ? 1 : 0)) * PR_W +
+                                                       j0);
+#pragma unroll
+                for (int j = 0; j < 16; j += 2) {
+                    const float2 a = slot[pad(j0 + j)], b = slot[pad(j0 + j + 1)];
+                    sd[j / 2] = make_float4(a.x, a.y, b.x, b.y);
+                }
             }
         }
         __syncthreads();
-        // ---- vertical census against the next row (the halo for row 7)
+        // ---- vertical census against the next row of the tile (seams: k_seam_check)
         if constexpr (UNWRAP) {
-            if (wave < PR_ROWS && live && (wave < PR_ROWS - 1 || halo) && r + 1 < H) {
+            if (wave < PR_ROWS - 1) {
                 const float2* nx = slot + PR_SLOT;
                 const float2 a0 = slot[0], b0 = nx[0];  // phi'(r, 0) = w(r, 0)
                 const float d0 = kTwoPiF * (float)(-fw_exact(a0.x, b0.x));
@@ -205,9 +214,10 @@ __global__ __launch_bounds__(PR_THREADS) void k_phase_rows(
                 }
             }
             if (__any(bad) && lane == 0) atomicOr(flags + f * 2, 1);
+            __syncthreads();  // every census read of the next slot precedes that row's FFT
         }
-        // ---- forward row FFT of phi0' + i phi1' (rows of the tile only)
-        if (wave < PR_ROWS) {
+        // ---- forward row FFT of phi0' + i phi1'
+        {
             __builtin_amdgcn_sched_barrier(0);
             float2 x[16];
 #pragma unroll
@@ -220,7 +230,7 @@ __global__ __launch_bounds__(PR_THREADS) void k_phase_rows(
         __syncthreads();
         // ---- whole 64-byte tile lines: Zt[f][rb][col][0..8)
         float2* dst = Zt + (long)f * H * PR_W + (long)rb * PR_W * PR_ROWS;
-        if (wave < PR_ROWS) {  // 512 threads: thread i writes column (i >> 3) + 64 k, row i & 7
+        {  // 512 threads: thread i writes column (i >> 3) + 64 k, row i & 7
             const int c0 = threadIdx.x >> 3, rl = threadIdx.x & 7;
             const float2* src = lds_p + OFF_SLOT + rl * PR_SLOT;
 #pragma unroll 4
@@ -230,13 +240,46 @@ __global__ __launch_bounds__(PR_THREADS) void k_phase_rows(
     }
 }
 
+// Census of the edges between tiles: row 8b+7 (last of tile b) against row
+// 8b+8 (first of tile b+1), both unwrapped without their column-0 offsets.
+// One wave per seam; lane L holds pixels 16L .. 16L+15.
+__global__ __launch_bounds__(256) void k_seam_check(const float2* __restrict__ seam, int H, int nb,
+                                                    int* __restrict__ flags) {
+    const int rbs = H / PR_ROWS;
+    const long seams = (long)nb * (rbs - 1);
+    const long sidx = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (sidx >= seams) return;
+    const int f = (int)(sidx / (rbs - 1)), b = (int)(sidx % (rbs - 1));
+    const int lane = threadIdx.x & 63;
+    const float4* a = reinterpret_cast<const float4*>(seam + (((long)f * rbs + b) * 2 + 1) * PR_W + lane * 16);
+    const float4* c = reinterpret_cast<const float4*>(seam + (((long)f * rbs + b + 1) * 2 + 0) * PR_W + lane * 16);
+    float4 av[8], cv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        av[j] = a[j];
+        cv[j] = c[j];
+    }
+    // phi'(r, 0) = w(r, 0): the column-0 jump of the true unwrap, exactly
+    const float a0x = __shfl(av[0].x, 0), a0y = __shfl(av[0].y, 0);
+    const float c0x = __shfl(cv[0].x, 0), c0y = __shfl(cv[0].y, 0);
+    const float d0 = kTwoPiF * (float)(-fw_exact(a0x, c0x));
+    const float d1 = kTwoPiF * (float)(-fw_exact(a0y, c0y));
+    int bad = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        bad |= (int)(fabsf(cv[j].x - av[j].x + d0) > kPR_VLim) | (int)(fabsf(cv[j].y - av[j].y + d1) > kPR_VLim);
+        bad |= (int)(fabsf(cv[j].z - av[j].z + d0) > kPR_VLim) | (int)(fabsf(cv[j].w - av[j].w + d1) > kPR_VLim);
+    }
+    if (__any(bad) && lane == 0) atomicOr(flags + f * 2, 1);
+}
+
 bool phase_rows_supported(int W, int B, int H) { return W == PR_W && B == PR_B && H % 16 == 0 && H >= 16; }
 
 int phase_rows_tile() { return PR_ROWS; }
 
 void phase_rows(bool unwrap, const float2* Ab, int H, int nb, int NCA, int ncc0, int ncc1, const float* theta,
                 const float2* pre, const float2* ptw, const float2* ztw, float* col0, int* flags, float2* Zt,
-                hipStream_t s) {
+                float2* seam, hipStream_t s) {
     static int ncu = 0;
     if (!ncu) {
         int dev = 0;
@@ -251,12 +294,15 @@ void phase_rows(bool unwrap, const float2* Ab, int H, int nb, int NCA, int ncc0,
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_phase_rows<true>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)PR_LDS);
         hipLaunchKernelGGL(k_phase_rows<true>, dim3(grid), dim3(PR_THREADS), PR_LDS, s, Ab, H, nb, NCA, ncc0, ncc1,
-                           theta, pre, ptw, ztw, col0, flags, Zt);
+                           theta, pre, ptw, ztw, col0, flags, Zt, seam);
+        const long seams = (long)nb * (H / PR_ROWS - 1);
+        if (seams > 0)
+            hipLaunchKernelGGL(k_seam_check, dim3((unsigned)((seams + 3) / 4)), dim3(256), 0, s, seam, H, nb, flags);
     } else {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_phase_rows<false>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)PR_LDS);
         hipLaunchKernelGGL(k_phase_rows<false>, dim3(grid), dim3(PR_THREADS), PR_LDS, s, Ab, H, nb, NCA, ncc0, ncc1,
-                           theta, pre, ptw, ztw, col0, flags, Zt);
+                           theta, pre, ptw, ztw, col0, flags, Zt, seam);
     }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) throw std::runtime_error(std::string("phase_rows launch: ") + hipGetErrorString(e));
