@@ -554,14 +554,30 @@ __global__ __launch_bounds__(C2RCfg<W>::THREADS) void k_int_c2r(const float2* __
     __syncthreads();
     const int NCH = W / 2 + 1;
     const int nblk = H / rpw;
-    for (int blk = blockIdx.x; blk < nb * nblk; blk += gridDim.x) {
+    // the next item's staged block (NCH x rpw values) is prefetched into registers
+    // while the current one is transformed (SPT values per thread, all in flight)
+    constexpr int SPT = ((W / 2 + 1) * C::RPW + C::THREADS - 1) / C::THREADS;
+    float2 pf[SPT];
+    auto fetch = [&](int blk) {
         const int f = blk / nblk, r0 = (blk % nblk) * rpw;
         const float2* src = Ht + (long)f * H * NCH;
-        for (int idx = threadIdx.x; idx < NCH * rpw; idx += C::THREADS) {
-            const int col = idx / rpw, rl = idx % rpw;
-            stage[col * (rpw + 1) + rl] = src[tix(r0 + rl, col, NCH)];
+#pragma unroll
+        for (int i = 0; i < SPT; ++i) {
+            const int idx = threadIdx.x + i * C::THREADS;
+            const int col = min(idx / rpw, NCH - 1), rl = idx % rpw;
+            pf[i] = src[tix(r0 + rl, col, NCH)];
+        }
+    };
+    if ((int)blockIdx.x < nb * nblk) fetch(blockIdx.x);
+    for (int blk = blockIdx.x; blk < nb * nblk; blk += gridDim.x) {
+        const int f = blk / nblk, r0 = (blk % nblk) * rpw;
+#pragma unroll
+        for (int i = 0; i < SPT; ++i) {
+            const int idx = threadIdx.x + i * C::THREADS;
+            if (idx < NCH * rpw) stage[(idx / rpw) * (rpw + 1) + idx % rpw] = pf[i];
         }
         __syncthreads();
+        if (blk + (int)gridDim.x < nb * nblk) fetch(blk + gridDim.x);
         for (int pr = team; pr < rpw / 2; pr += TEAMS) {
             float2 x[E];
 #pragma unroll
