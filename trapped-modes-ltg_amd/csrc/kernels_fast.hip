@@ -47,9 +47,12 @@ constexpr int BLOCK = 256;
 #endif
 // The column kernels hold two transforms' worth of state (130-186 VGPRs
 // unconstrained): 3 waves/SIMD (168 VGPRs) up to 2048 points, 2 at 4096.
+#ifndef FCD_COL_WAVES
+#define FCD_COL_WAVES 2
+#endif
 template <int N>
 struct ColWaves {
-    static constexpr int V = N >= 4096 ? 2 : 3;
+    static constexpr int V = N >= 4096 ? 2 : FCD_COL_WAVES;
 };
 constexpr float kPiF = 3.14159265358979f;
 constexpr float kTwoPiF = 6.28318530717959f;
@@ -444,23 +447,38 @@ __global__ __launch_bounds__(KCfg<H>::THREADS, ColWaves<H>::V) void k_int_cols(c
     __syncthreads();
     const int NCH = W / 2 + 1;
     const int items = nb * NCH;
+    const int zmask = (1 << zts) - 1;
+    // Both columns of the NEXT item are loaded into registers while the current
+    // item is transformed (loads issued before the current item's stores).
+    float2 py[E], px[E];
+    auto fetch = [&](int item) {
+        const bool valid = item < items;
+        const int f = valid ? item / NCH : 0, col = valid ? item % NCH : 0;
+        const int colm = (W - col) & (W - 1);
+        const float2* src = Zt + (long)f * H * W;
+#pragma unroll
+        for (int q = 0; q < E; ++q) {
+            const int rr = t + TT * q;
+            const long tl = ((long)(rr >> zts) * W) << zts;
+            py[q] = src[tl + ((long)colm << zts) + (rr & zmask)];
+            px[q] = src[tl + ((long)col << zts) + (rr & zmask)];
+        }
+    };
+    fetch(blockIdx.x * TEAMS + team);
     for (int base = blockIdx.x * TEAMS; base < items; base += gridDim.x * TEAMS) {
         const int item = base + team;
         const bool valid = item < items;
         const int f = valid ? item / NCH : 0, col = valid ? item % NCH : 0;
         const int colm = (W - col) & (W - 1);
-        const float2* src = Zt + (long)f * H * W;
+        float2 x[E];
         {   // Z(:, -c) first, parked in s2 so only one column is live in registers
             float2 y[E];
 #pragma unroll
             for (int q = 0; q < E; ++q) {
-#ifdef FCD_EXP_ZT_ROWMAJOR
-                y[q] = src[(long)(t + TT * q) * W + colm];
-#else
-                const int rr = t + TT * q;
-                y[q] = src[((long)(rr >> zts) * W + colm) * (1 << zts) + (rr & ((1 << zts) - 1))];
-#endif
+                y[q] = py[q];
+                x[q] = px[q];
             }
+            if (base + gridDim.x * TEAMS < items) fetch(base + gridDim.x * TEAMS + team);
             if (colk && colm == 0) {  // column-0 unwrap offsets of the fused path: row DC bins
                 const float sc = 6.28318530717959f * (float)W;
 #pragma unroll
@@ -474,16 +492,6 @@ __global__ __launch_bounds__(KCfg<H>::THREADS, ColWaves<H>::V) void k_int_cols(c
             if constexpr (!Sched<H>::WAVE_LOCAL) __syncthreads();
 #pragma unroll
             for (int q = 0; q < E; ++q) s2[pad(t + TT * q)] = y[q];
-        }
-        float2 x[E];
-#pragma unroll
-        for (int q = 0; q < E; ++q) {
-#ifdef FCD_EXP_ZT_ROWMAJOR
-            x[q] = src[(long)(t + TT * q) * W + col];
-#else
-            const int rr = t + TT * q;
-            x[q] = src[((long)(rr >> zts) * W + col) * (1 << zts) + (rr & ((1 << zts) - 1))];
-#endif
         }
         if (colk && col == 0) {
             const float sc = 6.28318530717959f * (float)W;
