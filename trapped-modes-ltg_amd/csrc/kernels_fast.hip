@@ -102,14 +102,24 @@ __global__ __launch_bounds__(KCfg<W>::THREADS, FCD_MIN_WAVES) void k_demod_rows(
     __syncthreads();
     const int NC = T.NC;
     const int rbs = H / TILE;
-    for (int blk = blockIdx.x; blk < nb * rbs; blk += gridDim.x) {
+    // the next row pair of this team is loaded while the current one is transformed
+    float2 xn[E];
+    auto fetch = [&](int blk, int pr) {
         const int f = blk / rbs, rb = blk % rbs;
+        const float* ra = frames + ((long)f * H + rb * TILE + 2 * pr) * W;
+#pragma unroll
+        for (int q = 0; q < E; ++q) xn[q] = make_float2(ra[t + TT * q], ra[W + t + TT * q]);
+    };
+    if ((int)blockIdx.x < nb * rbs) fetch(blockIdx.x, team);
+    for (int blk = blockIdx.x; blk < nb * rbs; blk += gridDim.x) {
         for (int pr = team; pr < TILE / 2; pr += TEAMS) {
-            const int r = rb * TILE + 2 * pr;
-            const float* ra = frames + ((long)f * H + r) * W;
             float2 x[E];
 #pragma unroll
-            for (int q = 0; q < E; ++q) x[q] = make_float2(ra[t + TT * q], ra[W + t + TT * q]);
+            for (int q = 0; q < E; ++q) x[q] = xn[q];
+            if (pr + TEAMS < TILE / 2)
+                fetch(blk, pr + TEAMS);
+            else if (blk + (int)gridDim.x < nb * rbs)
+                fetch(blk + gridDim.x, team);
             fft.template run<false>(x, s, t);
             if constexpr (!Sched<W>::WAVE_LOCAL) __syncthreads();
 #pragma unroll
@@ -123,6 +133,7 @@ __global__ __launch_bounds__(KCfg<W>::THREADS, FCD_MIN_WAVES) void k_demod_rows(
                 stage[i * (TILE + 1) + 2 * pr + 1] = make_float2(0.5f * (zk.y + zm.y), -0.5f * (zk.x - zm.x));
             }
         }
+        const int f = blk / rbs, rb = blk % rbs;
         __syncthreads();
         float2* dst = Xb + (long)f * H * NC + (long)rb * NC * TILE;
         for (int idx = threadIdx.x; idx < NC * TILE; idx += C::THREADS)
