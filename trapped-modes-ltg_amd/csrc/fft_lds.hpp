@@ -16,10 +16,75 @@
 
 namespace fcdk {
 
+#ifndef FCD_PACKED
+#define FCD_PACKED 1  // complex arithmetic on packed-FP32 VALU ops (v_pk_add/mul/fma_f32: two lanes of work per op)
+#endif
+typedef float fv2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ fv2 pv(float2 a) { return fv2{a.x, a.y}; }
+__device__ __forceinline__ float2 vp(fv2 v) { return make_float2(v.x, v.y); }
+#if FCD_PACKED
+// The swaps and sign flips of complex products and of +-i multiplications are
+// VOP3P operand modifiers (op_sel / op_sel_hi / neg_lo / neg_hi); the compiler
+// does not fold a lane swap into them, so those forms are written out
+// (encodings checked on the GPU by tools/pktest.hip).
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return vp(pv(a) + pv(b)); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return vp(pv(a) - pv(b)); }
+// a * b
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+    fv2 t, r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(pv(a)), "v"(pv(b)));
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
+        : "=v"(r)
+        : "v"(pv(a)), "v"(pv(b)), "v"(t));
+    return vp(r);
+}
+// a * conj(b)
+__device__ __forceinline__ float2 cmulc(float2 a, float2 b) {
+    fv2 t, r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1] neg_hi:[0,1]" : "=v"(t) : "v"(pv(a)), "v"(pv(b)));
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1]" : "=v"(r) : "v"(pv(a)), "v"(pv(b)), "v"(t));
+    return vp(r);
+}
+// a + i b, a - i b
+__device__ __forceinline__ float2 caddi(float2 a, float2 b) {
+    fv2 r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(pv(a)), "v"(pv(b)));
+    return vp(r);
+}
+__device__ __forceinline__ float2 csubi(float2 a, float2 b) {
+    fv2 r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(pv(a)), "v"(pv(b)));
+    return vp(r);
+}
+// i a, -i a
+__device__ __forceinline__ float2 cmuli(float2 a) {
+    fv2 r;
+    asm("v_pk_add_f32 %0, 0, %1 op_sel:[0,1] op_sel_hi:[0,0] neg_lo:[0,1]" : "=v"(r) : "v"(pv(a)));
+    return vp(r);
+}
+__device__ __forceinline__ float2 cmulmi(float2 a) {
+    fv2 r;
+    asm("v_pk_add_f32 %0, 0, %1 op_sel:[0,1] op_sel_hi:[0,0] neg_hi:[0,1]" : "=v"(r) : "v"(pv(a)));
+    return vp(r);
+}
+#else
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
     return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ float2 cmulc(float2 a, float2 b) {
+    return make_float2(a.x * b.x + a.y * b.y, a.y * b.x - a.x * b.y);
+}
+__device__ __forceinline__ float2 caddi(float2 a, float2 b) { return make_float2(a.x - b.y, a.y + b.x); }
+__device__ __forceinline__ float2 csubi(float2 a, float2 b) { return make_float2(a.x + b.y, a.y - b.x); }
+__device__ __forceinline__ float2 cmuli(float2 a) { return make_float2(-a.y, a.x); }
+__device__ __forceinline__ float2 cmulmi(float2 a) { return make_float2(a.y, -a.x); }
+#endif
+// a * w (forward) or a * conj(w) (inverse) for a forward twiddle w
+template <bool INV>
+__device__ __forceinline__ float2 cmul_dir(float2 a, float2 w) {
+    return INV ? cmulc(a, w) : cmul(a, w);
 }
 __device__ __forceinline__ float2 cconj(float2 a) { return make_float2(a.x, -a.y); }
 __device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
@@ -61,24 +126,43 @@ __device__ __forceinline__ float2 twc(float2 v) {
     if constexpr (m == 0) {
         return v;
     } else if constexpr (m == 4) {
-        return INV ? make_float2(-v.y, v.x) : make_float2(v.y, -v.x);
+        return INV ? cmuli(v) : cmulmi(v);
     } else if constexpr (m == 8) {
         return make_float2(-v.x, -v.y);
     } else if constexpr (m == 12) {
-        return INV ? make_float2(v.y, -v.x) : make_float2(-v.y, v.x);
+        return INV ? cmulmi(v) : cmuli(v);
     } else {
         const float c = kC16[m];
         const float s = INV ? kS16[m] : -kS16[m];
+#if FCD_PACKED
+        const fv2 V = pv(v);
+        return vp(__builtin_elementwise_fma(V.yy, fv2{-s, c}, V.xx * fv2{c, s}));
+#else
         return make_float2(v.x * c - v.y * s, v.x * s + v.y * c);
+#endif
     }
 }
 
 template <int R, int K, bool INV>
 __device__ __forceinline__ void dft_combine(float2* a, const float2* e, const float2* o) {
     if constexpr (K < R / 2) {
-        const float2 t = twc<R, K, INV>(o[K]);
-        a[K] = cadd(e[K], t);
-        a[K + R / 2] = csub(e[K], t);
+        constexpr int m = (K * (16 / R)) & 15;
+        if constexpr (m == 4 || m == 12) {  // W = -+i: the product folds into the add
+            if constexpr ((m == 4) != INV) {
+                a[K] = csubi(e[K], o[K]);
+                a[K + R / 2] = caddi(e[K], o[K]);
+            } else {
+                a[K] = caddi(e[K], o[K]);
+                a[K + R / 2] = csubi(e[K], o[K]);
+            }
+        } else if constexpr (m == 8) {
+            a[K] = csub(e[K], o[K]);
+            a[K + R / 2] = cadd(e[K], o[K]);
+        } else {
+            const float2 t = twc<R, K, INV>(o[K]);
+            a[K] = cadd(e[K], t);
+            a[K + R / 2] = csub(e[K], t);
+        }
         dft_combine<R, K + 1, INV>(a, e, o);
     }
 }
@@ -86,11 +170,11 @@ __device__ __forceinline__ void dft_combine(float2* a, const float2* e, const fl
 template <bool INV>
 __device__ __forceinline__ void bfly4(float2& a0, float2& a1, float2& a2, float2& a3) {
     const float2 t0 = cadd(a0, a2), t1 = csub(a0, a2), t2 = cadd(a1, a3), t3 = csub(a1, a3);
-    const float2 u3 = INV ? make_float2(-t3.y, t3.x) : make_float2(t3.y, -t3.x);  // (+/-i) * t3
     a0 = cadd(t0, t2);
     a2 = csub(t0, t2);
-    a1 = cadd(t1, u3);
-    a3 = csub(t1, u3);
+    // a1 = t1 + u3, a3 = t1 - u3 with u3 = (-/+i) t3
+    a1 = INV ? caddi(t1, t3) : csubi(t1, t3);
+    a3 = INV ? csubi(t1, t3) : caddi(t1, t3);
 }
 
 template <int R, int R1, int N1, int K2, bool INV>
@@ -175,8 +259,7 @@ __device__ __forceinline__ void stockham_pass(float2* s, const float2* __restric
 #pragma unroll
             for (int r = 1; r < R; ++r) {
                 float2 w = tw[r * k * step];
-                if (INV) w.y = -w.y;
-                a[b][r] = cmul(a[b][r], w);
+                a[b][r] = cmul_dir<INV>(a[b][r], w);
             }
         }
         dft_reg<R, INV>(a[b]);

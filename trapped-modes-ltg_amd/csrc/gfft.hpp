@@ -118,7 +118,7 @@ struct GroupFFT {
 #pragma unroll
                 for (int r = 1; r < R; ++r) {
                     const float2 w = tw[S::REGOFF(P) + b * (R - 1) + r - 1];
-                    a[b][r] = INV ? cmul(a[b][r], make_float2(w.x, -w.y)) : cmul(a[b][r], w);
+                    a[b][r] = cmul_dir<INV>(a[b][r], w);
                 }
             }
             dft_reg<R, INV>(a[b]);
@@ -163,7 +163,7 @@ struct GroupFFT {
 #pragma unroll
                 for (int r = 1; r < R; ++r) {
                     const float2 w = tw[S::REGOFF(P) + b * (R - 1) + r - 1];
-                    a[b][r] = INV ? cmul(a[b][r], make_float2(w.x, -w.y)) : cmul(a[b][r], w);
+                    a[b][r] = cmul_dir<INV>(a[b][r], w);
                 }
             }
             dft_reg<R, INV>(a[b]);
@@ -219,7 +219,7 @@ struct GroupFFTTab {
 #pragma unroll
                 for (int r = 1; r < R; ++r) {
                     const float2 w = tk[r];
-                    a[b][r] = INV ? cmul(a[b][r], make_float2(w.x, -w.y)) : cmul(a[b][r], w);
+                    a[b][r] = cmul_dir<INV>(a[b][r], w);
                 }
             }
             dft_reg<R, INV>(a[b]);

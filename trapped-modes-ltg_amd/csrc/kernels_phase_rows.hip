@@ -41,7 +41,12 @@ namespace {
 
 constexpr int PR_W = 1024;            // row length of the fused kernel
 constexpr int PR_B = 128;             // band window
-constexpr int PR_ROWS = 8;            // output rows per tile (Zt tile height)
+#ifndef FCD_PR_ROWS
+#define FCD_PR_ROWS 8
+#endif
+constexpr int PR_ROWS = FCD_PR_ROWS;  // rows per tile (one wave each)
+constexpr int PR_ZT = 8;              // Zt tile height (int_rows.inc zt_rows(1024))
+static_assert(PR_ZT % PR_ROWS == 0, "a tile covers part of one Zt tile");
 constexpr int PR_WAVES = PR_ROWS;     // one wave per row
 constexpr int PR_THREADS = 64 * PR_WAVES;
 constexpr int PR_G = PR_B / 16, PR_L = PR_W / PR_B;
@@ -54,7 +59,8 @@ constexpr int OFF_PRE = OFF_STAGE + 2 * PR_B * PR_SROW;        // [16][64] pre-t
 constexpr int OFF_ZTAB = OFF_PRE + 16 * 64;                    // z-FFT twiddles
 constexpr int OFF_BTAB = OFF_ZTAB + PR_ZTAB;                   // band-FFT twiddles
 constexpr int OFF_SLOT = (OFF_BTAB + GSched<PR_B>::TABLE + 1) & ~1;  // 16-byte aligned slots
-constexpr size_t PR_LDS = (size_t)(OFF_SLOT + PR_WAVES * PR_SLOT) * 8;
+constexpr int OFF_PREV = OFF_SLOT + PR_WAVES * PR_SLOT;              // last unwrapped row of the previous tile
+constexpr size_t PR_LDS = (size_t)(OFF_PREV + PR_SLOT) * 8;
 static_assert(PR_LDS <= 160 * 1024, "fused kernel LDS");
 static_assert(PR_L * GSched<PR_B>::REGION <= PR_SLOT, "band exchange must fit the slot");
 
@@ -75,11 +81,26 @@ __device__ __forceinline__ int fw_exact(float a, float b) {
 
 }  // namespace
 
+#ifdef FCD_STAMPS
+// diagnostic: per-phase cycle totals of block 0, per wave (tools/prstamp.cpp)
+__device__ unsigned long long g_pr_stamps[PR_WAVES * 16];
+#define PR_STAMP(i)                                                    \
+    do {                                                               \
+        const unsigned long long t_ = __builtin_readcyclecounter();   \
+        ph[(i)] += t_ - tprev;                                         \
+        tprev = t_;                                                    \
+    } while (0)
+#else
+#define PR_STAMP(i) \
+    do {            \
+    } while (0)
+#endif
+
 template <bool UNWRAP>
 __global__ __launch_bounds__(PR_THREADS) void k_phase_rows(
     const float2* __restrict__ Ab, int H, int nb, int NCA, int ncc0, int ncc1, const float* __restrict__ theta,
     const float2* __restrict__ pre, const float2* __restrict__ ptw, const float2* __restrict__ ztw,
-    float* __restrict__ col0, int* __restrict__ flags, float2* __restrict__ Zt, float2* __restrict__ seam) {
+    float* __restrict__ col0, int* __restrict__ flags, float2* __restrict__ Zt, float2* __restrict__ seam, int per) {
     extern __shared__ __attribute__((aligned(16))) float2 lds_p[];
     float2* const stage = lds_p + OFF_STAGE;
     float2* const ptl = lds_p + OFF_PRE;
@@ -87,42 +108,58 @@ __global__ __launch_bounds__(PR_THREADS) void k_phase_rows(
     float2* const btab = lds_p + OFF_BTAB;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int g = lane / PR_G, t = lane % PR_G;  // band group / lane in group
-    float2* const slot = lds_p + OFF_SLOT + wave * PR_SLOT;
+    // LDS slot of row w of the tile (PR_SLOT float2, padded): the last row
+    // alternates between two slots, so the previous tile's last unwrapped row
+    // survives for the census against this tile's first row (k = tile parity)
+    auto row_slot = [&](int w, int k) {
+        return lds_p + (w == PR_ROWS - 1 && k ? OFF_PREV : OFF_SLOT + w * PR_SLOT);
+    };
     for (int i = threadIdx.x; i < GSched<PR_B>::TABLE; i += PR_THREADS) btab[i] = ptw[i];
     for (int i = threadIdx.x; i < 16 * 64; i += PR_THREADS) ptl[(i % 16) * 64 + i / 16] = pre[i];
     for (int i = threadIdx.x; i < PR_ZTAB; i += PR_THREADS) ztab[i] = ztw[i];
     const int rbs = H / PR_ROWS;
     const int items = nb * rbs;
     const int tiles16 = H / 16;
-    // staged band values of the next item, prefetched into registers
-    constexpr int NST = 2 * PR_B * PR_SROW;              // (carrier, slot, row) entries, SROW-pitched
+    // this block's contiguous range of tiles: consecutive tiles of a frame are
+    // checked against each other here, only the range edges go to k_seam_check
+    const int it0 = blockIdx.x * per, it1 = min(it0 + per, items);
+    // staged band values of the next item, prefetched into registers: entry
+    // e = (c, j, row) with row fastest, 8 rows = one 64-byte run of Ab's 16-row tile
+    constexpr int NST = 2 * PR_B * PR_ROWS;
     constexpr int SPT = (NST + PR_THREADS - 1) / PR_THREADS;
     float2 pf[SPT];
     auto fetch = [&](int blk) {
         const int f = blk / rbs, rb = blk % rbs;
+        const int r = rb * PR_ROWS + (threadIdx.x % PR_ROWS);
 #pragma unroll
         for (int i = 0; i < SPT; ++i) {
             const int e = threadIdx.x + i * PR_THREADS;
-            const int c = e / (PR_B * PR_SROW), rem = e % (PR_B * PR_SROW), j = rem / PR_SROW, rr = rem % PR_SROW;
-            const int r = min(rb * PR_ROWS + rr, H - 1);
-            const int ncc = c ? ncc1 : ncc0;
+            const int c = e / (PR_B * PR_ROWS), j = (e / PR_ROWS) % PR_B;
             float2 v = make_float2(0.f, 0.f);
-            if (e < NST && j < ncc && rr < PR_ROWS)
+            if ((NST % PR_THREADS == 0 || e < NST) && j < (c ? ncc1 : ncc0))
                 v = Ab[((((long)f * 2 + c) * tiles16 + (r >> 4)) * NCA + j) * 16 + (r & 15)];
             pf[i] = v;
         }
     };
-    if ((int)blockIdx.x < items) fetch(blockIdx.x);
-    for (int blk = blockIdx.x; blk < items; blk += gridDim.x) {
+    if (it0 < it1) fetch(it0);
+#ifdef FCD_STAMPS
+    unsigned long long ph[16] = {}, tprev = __builtin_readcyclecounter();
+#endif
+    for (int blk = it0; blk < it1; ++blk) {
         const int f = blk / rbs, rb = blk % rbs;
         const int r = rb * PR_ROWS + wave;           // this wave's row
+        const int par = (blk - it0) & 1;
+        float2* const slot = row_slot(wave, par);    // band exchange, unwrapped row
+        PR_STAMP(0);
 #pragma unroll
         for (int i = 0; i < SPT; ++i) {
             const int e = threadIdx.x + i * PR_THREADS;
-            if (e < NST) stage[e] = pf[i];  // stage[(c*B + j)*SROW + row]
+            if (NST % PR_THREADS == 0 || e < NST) stage[(e / PR_ROWS) * PR_SROW + e % PR_ROWS] = pf[i];
         }
         __syncthreads();
-        if (blk + (int)gridDim.x < items) fetch(blk + gridDim.x);
+        PR_STAMP(1);
+        if (blk + 1 < it1) fetch(blk + 1);
+        PR_STAMP(2);
         // ---- band transforms of both carriers -> wrapped phases (natural strided)
         float w0[16], w1[16];
         {
@@ -147,6 +184,7 @@ __global__ __launch_bounds__(PR_THREADS) void k_phase_rows(
                     else
                         w1[q] = wq;
                 }
+                PR_STAMP(3 + c);
             }
         }
         // ---- natural strided -> blocked through the slot
@@ -189,7 +227,7 @@ __global__ __launch_bounds__(PR_THREADS) void k_phase_rows(
             }
         }
         if constexpr (UNWRAP) {  // first and last unwrapped rows of the tile -> seam buffer (k_seam_check)
-            if (wave == 0 || wave == PR_ROWS - 1) {
+            if ((wave == 0 && blk == it0 && rb > 0) || (wave == PR_ROWS - 1 && blk == it1 - 1 && rb < rbs - 1)) {
                 float4* sd = reinterpret_cast<float4*>(seam + (((long)f * (H / PR_ROWS) + rb) * 2 + (wave ? 1 : 0)) * PR_W +
                                                        j0);
 #pragma unroll
@@ -199,57 +237,76 @@ __global__ __launch_bounds__(PR_THREADS) void k_phase_rows(
                 }
             }
         }
+        PR_STAMP(5);
         __syncthreads();
+        PR_STAMP(6);
         // ---- vertical census against the next row of the tile (seams: k_seam_check)
         if constexpr (UNWRAP) {
-            if (wave < PR_ROWS - 1) {
-                const float2* nx = slot + PR_SLOT;
-                const float2 a0 = slot[0], b0 = nx[0];  // phi'(r, 0) = w(r, 0)
+            if (wave < PR_ROWS - 1 || (blk > it0 && rb > 0)) {
+                // rows (wave, wave + 1); the last wave: the previous tile's last row and row 0
+                const bool up = wave == PR_ROWS - 1;
+                const float2* a_row = up ? row_slot(PR_ROWS - 1, par ^ 1) : slot;
+                const float2* nx = up ? row_slot(0, 0) : row_slot(wave + 1, par);
+                const float2 a0 = a_row[0], b0 = nx[0];  // phi'(r, 0) = w(r, 0)
                 const float d0 = kTwoPiF * (float)(-fw_exact(a0.x, b0.x));
                 const float d1 = kTwoPiF * (float)(-fw_exact(a0.y, b0.y));
 #pragma unroll
                 for (int j = 0; j < 16; ++j) {
-                    const float2 a = slot[pad(j0 + j)], b = nx[pad(j0 + j)];
+                    const float2 a = a_row[pad(j0 + j)], b = nx[pad(j0 + j)];
                     bad |= (int)(fabsf(b.x - a.x + d0) > kPR_VLim) | (int)(fabsf(b.y - a.y + d1) > kPR_VLim);
                 }
             }
             if (__any(bad) && lane == 0) atomicOr(flags + f * 2, 1);
+            PR_STAMP(7);
             __syncthreads();  // every census read of the next slot precedes that row's FFT
         }
+        PR_STAMP(8);
         // ---- forward row FFT of phi0' + i phi1'
         {
             __builtin_amdgcn_sched_barrier(0);
             float2 x[16];
 #pragma unroll
             for (int q = 0; q < 16; ++q) x[q] = slot[pad(lane + 64 * q)];
-            GroupFFTTab<PR_W>::template run<false>(x, slot, lane, ztab);
+            // the last row transforms in its other slot (the previous tile's row,
+            // no longer needed): its unwrapped row stays for the next census
+            float2* const zs = row_slot(wave, par ^ 1);
+            GroupFFTTab<PR_W>::template run<false>(x, zs, lane, ztab);
             wave_sync();
 #pragma unroll
-            for (int q = 0; q < 16; ++q) slot[pad(lane + 64 * q)] = x[q];
+            for (int q = 0; q < 16; ++q) zs[pad(lane + 64 * q)] = x[q];
         }
+        PR_STAMP(9);
         __syncthreads();
+        PR_STAMP(10);
         // ---- whole 64-byte tile lines: Zt[f][rb][col][0..8)
-        float2* dst = Zt + (long)f * H * PR_W + (long)rb * PR_W * PR_ROWS;
-        {  // 512 threads: thread i writes column (i >> 3) + 64 k, row i & 7
-            const int c0 = threadIdx.x >> 3, rl = threadIdx.x & 7;
-            const float2* src = lds_p + OFF_SLOT + rl * PR_SLOT;
+        {  // thread i writes column i / ROWS + 64 k, row i % ROWS
+            const int r0 = rb * PR_ROWS;
+            float2* dst = Zt + (long)f * H * PR_W + (long)(r0 / PR_ZT) * PR_W * PR_ZT + (r0 % PR_ZT);
+            const int c0 = threadIdx.x / PR_ROWS, rl = threadIdx.x % PR_ROWS;
+            const float2* src = row_slot(rl, par ^ 1);
 #pragma unroll 4
-            for (int k = 0; k < PR_W * PR_ROWS / 512; ++k) dst[threadIdx.x + 512 * k] = src[pad(c0 + 64 * k)];
+            for (int k = 0; k < PR_W / 64; ++k) dst[(c0 + 64 * k) * PR_ZT + rl] = src[pad(c0 + 64 * k)];
         }
+        PR_STAMP(11);
         __syncthreads();
+        PR_STAMP(12);
     }
+#ifdef FCD_STAMPS
+    if (blockIdx.x == 0 && lane == 0)
+        for (int i = 0; i < 16; ++i) g_pr_stamps[wave * 16 + i] = ph[i];
+#endif
 }
 
-// Census of the edges between tiles: row 8b+7 (last of tile b) against row
-// 8b+8 (first of tile b+1), both unwrapped without their column-0 offsets.
-// One wave per seam; lane L holds pixels 16L .. 16L+15.
-__global__ __launch_bounds__(256) void k_seam_check(const float2* __restrict__ seam, int H, int nb,
+// Census of the edges between the tile ranges of k_phase_rows' blocks (the
+// edges inside a range are checked there): the last row of tile it - 1 against
+// the first row of tile it, it = k * per, both unwrapped without their
+// column-0 offsets.  One wave per range edge; lane L holds pixels 16L .. 16L+15.
+__global__ __launch_bounds__(256) void k_seam_check(const float2* __restrict__ seam, int H, int nb, int per,
                                                     int* __restrict__ flags) {
     const int rbs = H / PR_ROWS;
-    const long seams = (long)nb * (rbs - 1);
-    const long sidx = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (sidx >= seams) return;
-    const int f = (int)(sidx / (rbs - 1)), b = (int)(sidx % (rbs - 1));
+    const long it = ((long)blockIdx.x * 4 + (threadIdx.x >> 6) + 1) * per;
+    if (it >= (long)nb * rbs || it % rbs == 0) return;
+    const int f = (int)(it / rbs), b = (int)(it % rbs) - 1;
     const int lane = threadIdx.x & 63;
     const float4* a = reinterpret_cast<const float4*>(seam + (((long)f * rbs + b) * 2 + 1) * PR_W + lane * 16);
     const float4* c = reinterpret_cast<const float4*>(seam + (((long)f * rbs + b + 1) * 2 + 0) * PR_W + lane * 16);
@@ -273,6 +330,12 @@ __global__ __launch_bounds__(256) void k_seam_check(const float2* __restrict__ s
     if (__any(bad) && lane == 0) atomicOr(flags + f * 2, 1);
 }
 
+#ifdef FCD_STAMPS
+extern "C" int fcd_debug_pr_stamps(unsigned long long* out) {
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pr_stamps), sizeof(g_pr_stamps));
+}
+#endif
+
 bool phase_rows_supported(int W, int B, int H) { return W == PR_W && B == PR_B && H % 16 == 0 && H >= 16; }
 
 int phase_rows_tile() { return PR_ROWS; }
@@ -288,21 +351,25 @@ void phase_rows(bool unwrap, const float2* Ab, int H, int nb, int NCA, int ncc0,
         if (!ncu) ncu = 256;
     }
     const long items = (long)nb * (H / PR_ROWS);
-    const int grid = (int)std::min<long>(items, ncu);
-    if (grid <= 0) return;
+    const int per_cu = std::max<int>(1, std::min<int>(160 * 1024 / (int)PR_LDS, 16 / PR_WAVES));
+    const int slots = (int)std::min<long>(items, (long)ncu * per_cu);
+    if (slots <= 0) return;
+    const int per = (int)((items + slots - 1) / slots);  // tiles per block, a contiguous range
+    const int grid = (int)((items + per - 1) / per);
     if (unwrap) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_phase_rows<true>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)PR_LDS);
         hipLaunchKernelGGL(k_phase_rows<true>, dim3(grid), dim3(PR_THREADS), PR_LDS, s, Ab, H, nb, NCA, ncc0, ncc1,
-                           theta, pre, ptw, ztw, col0, flags, Zt, seam);
-        const long seams = (long)nb * (H / PR_ROWS - 1);
-        if (seams > 0)
-            hipLaunchKernelGGL(k_seam_check, dim3((unsigned)((seams + 3) / 4)), dim3(256), 0, s, seam, H, nb, flags);
+                           theta, pre, ptw, ztw, col0, flags, Zt, seam, per);
+        const int edges = grid - 1;  // range edges (those at frame starts return at once)
+        if (edges > 0)
+            hipLaunchKernelGGL(k_seam_check, dim3((unsigned)((edges + 3) / 4)), dim3(256), 0, s, seam, H, nb, per,
+                               flags);
     } else {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_phase_rows<false>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)PR_LDS);
         hipLaunchKernelGGL(k_phase_rows<false>, dim3(grid), dim3(PR_THREADS), PR_LDS, s, Ab, H, nb, NCA, ncc0, ncc1,
-                           theta, pre, ptw, ztw, col0, flags, Zt, seam);
+                           theta, pre, ptw, ztw, col0, flags, Zt, seam, per);
     }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) throw std::runtime_error(std::string("phase_rows launch: ") + hipGetErrorString(e));

@@ -109,7 +109,7 @@ struct RegFFT {
 #pragma unroll
                 for (int r = 1; r < R; ++r) {
                     const float2 w = twk[r];
-                    a[b][r] = INV ? cmul(a[b][r], make_float2(w.x, -w.y)) : cmul(a[b][r], w);
+                    a[b][r] = cmul_dir<INV>(a[b][r], w);
                 }
             }
             dft_reg<R, INV>(a[b]);

@@ -11,6 +11,9 @@
 #include <vector>
 
 #include "../csrc/kernels.hpp"
+#ifdef FCD_STAMPS
+extern "C" int fcd_debug_pr_stamps(unsigned long long* out);
+#endif
 
 #define CK(x)                                                                 \
     do {                                                                      \
@@ -141,10 +144,24 @@ int main(int argc, char** argv) {
             float2* ztw = dalloc<float2>(N);
             CK(hipMemcpy(ztw, ones.data(), N * 8, hipMemcpyHostToDevice));
             float* col0 = dalloc<float>((size_t)nb * 2 * H);
-            float2* seam = dalloc<float2>((size_t)nb * (H / 8) * 2 * W);
+            float2* seam = dalloc<float2>((size_t)nb * (H / fcdk::phase_rows_tile()) * 2 * W);
             timeit("phase_rows (fused)", 16.0 * H * NCA + 2 * f, [&] {
                 fcdk::phase_rows(true, Ab, H, nb, NCA, NCc, NCc, theta, pre, ptw, ztw, col0, res, Zt, seam, s);
             });
+#ifdef FCD_STAMPS
+            {
+                std::vector<unsigned long long> st(8 * 16);
+                CK(hipDeviceSynchronize());
+                fcd_debug_pr_stamps(st.data());
+                const char* names[13] = {"loop", "stage+bar", "fetch", "band0", "band1", "unwrap", "bar1",
+                                         "census", "bar2", "zfft", "bar3", "writeout", "bar4"};
+                for (int w = 0; w < 8; ++w) {
+                    printf("wave %d:", w);
+                    for (int i = 0; i < 13; ++i) printf(" %s=%llu", names[i], st[w * 16 + i]);
+                    printf("\n");
+                }
+            }
+#endif
         }
     }
     timeit("colk", 8.0 * H, [&] { fcdk::unwrap_colk(wrapped, 2 * nb, H, W, colk, s); });
