@@ -184,6 +184,7 @@ struct fcd_ctx {
     DevBuf Xb, Ab, Zt, Ht, fk, fres; // per-chunk intermediates; fk: k-fields for the fix-up pass
     int band_B = 0;                  // band window of the pruned inverse (0: full-length k_demod_phase)
     DevBuf band_pre, band_ptw, theta_b;  // its pre-twiddles, pass twiddles, reference angle of the band
+    DevBuf theta_p;                      // theta_b in k_phase_rows' lane-contiguous order
     bool fused_ok = false;           // k_phase_rows applies (height-only calls)
     bool force_unfused = false;      // FCD_UNFUSED=1: take the unfused chain (A/B measurement)
     DevBuf ztw, col0, seam;          // its 1024-point group-FFT twiddles; column-0 wrapped values [f][2][H];
@@ -597,6 +598,7 @@ void build_demod_tables(fcd_ctx* c, hipStream_t s) {
     c->fused_ok = c->band_B && fcdk::phase_rows_supported(W, c->band_B, H);
     std::vector<float2> ztw;
     if (c->fused_ok) {
+        c->theta_p.ensure(2 * (size_t)c->hw() * sizeof(float));
         ztw = group_twiddles(W);
         c->ztw.ensure(ztw.size() * sizeof(float2));
         upload(c->ztw.p, ztw.data(), ztw.size() * sizeof(float2), s);
@@ -659,6 +661,7 @@ void band_reference(fcd_ctx* c, const float* dref, hipStream_t s) {
     fcdk::demod_cols(c->H, c->Xb.as<float2>(), 1, T, c->Ab.as<float2>(), c->NCA, c->twp_col.as<float2>(), s);
     fcdk::band_phase(c->W, c->band_B, true, c->Ab.as<float2>(), c->H, 1, c->NCA, c->NCc[0], c->NCc[1], nullptr,
                      c->theta_b.as<float>(), c->band_pre.as<float2>(), c->band_ptw.as<float2>(), s);
+    if (c->fused_ok) fcdk::phase_rows_theta(c->theta_b.as<float>(), c->H, c->theta_p.as<float>(), s);
 }
 
 }  // namespace
@@ -888,7 +891,7 @@ FCD_API int fcd_process(fcd_ctx* c, const float* frames, int n_frames, int flags
                                  s);
                 if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
                 fcdk::phase_rows(unwrap != 0, c->Ab.as<float2>(), c->H, nb, c->NCA, c->NCc[0], c->NCc[1],
-                                 c->theta_b.as<float>(), c->band_pre.as<float2>(), c->band_ptw.as<float2>(),
+                                 c->theta_p.as<float>(), c->band_pre.as<float2>(), c->band_ptw.as<float2>(),
                                  c->ztw.as<float2>(), c->col0.as<float>(), res ? res + (size_t)f0 * 2 : nullptr,
                                  c->Zt.as<float2>(), c->seam.as<float2>(), s);
                 if (unwrap) fcdk::unwrap_colk_compact(c->col0.as<float>(), 2 * nb, c->H, c->colk.as<int>(), s);

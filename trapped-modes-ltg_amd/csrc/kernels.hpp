@@ -73,6 +73,8 @@ void unwrap_colk(const float* w, int nmaps, int H, int W, int* colk, hipStream_t
 void unwrap_colk_compact(const float* col0, int nmaps, int H, int* colk, hipStream_t s);
 // fused band transform + phase + unwrap + z-row FFT (kernels_phase_rows.hip)
 bool phase_rows_supported(int W, int B, int H);
+// theta [2][H][W] -> the lane-contiguous copy phase_rows reads (its `theta`)
+void phase_rows_theta(const float* theta, int H, float* thp, hipStream_t s);
 int phase_rows_tile();
 void phase_rows(bool unwrap, const float2* Ab, int H, int nb, int NCA, int ncc0, int ncc1, const float* theta,
                 const float2* pre, const float2* ptw, const float2* ztw, float* col0, int* flags, float2* Zt,

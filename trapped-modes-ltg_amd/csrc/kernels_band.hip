@@ -114,7 +114,7 @@ __global__ __launch_bounds__((BPCfg<W, B>::THREADS), FCD_BAND_WAVES) void k_band
         fetch(blockIdx.x);
         th_load(blockIdx.x, team);
     }
-    int st = 0;
+    [[maybe_unused]] int st = 0;
     for (int blk = blockIdx.x; blk < items; blk += gridDim.x) {
         const int f = blk / (2 * rbs), c = (blk / rbs) % 2, rb = blk % rbs;
         const int ncc = c ? ncc1 : ncc0;

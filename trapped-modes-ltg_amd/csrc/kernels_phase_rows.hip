@@ -163,12 +163,25 @@ __global__ __launch_bounds__(PR_THREADS) void k_phase_rows(
         // ---- band transforms of both carriers -> wrapped phases (natural strided)
         float w0[16], w1[16];
         {
-            const int rr = r;
+            // the reference angles of this lane's 16 pixels, both carriers, issued
+            // before the transforms: lane-contiguous in the permuted copy
+            float4 th4[2][4];
 #pragma unroll
             for (int c = 0; c < 2; ++c) {
-                float th[16];  // issued before the transform: the latency hides behind it
+                const float4* tp = reinterpret_cast<const float4*>(theta + ((long)c * H + r) * PR_W) + lane * 4;
 #pragma unroll
-                for (int q = 0; q < 16; ++q) th[q] = theta[((long)c * H + rr) * PR_W + g + PR_L * t + 64 * q];
+                for (int k = 0; k < 4; ++k) th4[c][k] = tp[k];
+            }
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                float th[16];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    th[4 * k] = th4[c][k].x;
+                    th[4 * k + 1] = th4[c][k].y;
+                    th[4 * k + 2] = th4[c][k].z;
+                    th[4 * k + 3] = th4[c][k].w;
+                }
                 float2 x[16];
 #pragma unroll
                 for (int q = 0; q < 16; ++q)
@@ -335,6 +348,25 @@ extern "C" int fcd_debug_pr_stamps(unsigned long long* out) {
     return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pr_stamps), sizeof(g_pr_stamps));
 }
 #endif
+
+// theta [2][H][W] (natural) -> the fused kernel's lane-contiguous copy: row
+// element g + L t + 64 q (lane = G g + t) at lane * 16 + q.
+__global__ __launch_bounds__(256) void k_theta_lanes(const float* __restrict__ theta, int rows,
+                                                     float* __restrict__ thp) {
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;  // destination index
+    if (i >= (long)rows * PR_W) return;
+    const long row = i / PR_W;
+    const int e = (int)(i % PR_W), lane = e / 16, q = e % 16;
+    const int g = lane / PR_G, t = lane % PR_G;
+    thp[i] = theta[row * PR_W + g + PR_L * t + 64 * q];
+}
+
+void phase_rows_theta(const float* theta, int H, float* thp, hipStream_t s) {
+    const long n = 2L * H * PR_W;
+    hipLaunchKernelGGL(k_theta_lanes, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, theta, 2 * H, thp);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) throw std::runtime_error(std::string("phase_rows_theta launch: ") + hipGetErrorString(e));
+}
 
 bool phase_rows_supported(int W, int B, int H) { return W == PR_W && B == PR_B && H % 16 == 0 && H >= 16; }
 
