@@ -184,7 +184,7 @@ struct fcd_ctx {
     DevBuf Xb, Ab, Zt, Ht, fk, fres; // per-chunk intermediates; fk: k-fields for the fix-up pass
     int band_B = 0;                  // band window of the pruned inverse (0: full-length k_demod_phase)
     DevBuf band_pre, band_ptw, theta_b;  // its pre-twiddles, pass twiddles, reference angle of the band
-    DevBuf theta_p;                      // theta_b in k_phase_rows' lane-contiguous order
+    DevBuf theta_p;                      // theta_b in the phase kernels' lane-contiguous order
     bool fused_ok = false;           // k_phase_rows applies (height-only calls)
     bool force_unfused = false;      // FCD_UNFUSED=1: take the unfused chain (A/B measurement)
     DevBuf ztw, col0, seam;          // its 1024-point group-FFT twiddles; column-0 wrapped values [f][2][H];
@@ -594,11 +594,11 @@ void build_demod_tables(fcd_ctx* c, hipStream_t s) {
         upload(c->band_pre.p, pre.data(), pre.size() * sizeof(float2), s);
         upload(c->band_ptw.p, ptw.data(), ptw.size() * sizeof(float2), s);
         c->theta_b.ensure(2 * (size_t)c->hw() * sizeof(float));
+        c->theta_p.ensure(2 * (size_t)c->hw() * sizeof(float));
     }
     c->fused_ok = c->band_B && fcdk::phase_rows_supported(W, c->band_B, H);
     std::vector<float2> ztw;
     if (c->fused_ok) {
-        c->theta_p.ensure(2 * (size_t)c->hw() * sizeof(float));
         ztw = group_twiddles(W);
         c->ztw.ensure(ztw.size() * sizeof(float2));
         upload(c->ztw.p, ztw.data(), ztw.size() * sizeof(float2), s);
@@ -645,7 +645,7 @@ void fast_demod(fcd_ctx* c, const float* frames, int nb, hipStream_t s) {
     fcdk::demod_cols(c->H, c->Xb.as<float2>(), nb, T, c->Ab.as<float2>(), c->NCA, c->twp_col.as<float2>(), s);
     if (c->band_B)
         fcdk::band_phase(c->W, c->band_B, false, c->Ab.as<float2>(), c->H, nb, c->NCA, c->NCc[0], c->NCc[1],
-                         c->theta_b.as<float>(), c->wrapped.as<float>(), c->band_pre.as<float2>(),
+                         c->theta_p.as<float>(), c->wrapped.as<float>(), c->band_pre.as<float2>(),
                          c->band_ptw.as<float2>(), s);
     else
         fcdk::demod_phase(c->W, c->Ab.as<float2>(), c->H, nb, c->NCA, T, c->theta.as<float>(), c->wrapped.as<float>(),
@@ -661,7 +661,7 @@ void band_reference(fcd_ctx* c, const float* dref, hipStream_t s) {
     fcdk::demod_cols(c->H, c->Xb.as<float2>(), 1, T, c->Ab.as<float2>(), c->NCA, c->twp_col.as<float2>(), s);
     fcdk::band_phase(c->W, c->band_B, true, c->Ab.as<float2>(), c->H, 1, c->NCA, c->NCc[0], c->NCc[1], nullptr,
                      c->theta_b.as<float>(), c->band_pre.as<float2>(), c->band_ptw.as<float2>(), s);
-    if (c->fused_ok) fcdk::phase_rows_theta(c->theta_b.as<float>(), c->H, c->theta_p.as<float>(), s);
+    fcdk::band_theta_lanes(c->W, c->band_B, c->theta_b.as<float>(), 2 * c->H, c->theta_p.as<float>(), s);
 }
 
 }  // namespace

@@ -64,6 +64,9 @@ void int_c2r(int W, const float2* Ht, int H, int nb, float* h, const float2* tw,
 int c2r_rows_per_block(int W);
 // band-pruned inverse row transform + phase (kernels_band.hip): B-point window
 // of the carrier band, W/B pre-twiddled group transforms per row.
+// theta [rows][W] (band_phase REF output) -> the lane-contiguous copy that
+// band_phase (REF = false) and phase_rows read as their `theta`
+void band_theta_lanes(int W, int B, const float* theta, int rows, float* thp, hipStream_t s);
 bool band_supported(int W, int B);
 void band_phase(int W, int B, bool ref, const float2* Ab, int H, int nb, int NCA, int ncc0, int ncc1,
                 const float* theta, float* out, const float2* pre, const float2* ptw, hipStream_t s);
@@ -73,8 +76,6 @@ void unwrap_colk(const float* w, int nmaps, int H, int W, int* colk, hipStream_t
 void unwrap_colk_compact(const float* col0, int nmaps, int H, int* colk, hipStream_t s);
 // fused band transform + phase + unwrap + z-row FFT (kernels_phase_rows.hip)
 bool phase_rows_supported(int W, int B, int H);
-// theta [2][H][W] -> the lane-contiguous copy phase_rows reads (its `theta`)
-void phase_rows_theta(const float* theta, int H, float* thp, hipStream_t s);
 int phase_rows_tile();
 void phase_rows(bool unwrap, const float2* Ab, int H, int nb, int NCA, int ncc0, int ncc1, const float* theta,
                 const float2* pre, const float2* ptw, const float2* ztw, float* col0, int* flags, float2* Zt,

@@ -101,13 +101,20 @@ __global__ __launch_bounds__((BPCfg<W, B>::THREADS), FCD_BAND_WAVES) void k_band
     // theta of the NEXT row this wave handles is loaded before the current row's
     // stores: vmcnt counts loads and stores in issue order, so a load issued after
     // a store batch cannot be waited for without waiting for those stores too.
+    // theta is the lane-contiguous copy (band_theta_lanes): 16 floats per lane
     float th[E];
     auto th_load = [&](int blk, int rl) {
         if constexpr (!REF) {
             const int c = (blk / rbs) % 2, rb = blk % rbs;
-            const float* tr = theta + ((long)c * H + rb * BTILE + rl) * W;
+            const float4* tr = reinterpret_cast<const float4*>(theta + ((long)c * H + rb * BTILE + rl) * W) + l * 4;
 #pragma unroll
-            for (int q = 0; q < E; ++q) th[q] = tr[g + L * t + RL * q];
+            for (int k = 0; k < 4; ++k) {
+                const float4 v = tr[k];
+                th[4 * k] = v.x;
+                th[4 * k + 1] = v.y;
+                th[4 * k + 2] = v.z;
+                th[4 * k + 3] = v.w;
+            }
         }
     };
     if ((int)blockIdx.x < items) {
@@ -178,6 +185,26 @@ extern "C" int fcd_debug_band_stamps(unsigned long long* out) {
     return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_band_stamps), sizeof(g_band_stamps));
 }
 #endif
+
+// theta [rows][W] (natural order, the REF output) -> the lane-contiguous copy
+// the phase kernels read: row element g + L t + RL q (lane l = G g + t of the
+// row's RL = W / 16 lanes) at l * 16 + q.
+__global__ __launch_bounds__(256) void k_theta_lanes(const float* __restrict__ theta, long n, int W, int B,
+                                                     float* __restrict__ thp) {
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;  // destination index
+    if (i >= n) return;
+    const long row = i / W;
+    const int e = (int)(i % W), l = e / 16, q = e % 16;
+    const int G = B / 16, L = W / B, RL = W / 16;
+    thp[i] = theta[row * W + (l / G) + L * (l % G) + RL * q];
+}
+
+void band_theta_lanes(int W, int B, const float* theta, int rows, float* thp, hipStream_t s) {
+    const long n = (long)rows * W;
+    hipLaunchKernelGGL(k_theta_lanes, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, theta, n, W, B, thp);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) throw std::runtime_error(std::string("band_theta_lanes launch: ") + hipGetErrorString(e));
+}
 
 // ------------------------------------------------------------------ launchers
 static int band_grid(long items, int per_cu) {

@@ -349,25 +349,6 @@ extern "C" int fcd_debug_pr_stamps(unsigned long long* out) {
 }
 #endif
 
-// theta [2][H][W] (natural) -> the fused kernel's lane-contiguous copy: row
-// element g + L t + 64 q (lane = G g + t) at lane * 16 + q.
-__global__ __launch_bounds__(256) void k_theta_lanes(const float* __restrict__ theta, int rows,
-                                                     float* __restrict__ thp) {
-    const long i = (long)blockIdx.x * 256 + threadIdx.x;  // destination index
-    if (i >= (long)rows * PR_W) return;
-    const long row = i / PR_W;
-    const int e = (int)(i % PR_W), lane = e / 16, q = e % 16;
-    const int g = lane / PR_G, t = lane % PR_G;
-    thp[i] = theta[row * PR_W + g + PR_L * t + 64 * q];
-}
-
-void phase_rows_theta(const float* theta, int H, float* thp, hipStream_t s) {
-    const long n = 2L * H * PR_W;
-    hipLaunchKernelGGL(k_theta_lanes, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, theta, 2 * H, thp);
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) throw std::runtime_error(std::string("phase_rows_theta launch: ") + hipGetErrorString(e));
-}
-
 bool phase_rows_supported(int W, int B, int H) { return W == PR_W && B == PR_B && H % 16 == 0 && H >= 16; }
 
 int phase_rows_tile() { return PR_ROWS; }
