@@ -81,6 +81,18 @@ __device__ __forceinline__ float2 csubi(float2 a, float2 b) { return make_float2
 __device__ __forceinline__ float2 cmuli(float2 a) { return make_float2(-a.y, a.x); }
 __device__ __forceinline__ float2 cmulmi(float2 a) { return make_float2(a.y, -a.x); }
 #endif
+#ifndef FCD_NT_STORES
+#define FCD_NT_STORES 1  // streaming (nt) stores for outputs no kernel re-reads soon
+#endif
+// Streaming store: the line is not kept in L2 / the Infinity Cache, so a large
+// output stream does not evict the small inputs every frame re-reads.
+__device__ __forceinline__ void st_stream(float* p, float v) {
+    if constexpr (FCD_NT_STORES) __builtin_nontemporal_store(v, p); else *p = v;
+}
+__device__ __forceinline__ void st_stream(float2* p, float2 v) {
+    if constexpr (FCD_NT_STORES) __builtin_nontemporal_store(pv(v), reinterpret_cast<fv2*>(p)); else *p = v;
+}
+
 // a * w (forward) or a * conj(w) (inverse) for a forward twiddle w
 template <bool INV>
 __device__ __forceinline__ float2 cmul_dir(float2 a, float2 w) {

@@ -35,6 +35,10 @@ namespace {
 #define FCD_BAND_WAVES 3  // min waves per SIMD (launch-bounds): 3 blocks of 4 waves per CU (168 VGPRs)
 #endif
 
+#ifndef FCD_BAND_NOTHETA
+#define FCD_BAND_NOTHETA 0  // diagnostic ablation only (wrong results): no reference-angle loads
+#endif
+
 #ifndef FCD_ATAN_GROUP
 #define FCD_ATAN_GROUP 4  // atan2 chains interleaved per scheduling group (0: unbounded)
 #endif
@@ -104,7 +108,10 @@ __global__ __launch_bounds__((BPCfg<W, B>::THREADS), FCD_BAND_WAVES) void k_band
     // theta is the lane-contiguous copy (band_theta_lanes): 16 floats per lane
     float th[E];
     auto th_load = [&](int blk, int rl) {
-        if constexpr (!REF) {
+        if constexpr (!REF && FCD_BAND_NOTHETA) {
+#pragma unroll
+            for (int q = 0; q < E; ++q) th[q] = 0.f;
+        } else if constexpr (!REF) {
             const int c = (blk / rbs) % 2, rb = blk % rbs;
             const float4* tr = reinterpret_cast<const float4*>(theta + ((long)c * H + rb * BTILE + rl) * W) + l * 4;
 #pragma unroll
@@ -170,7 +177,10 @@ __global__ __launch_bounds__((BPCfg<W, B>::THREADS), FCD_BAND_WAVES) void k_band
                 } else {
                     // wrap to [-pi, pi]: d - 2 pi rint(d / 2 pi), |d| < 2 pi
                     const float d = thc[q] - a;
-                    o[n] = fmaf(-6.28318530717959f, rintf(d * 0.159154943091895f), d);
+                    const float w = fmaf(-6.28318530717959f, rintf(d * 0.159154943091895f), d);
+                    // streaming store (nt): the 8 N^2-byte phase stream must not evict
+                    // the reference angles from the caches every frame
+                    st_stream(o + n, w);
                 }
             }
             STAMP(st++);

@@ -618,8 +618,8 @@ __global__ __launch_bounds__(C2RCfg<W>::THREADS) void k_int_c2r(const float2* __
             float* h1 = hout + ((long)f * H + r0 + 2 * pr) * W;
 #pragma unroll
             for (int q = 0; q < E; ++q) {
-                h1[t + TT * q] = x[q].x;
-                h1[W + t + TT * q] = x[q].y;
+                st_stream(h1 + t + TT * q, x[q].x);
+                st_stream(h1 + W + t + TT * q, x[q].y);
             }
         }
         __syncthreads();

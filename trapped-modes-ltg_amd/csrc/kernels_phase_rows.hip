@@ -298,7 +298,7 @@ __global__ __launch_bounds__(PR_THREADS) void k_phase_rows(
             const int c0 = threadIdx.x / PR_ROWS, rl = threadIdx.x % PR_ROWS;
             const float2* src = row_slot(rl, par ^ 1);
 #pragma unroll 4
-            for (int k = 0; k < PR_W / 64; ++k) dst[(c0 + 64 * k) * PR_ZT + rl] = src[pad(c0 + 64 * k)];
+            for (int k = 0; k < PR_W / 64; ++k) st_stream(dst + (c0 + 64 * k) * PR_ZT + rl, src[pad(c0 + 64 * k)]);
         }
         PR_STAMP(11);
         __syncthreads();
