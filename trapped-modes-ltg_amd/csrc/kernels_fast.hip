@@ -426,7 +426,7 @@ __global__ __launch_bounds__(KCfg<W>::THREADS, FCD_MIN_WAVES) void k_int_rows(co
 #ifdef FCD_EXP_ZT_ROWMAJOR
                 dst[(long)r * W + t + TT * q] = x[q];  // timing experiment only (wrong layout)
 #else
-                dst[tix(r, t + TT * q, W)] = x[q];
+                st_stream(dst + tix(r, t + TT * q, W), x[q]);
 #endif
             }
         }
