@@ -604,13 +604,15 @@ void build_demod_tables(fcd_ctx* c, hipStream_t s) {
         upload(c->ztw.p, ztw.data(), ztw.size() * sizeof(float2), s);
     }
     HIPCHK(hipStreamSynchronize(s));  // host vectors die here
-    // workspace per frame: Xb + Ab + wrapped + Zt + Ht (+ k for the fix-up path)
+    // workspace per frame: Xb + Ab + wrapped + Zt + Ht + k (fix-up path)
     const long hw = c->hw();
-    const long per_frame = 8L * H * c->NC + 16L * H * c->NCA + 8L * hw + 8L * hw + 8L * H * (W / 2 + 1);
-    // frames per launch: 32 keeps every kernel's grid several waves deep (measured
-    // 25.5 -> 21.1 us/frame from 8 to 32 frames at 1024^2); ~0.7 GB of workspace
-    const long budget = (long)fcd_env_int("FCD_CHUNK_MB", 768) << 20;
-    c->fchunk = (int)std::max(1L, std::min((long)fcd_env_int("FCD_CHUNK_MAX", 32), budget / per_frame));
+    const long per_frame = 8L * H * c->NC + 16L * H * c->NCA + 8L * hw + 8L * hw + 8L * H * (W / 2 + 1) + 8L * hw;
+    // frames per launch: large launches amortise every kernel's tail wave; at
+    // 1024^2 (bench.py, 256 frames) 8 / 32 / 128 / 256 frames per launch gave
+    // 50.5k / 63.5k / 68.1k / 68.9k frames/s.  8 GiB of workspace by default
+    // (of 288 GB HBM): 256 frames at 1024^2, 16 at 4096^2.
+    const long budget = (long)fcd_env_int("FCD_CHUNK_MB", 8192) << 20;
+    c->fchunk = (int)std::max(1L, std::min((long)fcd_env_int("FCD_CHUNK_MAX", 256), budget / per_frame));
     const size_t nb = (size_t)c->fchunk;
     c->Xb.ensure(nb * H * c->NC * sizeof(float2));
     c->Ab.ensure(nb * 2 * H * c->NCA * sizeof(float2));

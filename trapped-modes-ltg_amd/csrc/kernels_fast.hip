@@ -108,9 +108,10 @@ __global__ __launch_bounds__(KCfg<W>::THREADS, FCD_MIN_WAVES) void k_demod_rows(
         const int f = blk / rbs, rb = blk % rbs;
         const float* ra = frames + ((long)f * H + rb * TILE + 2 * pr) * W;
 #pragma unroll
-        for (int q = 0; q < E; ++q) xn[q] = make_float2(ra[t + TT * q], ra[W + t + TT * q]);
+        for (int q = 0; q < E; ++q)
+            xn[q] = make_float2(__builtin_nontemporal_load(ra + t + TT * q), __builtin_nontemporal_load(ra + W + t + TT * q));
     };
-    if ((int)blockIdx.x < nb * rbs) fetch(blockIdx.x, team);
+    if ((int)blockIdx.x < nb * rbs && team < TILE / 2) fetch(blockIdx.x, team);  // teams past the tile's pairs idle
     for (int blk = blockIdx.x; blk < nb * rbs; blk += gridDim.x) {
         for (int pr = team; pr < TILE / 2; pr += TEAMS) {
             float2 x[E];
