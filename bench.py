@@ -42,6 +42,11 @@ def load_traffic(n, chunk):
     return t
 
 
+def log(msg):
+    """Progress on stderr (keeps long profiled runs visibly alive; stdout holds only the JSON line)."""
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
 def cpu_baseline(size, frames, seconds_cap=25.0):
     """The CPU oracle (numpy/scipy FFTs + C Herraez unwrap), 1 core, bounded sample."""
     import numpy as np
@@ -89,6 +94,7 @@ def main():
 
     # synthetic batch, generated in HBM; rank r owns frames [r*B, (r+1)*B)
     ref_t, frames = make_frames_torch(n, B, seed=rank * B, device=dev)
+    log(f"rank {rank}: {B} frames of {n}x{n} generated on {dev}")
     heights = torch.empty((B, n, n), dtype=torch.float32, device=dev)
     eng = _lib.Engine((n, n), device=local)
     eng.set_reference(ref_t.cpu().numpy(), SQUARE_SIZE)
@@ -100,6 +106,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
+    log(f"rank {rank}: warmup done")
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
     if world > 1:
@@ -114,6 +121,7 @@ def main():
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
+    log(f"rank {rank}: timed steps done ({wall:.3f} s)")
     # per-stage device time from the engine's own HIP events (separate, profiled
     # passes, so the headline timing above carries no event overhead):
     #  (1) the headline path itself (heights only: fused band transform + unwrap + row

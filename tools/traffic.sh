@@ -8,8 +8,13 @@ tag=${1:-traffic}
 out=gpurun_out/$tag
 mkdir -p $out
 export TMPDIR=/tmp
+# heartbeat: PMC passes serialise every dispatch and can stay silent for minutes
+( while sleep 30; do date +%T >> $out/heartbeat.txt; done ) &
+hb=$!
+trap 'kill $hb 2>/dev/null' EXIT
 for c in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $c -f csv -d $out/$c -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > $out/$c.log 2>&1 || { echo "pmc $c failed"; tail -5 $out/$c.log; exit 1; }
+  timeout -k 10 420 rocprofv3 --kernel-trace --pmc $c -f csv -d $out/$c -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > $out/$c.log 2>&1 || { echo "pmc $c failed"; tail -5 $out/$c.log; exit 1; }
+  echo "pmc $c done"
   timeout -k 10 120 rocprofv3 --kernel-trace --pmc $c -f csv -d $out/cal_$c -o run -- trapped-modes-ltg_amd/tools/membench cal > $out/cal_$c.log 2>&1 || { echo "calibration $c failed"; tail -5 $out/cal_$c.log; exit 1; }
 done
 echo traffic passes done
