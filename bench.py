@@ -192,7 +192,7 @@ def main():
         "dtype": "f32",
         "data": "synthetic: pattern.py geometry (10-px binary checkerboard, 0/65535) warped by seeded Gaussian bumps, "
                 "generated on device (bench_data.py)",
-        "config": {"workload": f"c2: {n}x{n} frames, {B} per GPU per step, full compute_height_map pipeline "
+        "config": {"workload": f"{ {1024: 'c2', 2048: 'c3', 4096: 'c5'}.get(n, 'custom')}: {n}x{n} frames, {B} per GPU per step, full compute_height_map pipeline "
                                f"(demod + unwrap + integration), reference state cached",
                    "frame": n, "batch_per_gpu": B, "global_batch": B * world,
                    "parallelism": f"frame-sharded x{world}, no collective in the compute"},

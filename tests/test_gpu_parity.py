@@ -356,3 +356,63 @@ def test_fused_census_sends_residue_frames_to_exact_pass(lib, golden, fused):
     assert int(st["fixup_frames"]) == frames.shape[0]
     hu, _, _ = eng.process(frames, 1.0, unwrap=True, want_phases=True)
     assert np.array_equal(hf, hu)
+
+
+def test_full_size_2048_vs_oracle(lib):
+    """configs[2] geometry (2048^2, HBM-bound regime): one rotated-board frame against the
+    oracle with unwrapping; peaks / cf bit-exact, phases up to one 2*pi*c, heights rel-L2."""
+    from oracle import fcd_oracle as O
+    from bench_data import make_frames_numpy
+    from pyfcd.fcd import fcd
+    ref, frames = make_frames_numpy(2048, 1, seed=11, rotate_deg=5.0)
+    hb, ph, cf = fcd.compute_height_maps(ref, frames, 0.001, height=1.0, return_phases=True)
+    ho, po, cfo, ex = O.compute_height_map(ref, frames[0], 0.001, height=1.0)
+    assert cf == cfo
+    carriers, _ = fcd.compute_carriers(ref, 0.001)
+    assert [c.pixels.tolist() for c in carriers] == [np.asarray(c.pixels).tolist() for c in ex["carriers"]]
+    assert all(O.count_residues(w) == 0 for w in ex["wrapped"])
+    d, _ = const_offset(ph[0], po)
+    assert np.abs(d).max() < 2e-4
+    assert rel_l2(hb[0], ho) < 1e-5
+    hf, _ = fcd.compute_height_maps(ref, frames, 0.001, height=1.0)  # height-only path
+    assert rel_l2(hf[0], ho) < 1e-5
+
+
+def test_full_size_4096_properties(lib):
+    """configs[4] frame size (4096^2, full pipeline incl. integration).  The oracle's
+    unwrap takes minutes at this size, so: (1) the wrapped phases and the no-unwrap height
+    against the oracle (FFTs only), (2) the unwrapped height of a residue-free frame
+    against the no-unwrap composition (equal where no 2*pi jump exists is not testable;
+    instead the k-field integrates the wrapped field exactly: wrapped + 2*pi*k has no
+    neighbour difference above pi), (3) the reference itself as the displaced frame gives
+    zero phase and zero height."""
+    from oracle import fcd_oracle as O
+    from bench_data import make_frames_numpy
+    from pyfcd.fcd import fcd
+    ref, frames = make_frames_numpy(4096, 1, seed=2, rotate_deg=5.0)
+    hn, phn, cf = fcd.compute_height_maps(ref, frames, 0.001, height=1.0, unwrap=False, return_phases=True)
+    ho, po, cfo, ex = O.compute_height_map(ref, frames[0], 0.001, height=1.0, unwrap_phases=False)
+    assert cf == cfo
+    assert wrap_diff(phn[0], po).max() < 2e-4
+    assert rel_l2(hn[0], ho) < 1e-5
+    hu, phu, _ = fcd.compute_height_maps(ref, frames, 0.001, height=1.0, return_phases=True)
+    assert wrap_diff(phu[0], phn[0]).max() < 1e-6
+    for m in phu[0]:
+        assert np.abs(np.diff(m, axis=0)).max() < np.pi and np.abs(np.diff(m, axis=1)).max() < np.pi
+    h0, p0, _ = fcd.compute_height_maps(ref, ref[None], 0.001, height=1.0, return_phases=True)
+    assert np.abs(p0).max() < 1e-3 and np.abs(h0).max() < 1e-6 * max(1.0, np.abs(hu).max())
+
+
+def test_empty_batch_and_errors(lib):
+    """Edge cases of the boundary: an empty batch returns empty stacks; mismatched
+    frame shapes and a zero height raise (the reference raises on both: numpy
+    broadcasting / ZeroDivisionError)."""
+    from bench_data import make_frames_numpy
+    from pyfcd.fcd import fcd
+    ref, frames = make_frames_numpy(256, 1, seed=1, rotate_deg=5.0)
+    h, cf = fcd.compute_height_maps(ref, frames[:0], 0.001, height=1.0)
+    assert h.shape == (0, 256, 256)
+    with pytest.raises(Exception):
+        fcd.compute_height_map(ref, frames[0][:128], 0.001, height=1.0)
+    with pytest.raises(Exception):
+        fcd.compute_height_map(ref, frames[0], 0.001, height=0.0)

@@ -852,6 +852,7 @@ FCD_API int fcd_process(fcd_ctx* c, const float* frames, int n_frames, int flags
         if (!c->has_ref) throw FcdError(FCD_E_STATE, "no reference set");
         if (!frames || n_frames < 0) throw FcdError(FCD_E_INVALID, "bad frames");
         if (!(height != 0.0)) throw FcdError(FCD_E_INVALID, "height must be non-zero");
+        if (n_frames == 0) return FCD_OK;
         hipStream_t s = c->pick(stream);
         const long hw = c->hw();
         const bool dev = flags == FCD_DEVICE_PTRS;
