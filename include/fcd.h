@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define FCD_ABI_VERSION 2
+#define FCD_ABI_VERSION 3
 
 enum {
     FCD_OK = 0,
@@ -43,6 +43,17 @@ enum {
 };
 
 enum { FCD_HOST_PTRS = 0, FCD_DEVICE_PTRS = 1 };
+
+/* Frame sample formats (fcd_process_raw).  The reference decodes every frame
+ * to float32 on the host (analyze.load_image, analyze.py:25-40); these let the
+ * raw camera samples cross PCIe and be widened on the device instead.
+ *   FCD_FMT_F32  float32 [rows][cols]
+ *   FCD_FMT_U8   uint8   [rows][cols]          (8-bit PNG / BMP)
+ *   FCD_FMT_U16  uint16  [rows][cols]          (16-bit, host byte order)
+ *   FCD_FMT_P10  10-bit samples packed MSB-first, each row padded to a whole
+ *                byte: rows * ceil(10 * cols / 8) bytes (TIFF BitsPerSample=10,
+ *                FillOrder=1, the examples' reference_df.tif / prueba1_*.tif) */
+enum { FCD_FMT_F32 = 0, FCD_FMT_U8 = 1, FCD_FMT_U16 = 2, FCD_FMT_P10 = 3 };
 
 typedef struct fcd_ctx fcd_ctx;
 
@@ -89,6 +100,23 @@ int fcd_get_carriers(fcd_ctx* ctx, float* ccsgn, uint8_t* mask);
  * Synchronises once per internal chunk when unwrap != 0 (residue census). */
 int fcd_process(fcd_ctx* ctx, const float* frames, int n_frames, int flags, double height, int unwrap,
                 float* height_out, float* wrapped_out, int32_t* k_out, void* stream);
+
+/* fcd_process for frames stored in a raw sample format (FCD_FMT_*): the same
+ * computation on the frames widened to float32 (exact: all samples < 2^24).
+ * With host pointers and only height_out requested the call pipelines host
+ * memory -> PCIe -> compute -> PCIe -> host memory over two slots and three
+ * streams; page-locked caller buffers (fcd_host_alloc) are DMA'd directly,
+ * pageable ones are staged through the context's pinned slots.  Replaces the
+ * analyze.folder loop body (analyze.py:216-246: load_image + compute_height_map). */
+int fcd_process_raw(fcd_ctx* ctx, const void* frames, int format, int n_frames, int flags, double height,
+                    int unwrap, float* height_out, float* wrapped_out, int32_t* k_out, void* stream);
+
+/* Bytes of one frame in `format` for this context's shape. */
+int fcd_frame_bytes(fcd_ctx* ctx, int format, int64_t* bytes);
+
+/* Page-locked host memory for frame / height stacks (no reference counterpart). */
+int fcd_host_alloc(int64_t bytes, void** out);
+int fcd_host_free(void* p);
 
 /* Replaces fcd.compute_phases(displaced_fft, carriers, unwrap) (fcd.py:103-120)
  * for n spectra (complex64 [n][rows][cols], unshifted fft2 output). */

@@ -11,6 +11,15 @@ for p in (ROOT, PKG):
     if p not in sys.path:
         sys.path.insert(0, p)
 
+# torch (used by some GPU tests for device buffers) ships its own libamdhip64.so.7;
+# loaded first, it is the one HIP runtime the engine library binds to as well (same
+# soname).  Loaded after the engine's /opt/rocm runtime it would be a second runtime
+# in the process, which finds no devices.  INTEGRATION.md §3.
+try:
+    import torch  # noqa: F401
+except ImportError:
+    pass
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); runs the engine's kernels")

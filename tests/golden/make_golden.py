@@ -19,6 +19,9 @@ Fixtures (all under tests/golden/):
                      pattern.py-style binary), full outputs of compute_height_map
   integrate.npz      fourier.integrate_in_fourier on seeded gradient fields
   val.npz            pyval.val(0, gauss_sin) accuracy (README.md:5-7 "< 0.52 %")
+  ingest.npz         analyze.load_image decodes of every example picture (sha256 of the
+                     float32 image), analyze.mask / center of camera frames, and the
+                     analyze.folder loop body's height maps with and without the mask
 """
 import os
 import sys
@@ -254,8 +257,74 @@ def make_val():
     print("val err %", err, "cf", cf)
 
 
+def make_ingest():
+    """Decoder, mask and folder-loop fixtures (analyze.py:25-40, 42-139, 216-246).
+
+    analyze.py itself cannot be imported here (its module imports cv2, absent), so the
+    mask / center steps call the same scikit-image / scipy functions with the same
+    arguments as analyze.py:86-100 and :119-137, and the folder loop body is
+    load_image -> [mask blend] -> fcd.compute_height_map -> [height *= ~mask] ->
+    float32, as analyze.py:216-246."""
+    import hashlib
+    from scipy.ndimage import uniform_filter
+    from skimage.measure import label, regionprops
+
+    out = {"versions": VERSIONS}
+    names = sorted(f for f in os.listdir(PICS) if os.path.isfile(os.path.join(PICS, f)))
+    mask_dir = os.path.join(PICS, "mask")
+    mask_names = sorted(f for f in os.listdir(mask_dir) if f.endswith(".tif"))
+    files = [n for n in names] + ["mask/" + n for n in mask_names]
+    dec_sha, dec_shape, dec_sum = [], [], []
+    for n in files:
+        a = io.imread(os.path.join(PICS, n), as_gray=True).astype(np.float32)  # analyze.py:40
+        dec_sha.append(hashlib.sha256(a.tobytes()).hexdigest())
+        dec_shape.append(a.shape)
+        dec_sum.append(float(a.astype(np.float64).sum()))
+    out.update(files=np.array(files), dec_sha=np.array(dec_sha), dec_shape=np.array(dec_shape),
+               dec_sum=np.array(dec_sum))
+
+    def mask_of(image, smoothed):  # analyze.py:86-94
+        smooth = uniform_filter(image, size=smoothed)
+        Mask = smooth < np.mean(smooth)
+        labels = label(Mask)
+        r = sorted(regionprops(labels), key=lambda r: r.area, reverse=True)[0]
+        return labels == r.label
+
+    def center_of(mask):  # analyze.py:119-137
+        props = regionprops(label(~mask))
+        n_rows, n_cols = mask.shape
+        holes = [r for r in props if r.bbox[0] > 0 and r.bbox[1] > 0 and r.bbox[2] < n_rows and r.bbox[3] < n_cols]
+        cy, cx = max(holes, key=lambda r: r.area).centroid
+        return int(cy), int(cx)
+
+    ref = io.imread(os.path.join(PICS, "reference_df.tif"), as_gray=True).astype(np.float32)
+    sq = 0.002
+    masks, centers, smooths, heights, hsum, hnorm, which = [], [], [], [], [], [], []
+    for idx, smoothed in ((4, 15), (5, 14), (8, 15)):
+        disp = io.imread(os.path.join(mask_dir, mask_names[idx]), as_gray=True).astype(np.float32)
+        m = mask_of(disp, smoothed)
+        masks.append(np.packbits(m))
+        centers.append(center_of(m))
+        smooths.append(smoothed)
+        for masked in (False, True):
+            img = np.where(m == 1, ref, disp) if masked else disp  # analyze.py:219
+            h, _, cf = fcd.compute_height_map(ref, img, sq, LAYERS)  # analyze.py:233-238
+            if masked:
+                h *= ~m  # analyze.py:241
+            h = h.astype(np.float32)  # analyze.py:248
+            heights.append(h[::4, ::4])
+            hsum.append(float(h.astype(np.float64).sum()))
+            hnorm.append(float(np.linalg.norm(h.astype(np.float64))))
+            which.append((idx, int(masked)))
+    out.update(mask_names=np.array(mask_names), mask_bits=np.stack(masks), mask_centers=np.array(centers),
+               mask_smoothed=np.array(smooths), folder_which=np.array(which), folder_h_sub=np.stack(heights),
+               folder_h_sum=np.array(hsum), folder_h_norm=np.array(hnorm), folder_sq=sq, folder_cf=cf)
+    np.savez_compressed(os.path.join(OUT, "ingest.npz"), **out)
+    print("ingest", len(files), "files; centers", centers, "cf", cf)
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["real_pair", "real_df", "unwrap", "synthetic", "integrate", "val"]
+    which = sys.argv[1:] or ["real_pair", "real_df", "unwrap", "synthetic", "integrate", "val", "ingest"]
     if "real_pair" in which:
         make_real_pair()
     if "real_df" in which:
@@ -268,3 +337,5 @@ if __name__ == "__main__":
         make_integrate()
     if "val" in which:
         make_val()
+    if "ingest" in which:
+        make_ingest()

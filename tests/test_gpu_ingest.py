@@ -1,0 +1,194 @@
+"""GPU checks of frame ingest and the batch driver:
+
+* fcd_process_raw on 8-bit, 16-bit and 10-bit-packed samples gives bit-identical
+  heights to fcd_process on the same samples widened to float32 on the host, through
+  every host path (pageable staging, page-locked buffers, the multi-chunk pipeline)
+  and with device pointers;
+* analyze.folder (the reference's analyze.py:142-286 contract) on 10-bit camera TIFFs
+  written from the golden frames: maps equal the reference's compute_height_map
+  outputs (real_df.npz), calibration_factor.npy equals the committed file's value, the
+  mask path equals the reference's masked loop body (ingest.npz), resume skips done
+  frames;
+* the examples/fcd_example.py chain (PNG / BMP through analyze.load_image) against the
+  real-pair golden.
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+LAYERS = [[5.7e-2, 1.0003], [1.2e-2, 1.48899], [4.3e-2, 1.34], [80e-2, 1.0003]]  # fcd_example.py:17
+
+
+def rel_l2(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / np.linalg.norm(b))
+
+
+@pytest.fixture(scope="module")
+def df(golden):
+    return golden("real_df")
+
+
+@pytest.fixture
+def fresh_engines():
+    from pyfcd import _lib
+    _lib._engines.clear()
+    yield
+    _lib._engines.clear()
+
+
+def _engine(ref, sq):
+    from pyfcd import _lib
+    eng = _lib.Engine(ref.shape)
+    eng.set_reference(ref, sq)
+    return eng
+
+
+@pytest.mark.parametrize("fmt_name", ["U8", "U16", "P10"])
+def test_raw_formats_equal_float32(df, fmt_name):
+    from pyfcd import _lib
+    from pydata import images
+    fmt = getattr(_lib, "FCD_FMT_" + fmt_name)
+    ref = df["ref_u16"].astype(np.float32)
+    samples = df["frames_u16"]
+    if fmt_name == "U8":
+        samples = (samples >> 2).astype(np.uint8)
+        raw = samples.reshape(len(samples), -1)
+    elif fmt_name == "U16":
+        raw = samples.view(np.uint8).reshape(len(samples), -1)
+    else:
+        raw = np.stack([images.pack10(s) for s in samples])
+    eng = _engine(ref, float(df["square_size"]))
+    assert raw.shape[1] == eng.frame_bytes(fmt)
+    want, _, _ = eng.process(samples.astype(np.float32), 1.0, unwrap=True, want_phases=False)
+    got = eng.process_raw(raw, fmt, len(samples), 1.0)
+    assert np.array_equal(got, want)
+    # page-locked input and output buffers (DMA straight from / to the caller's pages)
+    pin_in = _lib.PinnedBuffer(raw.shape, np.uint8)
+    pin_out = _lib.PinnedBuffer((len(samples),) + ref.shape, np.float32)
+    pin_in.array[:] = raw
+    eng.process_raw(pin_in.array, fmt, len(samples), 1.0, out=pin_out.array)
+    assert np.array_equal(pin_out.array, want)
+    pin_in.free()
+    pin_out.free()
+
+
+def test_host_pipeline_many_chunks(monkeypatch, fresh_engines):
+    """More frames than one pipeline slot (FCD_PIPE_MB=1 -> 1 frame per slot at 512^2):
+    every chunk boundary of the two-slot, three-stream pipeline, against the
+    device-pointer path on the same frames (bit-identical)."""
+    import torch
+    from pyfcd import _lib
+    from bench_data import make_frames_numpy
+    monkeypatch.setenv("FCD_PIPE_MB", "1")
+    ref, frames = make_frames_numpy(512, 7, seed=4, rotate_deg=5.0)
+    eng = _engine(ref, 0.001)
+    got, _, _ = eng.process(frames, 1.0, unwrap=True, want_phases=False)
+    u16 = np.clip(frames / frames.max() * 1023, 0, 1023).astype(np.uint16)
+    raw = np.stack([__import__("pydata.images", fromlist=["pack10"]).pack10(f) for f in u16])
+    got10 = eng.process_raw(raw, _lib.FCD_FMT_P10, len(u16), 1.0)
+    dev = torch.device("cuda", 0)
+    fd = torch.from_numpy(frames).to(dev)
+    hd = torch.empty_like(fd)
+    eng.process_device(fd.data_ptr(), len(frames), 1.0, True, hd.data_ptr())
+    torch.cuda.synchronize()
+    assert np.array_equal(got, hd.cpu().numpy())
+    fd = torch.from_numpy(u16.astype(np.float32)).to(dev)
+    eng.process_device(fd.data_ptr(), len(frames), 1.0, True, hd.data_ptr())
+    torch.cuda.synchronize()
+    assert np.array_equal(got10, hd.cpu().numpy())
+
+
+def test_device_raw_pointer_path(df):
+    import ctypes
+    import torch
+    from pyfcd import _lib
+    from pydata import images
+    ref = df["ref_u16"].astype(np.float32)
+    eng = _engine(ref, float(df["square_size"]))
+    raw = np.stack([images.pack10(s) for s in df["frames_u16"]])
+    want, _, _ = eng.process(df["frames_u16"].astype(np.float32), 1.0, unwrap=True, want_phases=False)
+    dev = torch.device("cuda", 0)
+    rd = torch.from_numpy(raw).to(dev)
+    hd = torch.empty((len(raw),) + ref.shape, dtype=torch.float32, device=dev)
+    lib = _lib.load_library()
+    _lib._check(lib.fcd_process_raw(eng.handle, ctypes.c_void_p(rd.data_ptr()), _lib.FCD_FMT_P10, len(raw),
+                                    _lib.FCD_DEVICE_PTRS, 1.0, 1, ctypes.c_void_p(hd.data_ptr()), None, None, None))
+    lib.fcd_synchronize(eng.handle)
+    torch.cuda.synchronize()
+    assert np.array_equal(hd.cpu().numpy(), want)
+
+
+def _write_folder(tmp_path, df, idx=None):
+    from pydata import images
+    d = tmp_path / "frames"
+    d.mkdir()
+    ref_path = str(d / "reference_df.tif")
+    images.write_tiff(ref_path, df["ref_u16"], bits=10)
+    names = [os.path.basename(str(n)) for n in df["names"]]
+    for i, (n, f) in enumerate(zip(names, df["frames_u16"])):
+        if idx is None or i in idx:
+            images.write_tiff(str(d / n), f, bits=10)
+    return ref_path, str(d), names
+
+
+def test_folder_matches_reference_maps(tmp_path, df, fresh_engines):
+    from pydata.analyze import analyze
+    ref_path, d, names = _write_folder(tmp_path, df)
+    analyze.folder(ref_path, d, LAYERS, float(df["square_size"]), batch=2)
+    maps = os.path.join(d, "maps")
+    assert np.load(os.path.join(maps, "calibration_factor.npy")).tolist() == df["committed_cf"].tolist()
+    order = sorted(range(3), key=lambda i: names[i])
+    for i in order:
+        h = np.load(os.path.join(maps, names[i].replace(".tif", "") + "_map.npy"))
+        assert h.dtype == np.float32 and h.shape == (1024, 1024)
+        # maps with 7..1611 residues; the reference seeds border reliabilities from rand()
+        assert rel_l2(h[::4, ::4], df["height_sub"][i]) < 1e-4, names[i]
+    # resume: nothing to do when every map exists; the last one is redone when removed
+    last = os.path.join(maps, sorted(names)[-1].replace(".tif", "") + "_map.npy")
+    before = np.load(last)
+    os.remove(last)
+    t0 = {n: os.path.getmtime(os.path.join(maps, n)) for n in os.listdir(maps) if n.endswith("_map.npy")}
+    analyze.folder(ref_path, d, LAYERS, float(df["square_size"]))
+    assert np.array_equal(np.load(last), before)
+    assert all(os.path.getmtime(os.path.join(maps, n)) == t for n, t in t0.items())
+
+
+def test_folder_mask_path_matches_reference(tmp_path, df, golden, fresh_engines):
+    """The camera frame mask/*0005.tif (real_df frame 1 = ingest fixture's mask frame 4),
+    smoothed=15: mask blend + height *= ~mask + centers.txt, against the reference's
+    loop body outputs."""
+    from pydata.analyze import analyze
+    g = golden("ingest")
+    assert str(g["mask_names"][4]).endswith("0005.tif") and os.path.basename(str(df["names"][1])) == str(
+        g["mask_names"][4])
+    ref_path, d, names = _write_folder(tmp_path, df, idx={1})
+    analyze.folder(ref_path, d, LAYERS, float(g["folder_sq"]), smoothed=int(g["mask_smoothed"][0]))
+    maps = os.path.join(d, "maps")
+    h = np.load(os.path.join(maps, names[1].replace(".tif", "") + "_map.npy"))
+    k = [tuple(w) for w in g["folder_which"].tolist()].index((4, 1))
+    assert rel_l2(h[::4, ::4], g["folder_h_sub"][k]) < 1e-4
+    want_mask = np.unpackbits(g["mask_bits"][0])[: h.size].reshape(h.shape).astype(bool)
+    assert np.all(h[want_mask] == 0)
+    lines = open(os.path.join(maps, "centers.txt")).read().splitlines()
+    assert lines == [f"0\t{tuple(int(v) for v in g['mask_centers'][0])}"]
+
+
+def test_fcd_example_chain_png_bmp(tmp_path, golden, fresh_engines):
+    """examples/fcd_example.py:10-23 with our pydata/pyfcd: PNG reference + BMP frame."""
+    from PIL import Image
+    from pydata.analyze import analyze
+    from pyfcd.fcd import fcd
+    r = golden("real_pair")
+    Image.fromarray(r["ref_u8"]).save(str(tmp_path / "reference_2.png"))
+    Image.fromarray(r["disp_u8"]).save(str(tmp_path / "frame.bmp"))
+    reference = analyze.load_image(str(tmp_path / "reference_2.png"))
+    displaced = analyze.load_image(str(tmp_path / "frame.bmp"))
+    assert np.array_equal(reference, r["ref_u8"].astype(np.float32))
+    values = fcd.compute_height_map(reference, displaced, float(r["square_size"]), LAYERS)
+    assert values[2] == float(r["cf"])
+    assert rel_l2(values[0][::4, ::4], r["height_sub"]) < 1e-4

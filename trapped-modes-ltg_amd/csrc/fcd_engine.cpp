@@ -16,6 +16,7 @@
 #include <numeric>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/fcd.h"
@@ -159,6 +160,27 @@ struct Blob {
     float value;
 };
 
+// Host-pointer pipeline state (fcd_process with host frames, heights only).
+struct HostPipe {
+    int nb = 0;                 // frames per slot
+    size_t in_bytes = 0;        // raw bytes per input slot
+    hipStream_t h2d = nullptr, d2h = nullptr;
+    void* pin_in[2] = {nullptr, nullptr};
+    float* pin_out[2] = {nullptr, nullptr};
+    DevBuf dev_raw[2], dev_out[2];
+    hipEvent_t ev_h2d[2] = {}, ev_free[2] = {}, ev_comp[2] = {}, ev_d2h[2] = {};
+    ~HostPipe() {
+        for (int i = 0; i < 2; ++i) {
+            if (pin_in[i]) (void)hipHostFree(pin_in[i]);
+            if (pin_out[i]) (void)hipHostFree(pin_out[i]);
+            for (hipEvent_t e : {ev_h2d[i], ev_free[i], ev_comp[i], ev_d2h[i]})
+                if (e) (void)hipEventDestroy(e);
+        }
+        if (h2d) (void)hipStreamDestroy(h2d);
+        if (d2h) (void)hipStreamDestroy(d2h);
+    }
+};
+
 }  // namespace
 
 struct fcd_ctx {
@@ -195,6 +217,8 @@ struct fcd_ctx {
     int chunk = 1;
     DevBuf spec, work, wrapped, kbuf, colk, rescnt, frames_in, out_h, scalar;
     DevBuf cand_idx, cand_val;
+    DevBuf fix_raw;  // raw samples of the frames redone by the exact pass
+    HostPipe pipe;
     // MST workspace
     DevBuf mst_comp, mst_off, mst_rel, mst_cw, mst_ce, mst_bw, mst_be, mst_link, mst_hooks, mst_ids;
     size_t mst_cap = 0;
@@ -845,79 +869,228 @@ FCD_API int fcd_get_carriers(fcd_ctx* c, float* ccsgn, uint8_t* mask) {
     })
 }
 
-FCD_API int fcd_process(fcd_ctx* c, const float* frames, int n_frames, int flags, double height, int unwrap,
-                        float* height_out, float* wrapped_out, int32_t* k_out, void* stream) {
-    FCD_TRY({
-        check_ctx(c);
-        if (!c->has_ref) throw FcdError(FCD_E_STATE, "no reference set");
-        if (!frames || n_frames < 0) throw FcdError(FCD_E_INVALID, "bad frames");
-        if (!(height != 0.0)) throw FcdError(FCD_E_INVALID, "height must be non-zero");
-        if (n_frames == 0) return FCD_OK;
-        hipStream_t s = c->pick(stream);
-        const long hw = c->hw();
-        const bool dev = flags == FCD_DEVICE_PTRS;
-        const fcd_ref_info& in = c->info;
-        const double det = in.frequencies[0][1] * in.frequencies[1][0] - in.frequencies[0][0] * in.frequencies[1][1];
-        const double sc = 1.0 / (det * height);
-        ensure_integ_tables(c, in.calibration_factor, s);
-        // h_hat = i/k^2 [(kx f1[0] - ky f1[1]) Phi0 + (ky f0[1] - kx f0[0]) Phi1] / (det * height)
-        const fcdk::IntegCoef coef = integ_coef(c, in.frequencies[1][0] * sc, -in.frequencies[1][1] * sc,
-                                                -in.frequencies[0][0] * sc, in.frequencies[0][1] * sc);
-        const int nbmax = c->fchunk;
-        c->frames_in.ensure((size_t)nbmax * hw * sizeof(float));
-        c->out_h.ensure((size_t)nbmax * hw * sizeof(float));
-        const hipMemcpyKind out_kind = dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
-        int* res = nullptr;
-        if (unwrap) {  // residue census of every map of the call
-            c->fres.ensure((size_t)n_frames * 2 * sizeof(int) + 16);
-            res = c->fres.as<int>();
-            HIPCHK(hipMemsetAsync(res, 0, (size_t)n_frames * 2 * sizeof(int), s));
+namespace {
+
+// First pass of one chunk: nb device-resident float32 frames through the
+// band-pruned pipeline with the residue-free unwrap, heights to hdst (device).
+void first_pass_chunk(fcd_ctx* c, const float* fr, int nb, bool unwrap, bool fused, int* res, float* hdst,
+                      int32_t* kdst, const fcdk::IntegCoef& coef, hipStream_t s) {
+    if (fused) {
+        // height only: band transforms, phase, unwrap and the z-row FFT in one
+        // pass (kernels_phase_rows.hip); colk lands in the spectra's DC bins
+        const fcdk::DemodTables T = demod_tables(c);
+        if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
+        fcdk::demod_rows(c->W, fr, c->H, nb, T, c->Xb.as<float2>(), c->twp_row.as<float2>(), s);
+        fcdk::demod_cols(c->H, c->Xb.as<float2>(), nb, T, c->Ab.as<float2>(), c->NCA, c->twp_col.as<float2>(), s);
+        if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
+        fcdk::phase_rows(unwrap, c->Ab.as<float2>(), c->H, nb, c->NCA, c->NCc[0], c->NCc[1], c->theta_p.as<float>(),
+                         c->band_pre.as<float2>(), c->band_ptw.as<float2>(), c->ztw.as<float2>(), c->col0.as<float>(),
+                         res, c->Zt.as<float2>(), c->seam.as<float2>(), s);
+        if (unwrap) fcdk::unwrap_colk_compact(c->col0.as<float>(), 2 * nb, c->H, c->colk.as<int>(), s);
+        if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
+        fcdk::int_cols(c->H, c->Zt.as<float2>(), c->W, nb, coef, c->Ht.as<float2>(), c->twp_col.as<float2>(), s,
+                       unwrap ? c->colk.as<int>() : nullptr);
+        fcdk::int_c2r(c->W, c->Ht.as<float2>(), c->H, nb, hdst, c->twp_row.as<float2>(), s);
+    } else {
+        if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
+        fast_demod(c, fr, nb, s);
+        if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
+        if (unwrap) fcdk::unwrap_colk(c->wrapped.as<float>(), 2 * nb, c->H, c->W, c->colk.as<int>(), s);
+        if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
+        fcdk::int_rows(c->W, unwrap ? 1 : 0, c->wrapped.as<float>(), c->colk.as<int>(), nullptr, kdst, res, c->H, nb,
+                       c->Zt.as<float2>(), c->twp_row.as<float2>(), s);
+        fcdk::int_cols(c->H, c->Zt.as<float2>(), c->W, nb, coef, c->Ht.as<float2>(), c->twp_col.as<float2>(), s);
+        fcdk::int_c2r(c->W, c->Ht.as<float2>(), c->H, nb, hdst, c->twp_row.as<float2>(), s);
+    }
+    if (c->profiling) {
+        HIPCHK(hipEventRecord(c->next_event(), s));
+        c->prof_frames += nb;
+    }
+}
+
+// Caller memory that is page-locked (fcd_host_alloc, hipHostRegister, torch
+// pin_memory) is copied by DMA straight from / to its own pages.
+bool host_pinned(const void* p) {
+    if (!p) return false;
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
+// memcpy between pageable and pinned host memory, split over threads (one
+// host thread moves ~10 GB/s; the PCIe link ~50 GB/s per direction).
+void par_copy(void* dst, const void* src, size_t bytes) {
+    constexpr size_t kPiece = 8u << 20;
+    const int nt = (int)std::min<size_t>(8, (bytes + kPiece - 1) / kPiece);
+    if (nt <= 1) {
+        std::memcpy(dst, src, bytes);
+        return;
+    }
+    const size_t part = (bytes / nt + 4095) & ~(size_t)4095;
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) {
+        const size_t o = part * t;
+        if (o >= bytes) break;
+        th.emplace_back([=] { std::memcpy((char*)dst + o, (const char*)src + o, std::min(part, bytes - o)); });
+    }
+    std::memcpy(dst, src, std::min(part, bytes));
+    for (auto& x : th) x.join();
+}
+
+void ensure_host_pipe(fcd_ctx* c, int format) {
+    HostPipe& P = c->pipe;
+    const long hw = c->hw();
+    if (!P.h2d) {
+        HIPCHK(hipStreamCreateWithFlags(&P.h2d, hipStreamNonBlocking));
+        HIPCHK(hipStreamCreateWithFlags(&P.d2h, hipStreamNonBlocking));
+        for (int i = 0; i < 2; ++i)
+            for (hipEvent_t* e : {&P.ev_h2d[i], &P.ev_free[i], &P.ev_comp[i], &P.ev_d2h[i]})
+                HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+        // 128 MiB of float32 frames per slot (32 frames at 1024^2): two slots in
+        // flight overlap the H2D copy, the compute and the D2H copy
+        const long budget = (long)fcd_env_int("FCD_PIPE_MB", 128) << 20;
+        P.nb = (int)std::max(1L, std::min((long)c->fchunk, budget / (hw * 4)));
+        const size_t out_b = (size_t)P.nb * hw * 4;
+        for (int i = 0; i < 2; ++i) {
+            HIPCHK(hipHostMalloc(&P.pin_out[i], out_b, hipHostMallocDefault));
+            P.dev_out[i].ensure(out_b);
         }
-        // ---- pass 1: every frame through the band-pruned pipeline with the residue-free unwrap
-        const bool fused = c->fused_ok && !wrapped_out && !k_out && !c->force_unfused;
+    }
+    const size_t in_b = (size_t)P.nb * fcdk::raw_frame_bytes(format, c->H, c->W);
+    if (in_b > P.in_bytes) {
+        for (int i = 0; i < 2; ++i) {
+            if (P.pin_in[i]) (void)hipHostFree(P.pin_in[i]);
+            P.pin_in[i] = nullptr;
+            HIPCHK(hipHostMalloc(&P.pin_in[i], in_b, hipHostMallocDefault));
+            P.dev_raw[i].ensure(in_b);
+        }
+        P.in_bytes = in_b;
+    }
+}
+
+// Host frames, heights only: three-stage pipeline over two slots.  While chunk
+// i computes on the context stream, chunk i+1's samples cross PCIe on the H2D
+// stream and chunk i-1's heights on the D2H stream; pageable caller memory is
+// staged through pinned slots by parallel memcpy, pinned caller memory is
+// DMA'd directly.
+void host_pipeline(fcd_ctx* c, const void* frames, int format, int n_frames, bool unwrap, bool fused, int* res,
+                   float* height_out, const fcdk::IntegCoef& coef, hipStream_t s) {
+    ensure_host_pipe(c, format);
+    HostPipe& P = c->pipe;
+    const long hw = c->hw();
+    const size_t rb = fcdk::raw_frame_bytes(format, c->H, c->W);
+    const bool pin_src = host_pinned(frames), pin_dst = host_pinned(height_out);
+    const int nchunks = (n_frames + P.nb - 1) / P.nb;
+    auto chunk_frames = [&](int i) { return std::min(P.nb, n_frames - i * P.nb); };
+    auto retire = [&](int i) {  // chunk i's heights: pinned slot -> caller memory
+        if (pin_dst || !height_out) return;
+        HIPCHK(hipEventSynchronize(P.ev_d2h[i & 1]));
+        par_copy(height_out + (size_t)i * P.nb * hw, P.pin_out[i & 1], (size_t)chunk_frames(i) * hw * 4);
+    };
+    for (int i = 0; i < nchunks; ++i) {
+        const int slot = i & 1, nb = chunk_frames(i);
+        const size_t f0 = (size_t)i * P.nb;
+        const char* src = static_cast<const char*>(frames) + f0 * rb;
+        if (!pin_src) {
+            if (i >= 2) HIPCHK(hipEventSynchronize(P.ev_h2d[slot]));  // slot's previous upload has left
+            par_copy(P.pin_in[slot], src, (size_t)nb * rb);
+            src = static_cast<const char*>(P.pin_in[slot]);
+        }
+        if (i >= 2) HIPCHK(hipStreamWaitEvent(P.h2d, P.ev_free[slot], 0));  // device slot consumed
+        HIPCHK(hipMemcpyAsync(P.dev_raw[slot].p, src, (size_t)nb * rb, hipMemcpyHostToDevice, P.h2d));
+        HIPCHK(hipEventRecord(P.ev_h2d[slot], P.h2d));
+        HIPCHK(hipStreamWaitEvent(s, P.ev_h2d[slot], 0));
+        const float* fr = P.dev_raw[slot].as<float>();
+        if (format != FCD_FMT_F32) {
+            fcdk::ingest(format, P.dev_raw[slot].p, nb, c->H, c->W, c->frames_in.as<float>(), s);
+            fr = c->frames_in.as<float>();
+            HIPCHK(hipEventRecord(P.ev_free[slot], s));
+        }
+        if (i >= 2) HIPCHK(hipStreamWaitEvent(s, P.ev_d2h[slot], 0));  // heights slot drained
+        first_pass_chunk(c, fr, nb, unwrap, fused, res ? res + f0 * 2 : nullptr, P.dev_out[slot].as<float>(),
+                         nullptr, coef, s);
+        if (format == FCD_FMT_F32) HIPCHK(hipEventRecord(P.ev_free[slot], s));
+        HIPCHK(hipEventRecord(P.ev_comp[slot], s));
+        if (height_out) {
+            HIPCHK(hipStreamWaitEvent(P.d2h, P.ev_comp[slot], 0));
+            float* dst = pin_dst ? height_out + f0 * hw : P.pin_out[slot];
+            HIPCHK(hipMemcpyAsync(dst, P.dev_out[slot].p, (size_t)nb * hw * 4, hipMemcpyDeviceToHost, P.d2h));
+            HIPCHK(hipEventRecord(P.ev_d2h[slot], P.d2h));
+        }
+        if (i >= 1) retire(i - 1);
+    }
+    if (nchunks >= 1) retire(nchunks - 1);
+    HIPCHK(hipStreamSynchronize(P.d2h));
+    HIPCHK(hipStreamSynchronize(P.h2d));
+}
+
+// Frames `idx` of a (host or device, any format) batch -> float32 in frames_in.
+void stage_frames(fcd_ctx* c, const void* frames, int format, bool dev, const int* idx, int n, hipStream_t s) {
+    const long hw = c->hw();
+    const size_t rb = fcdk::raw_frame_bytes(format, c->H, c->W);
+    const hipMemcpyKind kind = dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    void* dst = c->frames_in.p;
+    if (format != FCD_FMT_F32) {
+        c->fix_raw.ensure((size_t)n * rb);
+        dst = c->fix_raw.p;
+    }
+    for (int i = 0; i < n; ++i)
+        HIPCHK(hipMemcpyAsync(static_cast<char*>(dst) + (size_t)i * rb,
+                              static_cast<const char*>(frames) + (size_t)idx[i] * rb, rb, kind, s));
+    if (format != FCD_FMT_F32) fcdk::ingest(format, dst, n, c->H, c->W, c->frames_in.as<float>(), s);
+    (void)hw;
+}
+
+int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int flags, double height, int unwrap,
+                 float* height_out, float* wrapped_out, int32_t* k_out, void* stream) {
+    check_ctx(c);
+    if (!c->has_ref) throw FcdError(FCD_E_STATE, "no reference set");
+    if (!frames || n_frames < 0) throw FcdError(FCD_E_INVALID, "bad frames");
+    if (fcdk::raw_frame_bytes(format, c->H, c->W) == 0) throw FcdError(FCD_E_INVALID, "unknown frame format");
+    if (!(height != 0.0)) throw FcdError(FCD_E_INVALID, "height must be non-zero");
+    if (n_frames == 0) return FCD_OK;
+    hipStream_t s = c->pick(stream);
+    const long hw = c->hw();
+    const bool dev = flags == FCD_DEVICE_PTRS;
+    const size_t rb = fcdk::raw_frame_bytes(format, c->H, c->W);
+    const fcd_ref_info& in = c->info;
+    const double det = in.frequencies[0][1] * in.frequencies[1][0] - in.frequencies[0][0] * in.frequencies[1][1];
+    const double sc = 1.0 / (det * height);
+    ensure_integ_tables(c, in.calibration_factor, s);
+    // h_hat = i/k^2 [(kx f1[0] - ky f1[1]) Phi0 + (ky f0[1] - kx f0[0]) Phi1] / (det * height)
+    const fcdk::IntegCoef coef = integ_coef(c, in.frequencies[1][0] * sc, -in.frequencies[1][1] * sc,
+                                            -in.frequencies[0][0] * sc, in.frequencies[0][1] * sc);
+    const int nbmax = c->fchunk;
+    c->frames_in.ensure((size_t)nbmax * hw * sizeof(float));
+    c->out_h.ensure((size_t)nbmax * hw * sizeof(float));
+    const hipMemcpyKind out_kind = dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+    int* res = nullptr;
+    if (unwrap) {  // residue census of every map of the call
+        c->fres.ensure((size_t)n_frames * 2 * sizeof(int) + 16);
+        res = c->fres.as<int>();
+        HIPCHK(hipMemsetAsync(res, 0, (size_t)n_frames * 2 * sizeof(int), s));
+    }
+    // ---- pass 1: every frame through the band-pruned pipeline with the residue-free unwrap
+    const bool fused = c->fused_ok && !wrapped_out && !k_out && !c->force_unfused;
+    if (!dev && !wrapped_out && !k_out) {
+        host_pipeline(c, frames, format, n_frames, unwrap != 0, fused, res, height_out, coef, s);
+    } else {
         for (int f0 = 0; f0 < n_frames; f0 += nbmax) {
             const int nb = std::min(nbmax, n_frames - f0);
-            const float* fr = frames + (size_t)f0 * hw;
-            if (!dev) {
-                upload(c->frames_in.p, fr, (size_t)nb * hw * sizeof(float), s);
+            const char* raw = static_cast<const char*>(frames) + (size_t)f0 * rb;
+            const float* fr = reinterpret_cast<const float*>(raw);
+            if (!dev || format != FCD_FMT_F32) {
+                std::vector<int> idx(nb);
+                std::iota(idx.begin(), idx.end(), 0);
+                stage_frames(c, raw, format, dev, idx.data(), nb, s);
                 fr = c->frames_in.as<float>();
             }
             float* hdst = (dev && height_out) ? height_out + (size_t)f0 * hw : c->out_h.as<float>();
             int32_t* kdst = k_out && unwrap ? (dev ? k_out + (size_t)f0 * 2 * hw : c->fk.as<int32_t>()) : nullptr;
-            if (fused) {
-                // height only: band transforms, phase, unwrap and the z-row FFT in one
-                // pass (kernels_phase_rows.hip); colk lands in the spectra's DC bins
-                const fcdk::DemodTables T = demod_tables(c);
-                if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
-                fcdk::demod_rows(c->W, fr, c->H, nb, T, c->Xb.as<float2>(), c->twp_row.as<float2>(), s);
-                fcdk::demod_cols(c->H, c->Xb.as<float2>(), nb, T, c->Ab.as<float2>(), c->NCA, c->twp_col.as<float2>(),
-                                 s);
-                if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
-                fcdk::phase_rows(unwrap != 0, c->Ab.as<float2>(), c->H, nb, c->NCA, c->NCc[0], c->NCc[1],
-                                 c->theta_p.as<float>(), c->band_pre.as<float2>(), c->band_ptw.as<float2>(),
-                                 c->ztw.as<float2>(), c->col0.as<float>(), res ? res + (size_t)f0 * 2 : nullptr,
-                                 c->Zt.as<float2>(), c->seam.as<float2>(), s);
-                if (unwrap) fcdk::unwrap_colk_compact(c->col0.as<float>(), 2 * nb, c->H, c->colk.as<int>(), s);
-                if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
-                fcdk::int_cols(c->H, c->Zt.as<float2>(), c->W, nb, coef, c->Ht.as<float2>(), c->twp_col.as<float2>(), s,
-                               unwrap ? c->colk.as<int>() : nullptr);
-                fcdk::int_c2r(c->W, c->Ht.as<float2>(), c->H, nb, hdst, c->twp_row.as<float2>(), s);
-            } else {
-            if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
-            fast_demod(c, fr, nb, s);
-            if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
-            if (unwrap) fcdk::unwrap_colk(c->wrapped.as<float>(), 2 * nb, c->H, c->W, c->colk.as<int>(), s);
-            if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
-            fcdk::int_rows(c->W, unwrap ? 1 : 0, c->wrapped.as<float>(), c->colk.as<int>(), nullptr, kdst,
-                           res ? res + (size_t)f0 * 2 : nullptr, c->H, nb, c->Zt.as<float2>(),
-                           c->twp_row.as<float2>(), s);
-            fcdk::int_cols(c->H, c->Zt.as<float2>(), c->W, nb, coef, c->Ht.as<float2>(), c->twp_col.as<float2>(), s);
-            fcdk::int_c2r(c->W, c->Ht.as<float2>(), c->H, nb, hdst, c->twp_row.as<float2>(), s);
-            }
-            if (c->profiling) {
-                HIPCHK(hipEventRecord(c->next_event(), s));
-                c->prof_frames += nb;
-            }
+            first_pass_chunk(c, fr, nb, unwrap != 0, fused, res ? res + (size_t)f0 * 2 : nullptr, hdst, kdst, coef, s);
             if (height_out && !dev)
                 HIPCHK(hipMemcpyAsync(height_out + (size_t)f0 * hw, hdst, (size_t)nb * hw * 4, out_kind, s));
             if (wrapped_out)
@@ -933,49 +1106,83 @@ FCD_API int fcd_process(fcd_ctx* c, const float* frames, int n_frames, int flags
             }
             if (!dev) HIPCHK(hipStreamSynchronize(s));
         }
-        if (!unwrap) return FCD_OK;
-        // ---- pass 2: frames whose maps have residues are redone with the Boruvka (MST) unwrap
-        std::vector<int> counts((size_t)n_frames * 2);
-        HIPCHK(hipMemcpyAsync(counts.data(), res, counts.size() * sizeof(int), hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
-        std::vector<int> redo;
-        for (int f = 0; f < n_frames; ++f)
-            if (counts[2 * (size_t)f] || counts[2 * (size_t)f + 1]) redo.push_back(f);
-        const auto fix_t0 = std::chrono::steady_clock::now();
-        struct FixTimer {
-            fcd_ctx* c;
-            std::chrono::steady_clock::time_point t0;
-            size_t n;
-            ~FixTimer() {
-                if (c->profiling) {
-                    c->prof_fix_ms +=
-                        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-                    c->prof_fix_frames += (long)n;
-                }
+    }
+    if (!unwrap) return FCD_OK;
+    // ---- pass 2: frames whose maps have residues are redone with the Boruvka (MST) unwrap
+    std::vector<int> counts((size_t)n_frames * 2);
+    HIPCHK(hipMemcpyAsync(counts.data(), res, counts.size() * sizeof(int), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    std::vector<int> redo;
+    for (int f = 0; f < n_frames; ++f)
+        if (counts[2 * (size_t)f] || counts[2 * (size_t)f + 1]) redo.push_back(f);
+    const auto fix_t0 = std::chrono::steady_clock::now();
+    struct FixTimer {
+        fcd_ctx* c;
+        std::chrono::steady_clock::time_point t0;
+        size_t n;
+        ~FixTimer() {
+            if (c->profiling) {
+                c->prof_fix_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+                c->prof_fix_frames += (long)n;
             }
-        } fix_timer{c, fix_t0, redo.size()};
-        for (size_t g0 = 0; g0 < redo.size(); g0 += nbmax) {
-            const int ng = (int)std::min<size_t>(nbmax, redo.size() - g0);
-            for (int i = 0; i < ng; ++i)
-                HIPCHK(hipMemcpyAsync(c->frames_in.as<float>() + (size_t)i * hw, frames + (size_t)redo[g0 + i] * hw,
-                                      hw * sizeof(float), dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
-            fast_demod(c, c->frames_in.as<float>(), ng, s);
-            int32_t* kf = c->fk.as<int32_t>();
-            unwrap_maps(c, c->wrapped.as<float>(), 2 * ng, kf, nullptr, s);
-            fcdk::int_rows(c->W, 2, c->wrapped.as<float>(), nullptr, kf, nullptr, nullptr, c->H, ng,
-                           c->Zt.as<float2>(), c->twp_row.as<float2>(), s);
-            fcdk::int_cols(c->H, c->Zt.as<float2>(), c->W, ng, coef, c->Ht.as<float2>(), c->twp_col.as<float2>(), s);
-            fcdk::int_c2r(c->W, c->Ht.as<float2>(), c->H, ng, c->out_h.as<float>(), c->twp_row.as<float2>(), s);
-            for (int i = 0; i < ng; ++i) {
-                const size_t f = (size_t)redo[g0 + i];
-                if (height_out)
-                    HIPCHK(hipMemcpyAsync(height_out + f * hw, c->out_h.as<float>() + (size_t)i * hw, hw * 4,
-                                          out_kind, s));
-                if (k_out)
-                    HIPCHK(hipMemcpyAsync(k_out + f * 2 * hw, kf + (size_t)i * 2 * hw, 2 * hw * 4, out_kind, s));
-            }
-            HIPCHK(hipStreamSynchronize(s));
         }
+    } fix_timer{c, fix_t0, redo.size()};
+    for (size_t g0 = 0; g0 < redo.size(); g0 += nbmax) {
+        const int ng = (int)std::min<size_t>(nbmax, redo.size() - g0);
+        stage_frames(c, frames, format, dev, redo.data() + g0, ng, s);
+        fast_demod(c, c->frames_in.as<float>(), ng, s);
+        int32_t* kf = c->fk.as<int32_t>();
+        unwrap_maps(c, c->wrapped.as<float>(), 2 * ng, kf, nullptr, s);
+        fcdk::int_rows(c->W, 2, c->wrapped.as<float>(), nullptr, kf, nullptr, nullptr, c->H, ng, c->Zt.as<float2>(),
+                       c->twp_row.as<float2>(), s);
+        fcdk::int_cols(c->H, c->Zt.as<float2>(), c->W, ng, coef, c->Ht.as<float2>(), c->twp_col.as<float2>(), s);
+        fcdk::int_c2r(c->W, c->Ht.as<float2>(), c->H, ng, c->out_h.as<float>(), c->twp_row.as<float2>(), s);
+        for (int i = 0; i < ng; ++i) {
+            const size_t f = (size_t)redo[g0 + i];
+            if (height_out)
+                HIPCHK(hipMemcpyAsync(height_out + f * hw, c->out_h.as<float>() + (size_t)i * hw, hw * 4, out_kind, s));
+            if (k_out) HIPCHK(hipMemcpyAsync(k_out + f * 2 * hw, kf + (size_t)i * 2 * hw, 2 * hw * 4, out_kind, s));
+        }
+        HIPCHK(hipStreamSynchronize(s));
+    }
+    return FCD_OK;
+}
+
+}  // namespace
+
+FCD_API int fcd_process(fcd_ctx* c, const float* frames, int n_frames, int flags, double height, int unwrap,
+                        float* height_out, float* wrapped_out, int32_t* k_out, void* stream) {
+    FCD_TRY(return process_impl(c, frames, FCD_FMT_F32, n_frames, flags, height, unwrap, height_out, wrapped_out,
+                                k_out, stream))
+}
+
+FCD_API int fcd_process_raw(fcd_ctx* c, const void* frames, int format, int n_frames, int flags, double height,
+                            int unwrap, float* height_out, float* wrapped_out, int32_t* k_out, void* stream) {
+    FCD_TRY(return process_impl(c, frames, format, n_frames, flags, height, unwrap, height_out, wrapped_out, k_out,
+                                stream))
+}
+
+FCD_API int fcd_frame_bytes(fcd_ctx* c, int format, int64_t* bytes) {
+    FCD_TRY({
+        check_ctx(c);
+        if (!bytes) throw FcdError(FCD_E_INVALID, "bytes is null");
+        const size_t b = fcdk::raw_frame_bytes(format, c->H, c->W);
+        if (!b) throw FcdError(FCD_E_INVALID, "unknown frame format");
+        *bytes = (int64_t)b;
+    })
+}
+
+FCD_API int fcd_host_alloc(int64_t bytes, void** out) {
+    FCD_TRY({
+        if (!out || bytes < 0) throw FcdError(FCD_E_INVALID, "bad arguments");
+        *out = nullptr;
+        HIPCHK(hipHostMalloc(out, (size_t)std::max<int64_t>(bytes, 1), hipHostMallocDefault));
+    })
+}
+
+FCD_API int fcd_host_free(void* p) {
+    FCD_TRY({
+        if (p) HIPCHK(hipHostFree(p));
     })
 }
 

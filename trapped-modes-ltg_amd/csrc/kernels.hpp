@@ -45,6 +45,9 @@ struct DemodTables {
 };
 
 bool fft_size_supported(int n);
+// frame ingest (kernels_ingest.hip): raw samples (FCD_FMT_*) -> float32 frames
+size_t raw_frame_bytes(int format, int H, int W);
+void ingest(int format, const void* raw, int nframes, int H, int W, float* out, hipStream_t s);
 
 // ---- band-pruned per-frame pipeline (kernels_fast.hip) ----
 void demod_rows(int W, const float* frames, int H, int nb, const DemodTables& T, float2* Xb, const float2* tw,

@@ -22,12 +22,18 @@ FCD_E_NOPEAKS = -5
 FCD_E_INTERNAL = -6
 FCD_HOST_PTRS = 0
 FCD_DEVICE_PTRS = 1
+# frame sample formats (fcd_process_raw)
+FCD_FMT_F32 = 0
+FCD_FMT_U8 = 1
+FCD_FMT_U16 = 2
+FCD_FMT_P10 = 3
 
 # Every symbol include/fcd.h declares (checked by tests/test_abi.py).
 EXPORTED = (
     "fcd_abi_version", "fcd_last_error", "fcd_create", "fcd_destroy", "fcd_synchronize",
     "fcd_set_reference", "fcd_get_carriers", "fcd_process", "fcd_phases_from_spectrum",
     "fcd_unwrap", "fcd_integrate", "fcd_fft2", "fcd_profile", "fcd_stage_times",
+    "fcd_process_raw", "fcd_frame_bytes", "fcd_host_alloc", "fcd_host_free",
 )
 
 
@@ -81,6 +87,10 @@ def load_library(path=None):
             "fcd_fft2": ([vp, vp, i32, i32, vp, vp], i32),
             "fcd_profile": ([vp, i32], i32),
             "fcd_stage_times": ([vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)], i32),
+            "fcd_process_raw": ([vp, vp, i32, i32, i32, f64, i32, vp, vp, vp, vp], i32),
+            "fcd_frame_bytes": ([vp, i32, ctypes.POINTER(ctypes.c_int64)], i32),
+            "fcd_host_alloc": ([ctypes.c_int64, ctypes.POINTER(vp)], i32),
+            "fcd_host_free": ([vp], i32),
         }
         for name, (args, res) in sig.items():
             fn = getattr(lib, name)
@@ -177,6 +187,25 @@ class Engine:
                                      hmap.ctypes.data, _ptr(wrapped), _ptr(k), None))
         return hmap, wrapped, k
 
+    def frame_bytes(self, fmt):
+        b = ctypes.c_int64()
+        _check(self._lib.fcd_frame_bytes(self._h, int(fmt), ctypes.byref(b)))
+        return b.value
+
+    def process_raw(self, raw, fmt, n, height, unwrap=True, out=None):
+        """Heights of n frames stored as raw samples (FCD_FMT_*) in the host buffer `raw`
+        (an ndarray of n * frame_bytes(fmt) bytes, e.g. a PinnedBuffer view); `out`: an
+        optional float32 [n, H, W] array (pinned memory skips the staging copy)."""
+        raw = np.ascontiguousarray(raw)
+        if raw.nbytes < n * self.frame_bytes(fmt):
+            raise ValueError(f"raw buffer holds {raw.nbytes} bytes, {n} frames need {n * self.frame_bytes(fmt)}")
+        hmap = out if out is not None else np.empty((n,) + self.shape, np.float32)
+        if hmap.dtype != np.float32 or hmap.shape[0] < n or hmap.shape[1:] != self.shape or not hmap.flags.c_contiguous:
+            raise ValueError("out must be a C-contiguous float32 [n, H, W] array")
+        _check(self._lib.fcd_process_raw(self._h, raw.ctypes.data, int(fmt), int(n), FCD_HOST_PTRS, float(height),
+                                         int(bool(unwrap)), hmap.ctypes.data, None, None, None))
+        return hmap[:n]
+
     def process_device(self, frames_ptr, n, height, unwrap, height_ptr, wrapped_ptr=None, k_ptr=None,
                        stream=None):
         """Device-pointer variant (e.g. torch tensors' data_ptr()); asynchronous on `stream`."""
@@ -251,3 +280,31 @@ def engine_for(shape, device=None):
             e = Engine(shape, device)
             _engines[key] = e
         return e
+
+
+class PinnedBuffer:
+    """Page-locked host memory from the engine (fcd_host_alloc) viewed as a numpy
+    array: frames decoded into it, or heights written to it, cross PCIe by DMA
+    without a staging copy."""
+
+    def __init__(self, shape, dtype):
+        lib = load_library()
+        self._lib = lib
+        self.nbytes = int(np.prod(shape)) * np.dtype(dtype).itemsize
+        p = ctypes.c_void_p()
+        _check(lib.fcd_host_alloc(self.nbytes, ctypes.byref(p)))
+        self._p = p
+        buf = (ctypes.c_char * max(self.nbytes, 1)).from_address(p.value)
+        self.array = np.frombuffer(buf, dtype=dtype, count=int(np.prod(shape))).reshape(shape)
+
+    def free(self):
+        if getattr(self, "_p", None):
+            self.array = None
+            self._lib.fcd_host_free(self._p)
+            self._p = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
