@@ -67,6 +67,47 @@ def cpu_baseline(size, frames, seconds_cap=25.0):
                       f"with carriers cached, scipy.fft workers=1, {dt:.1f} s"}
 
 
+def _cpu_worker(args):
+    """One process of the all-cores CPU baseline: its own seeded frames, carriers once,
+    then `count` frames through the oracle; returns (frames, seconds)."""
+    size, count, seed = args
+    for p in (ROOT, os.path.join(ROOT, "trapped-modes-ltg_amd")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from bench_data import make_frames_numpy
+    from oracle import fcd_oracle as O
+    ref, fr = make_frames_numpy(size, count, seed=seed)
+    carriers = O.compute_carriers(ref, 0.001)
+    t0 = time.perf_counter()
+    for f in fr:
+        O.compute_height_map(ref, f, 0.001, height=1.0, carriers=carriers)
+    return len(fr), time.perf_counter() - t0
+
+
+def cpu_baseline_all_cores(size, workers=16, per_worker=6):
+    """The same oracle on `workers` host cores (one process per core, frames split
+    between them): total frames / slowest worker's time.  16 workers =
+    the GPU box's CPU share per GPU."""
+    import multiprocessing as mp
+    env = {k: os.environ.get(k) for k in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS")}
+    for k in env:
+        os.environ[k] = "1"
+    try:
+        with mp.get_context("spawn").Pool(workers) as pool:
+            res = pool.map(_cpu_worker, [(size, per_worker, 1000 + w) for w in range(workers)])
+    finally:
+        for k, v in env.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    frames = sum(r[0] for r in res)
+    wall = max(r[1] for r in res)
+    return {"value": frames / wall, "unit": "frames/s", "cores": workers, "kind": "port",
+            "sample": f"{frames} frames of {size}x{size} ({per_worker} per process, {workers} processes, one core "
+                      f"each), oracle/fcd_oracle.compute_height_map with carriers cached, slowest process {wall:.1f} s"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -76,6 +117,7 @@ def main():
     ap.add_argument("--batch", type=int, default=256, help="frames per GPU per step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=12)
+    ap.add_argument("--cpu-workers", type=int, default=16, help="processes of the all-cores CPU baseline")
     ap.add_argument("--gather", action="store_true", help="also time an RCCL gather of the heights to rank 0")
     args = ap.parse_args()
 
@@ -213,7 +255,10 @@ def main():
     if gather_ms is not None:
         out["gather_ms"] = round(gather_ms, 3)
     if world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(n, args.cpu_frames)
+        log("CPU baseline (oracle, 1 core, then all cores)")
+        single = cpu_baseline(n, args.cpu_frames)
+        out["cpu_baseline"] = cpu_baseline_all_cores(n, workers=args.cpu_workers)
+        out["cpu_baseline"]["single_core"] = single
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -168,19 +168,20 @@ __global__ __launch_bounds__((BPCfg<W, B>::THREADS), FCD_BAND_WAVES) void k_band
             STAMP(st++);
             float* o = out + row * W;
 #pragma unroll
-            for (int q = 0; q < E; ++q) {
+            for (int q = 0; q < E; q += 2) {  // pixel pairs: packed atan2 / wrap
                 if (FCD_ATAN_GROUP && q % FCD_ATAN_GROUP == 0) __builtin_amdgcn_sched_barrier(0);  // bound the atan2 chains in flight
                 const int n = g + L * t + RL * q;
-                const float a = fast_atan2(x[q].y, x[q].x);
                 if constexpr (REF) {
-                    o[n] = a;
+                    const fv2 a = fast_atan2_pk(fv2{x[q].y, x[q + 1].y}, fv2{x[q].x, x[q + 1].x});
+                    o[n] = a.x;
+                    o[n + RL] = a.y;
                 } else {
                     // wrap to [-pi, pi]: d - 2 pi rint(d / 2 pi), |d| < 2 pi
-                    const float d = thc[q] - a;
-                    const float w = fmaf(-6.28318530717959f, rintf(d * 0.159154943091895f), d);
+                    const fv2 w = wrapped_phase_pk(fv2{thc[q], thc[q + 1]}, x[q], x[q + 1]);
                     // streaming store (nt): the 8 N^2-byte phase stream must not evict
                     // the reference angles from the caches every frame
-                    st_stream(o + n, w);
+                    st_stream(o + n, w.x);
+                    st_stream(o + n + RL, w.y);
                 }
             }
             STAMP(st++);

@@ -188,14 +188,16 @@ __global__ __launch_bounds__(PR_THREADS) void k_phase_rows(
                     x[q] = cmul(stage[(c * PR_B + t + PR_G * q) * PR_SROW + wave], ptl[q * 64 + lane]);
                 GroupFFTTab<PR_B>::template run<true>(x, slot + g * GSched<PR_B>::REGION, t, btab);
 #pragma unroll
-                for (int q = 0; q < 16; ++q) {
+                for (int q = 0; q < 16; q += 2) {  // pixel pairs: packed atan2 / wrap
                     if (q % 4 == 0) __builtin_amdgcn_sched_barrier(0);
-                    const float d = th[q] - fast_atan2(x[q].y, x[q].x);
-                    const float wq = fmaf(-kTwoPiF, rintf(d * 0.159154943091895f), d);
-                    if (c == 0)
-                        w0[q] = wq;
-                    else
-                        w1[q] = wq;
+                    const fv2 wq = wrapped_phase_pk(fv2{th[q], th[q + 1]}, x[q], x[q + 1]);
+                    if (c == 0) {
+                        w0[q] = wq.x;
+                        w0[q + 1] = wq.y;
+                    } else {
+                        w1[q] = wq.x;
+                        w1[q + 1] = wq.y;
+                    }
                 }
                 PR_STAMP(3 + c);
             }
