@@ -37,7 +37,7 @@ def load_traffic(n, chunk):
             t = json.load(f)
     except (OSError, ValueError):
         return None
-    if t.get("frame") != n or t.get("chunk") != chunk:
+    if t.get("frame") != n:
         return None
     return t
 
@@ -129,7 +129,10 @@ def main():
 
     rank, world, local = dist_env()
     if world > 1:
-        dist.init_process_group("nccl", init_method="env://")
+        # "nccl" is RCCL on ROCm (one process per GPU, xGMI); FCD_BENCH_BACKEND=gloo only
+        # to rehearse N ranks sharing the GPUs of a smaller box
+        dist.init_process_group(os.environ.get("FCD_BENCH_BACKEND", "nccl"), init_method="env://")
+    local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     n, B = args.size, args.batch
@@ -220,6 +223,9 @@ def main():
                  if k in path_names}  # us per frame
     per_frame["fixup_frames_per_step"] = fix_frames / prof_steps
     traffic = load_traffic(n, chunk)
+    traffic_launch = None
+    if traffic:  # measured per frame at traffic["chunk"] frames per launch; scaled to this launch size
+        traffic_launch = int(round(traffic["demod_group_bytes_per_frame"] * demod_frames_per_launch))
     out = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -240,13 +246,14 @@ def main():
                    "parallelism": f"frame-sharded x{world}, no collective in the compute"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic["demod_group_bytes_per_launch"] if traffic else None,
+                     "traffic": traffic_launch,
                      "kernel": "demod launch group k_demod_rows + k_demod_cols + k_band_phase "
                                "(frame f32 in -> 2 wrapped phases f32 out), 12*N^2 B/frame",
                      "frames_per_launch": round(demod_frames_per_launch, 2),
                      "us_per_launch": round(demod_us_per_launch, 2),
                      "algorithmic_bytes_per_launch": int(demod_bytes * demod_frames_per_launch),
-                     "traffic_source": traffic["source"] if traffic else None,
+                     "traffic_source": (traffic["source"] + f"; measured at {traffic['chunk']} frames per launch, "
+                                        "per-frame bytes x frames per launch") if traffic else None,
                      "measured_as": "separate profiled pass of the same frames with the wrapped phases written "
                                     "(the headline path fuses the band transform with the unwrap)"},
         "stage_us_per_frame": per_frame,
