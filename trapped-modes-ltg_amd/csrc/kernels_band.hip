@@ -39,6 +39,14 @@ namespace {
 #define FCD_BAND_NOTHETA 0  // diagnostic ablation only (wrong results): no reference-angle loads
 #endif
 
+#ifndef FCD_BAND_FMAJOR
+#define FCD_BAND_FMAJOR 1  // item order frame-fastest: concurrent blocks share the (carrier, row tile) and its theta
+#endif
+
+#ifndef FCD_BAND_NOSTORE
+#define FCD_BAND_NOSTORE 0  // diagnostic ablation only (no output): phase stores suppressed
+#endif
+
 #ifndef FCD_ATAN_GROUP
 #define FCD_ATAN_GROUP 4  // atan2 chains interleaved per scheduling group (0: unbounded)
 #endif
@@ -86,6 +94,12 @@ __global__ __launch_bounds__((BPCfg<W, B>::THREADS), FCD_BAND_WAVES) void k_band
     for (int i = threadIdx.x; i < RL * E; i += C::THREADS) ptl[(i % E) * RL + i / E] = pre[i];
     const int rbs = H / BTILE;
     const int items = nb * 2 * rbs;
+    // item -> (frame, carrier, row tile).  Frame-fastest order: the blocks running
+    // at one time work on the same (carrier, row tile) of different frames, so the
+    // tile's reference angles (64 KB) are read from HBM once and then hit in L2.
+    auto item_f = [&](int blk) { return FCD_BAND_FMAJOR ? blk % nb : blk / (2 * rbs); };
+    auto item_c = [&](int blk) { return FCD_BAND_FMAJOR ? (blk / nb) % 2 : (blk / rbs) % 2; };
+    auto item_rb = [&](int blk) { return FCD_BAND_FMAJOR ? blk / (2 * nb) : blk % rbs; };
     // Tile staging is software-pipelined: the next item's tile is loaded into
     // registers (SPT values per thread, all loads in flight at once) while
     // the current item's rows are transformed.
@@ -94,7 +108,7 @@ __global__ __launch_bounds__((BPCfg<W, B>::THREADS), FCD_BAND_WAVES) void k_band
     const int tile_n = NCA * BTILE;
     float2 pf[SPT];
     auto tile_src = [&](int blk) {
-        const int f = blk / (2 * rbs), c = (blk / rbs) % 2, rb = blk % rbs;
+        const int f = item_f(blk), c = item_c(blk), rb = item_rb(blk);
         return Ab + (((long)f * 2 + c) * rbs + rb) * (long)tile_n;
     };
     auto fetch = [&](int blk) {
@@ -112,7 +126,7 @@ __global__ __launch_bounds__((BPCfg<W, B>::THREADS), FCD_BAND_WAVES) void k_band
 #pragma unroll
             for (int q = 0; q < E; ++q) th[q] = 0.f;
         } else if constexpr (!REF) {
-            const int c = (blk / rbs) % 2, rb = blk % rbs;
+            const int c = item_c(blk), rb = item_rb(blk);
             const float4* tr = reinterpret_cast<const float4*>(theta + ((long)c * H + rb * BTILE + rl) * W) + l * 4;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -130,7 +144,7 @@ __global__ __launch_bounds__((BPCfg<W, B>::THREADS), FCD_BAND_WAVES) void k_band
     }
     [[maybe_unused]] int st = 0;
     for (int blk = blockIdx.x; blk < items; blk += gridDim.x) {
-        const int f = blk / (2 * rbs), c = (blk / rbs) % 2, rb = blk % rbs;
+        const int f = item_f(blk), c = item_c(blk), rb = item_rb(blk);
         const int ncc = c ? ncc1 : ncc0;
         STAMP(st++);
         // slots [ncc, B) are staged as zeros: the transform input needs no select
@@ -180,8 +194,10 @@ __global__ __launch_bounds__((BPCfg<W, B>::THREADS), FCD_BAND_WAVES) void k_band
                     const fv2 w = wrapped_phase_pk(fv2{thc[q], thc[q + 1]}, x[q], x[q + 1]);
                     // streaming store (nt): the 8 N^2-byte phase stream must not evict
                     // the reference angles from the caches every frame
-                    st_stream(o + n, w.x);
-                    st_stream(o + n + RL, w.y);
+                    if (!FCD_BAND_NOSTORE || w.x == 1234.5f) {
+                        st_stream(o + n, w.x);
+                        st_stream(o + n + RL, w.y);
+                    }
                 }
             }
             STAMP(st++);

@@ -476,10 +476,18 @@ __global__ __launch_bounds__(KCfg<H>::THREADS, ColWaves<H>::V) void k_int_cols(c
             px[q] = src[tl + ((long)col << zts) + (rr & zmask)];
         }
     };
-    fetch(blockIdx.x * TEAMS + team);
-    for (int base = blockIdx.x * TEAMS; base < items; base += gridDim.x * TEAMS) {
+    // Each block walks a CONTIGUOUS range of columns: Zt's 8-row tiles hold a
+    // column's rows in 64 bytes, half a 128-byte line whose other half is the
+    // neighbouring column; the mirror columns W - c of consecutive items pair up
+    // off by one, so grid-striding fetched every mirror line twice (1.5x the
+    // compulsory Zt bytes).  In a contiguous range the neighbour is the next
+    // iteration's item and its half line is still in L2.
+    const int per = (items + gridDim.x - 1) / gridDim.x;
+    const int i0 = blockIdx.x * per, i1 = min(i0 + per, items);
+    fetch(i0 + team < i1 ? i0 + team : items);
+    for (int base = i0; base < i1; base += TEAMS) {
         const int item = base + team;
-        const bool valid = item < items;
+        const bool valid = item < i1;
         const int f = valid ? item / NCH : 0, col = valid ? item % NCH : 0;
         const int colm = (W - col) & (W - 1);
         float2 x[E];
@@ -490,7 +498,7 @@ __global__ __launch_bounds__(KCfg<H>::THREADS, ColWaves<H>::V) void k_int_cols(c
                 y[q] = py[q];
                 x[q] = px[q];
             }
-            if (base + gridDim.x * TEAMS < items) fetch(base + gridDim.x * TEAMS + team);
+            if (base + TEAMS < i1) fetch(base + TEAMS + team < i1 ? base + TEAMS + team : items);
             if (colk && colm == 0) {  // column-0 unwrap offsets of the fused path: row DC bins
                 const float sc = 6.28318530717959f * (float)W;
 #pragma unroll

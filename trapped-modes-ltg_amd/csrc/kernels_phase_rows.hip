@@ -45,6 +45,9 @@ constexpr int PR_B = 128;             // band window
 #define FCD_PR_ROWS 8
 #endif
 constexpr int PR_ROWS = FCD_PR_ROWS;  // rows per tile (one wave each)
+#ifndef FCD_PR_ATAN_GROUP
+#define FCD_PR_ATAN_GROUP 4  // atan2 chains per scheduling group (0: unbounded)
+#endif
 constexpr int PR_ZT = 8;              // Zt tile height (int_rows.inc zt_rows(1024))
 static_assert(PR_ZT % PR_ROWS == 0, "a tile covers part of one Zt tile");
 constexpr int PR_WAVES = PR_ROWS;     // one wave per row
@@ -189,7 +192,7 @@ __global__ __launch_bounds__(PR_THREADS) void k_phase_rows(
                 GroupFFTTab<PR_B>::template run<true>(x, slot + g * GSched<PR_B>::REGION, t, btab);
 #pragma unroll
                 for (int q = 0; q < 16; q += 2) {  // pixel pairs: packed atan2 / wrap
-                    if (q % 4 == 0) __builtin_amdgcn_sched_barrier(0);
+                    if (FCD_PR_ATAN_GROUP && q % FCD_PR_ATAN_GROUP == 0) __builtin_amdgcn_sched_barrier(0);
                     const fv2 wq = wrapped_phase_pk(fv2{th[q], th[q + 1]}, x[q], x[q + 1]);
                     if (c == 0) {
                         w0[q] = wq.x;
