@@ -247,6 +247,88 @@ struct GroupFFTTab {
     }
 };
 
+// Two independent transforms of the same length advanced in lockstep (the two
+// carriers of one row in the fused kernel): each pass's twiddles are read once
+// for both, and both transforms' values cross the float-half exchange between
+// the same pair of wave syncs, so one transform's LDS round trip hides behind
+// the other's arithmetic.  s0 / s1: two FLOAT regions of GSched<B>::REGION.
+template <int B>
+struct GroupFFTTab2 {
+    using S = GSched<B>;
+    static constexpr int E = S::E, G = S::G, NP = S::NP;
+
+    template <bool INV>
+    __device__ __forceinline__ static void run_half(float2 (&x0)[E], float2 (&x1)[E], float* s0, float* s1, int t,
+                                                    const float2* tab) {
+        pass<0, INV>(x0, x1, s0, s1, t, tab);
+    }
+
+    template <int P, bool INV>
+    __device__ __forceinline__ static void pass(float2 (&x0)[E], float2 (&x1)[E], float* s0, float* s1, int t,
+                                                const float2* tab) {
+        constexpr int R = S::radix(P), L = S::ell(P), BPT = E / R;
+        float2 a0[BPT][R], a1[BPT][R];
+#pragma unroll
+        for (int b = 0; b < BPT; ++b) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                a0[b][r] = x0[b + BPT * r];
+                a1[b][r] = x1[b + BPT * r];
+            }
+            if constexpr (P > 0) {
+                const int k = (t + b * G) & (L - 1);
+                const float2* tk = tab + S::passoff(P) + k * (R - 1) - 1;
+#pragma unroll
+                for (int r = 1; r < R; ++r) {
+                    const float2 w = tk[r];
+                    a0[b][r] = cmul_dir<INV>(a0[b][r], w);
+                    a1[b][r] = cmul_dir<INV>(a1[b][r], w);
+                }
+            }
+            dft_reg<R, INV>(a0[b]);
+            dft_reg<R, INV>(a1[b]);
+        }
+        if constexpr (P + 1 == NP) {
+#pragma unroll
+            for (int b = 0; b < BPT; ++b)
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    x0[b + BPT * r] = a0[b][r];
+                    x1[b + BPT * r] = a1[b][r];
+                }
+        } else {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                wave_sync();
+#pragma unroll
+                for (int b = 0; b < BPT; ++b) {
+                    const int j = t + b * G;
+                    const int k = j & (L - 1);
+                    const int base = (j - k) * R + k;
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        s0[pad(base + r * L)] = h ? a0[b][r].y : a0[b][r].x;
+                        s1[pad(base + r * L)] = h ? a1[b][r].y : a1[b][r].x;
+                    }
+                }
+                wave_sync();
+#pragma unroll
+                for (int q = 0; q < E; ++q) {
+                    const float v0 = s0[pad(t + G * q)], v1 = s1[pad(t + G * q)];
+                    if (h) {
+                        x0[q].y = v0;
+                        x1[q].y = v1;
+                    } else {
+                        x0[q].x = v0;
+                        x1[q].x = v1;
+                    }
+                }
+            }
+            pass<P + 1, INV>(x0, x1, s0, s1, t, tab);
+        }
+    }
+};
+
 // atan2(y, x) in f32: |error| <= ~2.5e-7 rad (degree-8 odd minimax-fit
 // polynomial on [0, 1] after the octant reduction, v_rcp_f32 division);
 // atan2(0, 0) = 0, like atan2f.  About 20 VALU operations.

@@ -45,6 +45,12 @@ constexpr int PR_B = 128;             // band window
 #define FCD_PR_ROWS 8
 #endif
 constexpr int PR_ROWS = FCD_PR_ROWS;  // rows per tile (one wave each)
+#ifndef FCD_PR_PAIRED
+#define FCD_PR_PAIRED 1  // both carriers' band transforms in lockstep
+#endif
+#ifndef FCD_PR_THETA_LATE
+#define FCD_PR_THETA_LATE 1  // paired path: reference angles loaded after the transforms (register pressure)
+#endif
 #ifndef FCD_PR_ATAN_GROUP
 #define FCD_PR_ATAN_GROUP 4  // atan2 chains per scheduling group (0: unbounded)
 #endif
@@ -66,6 +72,7 @@ constexpr int OFF_PREV = OFF_SLOT + PR_WAVES * PR_SLOT;              // last unw
 constexpr size_t PR_LDS = (size_t)(OFF_PREV + PR_SLOT) * 8;
 static_assert(PR_LDS <= 160 * 1024, "fused kernel LDS");
 static_assert(PR_L * GSched<PR_B>::REGION <= PR_SLOT, "band exchange must fit the slot");
+static_assert(2 * PR_L * GSched<PR_B>::REGION <= 2 * PR_SLOT, "paired float-half band exchange must fit the slot");
 
 constexpr float kTwoPiF = 6.28318530717959f;
 constexpr float kPR_VLim = 3.14159265f - 4e-3f;
@@ -99,8 +106,11 @@ __device__ unsigned long long g_pr_stamps[PR_WAVES * 16];
     } while (0)
 #endif
 
+#ifndef FCD_PR_MINB
+#define FCD_PR_MINB 1  // workgroups per CU the register allocation must allow (launch-bounds)
+#endif
 template <bool UNWRAP>
-__global__ __launch_bounds__(PR_THREADS) void k_phase_rows(
+__global__ __launch_bounds__(PR_THREADS, FCD_PR_MINB) void k_phase_rows(
     const float2* __restrict__ Ab, int H, int nb, int NCA, int ncc0, int ncc1, const float* __restrict__ theta,
     const float2* __restrict__ pre, const float2* __restrict__ ptw, const float2* __restrict__ ztw,
     float* __restrict__ col0, int* __restrict__ flags, float2* __restrict__ Zt, float2* __restrict__ seam, int per) {
@@ -169,12 +179,50 @@ __global__ __launch_bounds__(PR_THREADS) void k_phase_rows(
             // the reference angles of this lane's 16 pixels, both carriers, issued
             // before the transforms: lane-contiguous in the permuted copy
             float4 th4[2][4];
+            auto load_theta = [&]() {
 #pragma unroll
-            for (int c = 0; c < 2; ++c) {
-                const float4* tp = reinterpret_cast<const float4*>(theta + ((long)c * H + r) * PR_W) + lane * 4;
+                for (int c = 0; c < 2; ++c) {
+                    const float4* tp = reinterpret_cast<const float4*>(theta + ((long)c * H + r) * PR_W) + lane * 4;
 #pragma unroll
-                for (int k = 0; k < 4; ++k) th4[c][k] = tp[k];
+                    for (int k = 0; k < 4; ++k) th4[c][k] = tp[k];
+                }
+            };
+#if FCD_PR_PAIRED && FCD_PR_THETA_LATE
+#else
+            load_theta();
+#endif
+#if FCD_PR_PAIRED
+            // both carriers' transforms in lockstep (GroupFFTTab2): float-half
+            // exchange regions of the two carriers side by side in the slot
+            float2 x0[16], x1[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const float2 p = ptl[q * 64 + lane];
+                x0[q] = cmul(stage[(t + PR_G * q) * PR_SROW + wave], p);
+                x1[q] = cmul(stage[(PR_B + t + PR_G * q) * PR_SROW + wave], p);
             }
+            float* const sx = reinterpret_cast<float*>(slot);
+            GroupFFTTab2<PR_B>::template run_half<true>(x0, x1, sx + g * GSched<PR_B>::REGION,
+                                                       sx + (PR_L + g) * GSched<PR_B>::REGION, t, btab);
+            PR_STAMP(3);
+#if FCD_PR_THETA_LATE
+            load_theta();
+#endif
+#pragma unroll
+            for (int q = 0; q < 16; q += 2) {  // pixel pairs: packed atan2 / wrap
+                if (FCD_PR_ATAN_GROUP && q % FCD_PR_ATAN_GROUP == 0) __builtin_amdgcn_sched_barrier(0);
+                const int k = q / 4, e = q % 4;
+                const fv2 t0 = e == 0 ? fv2{th4[0][k].x, th4[0][k].y} : fv2{th4[0][k].z, th4[0][k].w};
+                const fv2 t1 = e == 0 ? fv2{th4[1][k].x, th4[1][k].y} : fv2{th4[1][k].z, th4[1][k].w};
+                const fv2 a0 = wrapped_phase_pk(t0, x0[q], x0[q + 1]);
+                const fv2 a1 = wrapped_phase_pk(t1, x1[q], x1[q + 1]);
+                w0[q] = a0.x;
+                w0[q + 1] = a0.y;
+                w1[q] = a1.x;
+                w1[q + 1] = a1.y;
+            }
+            PR_STAMP(4);
+#else
 #pragma unroll
             for (int c = 0; c < 2; ++c) {
                 float th[16];
@@ -204,6 +252,7 @@ __global__ __launch_bounds__(PR_THREADS) void k_phase_rows(
                 }
                 PR_STAMP(3 + c);
             }
+#endif
         }
         // ---- natural strided -> blocked through the slot
         wave_sync();
