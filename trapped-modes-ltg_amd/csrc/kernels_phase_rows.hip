@@ -263,32 +263,43 @@ __global__ __launch_bounds__(PR_THREADS, FCD_PR_MINB) void k_phase_rows(
         }
         wave_sync();
         const int j0 = lane * 16;
-        float* const sf = reinterpret_cast<float*>(slot);  // map m of pixel n at sf[2 * pad(n) + m]
+        // both maps at once: pixel n of map 0 / 1 is slot[pad(n)].x / .y (64-bit LDS
+        // accesses, the two maps' scans interleaved)
         int bad = 0;
+        {
+            float2 v[17];
 #pragma unroll
-        for (int m = 0; m < 2; ++m) {
-            float v[17];
-#pragma unroll
-            for (int j = 0; j < 16; ++j) v[j] = sf[2 * pad(j0 + j) + m];
-            v[16] = lane < 63 ? sf[2 * pad(j0 + 16) + m] : 0.f;
-            if (lane == 0) col0[((long)f * 2 + m) * H + r] = v[0];
+            for (int j = 0; j < 16; ++j) v[j] = slot[pad(j0 + j)];
+            v[16] = lane < 63 ? slot[pad(j0 + 16)] : make_float2(0.f, 0.f);
+            if (lane == 0) {
+                col0[((long)f * 2 + 0) * H + r] = v[0].x;
+                col0[((long)f * 2 + 1) * H + r] = v[0].y;
+            }
             if constexpr (UNWRAP) {
-                int amb = 0, hb = 0;  // 2-bit codes of h + 1
+                int amb = 0, hb0 = 0, hb1 = 0;  // 2-bit codes of h + 1
 #pragma unroll
                 for (int j = 0; j < 16; ++j) {
-                    const int h = (j0 + j + 1 < PR_W) ? fw_amb(v[j], v[j + 1], amb) : 0;
-                    hb |= (h + 1) << (2 * j);
+                    const bool in = j0 + j + 1 < PR_W;
+                    const int h0 = in ? fw_amb(v[j].x, v[j + 1].x, amb) : 0;
+                    const int h1 = in ? fw_amb(v[j].y, v[j + 1].y, amb) : 0;
+                    hb0 |= (h0 + 1) << (2 * j);
+                    hb1 |= (h1 + 1) << (2 * j);
                 }
-                int run = 0;  // (1 - h) increments of the segment
-#pragma unroll
-                for (int j = 0; j < 16; ++j) run += 2 - ((hb >> (2 * j)) & 3);
-                const int incl = team_scan_incl_dpp<64>(run);
-                int acc = incl - run - j0;  // k' at the segment start
-                wave_sync();                // every lane has read its neighbour's first value
+                int run0 = 0, run1 = 0;  // (1 - h) increments of the segment
 #pragma unroll
                 for (int j = 0; j < 16; ++j) {
-                    sf[2 * pad(j0 + j) + m] = fmaf((float)acc, kTwoPiF, v[j]);
-                    acc -= ((hb >> (2 * j)) & 3) - 1;
+                    run0 += 2 - ((hb0 >> (2 * j)) & 3);
+                    run1 += 2 - ((hb1 >> (2 * j)) & 3);
+                }
+                const int incl0 = team_scan_incl_dpp<64>(run0);
+                const int incl1 = team_scan_incl_dpp<64>(run1);
+                int acc0 = incl0 - run0 - j0, acc1 = incl1 - run1 - j0;  // k' at the segment start
+                wave_sync();  // every lane has read its neighbour's first value
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    slot[pad(j0 + j)] = make_float2(fmaf((float)acc0, kTwoPiF, v[j].x), fmaf((float)acc1, kTwoPiF, v[j].y));
+                    acc0 -= ((hb0 >> (2 * j)) & 3) - 1;
+                    acc1 -= ((hb1 >> (2 * j)) & 3) - 1;
                 }
                 bad |= amb;
             }
