@@ -44,6 +44,12 @@ struct DemodTables {
     int NCc[2];
 };
 
+// Zt (row spectra of phi0 + i phi1) tile height at W <= 1024: every column
+// segment of a tile is one run of FCD_ZT_1024 * 8 bytes (shared by the fused
+// kernel's write-out, k_int_rows2 and the column kernels).
+#ifndef FCD_ZT_1024
+#define FCD_ZT_1024 8
+#endif
 bool fft_size_supported(int n);
 // frame ingest (kernels_ingest.hip): raw samples (FCD_FMT_*) -> float32 frames
 size_t raw_frame_bytes(int format, int H, int W);

@@ -54,7 +54,7 @@ constexpr int PR_ROWS = FCD_PR_ROWS;  // rows per tile (one wave each)
 #ifndef FCD_PR_ATAN_GROUP
 #define FCD_PR_ATAN_GROUP 4  // atan2 chains per scheduling group (0: unbounded)
 #endif
-constexpr int PR_ZT = 8;              // Zt tile height (int_rows.inc zt_rows(1024))
+constexpr int PR_ZT = FCD_ZT_1024;    // Zt tile height (int_rows.inc zt_rows(1024))
 static_assert(PR_ZT % PR_ROWS == 0, "a tile covers part of one Zt tile");
 constexpr int PR_WAVES = PR_ROWS;     // one wave per row
 constexpr int PR_THREADS = 64 * PR_WAVES;
