@@ -23,6 +23,7 @@
 #include <string>
 
 #include "kernels.hpp"
+#include "gfft.hpp"
 #include "regfft.hpp"
 
 namespace fcdk {
@@ -253,12 +254,11 @@ __global__ __launch_bounds__(KCfg<W>::THREADS, FCD_MIN_WAVES) void k_demod_phase
             const float* th = theta + ((long)c * H + r) * W;
             float* wo = wrapped + (((long)f * 2 + c) * H + r) * W;
 #pragma unroll
-            for (int q = 0; q < E; ++q) {
+            for (int q = 0; q < E; q += 2) {  // pixel pairs: packed atan2 + wrap (gfft.hpp)
                 const int i = t + TT * q;
-                float d = th[i] - atan2f(x[q].y, x[q].x);
-                if (d > kPiF) d -= kTwoPiF;
-                else if (d < -kPiF) d += kTwoPiF;
-                wo[i] = d;
+                const fv2 w = wrapped_phase_pk(fv2{th[i], th[i + TT]}, x[q], x[q + 1]);
+                st_stream(wo + i, w.x);
+                st_stream(wo + i + TT, w.y);
             }
         }
         __syncthreads();
@@ -596,8 +596,15 @@ __global__ __launch_bounds__(C2RCfg<W>::THREADS) void k_int_c2r(const float2* __
             pf[i] = src[tix(r0 + rl, col, NCH)];
         }
     };
-    if ((int)blockIdx.x < nb * nblk) fetch(blockIdx.x);
-    for (int blk = blockIdx.x; blk < nb * nblk; blk += gridDim.x) {
+    // XCD-aware order: workgroups are dealt round-robin to the 8 XCDs, each with
+    // its own L2.  Below W = 1024 a staged block is only rpw of a 16-row Ht tile's
+    // rows, so the 16 / rpw blocks of one tile read the same 128-byte lines: give
+    // them consecutive virtual ids on ONE XCD (b % 8 = XCD, b / 8 = slot) so the
+    // lines are fetched into one L2 once instead of into several.
+    const int G = gridDim.x;
+    const int vb = (G % 8 == 0) ? (int)(blockIdx.x % 8) * (G / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
+    if (vb < nb * nblk) fetch(vb);
+    for (int blk = vb; blk < nb * nblk; blk += G) {
         const int f = blk / nblk, r0 = (blk % nblk) * rpw;
 #pragma unroll
         for (int i = 0; i < SPT; ++i) {
@@ -605,7 +612,7 @@ __global__ __launch_bounds__(C2RCfg<W>::THREADS) void k_int_c2r(const float2* __
             if (idx < NCH * rpw) stage[(idx / rpw) * (rpw + 1) + idx % rpw] = pf[i];
         }
         __syncthreads();
-        if (blk + (int)gridDim.x < nb * nblk) fetch(blk + gridDim.x);
+        if (blk + G < nb * nblk) fetch(blk + G);
         for (int pr = team; pr < rpw / 2; pr += TEAMS) {
             float2 x[E];
 #pragma unroll
