@@ -82,6 +82,15 @@ int fcd_synchronize(fcd_ctx* ctx);
  * (fourier.py:7-41) and Carrier.__init__ (carriers.py:10-24).  Synchronises. */
 int fcd_set_reference(fcd_ctx* ctx, const float* reference, int flags, double square_size, fcd_ref_info* info);
 
+/* fourier.find_peaks (fourier.py:7-41) + fcd.compute_calibration_factor
+ * (fcd.py:72-101) for n images (many-reference workloads)
+ * WITHOUT replacing the context's reference: infos[i] gets what
+ * fcd_set_reference(images[i]) would report (peaks, radius, calibration factor,
+ * carrier frequencies, disk pixel counts, blobs, threshold).  The |F| high-pass,
+ * threshold and candidate extraction run on the device, the labelling of the
+ * few above-threshold pixels on the host.  Synchronises. */
+int fcd_find_peaks(fcd_ctx* ctx, const float* images, int n, int flags, double square_size, fcd_ref_info* infos);
+
 /* Carrier arrays for the Python mirror: ccsgn complex64 [2][rows][cols]
  * (carriers.py:22-24, normalised like scipy ifft2) and the ifftshifted disk
  * masks uint8 [2][rows][cols] (carriers.py:17-20).  Host pointers, either may

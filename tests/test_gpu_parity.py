@@ -416,3 +416,33 @@ def test_empty_batch_and_errors(lib):
         fcd.compute_height_map(ref, frames[0][:128], 0.001, height=1.0)
     with pytest.raises(Exception):
         fcd.compute_height_map(ref, frames[0], 0.001, height=0.0)
+
+
+def test_find_peaks_batch_matches_reference_setup(lib, golden):
+    """fcd_find_peaks (many references in one call): every field equal to
+    what fcd_set_reference reports and to the reference's golden values (bit-exact), and
+    the engine's current reference (its heights) untouched."""
+    from bench_data import make_frames_numpy
+    from pyfcd.fcd import fcd
+    r = golden("real_pair")
+    d = golden("real_df")
+    refs = np.stack([r["ref_u8"].astype(np.float32), d["ref_u16"].astype(np.float32)])
+    eng = lib.Engine(refs.shape[1:])
+    ref_s, frames = make_frames_numpy(1024, 1, seed=9, rotate_deg=5.0)
+    eng.set_reference(ref_s, 0.001)
+    h_before, _, _ = eng.process(frames, 1.0, want_phases=False)
+    infos = eng.find_peaks(refs, 0.0022)
+    h_after, _, _ = eng.process(frames, 1.0, want_phases=False)
+    assert np.array_equal(h_before, h_after)
+    for img, info in zip(refs, infos):
+        e2 = lib.Engine(refs.shape[1:])
+        want = e2.set_reference(img, 0.0022)
+        for k in ("radius", "calibration_factor", "threshold", "n_blobs"):
+            assert getattr(info, k) == getattr(want, k), k
+        for k in ("peaks", "frequencies", "mask_count", "blob_peaks"):
+            assert np.array_equal(np.ctypeslib.as_array(getattr(info, k)), np.ctypeslib.as_array(getattr(want, k))), k
+    assert np.array_equal(np.ctypeslib.as_array(infos[0].peaks), r["peaks"])
+    assert infos[0].calibration_factor == float(r["cf"])
+    out = fcd.compute_calibration_factors(0.002, refs[1:])
+    assert out[0][0] == float(d["committed_cf"][0])
+    assert [p.tolist() for p in out[0][1]] == d["peaks"].tolist()

@@ -690,6 +690,52 @@ void band_reference(fcd_ctx* c, const float* dref, hipStream_t s) {
     fcdk::band_theta_lanes(c->W, c->band_B, c->theta_b.as<float>(), 2 * c->H, c->theta_p.as<float>(), s);
 }
 
+// fourier.find_peaks + compute_calibration_factor + the carrier disks for one
+// device-resident image: sets c->info and c->disk_rows_host (fcd.py:53-101,
+// fourier.py:7-41).  Uses the chunk workspace (spec, wrapped, scalar, cand_*).
+void find_peaks_device(fcd_ctx* c, const float* dref, double square_size, hipStream_t s) {
+    const long hw = c->hw();
+    // fourier.find_peaks: |fftshift(fft2(ref - mean))| * highpass  (fourier.py:18-34)
+    double* dmean = c->scalar.as<double>();
+    fcdk::mean_f64(dref, hw, dmean, s);
+    double mean = 0;
+    HIPCHK(hipMemcpyAsync(&mean, dmean, sizeof(double), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    const float meanf = (float)(mean / (double)hw);
+    float2* F = c->spec.as<float2>();
+    fft2_real(c, dref, F, 1, meanf, s);
+    const std::vector<double> krs = wavenumber(c->H, 1.0, true), kcs = wavenumber(c->W, 1.0, true);
+    DevBuf ktab;
+    ktab.ensure((c->H + c->W) * sizeof(double));
+    upload(ktab.p, krs.data(), c->H * sizeof(double), s);
+    upload(ktab.as<double>() + c->H, kcs.data(), c->W * sizeof(double), s);
+    const double kmin = 4 * kPi / (double)std::min(c->H, c->W);
+    float* mag = c->wrapped.as<float>();
+    unsigned* maxbits = reinterpret_cast<unsigned*>(c->scalar.as<char>() + 16);
+    int* count = reinterpret_cast<int*>(c->scalar.as<char>() + 32);
+    fcdk::spectrum_mag(F, mag, maxbits, c->H, c->W, ktab.as<double>(), ktab.as<double>() + c->H, kmin * kmin, s);
+    const int cap = 1 << 16;
+    c->cand_idx.ensure(cap * sizeof(int));
+    c->cand_val.ensure(cap * sizeof(float));
+    fcdk::spectrum_candidates(mag, maxbits, c->H, c->W, count, c->cand_idx.as<int>(), c->cand_val.as<float>(),
+                              cap, s);
+    int ncand = 0;
+    unsigned mb = 0;
+    HIPCHK(hipMemcpyAsync(&ncand, count, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(&mb, maxbits, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (ncand > cap) throw FcdError(FCD_E_UNSUPPORTED, "find_peaks: too many pixels above threshold");
+    std::vector<int> cidx(ncand);
+    std::vector<float> cval(ncand);
+    if (ncand) {
+        HIPCHK(hipMemcpy(cidx.data(), c->cand_idx.p, ncand * sizeof(int), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(cval.data(), c->cand_val.p, ncand * sizeof(float), hipMemcpyDeviceToHost));
+    }
+    float mx;
+    std::memcpy(&mx, &mb, 4);
+    find_carriers_host(c, cidx, cval, 0.5f * mx, square_size);
+}
+
 }  // namespace
 
 // ====================================================================== C ABI
@@ -781,45 +827,8 @@ FCD_API int fcd_set_reference(fcd_ctx* c, const float* reference, int flags, dou
             upload(c->frames_in.p, reference, hw * sizeof(float), s);
             dref = c->frames_in.as<float>();
         }
-        // fourier.find_peaks: |fftshift(fft2(ref - mean))| * highpass  (fourier.py:18-34)
-        double* dmean = c->scalar.as<double>();
-        fcdk::mean_f64(dref, hw, dmean, s);
-        double mean = 0;
-        HIPCHK(hipMemcpyAsync(&mean, dmean, sizeof(double), hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
-        const float meanf = (float)(mean / (double)hw);
+        find_peaks_device(c, dref, square_size, s);
         float2* F = c->spec.as<float2>();
-        fft2_real(c, dref, F, 1, meanf, s);
-        const std::vector<double> krs = wavenumber(c->H, 1.0, true), kcs = wavenumber(c->W, 1.0, true);
-        DevBuf ktab;
-        ktab.ensure((c->H + c->W) * sizeof(double));
-        upload(ktab.p, krs.data(), c->H * sizeof(double), s);
-        upload(ktab.as<double>() + c->H, kcs.data(), c->W * sizeof(double), s);
-        const double kmin = 4 * kPi / (double)std::min(c->H, c->W);
-        float* mag = c->wrapped.as<float>();
-        unsigned* maxbits = reinterpret_cast<unsigned*>(c->scalar.as<char>() + 16);
-        int* count = reinterpret_cast<int*>(c->scalar.as<char>() + 32);
-        fcdk::spectrum_mag(F, mag, maxbits, c->H, c->W, ktab.as<double>(), ktab.as<double>() + c->H, kmin * kmin, s);
-        const int cap = 1 << 16;
-        c->cand_idx.ensure(cap * sizeof(int));
-        c->cand_val.ensure(cap * sizeof(float));
-        fcdk::spectrum_candidates(mag, maxbits, c->H, c->W, count, c->cand_idx.as<int>(), c->cand_val.as<float>(),
-                                  cap, s);
-        int ncand = 0;
-        unsigned mb = 0;
-        HIPCHK(hipMemcpyAsync(&ncand, count, sizeof(int), hipMemcpyDeviceToHost, s));
-        HIPCHK(hipMemcpyAsync(&mb, maxbits, sizeof(unsigned), hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
-        if (ncand > cap) throw FcdError(FCD_E_UNSUPPORTED, "find_peaks: too many pixels above threshold");
-        std::vector<int> cidx(ncand);
-        std::vector<float> cval(ncand);
-        if (ncand) {
-            HIPCHK(hipMemcpy(cidx.data(), c->cand_idx.p, ncand * sizeof(int), hipMemcpyDeviceToHost));
-            HIPCHK(hipMemcpy(cval.data(), c->cand_val.p, ncand * sizeof(float), hipMemcpyDeviceToHost));
-        }
-        float mx;
-        std::memcpy(&mx, &mb, 4);
-        find_carriers_host(c, cidx, cval, 0.5f * mx, square_size);
         c->disk_rows.ensure(c->disk_rows_host.size() * sizeof(int));
         upload(c->disk_rows.p, c->disk_rows_host.data(), c->disk_rows_host.size() * sizeof(int), s);
         build_demod_tables(c, s);
@@ -840,6 +849,39 @@ FCD_API int fcd_set_reference(fcd_ctx* c, const float* reference, int flags, dou
         HIPCHK(hipStreamSynchronize(s));
         c->has_ref = true;
         if (info) *info = c->info;
+    })
+}
+
+FCD_API int fcd_find_peaks(fcd_ctx* c, const float* images, int n, int flags, double square_size,
+                           fcd_ref_info* infos) {
+    FCD_TRY({
+        check_ctx(c);
+        if (!images || !infos || n < 0) throw FcdError(FCD_E_INVALID, "bad arguments");
+        hipStream_t s = c->own;
+        const long hw = c->hw();
+        // the context's reference (if any) is kept: its per-reference host state is
+        // restored afterwards; the device state find_peaks_device touches is workspace
+        const fcd_ref_info keep_info = c->info;
+        const std::vector<int> keep_rows = c->disk_rows_host;
+        struct Restore {
+            fcd_ctx* c;
+            const fcd_ref_info& info;
+            const std::vector<int>& rows;
+            ~Restore() {
+                c->info = info;
+                c->disk_rows_host = rows;
+            }
+        } restore{c, keep_info, keep_rows};
+        for (int i = 0; i < n; ++i) {
+            const float* img = images + (size_t)i * hw;
+            if (flags != FCD_DEVICE_PTRS) {
+                c->frames_in.ensure(hw * sizeof(float));
+                upload(c->frames_in.p, img, hw * sizeof(float), s);
+                img = c->frames_in.as<float>();
+            }
+            find_peaks_device(c, img, square_size, s);
+            infos[i] = c->info;
+        }
     })
 }
 

@@ -33,7 +33,7 @@ EXPORTED = (
     "fcd_abi_version", "fcd_last_error", "fcd_create", "fcd_destroy", "fcd_synchronize",
     "fcd_set_reference", "fcd_get_carriers", "fcd_process", "fcd_phases_from_spectrum",
     "fcd_unwrap", "fcd_integrate", "fcd_fft2", "fcd_profile", "fcd_stage_times",
-    "fcd_process_raw", "fcd_frame_bytes", "fcd_host_alloc", "fcd_host_free",
+    "fcd_process_raw", "fcd_frame_bytes", "fcd_host_alloc", "fcd_host_free", "fcd_find_peaks",
 )
 
 
@@ -91,6 +91,7 @@ def load_library(path=None):
             "fcd_frame_bytes": ([vp, i32, ctypes.POINTER(ctypes.c_int64)], i32),
             "fcd_host_alloc": ([ctypes.c_int64, ctypes.POINTER(vp)], i32),
             "fcd_host_free": ([vp], i32),
+            "fcd_find_peaks": ([vp, vp, i32, i32, f64, ctypes.POINTER(FcdRefInfo)], i32),
         }
         for name, (args, res) in sig.items():
             fn = getattr(lib, name)
@@ -158,6 +159,19 @@ class Engine:
         self.ref_copy = ref.copy()
         self.ref_square_size = float(square_size)
         return info
+
+    def find_peaks(self, images, square_size=1.0):
+        """fcd_find_peaks: FcdRefInfo per image of a [n, H, W] (or [H, W]) stack, the
+        context's reference untouched."""
+        imgs = _f32(images)
+        if imgs.ndim == 2:
+            imgs = imgs[None]
+        if imgs.shape[1:] != self.shape:
+            raise ValueError(f"image shape {imgs.shape[1:]} != engine shape {self.shape}")
+        infos = (FcdRefInfo * max(len(imgs), 1))()
+        _check(self._lib.fcd_find_peaks(self._h, imgs.ctypes.data, len(imgs), FCD_HOST_PTRS, float(square_size),
+                                        infos))
+        return [infos[i] for i in range(len(imgs))]
 
     def matches(self, reference, square_size):
         if self.ref_copy is None or self.ref_square_size != float(square_size):

@@ -127,6 +127,21 @@ class fcd:
         return cf, peaks
 
     @classmethod
+    def compute_calibration_factors(cls, square_size, references):
+        """[(calibration_factor, (peak0, peak1))] for a stack of references in one call
+        (compute_calibration_factor, fcd.py:72-101, for many-reference workloads; the
+        engine's current reference is left in place)."""
+        refs = np.asarray(references)
+        if refs.ndim == 2:
+            refs = refs[None]
+        eng = _lib.engine_for(refs.shape[1:])
+        out = []
+        for info in eng.find_peaks(refs, square_size):
+            out.append((info.calibration_factor, (np.array([info.peaks[0][0], info.peaks[0][1]]),
+                                                  np.array([info.peaks[1][0], info.peaks[1][1]]))))
+        return out
+
+    @classmethod
     def compute_phases(cls, displaced_fft, carriers, unwrap=True):
         """Phase maps [2, H, W] float64 from an unshifted spectrum (fcd.py:103-120), on the device."""
         eng = getattr(carriers[0], "_engine", None)

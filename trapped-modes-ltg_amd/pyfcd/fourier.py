@@ -31,11 +31,12 @@ class fourier:
     def find_peaks(cls, image):
         """(rightmost_peak, perpendicular_peak) in fftshifted pixel coordinates.
 
-        Reference: fourier.py:7-41.  Runs on the device (engine set_reference).
+        Reference: fourier.py:7-41.  Runs on the device (fcd_find_peaks); the
+        engine's current reference is left in place.
         """
         img = np.asarray(image)
         eng = _lib.engine_for(img.shape)
-        info = eng.set_reference(img, 1.0)
+        info = eng.find_peaks(img, 1.0)[0]
         return (np.array([info.peaks[0][0], info.peaks[0][1]]),
                 np.array([info.peaks[1][0], info.peaks[1][1]]))
 

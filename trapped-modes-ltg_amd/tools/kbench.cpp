@@ -13,6 +13,7 @@
 #include "../csrc/kernels.hpp"
 #ifdef FCD_STAMPS
 extern "C" int fcd_debug_pr_stamps(unsigned long long* out);
+extern "C" int fcd_debug_band_stamps(unsigned long long* out);
 #endif
 
 #define CK(x)                                                                 \
@@ -140,6 +141,30 @@ int main(int argc, char** argv) {
             timeit("band_phase", 16.0 * H * NCA + 8 * f, [&] {
                 fcdk::band_phase(W, Bw, false, Ab, H, nb, NCA, NCc, NCc, theta, wrapped, pre, ptw, s);
             });
+#ifdef FCD_STAMPS
+        if (fcdk::band_supported(W, Bw)) {  // block 0, wave 0 of the last band_phase launch: cycle split
+            std::vector<unsigned long long> st(512);
+            CK(hipDeviceSynchronize());
+            fcd_debug_band_stamps(st.data());
+            const int RPW = 4;  // rows per wave per 16-row tile at W = 1024 (4 waves per block)
+            const int per_item = 2 + 4 * RPW;
+            double stage = 0, cm = 0, ff = 0, ph = 0, gap = 0;
+            int n = 0;
+            for (int it = 0; (it + 1) * per_item + 1 < 512; ++it, ++n) {
+                const unsigned long long* a = st.data() + it * per_item;
+                stage += a[1] - a[0];
+                for (int r = 0; r < RPW; ++r) {
+                    const unsigned long long* b = a + 2 + 4 * r;
+                    gap += b[0] - (r ? b[-1] : a[1]);
+                    cm += b[1] - b[0];
+                    ff += b[2] - b[1];
+                    ph += b[3] - b[2];
+                }
+            }
+            std::printf("band stamps (memtime ticks per item, %d items): stage+bar %.0f  row-gap %.0f  cmul %.0f  fft %.0f  phase+store %.0f\n",
+                        n, stage / n, gap / n, cm / n, ff / n, ph / n);
+        }
+#endif
         if (fcdk::phase_rows_supported(W, Bw, H)) {
             float2* ztw = dalloc<float2>(N);
             CK(hipMemcpy(ztw, ones.data(), N * 8, hipMemcpyHostToDevice));
