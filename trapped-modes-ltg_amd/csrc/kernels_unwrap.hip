@@ -229,10 +229,11 @@ __global__ void k_mst_cand(const int* __restrict__ map_ids, int nact, int H, int
     if (j > 0) consider(v - 1, i * (W - 1) + j - 1);
     if (i + 1 < H) consider(v + W, nh + i * W + j);
     if (i > 0) consider(v - W, nh + (i - 1) * W + j);
-    m.cand_w[v] = bw;
     m.cand_e[v] = be;
-    m.link[v] = pack_link((int)v, 0);
-    if (be != 0x7fffffff) atomicMin(m.best_w + cv, (unsigned long long)__double_as_longlong(bw));
+    if (be != 0x7fffffff) {  // interior vertices (no outgoing edge) skip the weight store: cand2 reads it only here
+        m.cand_w[v] = bw;
+        atomicMin(m.best_w + cv, (unsigned long long)__double_as_longlong(bw));
+    }
 }
 
 __global__ void k_mst_cand2(int nact, int H, int W, MstWork m) {
@@ -258,7 +259,11 @@ __global__ void k_mst_hook(const float* __restrict__ w, const int* __restrict__ 
     const long hw = (long)H * W;
     const long c = (long)blockIdx.x * blockDim.x + threadIdx.x;
     bool hooked = false;
-    if (c < nact * hw && m.comp[c] == (int)c) hooked = mst_hook_one(w, map_ids, H, W, m, c);
+    if (c < nact * hw && m.comp[c] == (int)c) {
+        // only roots carry a link (read by k_mst_jump / k_mst_update): self unless hooked
+        hooked = mst_hook_one(w, map_ids, H, W, m, c);
+        if (!hooked) m.link[c] = pack_link((int)c, 0);
+    }
     count_hook(hooked, m.nhooks);
 }
 
@@ -320,8 +325,10 @@ __global__ void k_mst_update(int nact, int H, int W, MstWork m) {
         m.comp[v] = r;
         m.off[v] += link_off(l);
     }
-    m.best_w[v] = 0x7ff0000000000000ull;  // bits of +inf (positive doubles order as uints)
-    m.best_e[v] = 0x7fffffff;
+    if (c == (int)v) {  // the next round's roots are among this round's: reset only those
+        m.best_w[v] = 0x7ff0000000000000ull;  // bits of +inf (positive doubles order as uints)
+        m.best_e[v] = 0x7fffffff;
+    }
 }
 
 __global__ void k_mst_reset(int nact, int H, int W, MstWork m) {
