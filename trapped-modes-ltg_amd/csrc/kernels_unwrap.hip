@@ -249,9 +249,13 @@ __device__ __forceinline__ bool mst_hook_one(const float* __restrict__ w, const 
                                              MstWork& m, long c);
 
 __device__ __forceinline__ void count_hook(bool hooked, int* nhooks) {
-    // one atomic per wave: a per-thread add on one word serialised ~1M times in round 1
+    // The host only needs "any hook this round" (convergence).  Even one atomic per
+    // wave serialises ~1.5 M times on one word in round 1 of a 96-map batch (half the
+    // fix-up pass); a wave that sees the flag already raised skips its atomic.
     const unsigned long long b = __ballot(hooked);
-    if ((threadIdx.x & 63) == 0 && b) atomicAdd(nhooks, __popcll(b));
+    if ((threadIdx.x & 63) == 0 && b &&
+        __hip_atomic_load(nhooks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+        atomicOr(nhooks, 1);
 }
 
 __global__ void k_mst_hook(const float* __restrict__ w, const int* __restrict__ map_ids, int nact, int H, int W,
