@@ -329,7 +329,8 @@ void unwrap_maps(fcd_ctx* c, const float* w, int nmaps, int32_t* k, int* res_hos
     // Boruvka halves the component count every round; check convergence every
     // third round (a round after convergence hooks nothing and changes nothing).
     for (; rounds < max_rounds; rounds += 3) {
-        for (int g = 0; g < 3; ++g) fcdk::mst_round(w, c->mst_ids.as<int>(), nact, c->H, c->W, m, s);
+        for (int g = 0; g < 3; ++g)
+            fcdk::mst_round(w, c->mst_ids.as<int>(), nact, c->H, c->W, m, s, rounds + g == 0);
         int hooks = 0;
         HIPCHK(hipMemcpyAsync(&hooks, m.nhooks, sizeof(int), hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));

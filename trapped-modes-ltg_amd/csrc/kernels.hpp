@@ -119,7 +119,8 @@ struct MstWork {
 };
 // Maps listed in map_ids (device int[nact]) of the wrapped stack w.
 void mst_init(const float* w, const int* map_ids, int nact, int H, int W, MstWork m, hipStream_t s);
-void mst_round(const float* w, const int* map_ids, int nact, int H, int W, MstWork m, hipStream_t s);
+// first: the round right after mst_init (every component a single vertex)
+void mst_round(const float* w, const int* map_ids, int nact, int H, int W, MstWork m, hipStream_t s, bool first = false);
 void mst_finalize(const int* map_ids, int nact, int H, int W, MstWork m, int32_t* k, hipStream_t s);
 
 // ---- integration ----

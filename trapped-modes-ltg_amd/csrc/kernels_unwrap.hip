@@ -204,6 +204,7 @@ __global__ void k_mst_rel(const float* __restrict__ w, const int* __restrict__ m
 }
 
 // Candidate: the lightest (rel_e, edge index) edge of v leaving its component.
+template <bool FIRST>
 __global__ void k_mst_cand(const int* __restrict__ map_ids, int nact, int H, int W, MstWork m) {
     const long hw = (long)H * W;
     const long v = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -229,6 +230,11 @@ __global__ void k_mst_cand(const int* __restrict__ map_ids, int nact, int H, int
     if (j > 0) consider(v - 1, i * (W - 1) + j - 1);
     if (i + 1 < H) consider(v + W, nh + i * W + j);
     if (i > 0) consider(v - W, nh + (i - 1) * W + j);
+    if constexpr (FIRST) {  // every component is one vertex: its candidate IS its best edge
+        m.best_w[v] = (unsigned long long)__double_as_longlong(bw);
+        m.best_e[v] = be;
+        return;
+    }
     m.cand_e[v] = be;
     if (be != 0x7fffffff) {  // interior vertices (no outgoing edge) skip the weight store: cand2 reads it only here
         m.cand_w[v] = bw;
@@ -302,20 +308,25 @@ __device__ __forceinline__ bool mst_hook_one(const float* __restrict__ w, const 
     return true;
 }
 
+// Pointer jumping with path compression.  Concurrent threads may read a link
+// before or after another thread compressed it; both are valid chains to the
+// same final root (the offsets add up either way), so 64-bit atomic loads and
+// stores of workgroup scope suffice: a stale L2 copy on another XCD only makes
+// a chain longer, never wrong.
 __global__ void k_mst_jump(int nact, int H, int W, MstWork m) {
     const long c = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= nact * (long)H * W) return;
     if (m.comp[c] != (int)c) return;
-    unsigned long long l = __hip_atomic_load(m.link + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned long long l = __hip_atomic_load(m.link + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     int p = link_parent(l), o = link_off(l);
     if (p == (int)c) return;
     for (;;) {
-        const unsigned long long l2 = __hip_atomic_load(m.link + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long l2 = __hip_atomic_load(m.link + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         const int pp = link_parent(l2);
         if (pp == p) break;
         o += link_off(l2);
         p = pp;
-        __hip_atomic_store(m.link + c, pack_link(p, o), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(m.link + c, pack_link(p, o), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
 }
 
@@ -323,7 +334,7 @@ __global__ void k_mst_update(int nact, int H, int W, MstWork m) {
     const long v = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (v >= nact * (long)H * W) return;
     const int c = m.comp[v];
-    const unsigned long long l = __hip_atomic_load(m.link + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long l = m.link[c];  // final after k_mst_jump (kernel boundary)
     const int r = link_parent(l);
     if (r != c) {
         m.comp[v] = r;
@@ -352,13 +363,18 @@ void mst_init(const float* w, const int* map_ids, int nact, int H, int W, MstWor
     FCD_CHECK_LAUNCH();
 }
 
-void mst_round(const float* w, const int* map_ids, int nact, int H, int W, MstWork m, hipStream_t s) {
+void mst_round(const float* w, const int* map_ids, int nact, int H, int W, MstWork m, hipStream_t s, bool first) {
     const long n = (long)nact * H * W;
     FCD_HIPCHK(hipMemsetAsync(m.nhooks, 0, sizeof(int), s));
-    hipLaunchKernelGGL(k_mst_cand, dim3(nblk(n)), dim3(256), 0, s, map_ids, nact, H, W, m);
-    FCD_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_mst_cand2, dim3(nblk(n)), dim3(256), 0, s, nact, H, W, m);
-    FCD_CHECK_LAUNCH();
+    if (first) {
+        hipLaunchKernelGGL(k_mst_cand<true>, dim3(nblk(n)), dim3(256), 0, s, map_ids, nact, H, W, m);
+        FCD_CHECK_LAUNCH();
+    } else {
+        hipLaunchKernelGGL(k_mst_cand<false>, dim3(nblk(n)), dim3(256), 0, s, map_ids, nact, H, W, m);
+        FCD_CHECK_LAUNCH();
+        hipLaunchKernelGGL(k_mst_cand2, dim3(nblk(n)), dim3(256), 0, s, nact, H, W, m);
+        FCD_CHECK_LAUNCH();
+    }
     hipLaunchKernelGGL(k_mst_hook, dim3(nblk(n)), dim3(256), 0, s, w, map_ids, nact, H, W, m);
     FCD_CHECK_LAUNCH();
     hipLaunchKernelGGL(k_mst_jump, dim3(nblk(n)), dim3(256), 0, s, nact, H, W, m);
