@@ -236,10 +236,25 @@ __global__ void k_mst_cand(const int* __restrict__ map_ids, int nact, int H, int
         return;
     }
     m.cand_e[v] = be;
-    if (be != 0x7fffffff) {  // interior vertices (no outgoing edge) skip the weight store: cand2 reads it only here
-        m.cand_w[v] = bw;
-        atomicMin(m.best_w + cv, (unsigned long long)__double_as_longlong(bw));
+    const bool has = be != 0x7fffffff;
+    if (has) m.cand_w[v] = bw;  // interior vertices (no outgoing edge) skip the weight store: cand2 reads it only here
+    // One atomicMin per run of consecutive lanes in the same component (a wave is
+    // 64 consecutive pixels of a row, so components cross it in runs): segmented
+    // suffix-min over the run, then the run's first lane updates the root.  Without
+    // it every boundary vertex of round 2 hit a device-scope atomic.
+    const int lane = threadIdx.x & 63;
+    const int cprev = __shfl_up(cv, 1, 64);
+    const unsigned long long heads = __ballot(lane == 0 || cprev != cv);
+    unsigned long long key = has ? (unsigned long long)__double_as_longlong(bw) : ~0ull;  // +doubles order as uints
+#pragma unroll
+    for (int sft = 1; sft < 64; sft <<= 1) {
+        const unsigned lo = __shfl_down((unsigned)key, sft, 64), hi = __shfl_down((unsigned)(key >> 32), sft, 64);
+        const unsigned long long other = ((unsigned long long)hi << 32) | lo;
+        // lane + sft is in this run iff no run starts in (lane, lane + sft]
+        const unsigned long long between = (lane + sft < 64) ? (heads >> (lane + 1)) & ((1ull << sft) - 1) : 1ull;
+        if (between == 0 && other < key) key = other;
     }
+    if (((heads >> lane) & 1) && key != ~0ull) atomicMin(m.best_w + cv, key);
 }
 
 __global__ void k_mst_cand2(int nact, int H, int W, MstWork m) {
