@@ -192,3 +192,20 @@ def test_fcd_example_chain_png_bmp(tmp_path, golden, fresh_engines):
     values = fcd.compute_height_map(reference, displaced, float(r["square_size"]), LAYERS)
     assert values[2] == float(r["cf"])
     assert rel_l2(values[0][::4, ::4], r["height_sub"]) < 1e-4
+
+
+def test_host_pipeline_follows_reference_change(df):
+    """The pipelined host path sizes its slots from the CURRENT reference's chunk
+    workspace: switching references between calls (different carrier bands, different
+    chunk sizes) keeps the host-path heights equal to the synchronous path's."""
+    from bench_data import make_frames_numpy
+    from pyfcd import _lib
+    ref_s, frames = make_frames_numpy(1024, 5, seed=21, rotate_deg=5.0)
+    eng = _engine(df["ref_u16"].astype(np.float32), float(df["square_size"]))
+    a = eng.process_raw(df["frames_u16"].astype(np.float32).reshape(3, -1).view(np.uint8), _lib.FCD_FMT_F32, 3, 1.0)
+    want_a, _, _ = eng.process(df["frames_u16"].astype(np.float32), 1.0, want_phases=True)
+    assert np.array_equal(a, want_a)
+    eng.set_reference(ref_s, 0.001)
+    b = eng.process_raw(frames.reshape(5, -1).view(np.uint8), _lib.FCD_FMT_F32, 5, 1.0)
+    want_b, _, _ = eng.process(frames, 1.0, want_phases=True)
+    assert rel_l2(b, want_b) < 1e-6

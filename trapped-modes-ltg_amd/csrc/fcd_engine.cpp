@@ -992,13 +992,24 @@ void ensure_host_pipe(fcd_ctx* c, int format) {
         for (int i = 0; i < 2; ++i)
             for (hipEvent_t* e : {&P.ev_h2d[i], &P.ev_free[i], &P.ev_comp[i], &P.ev_d2h[i]})
                 HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
-        // 128 MiB of float32 frames per slot (32 frames at 1024^2): two slots in
-        // flight overlap the H2D copy, the compute and the D2H copy
-        const long budget = (long)fcd_env_int("FCD_PIPE_MB", 128) << 20;
-        P.nb = (int)std::max(1L, std::min((long)c->fchunk, budget / (hw * 4)));
-        const size_t out_b = (size_t)P.nb * hw * 4;
+    }
+    // 128 MiB of float32 frames per slot (32 frames at 1024^2): two slots in flight
+    // overlap the H2D copy, the compute and the D2H copy.  Never more frames than the
+    // chunk workspace of the current reference holds (fchunk changes with it).
+    const long budget = (long)fcd_env_int("FCD_PIPE_MB", 128) << 20;
+    const int nb = (int)std::max(1L, std::min((long)c->fchunk, budget / (hw * 4)));
+    if (nb != P.nb) {
         for (int i = 0; i < 2; ++i) {
-            HIPCHK(hipHostMalloc(&P.pin_out[i], out_b, hipHostMallocDefault));
+            if (P.pin_out[i]) (void)hipHostFree(P.pin_out[i]);
+            if (P.pin_in[i]) (void)hipHostFree(P.pin_in[i]);
+            P.pin_out[i] = nullptr;
+            P.pin_in[i] = nullptr;
+        }
+        P.in_bytes = 0;
+        P.nb = nb;
+        const size_t out_b = (size_t)nb * hw * 4;
+        for (int i = 0; i < 2; ++i) {
+            HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&P.pin_out[i]), out_b, hipHostMallocDefault));
             P.dev_out[i].ensure(out_b);
         }
     }
@@ -1024,6 +1035,16 @@ void host_pipeline(fcd_ctx* c, const void* frames, int format, int n_frames, boo
     ensure_host_pipe(c, format);
     HostPipe& P = c->pipe;
     const long hw = c->hw();
+    // on any exit (an error included) no copy may still target the caller's memory
+    struct Drain {
+        HostPipe& P;
+        hipStream_t s;
+        ~Drain() {
+            (void)hipStreamSynchronize(s);
+            (void)hipStreamSynchronize(P.h2d);
+            (void)hipStreamSynchronize(P.d2h);
+        }
+    } drain{P, s};
     const size_t rb = fcdk::raw_frame_bytes(format, c->H, c->W);
     const bool pin_src = host_pinned(frames), pin_dst = host_pinned(height_out);
     const int nchunks = (n_frames + P.nb - 1) / P.nb;
