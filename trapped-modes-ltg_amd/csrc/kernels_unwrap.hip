@@ -52,10 +52,20 @@ __device__ __forceinline__ double wrapd(double x) {
     return x > kPi ? __dsub_rn(x, kTwoPi) : (x < -kPi ? __dadd_rn(x, kTwoPi) : x);
 }
 
+// XCD-aware block id for the one-thread-per-pixel stencil kernels: workgroups are
+// dealt round-robin to the 8 XCDs (block b -> XCD b % 8), each with its own L2, so
+// consecutive blocks (consecutive quarter rows) land on different L2s and every
+// row's neighbours above and below are fetched again by other XCDs.  Renumbering
+// b -> (b % 8) * (G / 8) + b / 8 keeps runs of consecutive rows on one XCD.
+__device__ __forceinline__ long xcd_block() {
+    const unsigned G = gridDim.x, b = blockIdx.x;
+    return (G % 8 == 0) ? (long)(b % 8) * (G / 8) + b / 8 : (long)b;
+}
+
 // ------------------------------------------------------------------ residues
 __global__ void k_residues(const float* __restrict__ w, int nmaps, int H, int W, int* counts) {
     const long hw = (long)H * W;
-    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long idx = xcd_block() * blockDim.x + threadIdx.x;
     int r = 0;
     int map = -1;
     if (idx < nmaps * hw) {
@@ -178,7 +188,7 @@ __device__ __forceinline__ int link_off(unsigned long long l) { return (int)(uns
 __global__ void k_mst_rel(const float* __restrict__ w, const int* __restrict__ map_ids, int nact, int H, int W,
                           double* __restrict__ rel, int* comp, int* off) {
     const long hw = (long)H * W;
-    const long v = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long v = xcd_block() * blockDim.x + threadIdx.x;
     if (v >= nact * hw) return;
     const int slot = (int)(v / hw);
     const long p = v % hw;
@@ -207,7 +217,7 @@ __global__ void k_mst_rel(const float* __restrict__ w, const int* __restrict__ m
 template <bool FIRST>
 __global__ void k_mst_cand(const int* __restrict__ map_ids, int nact, int H, int W, MstWork m) {
     const long hw = (long)H * W;
-    const long v = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long v = xcd_block() * blockDim.x + threadIdx.x;
     if (v >= nact * hw) return;
     (void)map_ids;
     const long base = (v / hw) * hw;
