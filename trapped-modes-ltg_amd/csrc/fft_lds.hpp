@@ -109,7 +109,12 @@ __host__ __device__ constexpr int ilog2c(int n) { return n <= 1 ? 0 : 1 + ilog2c
 #ifndef FCD_ELEMS_1024
 #define FCD_ELEMS_1024 8
 #endif
-__host__ __device__ constexpr int fft_elems(int n) { return n >= 1024 ? FCD_ELEMS_1024 : (n >= 512 ? 8 : 4); }
+#ifndef FCD_ELEMS_2048
+#define FCD_ELEMS_2048 FCD_ELEMS_1024  // 2048- and 4096-point transforms
+#endif
+__host__ __device__ constexpr int fft_elems(int n) {
+    return n >= 2048 ? FCD_ELEMS_2048 : (n >= 1024 ? FCD_ELEMS_1024 : (n >= 512 ? 8 : 4));
+}
 // Threads per team.
 __host__ __device__ constexpr int fft_team(int n) { return n / fft_elems(n); }
 // Padded LDS index: one spare complex per 16.  With this padding every
