@@ -39,6 +39,10 @@ namespace {
 #define FCD_BAND_NOTHETA 0  // diagnostic ablation only (wrong results): no reference-angle loads
 #endif
 
+#ifndef FCD_BAND_THREADS_2048
+#define FCD_BAND_THREADS_2048 512  // workgroup size of the 2048-point band kernel (256: 25.1, 512: 22.5, 768: 23.4 us/frame, kbench r01ar)
+#endif
+
 #ifndef FCD_BAND_FMAJOR
 #define FCD_BAND_FMAJOR 1  // item order frame-fastest: concurrent blocks share the (carrier, row tile) and its theta
 #endif
@@ -59,7 +63,10 @@ struct BPCfg {
     static constexpr int G = B / 16;        // lanes per group transform
     static constexpr int L = W / B;         // groups per row
     static constexpr int RL = W / 16;       // lanes per row
-    static constexpr int THREADS = (16 * RL) < 256 ? 16 * RL : 256;
+    // 2048-point rows (2 waves each): with 256 threads the 68 KB of LDS allow 2
+    // workgroups = 8 waves per CU; FCD_BAND_THREADS_2048 / 128 rows in flight in one
+    // workgroup share one staged tile among more waves
+    static constexpr int THREADS = (16 * RL) < 256 ? 16 * RL : (W == 2048 ? FCD_BAND_THREADS_2048 : 256);
     static constexpr int RP = THREADS / RL; // rows in flight per workgroup
     static constexpr int REGION = GSched<B>::REGION;
     static constexpr bool XCH = GSched<B>::NP > 1;
