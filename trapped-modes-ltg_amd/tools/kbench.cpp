@@ -205,6 +205,7 @@ int main(int argc, char** argv) {
     {
         int Bw = 16;
         while (Bw < NCc) Bw *= 2;
+        if (!fcdk::band_supported(W, Bw)) return 0;  // 4096: full-length demod only
         std::vector<float2> ones(N, make_float2(1.f, 0.f));
         float2* pre = dalloc<float2>(N);
         float2* ptw = dalloc<float2>(N);
