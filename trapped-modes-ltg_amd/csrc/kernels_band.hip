@@ -47,6 +47,10 @@ namespace {
 #define FCD_BAND_FMAJOR 1  // item order frame-fastest: concurrent blocks share the (carrier, row tile) and its theta
 #endif
 
+#ifndef FCD_BAND_ABL
+#define FCD_BAND_ABL 0  // diagnostic ablations only (wrong results): 1 no transform, 2 no atan2, 4 no LDS stage reads
+#endif
+
 #ifndef FCD_BAND_NOSTORE
 #define FCD_BAND_NOSTORE 0  // diagnostic ablation only (no output): phase stores suppressed
 #endif
@@ -182,10 +186,15 @@ __global__ __launch_bounds__((BPCfg<W, B>::THREADS), FCD_BAND_WAVES) void k_band
             else if (nblk < items)
                 th_load(nblk, team);
             float2 x[E];
+            if constexpr (FCD_BAND_ABL & 4) {  // diagnostic: no staged-tile / pre-twiddle LDS reads
 #pragma unroll
-            for (int q = 0; q < E; ++q) x[q] = cmul(stage[(t + G * q) * SROW + rl], ptl[q * RL + l]);
+                for (int q = 0; q < E; ++q) x[q] = make_float2(thc[q], (float)(q + rl));
+            } else {
+#pragma unroll
+                for (int q = 0; q < E; ++q) x[q] = cmul(stage[(t + G * q) * SROW + rl], ptl[q * RL + l]);
+            }
             STAMP(st++);
-            fft.template run_half<true>(x, s, t);
+            if constexpr (!(FCD_BAND_ABL & 1)) fft.template run_half<true>(x, s, t);  // 1: no transform
             STAMP(st++);
             float* o = out + row * W;
 #pragma unroll
@@ -198,7 +207,8 @@ __global__ __launch_bounds__((BPCfg<W, B>::THREADS), FCD_BAND_WAVES) void k_band
                     o[n + RL] = a.y;
                 } else {
                     // wrap to [-pi, pi]: d - 2 pi rint(d / 2 pi), |d| < 2 pi
-                    const fv2 w = wrapped_phase_pk(fv2{thc[q], thc[q + 1]}, x[q], x[q + 1]);
+                    const fv2 w = (FCD_BAND_ABL & 2) ? fv2{x[q].x - thc[q], x[q + 1].x - thc[q + 1]}  // 2: no atan2
+                                                     : wrapped_phase_pk(fv2{thc[q], thc[q + 1]}, x[q], x[q + 1]);
                     // streaming store (nt): the 8 N^2-byte phase stream must not evict
                     // the reference angles from the caches every frame
                     if (!FCD_BAND_NOSTORE || w.x == 1234.5f) {

@@ -19,7 +19,35 @@ __global__ void strided(const float* __restrict__ a, float* __restrict__ b, long
         for (int q = 0; q < 8; ++q) b[r * 1024 + t + 128 * q] = x[q];
     }
 }
+// write-only streams (the phase kernels' output pattern): plain or non-temporal
+template <class T, bool NT>
+__global__ void fillk(T* __restrict__ b, long n, T v) {
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+        if constexpr (NT) __builtin_nontemporal_store(v, b + i); else b[i] = v;
+    }
+}
+typedef float fv4m __attribute__((ext_vector_type(4)));
 int main(int argc, char** argv) {
+    if (argc > 1 && argv[1][0] == 'w') {  // write-only bandwidth over 2 GiB (past the 256 MiB MALL)
+        const long wb = 2048L << 20;
+        float* w;
+        CK(hipMalloc(&w, wb));
+        hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
+        auto runw = [&](const char* name, auto fn) {
+            for (int i = 0; i < 2; ++i) fn();
+            hipEventRecord(e0); for (int i = 0; i < 5; ++i) fn(); hipEventRecord(e1); hipEventSynchronize(e1);
+            float ms; hipEventElapsedTime(&ms, e0, e1);
+            printf("%-28s %8.1f GB/s (write only)\n", name, 1.0 * wb * 5 / (ms * 1e-3) / 1e9);
+        };
+        for (int g : {2048, 8192}) {
+            printf("grid %d x 256\n", g);
+            runw("fill 4B plain", [&] { fillk<float, false><<<g, 256>>>(w, wb / 4, 1.f); });
+            runw("fill 4B nt", [&] { fillk<float, true><<<g, 256>>>(w, wb / 4, 1.f); });
+            runw("fill 16B plain", [&] { fillk<fv4m, false><<<g, 256>>>((fv4m*)w, wb / 16, fv4m{1, 1, 1, 1}); });
+            runw("fill 16B nt", [&] { fillk<fv4m, true><<<g, 256>>>((fv4m*)w, wb / 16, fv4m{1, 1, 1, 1}); });
+        }
+        return 0;
+    }
     const long bytes = 512L << 20;
     float *a, *b;
     CK(hipMalloc(&a, bytes)); CK(hipMalloc(&b, bytes));
@@ -31,7 +59,7 @@ int main(int argc, char** argv) {
         float ms; hipEventElapsedTime(&ms, e0, e1);
         printf("%-28s %8.1f GB/s (read+write)\n", name, 2.0 * bytes * 10 / (ms * 1e-3) / 1e9);
     };
-    if (argc > 1) {  // PMC calibration: one launch of each width over 512 MiB (known bytes)
+    if (argc > 1) {  // PMC calibration (argument "cal"): one launch of each width over 512 MiB (known bytes)
         copyk<float><<<2048, 256>>>(a, b, bytes / 4);
         copyk<float2><<<2048, 256>>>((float2*)a, (float2*)b, bytes / 8);
         copyk<float4><<<2048, 256>>>((float4*)a, (float4*)b, bytes / 16);
