@@ -446,3 +446,22 @@ def test_find_peaks_batch_matches_reference_setup(lib, golden):
     out = fcd.compute_calibration_factors(0.002, refs[1:])
     assert out[0][0] == float(d["committed_cf"][0])
     assert [p.tolist() for p in out[0][1]] == d["peaks"].tolist()
+
+
+@pytest.mark.parametrize("rows,cols", [(512, 1024), (1024, 512), (256, 128)])
+def test_non_square_frames_vs_oracle(lib, golden, rows, cols):
+    """H != W (the reference takes any frame shape; the engine any power-of-two pair): a
+    crop of the 10-bit camera pair through the whole pipeline against the oracle."""
+    from oracle import fcd_oracle as O
+    from pyfcd.fcd import fcd
+    d = golden("real_df")
+    r0, c0 = (1024 - rows) // 2, (1024 - cols) // 2
+    ref = d["ref_u16"][r0:r0 + rows, c0:c0 + cols].astype(np.float32)
+    disp = d["frames_u16"][0][r0:r0 + rows, c0:c0 + cols].astype(np.float32)
+    sq = float(d["square_size"])
+    h, ph, cf = fcd.compute_height_map(ref, disp, sq, height=1.0)
+    ho, po, cfo, ex = O.compute_height_map(ref, disp, sq, height=1.0)
+    assert cf == cfo
+    carriers, _ = fcd.compute_carriers(ref, sq)
+    assert [c.pixels.tolist() for c in carriers] == [np.asarray(c.pixels).tolist() for c in ex["carriers"]]
+    assert rel_l2(h, ho) < 1e-4, rel_l2(h, ho)
