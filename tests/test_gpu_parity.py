@@ -465,3 +465,17 @@ def test_non_square_frames_vs_oracle(lib, golden, rows, cols):
     carriers, _ = fcd.compute_carriers(ref, sq)
     assert [c.pixels.tolist() for c in carriers] == [np.asarray(c.pixels).tolist() for c in ex["carriers"]]
     assert rel_l2(h, ho) < 1e-4, rel_l2(h, ho)
+
+
+def test_reference_without_carriers_raises(lib):
+    """A reference with no checkerboard (flat / pure noise below the high-pass threshold
+    structure) has no carrier peaks: the reference raises (min() of an empty sequence /
+    IndexError, fcd.py:68, fourier.py:38); the engine raises FcdError and keeps working."""
+    from pyfcd.fcd import fcd
+    flat = np.full((256, 256), 7.0, np.float32)
+    with pytest.raises(Exception):
+        fcd.compute_height_map(flat, flat, 0.001, height=1.0)
+    from bench_data import make_frames_numpy
+    ref, frames = make_frames_numpy(256, 1, seed=2, rotate_deg=5.0)
+    h, _, _ = fcd.compute_height_map(ref, frames[0], 0.001, height=1.0)
+    assert np.isfinite(h).all()
