@@ -26,6 +26,17 @@ __global__ void fillk(T* __restrict__ b, long n, T v) {
         if constexpr (NT) __builtin_nontemporal_store(v, b + i); else b[i] = v;
     }
 }
+// the band kernel's store pattern: one wave per 4 KB row, 16 stores of 256 B each
+// (lanes permuted inside the 256 B as n = g + 8 t), rows grid-strided over waves
+__global__ void rowfill(float* __restrict__ b, long rows) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int n0 = (lane >> 3) + 8 * (lane & 7);
+    for (long r = blockIdx.x * 4L + w; r < rows; r += gridDim.x * 4L) {
+        float* o = b + r * 1024;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) __builtin_nontemporal_store(1.f, o + n0 + 64 * q);
+    }
+}
 typedef float fv4m __attribute__((ext_vector_type(4)));
 int main(int argc, char** argv) {
     if (argc > 1 && argv[1][0] == 'w') {  // write-only bandwidth over 2 GiB (past the 256 MiB MALL)
@@ -45,6 +56,7 @@ int main(int argc, char** argv) {
             runw("fill 4B nt", [&] { fillk<float, true><<<g, 256>>>(w, wb / 4, 1.f); });
             runw("fill 16B plain", [&] { fillk<fv4m, false><<<g, 256>>>((fv4m*)w, wb / 16, fv4m{1, 1, 1, 1}); });
             runw("fill 16B nt", [&] { fillk<fv4m, true><<<g, 256>>>((fv4m*)w, wb / 16, fv4m{1, 1, 1, 1}); });
+            runw("row pattern 4B nt", [&] { rowfill<<<g, 256>>>(w, wb / 4096); });
         }
         return 0;
     }
