@@ -62,14 +62,40 @@ __device__ __forceinline__ long tix(int row, int col, int ncols) {
     return ((long)(row >> 4) * ncols + col) * TILE + (row & 15);
 }
 
-template <int N>
+// Workgroup size of k_int_cols: more teams per workgroup share one twiddle table.
+#ifndef FCD_INTCOLS_BLOCK
+#define FCD_INTCOLS_BLOCK 256
+#endif
+
+template <int N, int B = BLOCK>
 struct KCfg {
     static constexpr int TT = Sched<N>::TT;
     static constexpr int E = Sched<N>::E;
-    static constexpr int THREADS = TT > BLOCK ? TT : BLOCK;  // 4096-point teams span 8 waves
+    static constexpr int THREADS = TT > B ? TT : B;  // 4096-point teams span 8 waves
     static constexpr int TEAMS = THREADS / TT;
     static constexpr int ROW = padded_len(N);  // float2 per team row
     static constexpr int NLEN = N;             // twiddle table entries (float2) at the LDS base
+};
+
+// Minimum waves per SIMD of k_int_cols: both columns' transforms stay in
+// registers (no LDS mirror exchange).  1024 points: 168 VGPRs, 3 waves/SIMD,
+// without spills only when the mirror column is not prefetched (r01be: 3.23 vs
+// 3.67 us/frame before; any spill costs more than the occupancy gains).
+#ifndef FCD_INTCOLS_WAVES
+#define FCD_INTCOLS_WAVES 3
+#endif
+// Prefetch the mirror column of the next item too (1), or load it at the top of
+// the item (0: 16 fewer VGPRs live across the transforms).
+#ifndef FCD_INTCOLS_PREF_Y
+#define FCD_INTCOLS_PREF_Y 0
+#endif
+#ifndef FCD_INTCOLS_PREF_X
+#define FCD_INTCOLS_PREF_X 1
+#endif
+template <int N>
+struct IntColsCfg : KCfg<N, FCD_INTCOLS_BLOCK> {
+    static constexpr int V = N <= 1024 ? FCD_INTCOLS_WAVES : ColWaves<N>::V;
+    static constexpr bool PREF_Y = N >= 4096 ? true : FCD_INTCOLS_PREF_Y;  // 4096: 2 waves/SIMD either way
 };
 
 // find_wrap(a, b) of the reference unwrapper with an f32 fast path:
@@ -444,16 +470,15 @@ __global__ __launch_bounds__(KCfg<W>::THREADS, FCD_MIN_WAVES) void k_int_rows(co
 
 // ------------------------------------------------------------------ I2
 template <int H>
-__global__ __launch_bounds__(KCfg<H>::THREADS, ColWaves<H>::V) void k_int_cols(const float2* __restrict__ Zt, int W, int nb, IntegCoef c,
+__global__ __launch_bounds__(IntColsCfg<H>::THREADS, IntColsCfg<H>::V) void k_int_cols(const float2* __restrict__ Zt, int W, int nb, IntegCoef c,
                                                     float2* __restrict__ Ht, const float2* __restrict__ tw, int zts,
                                                     const int* __restrict__ colk) {
-    using C = KCfg<H>;
+    using C = IntColsCfg<H>;
     constexpr int TT = C::TT, E = C::E, TEAMS = C::TEAMS;
     extern __shared__ __attribute__((aligned(16))) float2 lds_raw[];
     float2* const lds = lds_raw + C::NLEN;  // lds_raw[0, NLEN): the twiddle table
     const int team = threadIdx.x / TT, t = threadIdx.x % TT;
     float2* s = lds + team * C::ROW;
-    float2* s2 = lds + (TEAMS + team) * C::ROW;
     RegFFT<H> fft;
     fft.init(tw, lds_raw, threadIdx.x, C::THREADS);
     __syncthreads();
@@ -463,18 +488,20 @@ __global__ __launch_bounds__(KCfg<H>::THREADS, ColWaves<H>::V) void k_int_cols(c
     // Both columns of the NEXT item are loaded into registers while the current
     // item is transformed (loads issued before the current item's stores).
     float2 py[E], px[E];
-    auto fetch = [&](int item) {
+    auto fetch_col = [&](int item, bool mirror, float2 (&v)[E]) {
         const bool valid = item < items;
         const int f = valid ? item / NCH : 0, col = valid ? item % NCH : 0;
-        const int colm = (W - col) & (W - 1);
-        const float2* src = Zt + (long)f * H * W;
+        const int cc = mirror ? (W - col) & (W - 1) : col;
+        const float2* src = Zt + (long)f * H * W + ((long)cc << zts);
 #pragma unroll
         for (int q = 0; q < E; ++q) {
             const int rr = t + TT * q;
-            const long tl = ((long)(rr >> zts) * W) << zts;
-            py[q] = src[tl + ((long)colm << zts) + (rr & zmask)];
-            px[q] = src[tl + ((long)col << zts) + (rr & zmask)];
+            v[q] = src[(((long)(rr >> zts) * W) << zts) + (rr & zmask)];
         }
+    };
+    auto fetch = [&](int item) {
+        if constexpr (C::PREF_Y) fetch_col(item, true, py);
+        if constexpr (FCD_INTCOLS_PREF_X) fetch_col(item, false, px);
     };
     // Each block walks a CONTIGUOUS range of columns: Zt's 8-row tiles hold a
     // column's rows in 64 bytes, half a 128-byte line whose other half is the
@@ -490,45 +517,37 @@ __global__ __launch_bounds__(KCfg<H>::THREADS, ColWaves<H>::V) void k_int_cols(c
         const bool valid = item < i1;
         const int f = valid ? item / NCH : 0, col = valid ? item % NCH : 0;
         const int colm = (W - col) & (W - 1);
-        float2 x[E];
-        {   // Z(:, -c) first, parked in s2 so only one column is live in registers
-            float2 y[E];
+        // Z(-ky, -c) straight from the INVERSE-direction (unnormalised) transform of
+        // column -c: sum_y z(y, -c) e^{+2 pi i ky y / H} at index ky, so both operands
+        // of the Hermitian split sit in the same lane and slot (no mirror exchange).
+        float2 x[E], y[E];
+        if constexpr (!C::PREF_Y) fetch_col(item < i1 ? item : items, true, py);
+        if constexpr (!FCD_INTCOLS_PREF_X) fetch_col(item < i1 ? item : items, false, px);
 #pragma unroll
-            for (int q = 0; q < E; ++q) {
-                y[q] = py[q];
-                x[q] = px[q];
-            }
-            if (base + TEAMS < i1) fetch(base + TEAMS + team < i1 ? base + TEAMS + team : items);
-            if (colk && colm == 0) {  // column-0 unwrap offsets of the fused path: row DC bins
-                const float sc = 6.28318530717959f * (float)W;
-#pragma unroll
-                for (int q = 0; q < E; ++q) {
-                    const int rr = t + TT * q;
-                    y[q].x += sc * (float)colk[((long)f * 2 + 0) * H + rr];
-                    y[q].y += sc * (float)colk[((long)f * 2 + 1) * H + rr];
-                }
-            }
-            fft.template run<false>(y, s, t);
-            if constexpr (!Sched<H>::WAVE_LOCAL) __syncthreads();
-#pragma unroll
-            for (int q = 0; q < E; ++q) s2[pad(t + TT * q)] = y[q];
+        for (int q = 0; q < E; ++q) {
+            y[q] = py[q];
+            x[q] = px[q];
         }
-        if (colk && col == 0) {
+        if (colk && (colm == 0 || col == 0)) {  // column-0 unwrap offsets of the fused path: row DC bins
             const float sc = 6.28318530717959f * (float)W;
 #pragma unroll
             for (int q = 0; q < E; ++q) {
                 const int rr = t + TT * q;
-                x[q].x += sc * (float)colk[((long)f * 2 + 0) * H + rr];
-                x[q].y += sc * (float)colk[((long)f * 2 + 1) * H + rr];
+                const float2 o = make_float2(sc * (float)colk[((long)f * 2 + 0) * H + rr],
+                                             sc * (float)colk[((long)f * 2 + 1) * H + rr]);
+                if (colm == 0) y[q] = make_float2(y[q].x + o.x, y[q].y + o.y);
+                if (col == 0) x[q] = make_float2(x[q].x + o.x, x[q].y + o.y);
             }
         }
-        fft.template run<false>(x, s, t);  // its exchange barriers also publish s2
+        fft.template run<true>(y, s, t);
+        if (base + TEAMS < i1) fetch(base + TEAMS + team < i1 ? base + TEAMS + team : items);
+        fft.template run<false>(x, s, t);
         const float kx = c.kxe[col], kx2 = c.kx2[col];
 #pragma unroll
         for (int q = 0; q < E; ++q) {
             const int i = t + TT * q;
             const float2 z = x[q];
-            const float2 zm = s2[pad((H - i) & (H - 1))];
+            const float2 zm = y[q];
             const float2 f0 = make_float2(0.5f * (z.x + zm.x), 0.5f * (z.y - zm.y));
             const float2 f1 = make_float2(0.5f * (z.y + zm.y), -0.5f * (z.x - zm.x));
             const float ky = c.kye[i];
@@ -738,8 +757,8 @@ static void launch_int_rows(int kmode, const float* w, const int* colk, const in
 template <int H>
 static void launch_int_cols(const float2* Zt, int W, int nb, const IntegCoef& c, float2* Ht, const float2* tw,
                             hipStream_t s, const int* colk) {
-    using C = KCfg<H>;
-    const size_t lds = (size_t)C::NLEN * 8 + (size_t)2 * C::TEAMS * C::ROW * 8;
+    using C = IntColsCfg<H>;
+    const size_t lds = (size_t)C::NLEN * 8 + (size_t)C::TEAMS * C::ROW * 8;
     set_lds(k_int_cols<H>, lds);
     const int grid = grid_for(((long)nb * (W / 2 + 1) + C::TEAMS - 1) / C::TEAMS, 4);
     const int zt = zt_rows(W);

@@ -153,6 +153,10 @@ class Engine:
         if ref.shape != self.shape:
             raise ValueError(f"reference shape {ref.shape} != engine shape {self.shape}")
         info = FcdRefInfo()
+        # a failed set_reference leaves the context without a reference: forget the
+        # cached one first so the next call with the old reference re-uploads it
+        self.ref_copy = None
+        self.ref_square_size = None
         _check(self._lib.fcd_set_reference(self._h, ref.ctypes.data, FCD_HOST_PTRS, float(square_size),
                                            ctypes.byref(info)))
         self.info = info
