@@ -209,3 +209,27 @@ def test_host_pipeline_follows_reference_change(df):
     b = eng.process_raw(frames.reshape(5, -1).view(np.uint8), _lib.FCD_FMT_F32, 5, 1.0)
     want_b, _, _ = eng.process(frames, 1.0, want_phases=True)
     assert rel_l2(b, want_b) < 1e-6
+
+
+def test_two_stream_split_equals_one_stream(df, monkeypatch):
+    """Device-pointer chunks run as two halves on two streams (FCD_STREAMS=2, the
+    default): heights bit-identical to the one-stream chain, with the exact MST pass
+    for the frames with residues running after the join (real frames, 7..1611
+    residues) and an odd frame count."""
+    import torch
+    from pyfcd import _lib
+    ref = df["ref_u16"].astype(np.float32)
+    frames = np.concatenate([df["frames_u16"], df["frames_u16"][:2]]).astype(np.float32)  # 5 frames
+    dev = torch.device("cuda", 0)
+    fd = torch.from_numpy(frames).to(dev)
+    out = {}
+    for ns in ("1", "2"):
+        monkeypatch.setenv("FCD_STREAMS", ns)
+        eng = _engine(ref, float(df["square_size"]))
+        hd = torch.empty_like(fd)
+        eng.process_device(fd.data_ptr(), len(frames), 1.0, True, hd.data_ptr())
+        torch.cuda.synchronize()
+        out[ns] = hd.cpu().numpy()
+    assert np.array_equal(out["1"], out["2"])
+    want, _, _ = _engine(ref, float(df["square_size"])).process(frames, 1.0, unwrap=True, want_phases=False)
+    assert np.array_equal(out["2"], want)

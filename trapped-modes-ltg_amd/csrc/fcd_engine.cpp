@@ -209,6 +209,9 @@ struct fcd_ctx {
     DevBuf theta_p;                      // theta_b in the phase kernels' lane-contiguous order
     bool fused_ok = false;           // k_phase_rows applies (height-only calls)
     bool force_unfused = false;      // FCD_UNFUSED=1: take the unfused chain (A/B measurement)
+    int nstreams = 2;                // FCD_STREAMS: device-path chunks split over 1 or 2 streams
+    hipStream_t aux = nullptr;       // the second stream and its fork / join events
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     DevBuf ztw, col0, seam;          // its 1024-point group-FFT twiddles; column-0 wrapped values [f][2][H];
                                      // first/last unwrapped rows of every tile [f][H/tile][2][W]
     size_t fres_cap = 0;
@@ -775,6 +778,7 @@ FCD_API int fcd_create(int device, int rows, int cols, fcd_ctx** out) {
         std::unique_ptr<fcd_ctx> c(new fcd_ctx());
         c->device = device;
         c->force_unfused = fcd_env_int("FCD_UNFUSED", 0) != 0;
+        c->nstreams = fcd_env_int("FCD_STREAMS", 2) >= 2 ? 2 : 1;
         c->H = rows;
         c->W = cols;
         HIPCHK(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking));
@@ -803,6 +807,12 @@ FCD_API int fcd_destroy(fcd_ctx* ctx) {
         (void)hipSetDevice(ctx->device);
         (void)hipStreamSynchronize(ctx->own);
         (void)hipStreamDestroy(ctx->own);
+        if (ctx->aux) {
+            (void)hipStreamSynchronize(ctx->aux);
+            (void)hipStreamDestroy(ctx->aux);
+            (void)hipEventDestroy(ctx->ev_fork);
+            (void)hipEventDestroy(ctx->ev_join);
+        }
         delete ctx;
     })
 }
@@ -916,24 +926,34 @@ namespace {
 
 // First pass of one chunk: nb device-resident float32 frames through the
 // band-pruned pipeline with the residue-free unwrap, heights to hdst (device).
+// fo: first workspace frame of the chunk (the fused chain's per-frame
+// intermediates are frame-strided, so disjoint frame ranges of one workspace can
+// run concurrently on different streams).
 void first_pass_chunk(fcd_ctx* c, const float* fr, int nb, bool unwrap, bool fused, int* res, float* hdst,
-                      int32_t* kdst, const fcdk::IntegCoef& coef, hipStream_t s) {
+                      int32_t* kdst, const fcdk::IntegCoef& coef, hipStream_t s, int fo = 0) {
     if (fused) {
         // height only: band transforms, phase, unwrap and the z-row FFT in one
         // pass (kernels_phase_rows.hip); colk lands in the spectra's DC bins
         const fcdk::DemodTables T = demod_tables(c);
+        const long H = c->H, W = c->W;
+        float2* Xb = c->Xb.as<float2>() + fo * H * c->NC;
+        float2* Ab = c->Ab.as<float2>() + fo * 2 * H * c->NCA;
+        float* col0 = c->col0.as<float>() + fo * 2 * H;
+        int* colk = c->colk.as<int>() + fo * 2 * H;
+        float2* Zt = c->Zt.as<float2>() + fo * H * W;
+        float2* seam = c->seam.as<float2>() + fo * (H / fcdk::phase_rows_tile()) * 2 * W;
+        float2* Ht = c->Ht.as<float2>() + fo * H * (W / 2 + 1);
         if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
-        fcdk::demod_rows(c->W, fr, c->H, nb, T, c->Xb.as<float2>(), c->twp_row.as<float2>(), s);
-        fcdk::demod_cols(c->H, c->Xb.as<float2>(), nb, T, c->Ab.as<float2>(), c->NCA, c->twp_col.as<float2>(), s);
+        fcdk::demod_rows(c->W, fr, c->H, nb, T, Xb, c->twp_row.as<float2>(), s);
+        fcdk::demod_cols(c->H, Xb, nb, T, Ab, c->NCA, c->twp_col.as<float2>(), s);
         if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
-        fcdk::phase_rows(unwrap, c->Ab.as<float2>(), c->H, nb, c->NCA, c->NCc[0], c->NCc[1], c->theta_p.as<float>(),
-                         c->band_pre.as<float2>(), c->band_ptw.as<float2>(), c->ztw.as<float2>(), c->col0.as<float>(),
-                         res, c->Zt.as<float2>(), c->seam.as<float2>(), s);
-        if (unwrap) fcdk::unwrap_colk_compact(c->col0.as<float>(), 2 * nb, c->H, c->colk.as<int>(), s);
+        fcdk::phase_rows(unwrap, Ab, c->H, nb, c->NCA, c->NCc[0], c->NCc[1], c->theta_p.as<float>(),
+                         c->band_pre.as<float2>(), c->band_ptw.as<float2>(), c->ztw.as<float2>(), col0, res, Zt, seam,
+                         s);
+        if (unwrap) fcdk::unwrap_colk_compact(col0, 2 * nb, c->H, colk, s);
         if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
-        fcdk::int_cols(c->H, c->Zt.as<float2>(), c->W, nb, coef, c->Ht.as<float2>(), c->twp_col.as<float2>(), s,
-                       unwrap ? c->colk.as<int>() : nullptr);
-        fcdk::int_c2r(c->W, c->Ht.as<float2>(), c->H, nb, hdst, c->twp_row.as<float2>(), s);
+        fcdk::int_cols(c->H, Zt, c->W, nb, coef, Ht, c->twp_col.as<float2>(), s, unwrap ? colk : nullptr);
+        fcdk::int_c2r(c->W, Ht, c->H, nb, hdst, c->twp_row.as<float2>(), s);
     } else {
         if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
         fast_demod(c, fr, nb, s);
@@ -1154,7 +1174,30 @@ int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int f
             }
             float* hdst = (dev && height_out) ? height_out + (size_t)f0 * hw : c->out_h.as<float>();
             int32_t* kdst = k_out && unwrap ? (dev ? k_out + (size_t)f0 * 2 * hw : c->fk.as<int32_t>()) : nullptr;
-            first_pass_chunk(c, fr, nb, unwrap != 0, fused, res ? res + (size_t)f0 * 2 : nullptr, hdst, kdst, coef, s);
+            int* rs = res ? res + (size_t)f0 * 2 : nullptr;
+            const int nsplit = fused && !c->profiling && nb >= 2 ? c->nstreams : 1;
+            if (nsplit == 2) {
+                // two halves of the chunk on two streams: kernels bound by different
+                // resources (HBM-bound c2r / demod_rows, latency-bound phase_rows /
+                // int_cols) overlap instead of running back to back
+                if (!c->aux) {
+                    HIPCHK(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
+                    HIPCHK(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+                    HIPCHK(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
+                }
+                const int na = (nb + 1) / 2, nb2 = nb - na;
+                // (r01bh/bi, 1024^2 x 256: 74.5k -> 75.7-76.3k frames/s; starting the
+                // second half after the first half's demod kernels instead: no gain)
+                HIPCHK(hipEventRecord(c->ev_fork, s));
+                HIPCHK(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
+                first_pass_chunk(c, fr, na, unwrap != 0, true, rs, hdst, nullptr, coef, s, 0);
+                first_pass_chunk(c, fr + (size_t)na * hw, nb2, unwrap != 0, true, rs ? rs + 2 * na : nullptr,
+                                 hdst + (size_t)na * hw, nullptr, coef, c->aux, na);
+                HIPCHK(hipEventRecord(c->ev_join, c->aux));
+                HIPCHK(hipStreamWaitEvent(s, c->ev_join, 0));
+            } else {
+                first_pass_chunk(c, fr, nb, unwrap != 0, fused, rs, hdst, kdst, coef, s);
+            }
             if (height_out && !dev)
                 HIPCHK(hipMemcpyAsync(height_out + (size_t)f0 * hw, hdst, (size_t)nb * hw * 4, out_kind, s));
             if (wrapped_out)
