@@ -37,6 +37,22 @@ __global__ void rowfill(float* __restrict__ b, long rows) {
         for (int q = 0; q < 16; ++q) __builtin_nontemporal_store(1.f, o + n0 + 64 * q);
     }
 }
+// IL: the block's 4 waves write 4 consecutive rows (16 KB) interleaved at 256 B
+// (store q of wave w -> 256-byte piece 4 q + w); PERM: the kernel's lane permutation
+template <bool IL, bool PERM>
+__global__ void rowfill2(float* __restrict__ b, long rows) {
+    extern __shared__ float lds_pad[];  // dynamic LDS only limits the resident blocks
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int n0 = PERM ? (lane >> 3) + 8 * (lane & 7) : lane;
+    if (rows < 0) lds_pad[threadIdx.x] = 0.f;
+    for (long r0 = blockIdx.x * 4L; r0 < rows; r0 += gridDim.x * 4L) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const long o = IL ? r0 * 1024 + (4 * q + w) * 64 : (r0 + w) * 1024 + 64 * q;
+            __builtin_nontemporal_store(1.f, b + o + n0);
+        }
+    }
+}
 typedef float fv4m __attribute__((ext_vector_type(4)));
 int main(int argc, char** argv) {
     if (argc > 1 && argv[1][0] == 'w') {  // write-only bandwidth over 2 GiB (past the 256 MiB MALL)
@@ -57,6 +73,11 @@ int main(int argc, char** argv) {
             runw("fill 16B plain", [&] { fillk<fv4m, false><<<g, 256>>>((fv4m*)w, wb / 16, fv4m{1, 1, 1, 1}); });
             runw("fill 16B nt", [&] { fillk<fv4m, true><<<g, 256>>>((fv4m*)w, wb / 16, fv4m{1, 1, 1, 1}); });
             runw("row pattern 4B nt", [&] { rowfill<<<g, 256>>>(w, wb / 4096); });
+            runw("row pattern, no perm", [&] { rowfill2<false, false><<<g, 256>>>(w, wb / 4096); });
+            runw("rows interleaved 256B", [&] { rowfill2<true, true><<<g, 256>>>(w, wb / 4096); });
+            runw("row pattern, 12 waves/CU", [&] { rowfill2<false, true><<<g, 256, 48 << 10>>>(w, wb / 4096); });
+            runw("interleaved, 12 waves/CU", [&] { rowfill2<true, true><<<g, 256, 48 << 10>>>(w, wb / 4096); });
+            runw("fill 4B nt, 12 waves/CU", [&] { rowfill2<true, false><<<g, 256, 48 << 10>>>(w, wb / 4096); });
         }
         return 0;
     }
