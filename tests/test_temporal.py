@@ -1,0 +1,166 @@
+"""Temporal post-analysis of the map stack (analyze.py:364-587):
+`analyze.block_split`, `analyze.block_amplitude`, `analyze.spectrogram`.
+
+Parity unpinned: the reference module imports cv2, absent here, so no reference-run
+vectors exist; the checker is oracle/temporal_oracle.py, the reference's own numpy /
+scipy calls restated on in-memory stacks.  The device DFTs accumulate in f64, so the
+comparisons are at 1e-9 relative (the reference's np.fft is f64 as well; its
+spectrogram of a float32 series runs in float32 inside scipy, which the f64 device
+result beats — compared here against scipy on the f64 series).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import temporal_oracle as ora
+
+TASA = 500.0
+
+
+def make_stack(T, n=64, seed=0, f0=25.0, zero_corner=True, nan_pixels=()):
+    """T maps of n x n: per-pixel harmonics of f0 (random amplitude / phase) + noise;
+    the first map's top-left corner is 0 (masked block pixels), a few pixels carry
+    NaN gaps in later maps (the spectrogram's interpolation path)."""
+    rng = np.random.default_rng(seed)
+    t = np.arange(T) / TASA
+    a1 = rng.uniform(0.5, 1.5, (n, n))
+    p1 = rng.uniform(-np.pi, np.pi, (n, n))
+    a2 = rng.uniform(0.1, 0.3, (n, n))
+    st = (a1[None] * np.cos(2 * np.pi * f0 * t[:, None, None] + p1[None])
+          + a2[None] * np.cos(2 * np.pi * 2 * f0 * t[:, None, None] + 2 * p1[None])
+          + 0.05 * rng.standard_normal((T, n, n)) + 0.2).astype(np.float32)
+    if zero_corner:
+        st[0, :5, :7] = 0.0
+    for (i, j, t0, t1) in nan_pixels:
+        st[t0:t1, i, j] = np.nan
+    return st
+
+
+def write_maps(folder, stack):
+    os.makedirs(folder, exist_ok=True)
+    for k, m in enumerate(stack):
+        np.save(os.path.join(folder, f"frame{k:05d}_map.npy"), m)
+    np.save(os.path.join(folder, "calibration_factor.npy"), np.array([1e-4]))
+
+
+def close_nan(a, b, rtol=1e-9, atol=0.0):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    assert a.shape == b.shape
+    assert np.array_equal(np.isnan(a), np.isnan(b))
+    ok = ~np.isnan(a)
+    scale = np.abs(b[ok]).max() if ok.any() else 1.0
+    np.testing.assert_allclose(a[ok], b[ok], rtol=0, atol=rtol * scale + atol)
+
+
+# ---------------------------------------------------------------- CPU: oracle / host logic
+def test_oracle_block_amplitude_recovers_harmonics():
+    st = make_stack(500, n=16, zero_corner=False)
+    harm, amps, phases, f0 = ora.block_amplitude(st, tasa=TASA, mode=3, num_blocks=4, block_index=0)
+    assert f0 == 25.0 and harm == [0.0, 25.0, 50.0]
+    assert np.allclose(amps[:, :, 0], 0.2, atol=0.01)  # mean
+    assert np.all(amps[:, :, 3] == 0)                   # the reference's unused column
+
+
+def test_spectro_params_match_scipy():
+    from scipy import signal
+    from pydata.analyze import analyze
+    for T, kw in [(300, {}), (300, {"nperseg": 64}), (300, {"nperseg": 64, "noverlap": 40}), (100, {}),
+                  (257, {"window": "hann", "nperseg": 32})]:
+        x = np.random.default_rng(T).standard_normal(T)
+        f_ref, t_ref, _ = signal.spectrogram(x, fs=125, **kw)
+        nperseg, noverlap, win, f, t = analyze._spectro_params(T, 125, kw)
+        assert np.array_equal(f, f_ref) and np.array_equal(t, t_ref), (T, kw)
+        assert len(win) == nperseg
+
+
+# ---------------------------------------------------------------- GPU: device vs oracle
+@pytest.mark.gpu
+@pytest.mark.parametrize("T,block", [(400, 0), (301, 3)])
+def test_block_amplitude_matches_oracle(tmp_path, T, block):
+    from pydata.analyze import analyze
+    st = make_stack(T, n=64, seed=T)
+    write_maps(str(tmp_path), st)
+    got = analyze.block_amplitude(str(tmp_path), tasa=TASA, mode=3, num_blocks=4, block_index=block)
+    want = ora.block_amplitude(st, tasa=TASA, mode=3, num_blocks=4, block_index=block)
+    assert got[3] == want[3] and got[0] == want[0]
+    close_nan(got[1], want[1])
+    ok = ~np.isnan(want[1][:, :, :3])
+    np.testing.assert_allclose(got[2][:, :, :3][ok], want[2][:, :, :3][ok], atol=1e-7)
+    if block == 0:
+        assert np.isnan(got[1][0, 0, 0])  # masked pixel (first map 0)
+    # given f0: only the harmonic bins are computed
+    got2 = analyze.block_amplitude(str(tmp_path), f0=50.0, tasa=TASA, mode=2, num_blocks=4, block_index=block)
+    want2 = ora.block_amplitude(st, f0=50.0, tasa=TASA, mode=2, num_blocks=4, block_index=block)
+    assert got2[0] == want2[0]
+    close_nan(got2[1], want2[1])
+
+
+@pytest.mark.gpu
+def test_block_amplitude_no_peak(tmp_path):
+    from pydata.analyze import analyze
+    # 3 maps: 2 non-negative bins, so find_peaks has no interior sample to report
+    st = np.random.default_rng(0).uniform(1, 2, (3, 32, 32)).astype(np.float32)
+    write_maps(str(tmp_path), st)
+    got = analyze.block_amplitude(str(tmp_path), tasa=TASA, mode=2, num_blocks=4)
+    want = ora.block_amplitude(st, tasa=TASA, mode=2, num_blocks=4)
+    assert len(got) == len(want) == 5 and got[3] is None and got[4] is None
+    assert np.array_equal(got[0], want[0]) and got[1].shape == want[1].shape
+
+
+@pytest.mark.gpu
+def test_temporal_engine_long_series():
+    """T above the LDS table (the global-table kernel), odd T, a sub-block."""
+    from pyfcd import _lib
+    eng = _lib.temporal_engine()
+    st = make_stack(9001, n=16, seed=5, zero_corner=False)
+    spec = np.fft.fft(st.astype(np.float64), axis=0)
+    nf = 4501
+    tot, cnt = eng.temporal_spectrum(st, nf)
+    assert np.all(cnt == 256)
+    np.testing.assert_allclose(tot, np.abs(spec[:nf]).sum(axis=(1, 2)), rtol=1e-9)
+    bins = [0, 450, 900, 4500]
+    X = eng.temporal_bins(st, bins, block=(4, 2, 8, 8))
+    close_nan(X.real, np.transpose(spec[bins, 4:12, 2:10], (1, 2, 0)).real)
+    close_nan(X.imag, np.transpose(spec[bins, 4:12, 2:10], (1, 2, 0)).imag)
+
+
+@pytest.mark.gpu
+def test_block_amplitude_zero_map(tmp_path):
+    from pydata.analyze import analyze
+    st = make_stack(256, n=32, seed=9)
+    zero = st.mean(axis=0)
+    write_maps(str(tmp_path), st)
+    got = analyze.block_amplitude(str(tmp_path), tasa=TASA, mode=2, num_blocks=4, block_index=2, zero=zero)
+    want = ora.block_amplitude(st, tasa=TASA, mode=2, num_blocks=4, block_index=2, zero=zero)
+    assert got[3] == want[3]
+    close_nan(got[1], want[1], rtol=1e-6)  # the maps minus a float32 mean, rounded to float32
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kw", [{"nperseg": 64}, {"nperseg": 50, "noverlap": 20, "window": "hann"}, {}])
+def test_spectrogram_block_matches_oracle(tmp_path, kw):
+    from pydata.analyze import analyze
+    st = make_stack(300, n=32, seed=3, nan_pixels=[(10, 12, 40, 45), (20, 3, 100, 101)])
+    write_maps(str(tmp_path), st)
+    t, f, S, avg = analyze.spectrogram(map_folder=str(tmp_path), fs=TASA, num_blocks=4, block_index=0, **kw)
+    # the oracle on the float64 series (scipy keeps float32 series in float32)
+    t2, f2, S2, avg2 = ora.spectrogram_block(st.astype(np.float64), fs=TASA, num_blocks=4, block_index=0, **kw)
+    assert np.array_equal(t, t2) and np.array_equal(f, f2)
+    close_nan(S, S2)
+    close_nan(avg, avg2)
+    assert np.isnan(S[0, 0]).all() and not np.isnan(S[10, 12]).any()
+
+
+@pytest.mark.gpu
+def test_spectrogram_series():
+    from pydata.analyze import analyze
+    x = make_stack(1000, n=1, seed=1, zero_corner=False)[:, 0, 0]
+    t, f, S = analyze.spectrogram(array=x, fs=TASA, nperseg=128)
+    t2, f2, S2 = ora.spectrogram_series(x.astype(np.float64), fs=TASA, nperseg=128)
+    assert np.array_equal(t, t2) and np.array_equal(f, f2)
+    close_nan(S, S2)
+    # and the reference's own float32 computation, to float32 accuracy
+    t3, f3, S3 = ora.spectrogram_series(x, fs=TASA, nperseg=128)
+    close_nan(S, S3, rtol=1e-5)

@@ -221,6 +221,8 @@ struct fcd_ctx {
     DevBuf spec, work, wrapped, kbuf, colk, rescnt, frames_in, out_h, scalar;
     DevBuf cand_idx, cand_val;
     DevBuf fix_raw;  // raw samples of the frames redone by the exact pass
+    // temporal analysis: staged block, exp table, bins, partial sums, output, window
+    DevBuf t_stage, t_tab, t_bins, t_part, t_out, t_win, t_wsum;
     HostPipe pipe;
     // MST workspace
     DevBuf mst_comp, mst_off, mst_rel, mst_cw, mst_ce, mst_bw, mst_be, mst_link, mst_hooks, mst_ids;
@@ -1418,6 +1420,150 @@ FCD_API int fcd_fft2(fcd_ctx* c, const float* in, int n, int flags, float* out, 
                 HIPCHK(hipStreamSynchronize(s));
             }
         }
+    })
+}
+
+namespace {
+
+// The block [r0, r0 + bh) x [c0, c0 + bw) of a [T][rows][cols] float32 stack on
+// the device: the caller's own memory (device pointers) or a staged copy of
+// just the block (host pointers).  Returns the block origin and its pitches.
+struct BlockView {
+    const float* p;
+    long frame_pitch, row_pitch;
+};
+
+BlockView stage_block(fcd_ctx* c, const float* stack, int T, int rows, int cols, int r0, int c0, int bh, int bw,
+                      bool dev, hipStream_t s) {
+    if (!stack || T <= 0 || rows <= 0 || cols <= 0 || bh <= 0 || bw <= 0 || r0 < 0 || c0 < 0 || r0 + bh > rows ||
+        c0 + bw > cols)
+        throw FcdError(FCD_E_INVALID, "bad stack / block arguments");
+    if (dev) return {stack + (long)r0 * cols + c0, (long)rows * cols, cols};
+    c->t_stage.ensure((size_t)T * bh * bw * sizeof(float));
+    float* d = c->t_stage.as<float>();
+    for (int t = 0; t < T; ++t)
+        HIPCHK(hipMemcpy2DAsync(d + (size_t)t * bh * bw, (size_t)bw * 4, stack + ((size_t)t * rows + r0) * cols + c0,
+                                (size_t)cols * 4, (size_t)bw * 4, bh, hipMemcpyHostToDevice, s));
+    return {d, (long)bh * bw, bw};
+}
+
+// exp(-2 pi i j / n), j < n, in f64 (the DFT kernels index it by (f t) mod n)
+void upload_exp_table(fcd_ctx* c, DevBuf& buf, int n, hipStream_t s) {
+    std::vector<double2> tab(n);
+    for (int j = 0; j < n; ++j) {
+        const double a = -2.0 * kPi * (double)j / (double)n;
+        tab[j] = make_double2(std::cos(a), std::sin(a));
+    }
+    buf.ensure((size_t)n * sizeof(double2));
+    upload(buf.p, tab.data(), (size_t)n * sizeof(double2), s);
+    HIPCHK(hipStreamSynchronize(s));  // tab dies here
+}
+
+}  // namespace
+
+FCD_API int fcd_temporal_spectrum(fcd_ctx* c, const float* stack, int T, int rows, int cols, int r0, int c0, int bh,
+                                  int bw, int flags, int nf, double* sum_count, void* stream) {
+    FCD_TRY({
+        check_ctx(c);
+        if (!sum_count || nf <= 0 || nf > T) throw FcdError(FCD_E_INVALID, "bad spectrum arguments");
+        hipStream_t s = c->pick(stream);
+        const BlockView v = stage_block(c, stack, T, rows, cols, r0, c0, bh, bw, flags == FCD_DEVICE_PTRS, s);
+        upload_exp_table(c, c->t_tab, T, s);
+        const int P = bh * bw, tiles = fcdk::temporal_dft_tiles(P);
+        c->t_part.ensure((size_t)tiles * nf * 2 * sizeof(double));
+        fcdk::temporal_dft(v.p, v.frame_pitch, v.row_pitch, bw, P, T, c->t_tab.as<double2>(), nullptr, nf, nullptr,
+                           c->t_part.as<double>(), s);
+        std::vector<double> part((size_t)tiles * nf * 2);
+        HIPCHK(hipMemcpyAsync(part.data(), c->t_part.p, part.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        for (int f = 0; f < nf; ++f) {  // fixed-order sum over the pixel tiles (deterministic)
+            double a = 0.0, n = 0.0;
+            for (int i = 0; i < tiles; ++i) {
+                a += part[((size_t)i * nf + f) * 2];
+                n += part[((size_t)i * nf + f) * 2 + 1];
+            }
+            sum_count[2 * f] = a;
+            sum_count[2 * f + 1] = n;
+        }
+    })
+}
+
+FCD_API int fcd_temporal_bins(fcd_ctx* c, const float* stack, int T, int rows, int cols, int r0, int c0, int bh,
+                              int bw, int flags, const int* bins, int nbins, double* x_out, void* stream) {
+    FCD_TRY({
+        check_ctx(c);
+        if (!bins || !x_out || nbins <= 0) throw FcdError(FCD_E_INVALID, "bad bins arguments");
+        for (int i = 0; i < nbins; ++i)
+            if (bins[i] < 0 || bins[i] >= T) throw FcdError(FCD_E_INVALID, "bin out of range");
+        hipStream_t s = c->pick(stream);
+        const bool dev = flags == FCD_DEVICE_PTRS;
+        const BlockView v = stage_block(c, stack, T, rows, cols, r0, c0, bh, bw, dev, s);
+        upload_exp_table(c, c->t_tab, T, s);
+        c->t_bins.ensure((size_t)nbins * sizeof(int));
+        upload(c->t_bins.p, bins, (size_t)nbins * sizeof(int), s);
+        const int P = bh * bw;
+        double2* out = reinterpret_cast<double2*>(x_out);
+        if (!dev) {
+            c->t_out.ensure((size_t)P * nbins * sizeof(double2));
+            out = c->t_out.as<double2>();
+        }
+        fcdk::temporal_dft(v.p, v.frame_pitch, v.row_pitch, bw, P, T, c->t_tab.as<double2>(), c->t_bins.as<int>(),
+                           nbins, out, nullptr, s);
+        if (!dev) {
+            HIPCHK(hipMemcpyAsync(x_out, out, (size_t)P * nbins * sizeof(double2), hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+        } else {
+            HIPCHK(hipStreamSynchronize(s));  // the bins buffer is reused by the next call
+        }
+    })
+}
+
+FCD_API int fcd_spectrogram(fcd_ctx* c, const float* stack, int T, int rows, int cols, int r0, int c0, int bh, int bw,
+                            int flags, int nperseg, int noverlap, const double* window, double fs, double* s_out,
+                            void* stream) {
+    FCD_TRY({
+        check_ctx(c);
+        if (!window || !s_out || nperseg < 1 || nperseg > T || noverlap < 0 || noverlap >= nperseg || !(fs > 0))
+            throw FcdError(FCD_E_INVALID, "bad spectrogram arguments");
+        if (nperseg > fcdk::spectro_max_nperseg()) throw FcdError(FCD_E_UNSUPPORTED, "nperseg too large");
+        hipStream_t s = c->pick(stream);
+        const bool dev = flags == FCD_DEVICE_PTRS;
+        const BlockView v = stage_block(c, stack, T, rows, cols, r0, c0, bh, bw, dev, s);
+        const int step = nperseg - noverlap, nseg = (T - nperseg) / step + 1, nf = nperseg / 2 + 1;
+        // window, its DFT W_f (the mean-removal term) and the density scale, in f64
+        std::vector<double2> tab(nperseg), wsum(nf);
+        double w2 = 0.0;
+        for (int j = 0; j < nperseg; ++j) {
+            const double a = -2.0 * kPi * (double)j / (double)nperseg;
+            tab[j] = make_double2(std::cos(a), std::sin(a));
+            w2 += window[j] * window[j];
+        }
+        for (int f = 0; f < nf; ++f) {
+            double re = 0.0, im = 0.0;
+            for (int n = 0; n < nperseg; ++n) {
+                const double2 e = tab[(size_t)((long)f * n % nperseg)];
+                re += window[n] * e.x;
+                im += window[n] * e.y;
+            }
+            wsum[f] = make_double2(re, im);
+        }
+        c->t_tab.ensure((size_t)nperseg * sizeof(double2));
+        c->t_win.ensure((size_t)nperseg * sizeof(double));
+        c->t_wsum.ensure((size_t)nf * sizeof(double2));
+        upload(c->t_tab.p, tab.data(), (size_t)nperseg * sizeof(double2), s);
+        upload(c->t_win.p, window, (size_t)nperseg * sizeof(double), s);
+        upload(c->t_wsum.p, wsum.data(), (size_t)nf * sizeof(double2), s);
+        const int P = bh * bw;
+        double* out = s_out;
+        if (!dev) {
+            c->t_out.ensure((size_t)P * nf * nseg * sizeof(double));
+            out = c->t_out.as<double>();
+        }
+        fcdk::spectrogram(v.p, v.frame_pitch, v.row_pitch, bw, P, nperseg, step, nseg, c->t_win.as<double>(),
+                          c->t_tab.as<double2>(), c->t_wsum.as<double2>(), nf, 1.0 / (fs * w2), out, s);
+        if (!dev)
+            HIPCHK(hipMemcpyAsync(s_out, out, (size_t)P * nf * nseg * sizeof(double), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));  // host vectors die here
     })
 }
 

@@ -132,4 +132,13 @@ void integ_multiply(const float2* Z, float2* Hh, int nbatch, int H, int W, Integ
 // phases f32 = w + 2pi k
 void compose_phase(const float* w, const int32_t* k, float* out, long n, hipStream_t s);
 
+// temporal analysis of a map stack (kernels_temporal.hip)
+void temporal_dft(const float* stack, long frame_pitch, long row_pitch, int bw, int P, int T, const double2* tab,
+                  const int* freqs, int nf, double2* out, double* partial, hipStream_t s);
+int temporal_dft_tiles(int P);
+int spectro_max_nperseg();
+void spectrogram(const float* stack, long frame_pitch, long row_pitch, int bw, int P, int nperseg, int step, int nseg,
+                 const double* win, const double2* tab, const double2* wsum, int nf, double scale, double* out,
+                 hipStream_t s);
+
 }  // namespace fcdk

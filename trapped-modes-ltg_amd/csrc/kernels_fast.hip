@@ -55,7 +55,6 @@ template <int N>
 struct ColWaves {
     static constexpr int V = N >= 4096 ? 2 : FCD_COL_WAVES;
 };
-constexpr float kPiF = 3.14159265358979f;
 constexpr float kTwoPiF = 6.28318530717959f;
 
 __device__ __forceinline__ long tix(int row, int col, int ncols) {

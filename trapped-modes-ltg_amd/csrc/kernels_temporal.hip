@@ -1,0 +1,228 @@
+// Temporal analysis of a height-map stack: per-pixel
+// DFTs along time for a spatial block of a [T][rows][cols] float32 stack, as
+// analyze.block_amplitude (analyze.py:543-587: np.fft.fft over time, f64) and
+// analyze.spectrogram (analyze.py:419-531: scipy.signal.spectrogram per pixel).
+//
+// The reference loops over pixels in Python; here one lane owns one pixel of
+// the block and walks its time series (a coalesced row-run of every frame,
+// no transpose of the stack), 16 frequencies per lane accumulated in f64.
+// The DFT is direct, not an FFT: T is any length (the number of maps), the
+// work is ~T x (T/2 + 1) complex MACs per pixel (1.3e11 flop for a 128 x 128
+// block of 2000 maps, ~2 ms of f64 VALU on the MI355X), and the exponentials
+// come from a table exp(-2 pi i j / T) built on the host in f64 and indexed by
+// (f t) mod T, kept incrementally per frequency (exact argument reduction).
+#include <hip/hip_runtime.h>
+
+#include <stdexcept>
+#include <string>
+
+#include "kernels.hpp"
+
+namespace fcdk {
+
+namespace {
+
+constexpr int TD_THREADS = 256;  // pixels per workgroup
+constexpr int TD_FT = 16;        // frequencies per lane
+constexpr int TD_LDS_TAB = 8192;  // table entries held in LDS (128 KiB of double2)
+
+// Pixel p of the block -> its element offset in frame 0.
+__device__ __forceinline__ long pix_off(int p, int bw, long row_pitch) { return (long)(p / bw) * row_pitch + p % bw; }
+
+}  // namespace
+
+// X(p, f_k) = sum_t x_p(t) exp(-2 pi i f_k t / T) for the frequencies of
+// blockIdx.y's tile: freqs[k] if freqs, else f = tile * 16 + k < nf.
+//   REDUCE: per-workgroup sums of |X| over the pixels whose X is not NaN and
+//           their count (np.nanmean's numerator / denominator) -> partial
+//           [gridDim.x][nf][2]; X itself is not stored.
+//   else:   X -> out [P][nf] (complex f64).
+template <bool REDUCE, bool LDS>
+__global__ __launch_bounds__(TD_THREADS) void k_tdft(const float* __restrict__ stack, long frame_pitch, long row_pitch,
+                                                     int bw, int P, int T, const double2* __restrict__ tab,
+                                                     const int* __restrict__ freqs, int nf, double2* __restrict__ out,
+                                                     double* __restrict__ partial) {
+    extern __shared__ double2 tab_lds[];
+    const double2* tb = tab;
+    if constexpr (LDS) {
+        for (int i = threadIdx.x; i < T; i += TD_THREADS) tab_lds[i] = tab[i];
+        __syncthreads();
+        tb = tab_lds;
+    }
+    const int p = blockIdx.x * TD_THREADS + threadIdx.x;
+    const bool live = p < P;
+    const float* xs = stack + (live ? pix_off(p, bw, row_pitch) : 0);
+    int fk[TD_FT], idx[TD_FT];
+    double re[TD_FT], im[TD_FT];
+#pragma unroll
+    for (int k = 0; k < TD_FT; ++k) {
+        const int j = blockIdx.y * TD_FT + k;
+        fk[k] = j < nf ? (freqs ? freqs[j] : j) : 0;
+        idx[k] = 0;
+        re[k] = 0.0;
+        im[k] = 0.0;
+    }
+#pragma unroll 2
+    for (int t = 0; t < T; ++t) {
+        const double x = live ? (double)__builtin_nontemporal_load(xs + (long)t * frame_pitch) : 0.0;
+#pragma unroll
+        for (int k = 0; k < TD_FT; ++k) {
+            const double2 w = tb[idx[k]];  // wave-uniform index: an LDS broadcast
+            re[k] = fma(x, w.x, re[k]);
+            im[k] = fma(x, w.y, im[k]);
+            idx[k] += fk[k];
+            idx[k] -= idx[k] >= T ? T : 0;
+        }
+    }
+    if constexpr (REDUCE) {
+        __shared__ double red[TD_THREADS / 64][TD_FT][2];
+        const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+        for (int k = 0; k < TD_FT; ++k) {
+            const double m = sqrt(re[k] * re[k] + im[k] * im[k]);
+            const bool ok = live && m == m;  // NaN samples make every bin NaN
+            double s = ok ? m : 0.0, c = ok ? 1.0 : 0.0;
+            for (int o = 32; o > 0; o >>= 1) {
+                s += __shfl_xor(s, o, 64);
+                c += __shfl_xor(c, o, 64);
+            }
+            if (lane == 0) {
+                red[wave][k][0] = s;
+                red[wave][k][1] = c;
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x < TD_FT * 2) {
+            const int k = threadIdx.x >> 1, e = threadIdx.x & 1;
+            const int j = blockIdx.y * TD_FT + k;
+            double acc = 0.0;
+#pragma unroll
+            for (int w = 0; w < TD_THREADS / 64; ++w) acc += red[w][k][e];
+            if (j < nf) partial[((long)blockIdx.x * nf + j) * 2 + e] = acc;
+        }
+    } else if (live) {
+#pragma unroll
+        for (int k = 0; k < TD_FT; ++k) {
+            const int j = blockIdx.y * TD_FT + k;
+            if (j < nf) out[(long)p * nf + j] = make_double2(re[k], im[k]);
+        }
+    }
+}
+
+// One-sided PSD of every segment of every pixel (scipy.signal.spectrogram with
+// detrend='constant', scaling='density', mode='psd'):
+//   X_f = sum_n (x_n - mean) w_n e_fn = sum_n x_n w_n e_fn - mean * W_f,
+//   W_f = sum_n w_n e_fn (host, f64), so the segment is read once;
+//   S_f = |X_f|^2 * scale, doubled except at DC and (even nperseg) Nyquist.
+// out [P][nf][nseg]; grid (pixel tiles, segments, frequency tiles).
+__global__ __launch_bounds__(TD_THREADS) void k_spectro(const float* __restrict__ stack, long frame_pitch,
+                                                        long row_pitch, int bw, int P, int nperseg, int step,
+                                                        int nseg, const double* __restrict__ win,
+                                                        const double2* __restrict__ tab,
+                                                        const double2* __restrict__ wsum, int nf, double scale,
+                                                        double* __restrict__ out) {
+    extern __shared__ double2 sp_lds[];
+    double2* const tb = sp_lds;                                     // [nperseg]
+    double* const wl = reinterpret_cast<double*>(sp_lds + nperseg);  // [nperseg]
+    for (int i = threadIdx.x; i < nperseg; i += TD_THREADS) {
+        tb[i] = tab[i];
+        wl[i] = win[i];
+    }
+    __syncthreads();
+    const int p = blockIdx.x * TD_THREADS + threadIdx.x;
+    const int seg = blockIdx.y;
+    const bool live = p < P;
+    const float* xs = stack + (live ? pix_off(p, bw, row_pitch) : 0) + (long)seg * step * frame_pitch;
+    int fk[TD_FT], idx[TD_FT];
+    double re[TD_FT], im[TD_FT];
+#pragma unroll
+    for (int k = 0; k < TD_FT; ++k) {
+        const int j = blockIdx.z * TD_FT + k;
+        fk[k] = j < nf ? j : 0;
+        idx[k] = 0;
+        re[k] = 0.0;
+        im[k] = 0.0;
+    }
+    double sum = 0.0;
+#pragma unroll 2
+    for (int n = 0; n < nperseg; ++n) {
+        const double x = live ? (double)xs[(long)n * frame_pitch] : 0.0;
+        sum += x;
+        const double xw = x * wl[n];
+#pragma unroll
+        for (int k = 0; k < TD_FT; ++k) {
+            const double2 w = tb[idx[k]];
+            re[k] = fma(xw, w.x, re[k]);
+            im[k] = fma(xw, w.y, im[k]);
+            idx[k] += fk[k];
+            idx[k] -= idx[k] >= nperseg ? nperseg : 0;
+        }
+    }
+    if (!live) return;
+    const double mean = sum / (double)nperseg;
+#pragma unroll
+    for (int k = 0; k < TD_FT; ++k) {
+        const int j = blockIdx.z * TD_FT + k;
+        if (j >= nf) continue;
+        const double2 W = wsum[j];
+        const double xr = re[k] - mean * W.x, xi = im[k] - mean * W.y;
+        double s = (xr * xr + xi * xi) * scale;
+        if (j > 0 && !(nperseg % 2 == 0 && j == nperseg / 2)) s *= 2.0;
+        out[((long)p * nf + j) * nseg + seg] = s;
+    }
+}
+
+namespace {
+
+void check_launch(const char* what) {
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+}  // namespace
+
+void temporal_dft(const float* stack, long frame_pitch, long row_pitch, int bw, int P, int T, const double2* tab,
+                  const int* freqs, int nf, double2* out, double* partial, hipStream_t s) {
+    if (P <= 0 || T <= 0 || nf <= 0) return;
+    const dim3 grid((unsigned)((P + TD_THREADS - 1) / TD_THREADS), (unsigned)((nf + TD_FT - 1) / TD_FT));
+    const bool lds = T <= TD_LDS_TAB;
+    const size_t lb = lds ? (size_t)T * sizeof(double2) : 0;
+    if (partial) {
+        if (lds) {
+            (void)hipFuncSetAttribute((const void*)k_tdft<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb);
+            hipLaunchKernelGGL((k_tdft<true, true>), grid, dim3(TD_THREADS), lb, s, stack, frame_pitch, row_pitch, bw,
+                               P, T, tab, freqs, nf, out, partial);
+        } else {
+            hipLaunchKernelGGL((k_tdft<true, false>), grid, dim3(TD_THREADS), 0, s, stack, frame_pitch, row_pitch, bw,
+                               P, T, tab, freqs, nf, out, partial);
+        }
+    } else {
+        if (lds) {
+            (void)hipFuncSetAttribute((const void*)k_tdft<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb);
+            hipLaunchKernelGGL((k_tdft<false, true>), grid, dim3(TD_THREADS), lb, s, stack, frame_pitch, row_pitch,
+                               bw, P, T, tab, freqs, nf, out, partial);
+        } else {
+            hipLaunchKernelGGL((k_tdft<false, false>), grid, dim3(TD_THREADS), 0, s, stack, frame_pitch, row_pitch,
+                               bw, P, T, tab, freqs, nf, out, partial);
+        }
+    }
+    check_launch("temporal_dft");
+}
+
+int temporal_dft_tiles(int P) { return (P + TD_THREADS - 1) / TD_THREADS; }
+
+int spectro_max_nperseg() { return 160 * 1024 / 24; }
+
+void spectrogram(const float* stack, long frame_pitch, long row_pitch, int bw, int P, int nperseg, int step, int nseg,
+                 const double* win, const double2* tab, const double2* wsum, int nf, double scale, double* out,
+                 hipStream_t s) {
+    if (P <= 0 || nseg <= 0) return;
+    const dim3 grid((unsigned)((P + TD_THREADS - 1) / TD_THREADS), (unsigned)nseg, (unsigned)((nf + TD_FT - 1) / TD_FT));
+    const size_t lb = (size_t)nperseg * (sizeof(double2) + sizeof(double));
+    (void)hipFuncSetAttribute((const void*)k_spectro, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb);
+    hipLaunchKernelGGL(k_spectro, grid, dim3(TD_THREADS), lb, s, stack, frame_pitch, row_pitch, bw, P, nperseg, step,
+                       nseg, win, tab, wsum, nf, scale, out);
+    check_launch("spectrogram");
+}
+
+}  // namespace fcdk

@@ -1,7 +1,9 @@
 """Drop-in for the hot-path part of `pydata.analyze` (/root/reference/pydata/analyze.py):
 the frame loader, the floating-structure mask, and the batch driver `analyze.folder`
-(SURVEY.md §8f rows 1-2).  The post-analysis members of the reference class (video,
-spectrogram, block_amplitude, polar warps, ...) are out of scope.
+(SURVEY.md §8f rows 1-2), and the temporal post-analysis of the map stack
+(`block_split`, `block_amplitude`, `spectrogram`; §8f row 4) on the device.  The other
+post-analysis members of the reference class (video, polar warps, ...) are out of scope
+(DESIGN.md §8).
 
 `analyze.folder` keeps the reference's contract -- directory of `.tif` frames ->
 `maps/{name}_map.npy` (float32) + `maps/calibration_factor.npy`, resumable at file
@@ -204,3 +206,145 @@ class analyze:
                 buf.free()
         if err:
             raise err[0]
+
+    # ---- temporal post-analysis of the map stack
+    @staticmethod
+    def _map_files(map_folder, t_limit=None):
+        files = sorted(f for f in os.listdir(map_folder) if f.endswith("_map.npy") and "calibration_factor" not in f)
+        return files[:t_limit]
+
+    @classmethod
+    def _block_stack(cls, map_folder, t_limit=None, num_blocks=64, block_index=0, zero=0):
+        """float32 [T, size, size] block of every map (memory-mapped reads of just the
+        block), NaN where the first map is 0 (analyze.py:386-417; `- zero` as
+        analyze.py:557-567)."""
+        files = cls._map_files(map_folder, t_limit)
+        first = np.load(os.path.join(map_folder, files[0]), mmap_mode="r")
+        H, W = first.shape
+        per_row = int(np.sqrt(num_blocks))
+        n = H // per_row
+        i0, j0 = (block_index // per_row) * n, (block_index % per_row) * n
+        valid = np.asarray(first[i0:i0 + n, j0:j0 + n]) != 0
+        z = zero
+        if np.ndim(zero) == 2:
+            z = np.asarray(zero)[i0:i0 + n, j0:j0 + n]
+        out = np.empty((len(files), n, n), np.float32)
+        for t, f in enumerate(files):
+            m = np.load(os.path.join(map_folder, f), mmap_mode="r")[i0:i0 + n, j0:j0 + n]
+            out[t] = np.where(valid, np.asarray(m) - z, np.nan)
+        return out
+
+    @classmethod
+    def block_split(cls, map_folder, t_limit=None, num_blocks=64, block_index=0):
+        """[size, size, T] float32 series of one spatial block (analyze.py:364-417)."""
+        return np.transpose(cls._block_stack(map_folder, t_limit, num_blocks, block_index), (1, 2, 0))
+
+    @classmethod
+    def block_amplitude(cls, map_folder, f0=None, tasa=500, mode=1, num_blocks=64, block_index=0, zero=0):
+        """(harmonics, amps, phases, f0) of every pixel of a block (analyze.py:543-587).
+
+        The temporal DFT runs on the device in f64 (fcd_temporal_spectrum for the
+        nanmean |spectrum| that locates f0, fcd_temporal_bins for the harmonics); the
+        reference's quirks are kept: amps / phases have mode + 1 columns of which
+        the first `mode` are filled, and no spectral peak returns five values."""
+        from scipy.signal import find_peaks
+        stack = cls._block_stack(map_folder, None, num_blocks, block_index, zero)
+        N, ny, nx = stack.shape
+        eng = _lib.temporal_engine()
+        freqs = np.fft.fftfreq(N, d=1 / tasa)
+        freqs = freqs[freqs >= 0]
+        if f0 is None:
+            tot, cnt = eng.temporal_spectrum(stack, len(freqs))
+            with np.errstate(invalid="ignore", divide="ignore"):
+                mean_spectrum = tot / cnt
+            peaks, _ = find_peaks(mean_spectrum)
+            if len(peaks) == 0:
+                return (np.zeros(mode), np.full((ny, nx, mode), None, dtype=object),
+                        np.full((ny, nx, mode), None, dtype=object), None, None)
+            f0 = freqs[peaks[np.argmax(mean_spectrum[peaks])]]
+        harmonics = [f0 * n for n in range(0, mode)]
+        idx = [int(np.argmin(np.abs(freqs - f))) for f in harmonics]
+        X = eng.temporal_bins(stack, idx)
+        amps = np.zeros((ny, nx, mode + 1))
+        phases = np.zeros((ny, nx, mode + 1))
+        amps[:, :, :mode] = np.abs(X) / N
+        amps[:, :, 1:mode] *= 2
+        phases[:, :, :mode] = np.angle(X)
+        return harmonics, amps, phases, f0
+
+    @staticmethod
+    def _spectro_params(T, fs, kwargs):
+        """scipy.signal.spectrogram's defaults: window ('tukey', .25), nperseg 256
+        (clipped to the series length), noverlap nperseg // 8."""
+        from scipy.signal import get_window
+        window = kwargs.get("window", ("tukey", 0.25))
+        nperseg = kwargs.get("nperseg")
+        if isinstance(window, (str, tuple)):
+            nperseg = 256 if nperseg is None else int(nperseg)
+            if nperseg > T:
+                nperseg = T
+            win = get_window(window, nperseg)
+        else:
+            win = np.asarray(window, np.float64)
+            if nperseg is None:
+                nperseg = len(win)
+            if len(win) != nperseg:
+                raise ValueError("value specified for nperseg is different from length of window")
+        noverlap = kwargs.get("noverlap")
+        noverlap = nperseg // 8 if noverlap is None else int(noverlap)
+        if noverlap >= nperseg:
+            raise ValueError("noverlap must be less than nperseg.")
+        f = np.fft.rfftfreq(nperseg, 1 / fs)
+        t = np.arange(nperseg / 2, T - nperseg / 2 + 1, nperseg - noverlap) / float(fs)
+        return nperseg, noverlap, np.asarray(win, np.float64), f, t
+
+    @classmethod
+    def spectrogram(cls, map_folder=None, array=None, fs=125, show=False, **kwargs):
+        """analyze.spectrogram (analyze.py:419-531): (t, f, Sxx) of one series, or
+        (t, f, Sxx_all [ny, nx, nf, nt], Sxx_avg) of every pixel of a block, one-sided
+        PSD (scipy.signal.spectrogram's density scaling, constant detrend) computed on
+        the device in f64.  Block pixels with NaN gaps are filled by np.interp first,
+        all-NaN pixels give NaN, as in the reference."""
+        block_kw = {k: kwargs[k] for k in ("t_limit", "num_blocks", "block_index") if k in kwargs}
+        eng = _lib.temporal_engine()
+        if map_folder is None:
+            if array is None:
+                raise ValueError("Any map_folder or array is needed")
+            x = np.asarray(array)
+            nperseg, noverlap, win, f, t = cls._spectro_params(len(x), fs, kwargs)
+            S = eng.spectrogram(x.astype(np.float32).reshape(-1, 1, 1), nperseg, noverlap, win, fs)[0, 0]
+            if show:
+                cls._show_spectrogram(t, f, S, "Spectrogram of some point")
+            return t, f, S
+        if array is not None:
+            raise ValueError("map_folder or array is needed, not both")
+        stack = cls._block_stack(map_folder, block_kw.get("t_limit"), block_kw.get("num_blocks", 64),
+                                 block_kw.get("block_index", 0))
+        N, ny, nx = stack.shape
+        bad = np.isnan(stack)
+        part = bad.any(axis=0) & ~bad.all(axis=0)
+        if part.any():  # NaN gaps inside a pixel's series: linear fill (analyze.py:512-517)
+            ar = np.arange(N)
+            for iy, ix in zip(*np.nonzero(part)):
+                ts = stack[:, iy, ix]
+                ok = ~np.isnan(ts)
+                stack[:, iy, ix] = np.interp(ar, ar[ok], ts[ok])
+        nperseg, noverlap, win, f, t = cls._spectro_params(N, fs, kwargs)
+        S = eng.spectrogram(stack, nperseg, noverlap, win, fs)
+        with np.errstate(invalid="ignore"):
+            avg = np.nanmean(S, axis=(0, 1))
+        if show:
+            cls._show_spectrogram(t, f, avg, "Average Spectrogram over block")
+        return t, f, S, avg
+
+    @staticmethod
+    def _show_spectrogram(t, f, S, title):
+        import matplotlib.pyplot as plt
+        plt.figure(figsize=(8, 4))
+        plt.pcolormesh(t, f, np.log10(S), shading="gouraud")
+        plt.ylabel("Frequency [Hz]")
+        plt.xlabel("Time [sec]")
+        plt.title(title)
+        plt.colorbar()
+        plt.tight_layout()
+        plt.show()

@@ -34,6 +34,7 @@ EXPORTED = (
     "fcd_set_reference", "fcd_get_carriers", "fcd_process", "fcd_phases_from_spectrum",
     "fcd_unwrap", "fcd_integrate", "fcd_fft2", "fcd_profile", "fcd_stage_times",
     "fcd_process_raw", "fcd_frame_bytes", "fcd_host_alloc", "fcd_host_free", "fcd_find_peaks",
+    "fcd_temporal_spectrum", "fcd_temporal_bins", "fcd_spectrogram",
 )
 
 
@@ -92,6 +93,9 @@ def load_library(path=None):
             "fcd_host_alloc": ([ctypes.c_int64, ctypes.POINTER(vp)], i32),
             "fcd_host_free": ([vp], i32),
             "fcd_find_peaks": ([vp, vp, i32, i32, f64, ctypes.POINTER(FcdRefInfo)], i32),
+            "fcd_temporal_spectrum": ([vp, vp] + [i32] * 9 + [vp, vp], i32),
+            "fcd_temporal_bins": ([vp, vp] + [i32] * 8 + [vp, i32, vp, vp], i32),
+            "fcd_spectrogram": ([vp, vp] + [i32] * 10 + [vp, f64, vp, vp], i32),
         }
         for name, (args, res) in sig.items():
             fn = getattr(lib, name)
@@ -285,6 +289,49 @@ class Engine:
         return out[0] if squeeze else out
 
 
+    # ---- temporal analysis of a [T][rows][cols] float32 map stack
+    @staticmethod
+    def _stack(stack, block):
+        st = np.asarray(stack)
+        if st.ndim != 3:
+            raise ValueError("stack must be [T, rows, cols]")
+        if st.dtype != np.float32 or not st.flags.c_contiguous:
+            st = np.ascontiguousarray(st, dtype=np.float32)
+        T, rows, cols = st.shape
+        r0, c0, bh, bw = block if block is not None else (0, 0, rows, cols)
+        return st, (int(T), int(rows), int(cols), int(r0), int(c0), int(bh), int(bw))
+
+    def temporal_spectrum(self, stack, nf, block=None):
+        """(sum of |X(f)| over non-NaN pixels, their count) for bins f < nf of the
+        temporal DFT of every pixel of the block (r0, c0, bh, bw)."""
+        st, dims = self._stack(stack, block)
+        sc = np.empty((int(nf), 2), np.float64)
+        _check(self._lib.fcd_temporal_spectrum(self._h, st.ctypes.data, *dims, FCD_HOST_PTRS, int(nf), sc.ctypes.data,
+                                               None))
+        return sc[:, 0], sc[:, 1]
+
+    def temporal_bins(self, stack, bins, block=None):
+        """complex128 [bh, bw, len(bins)]: the temporal DFT of every pixel at `bins`."""
+        st, dims = self._stack(stack, block)
+        b = np.ascontiguousarray(bins, dtype=np.int32)
+        out = np.empty((dims[5], dims[6], len(b)), np.complex128)
+        _check(self._lib.fcd_temporal_bins(self._h, st.ctypes.data, *dims, FCD_HOST_PTRS, b.ctypes.data, len(b),
+                                           out.ctypes.data, None))
+        return out
+
+    def spectrogram(self, stack, nperseg, noverlap, window, fs, block=None):
+        """float64 [bh, bw, nperseg // 2 + 1, nseg] one-sided PSD of every pixel's series."""
+        st, dims = self._stack(stack, block)
+        w = np.ascontiguousarray(window, dtype=np.float64)
+        if w.shape != (int(nperseg),):
+            raise ValueError("window length must equal nperseg")
+        nseg = (dims[0] - nperseg) // (nperseg - noverlap) + 1
+        out = np.empty((dims[5], dims[6], nperseg // 2 + 1, max(nseg, 0)), np.float64)
+        _check(self._lib.fcd_spectrogram(self._h, st.ctypes.data, *dims, FCD_HOST_PTRS, int(nperseg), int(noverlap),
+                                         w.ctypes.data, float(fs), out.ctypes.data, None))
+        return out
+
+
 _engines = {}
 _engines_lock = threading.Lock()
 
@@ -298,6 +345,12 @@ def engine_for(shape, device=None):
             e = Engine(shape, device)
             _engines[key] = e
         return e
+
+
+def temporal_engine(device=None):
+    """The engine context the temporal-analysis calls run on (any frame shape will
+    do: they take the stack's own shape)."""
+    return engine_for((64, 64), device)
 
 
 class PinnedBuffer:
