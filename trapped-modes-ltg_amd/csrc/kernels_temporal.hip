@@ -25,6 +25,7 @@ namespace {
 constexpr int TD_THREADS = 256;  // pixels per workgroup
 constexpr int TD_FT = 16;        // frequencies per lane
 constexpr int TD_LDS_TAB = 8192;  // table entries held in LDS (128 KiB of double2)
+constexpr int TD_BATCH = 8;       // samples per load batch
 
 // Pixel p of the block -> its element offset in frame 0.
 __device__ __forceinline__ long pix_off(int p, int bw, long row_pitch) { return (long)(p / bw) * row_pitch + p % bw; }
@@ -51,6 +52,8 @@ __global__ __launch_bounds__(TD_THREADS) void k_tdft(const float* __restrict__ s
     }
     const int p = blockIdx.x * TD_THREADS + threadIdx.x;
     const bool live = p < P;
+    // lanes past the block read pixel 0 (loads stay unconditional, so a batch of
+    // them is in flight at once); their sums are never used
     const float* xs = stack + (live ? pix_off(p, bw, row_pitch) : 0);
     int fk[TD_FT], idx[TD_FT];
     double re[TD_FT], im[TD_FT];
@@ -62,9 +65,7 @@ __global__ __launch_bounds__(TD_THREADS) void k_tdft(const float* __restrict__ s
         re[k] = 0.0;
         im[k] = 0.0;
     }
-#pragma unroll 2
-    for (int t = 0; t < T; ++t) {
-        const double x = live ? (double)__builtin_nontemporal_load(xs + (long)t * frame_pitch) : 0.0;
+    auto step = [&](double x) {
 #pragma unroll
         for (int k = 0; k < TD_FT; ++k) {
             const double2 w = tb[idx[k]];  // wave-uniform index: an LDS broadcast
@@ -73,7 +74,18 @@ __global__ __launch_bounds__(TD_THREADS) void k_tdft(const float* __restrict__ s
             idx[k] += fk[k];
             idx[k] -= idx[k] >= T ? T : 0;
         }
+    };
+    // TD_BATCH samples loaded before any is used: that many loads in flight per
+    // wave (few-bin calls have little arithmetic per sample to hide the latency)
+    int t = 0;
+    for (; t + TD_BATCH <= T; t += TD_BATCH) {
+        float xb[TD_BATCH];
+#pragma unroll
+        for (int u = 0; u < TD_BATCH; ++u) xb[u] = __builtin_nontemporal_load(xs + (long)(t + u) * frame_pitch);
+#pragma unroll
+        for (int u = 0; u < TD_BATCH; ++u) step((double)xb[u]);
     }
+    for (; t < T; ++t) step((double)__builtin_nontemporal_load(xs + (long)t * frame_pitch));
     if constexpr (REDUCE) {
         __shared__ double red[TD_THREADS / 64][TD_FT][2];
         const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -144,9 +156,7 @@ __global__ __launch_bounds__(TD_THREADS) void k_spectro(const float* __restrict_
         im[k] = 0.0;
     }
     double sum = 0.0;
-#pragma unroll 2
-    for (int n = 0; n < nperseg; ++n) {
-        const double x = live ? (double)xs[(long)n * frame_pitch] : 0.0;
+    auto sample = [&](int n, double x) {
         sum += x;
         const double xw = x * wl[n];
 #pragma unroll
@@ -157,7 +167,16 @@ __global__ __launch_bounds__(TD_THREADS) void k_spectro(const float* __restrict_
             idx[k] += fk[k];
             idx[k] -= idx[k] >= nperseg ? nperseg : 0;
         }
+    };
+    int n = 0;  // unconditional batched loads, as k_tdft
+    for (; n + TD_BATCH <= nperseg; n += TD_BATCH) {
+        float xb[TD_BATCH];
+#pragma unroll
+        for (int u = 0; u < TD_BATCH; ++u) xb[u] = xs[(long)(n + u) * frame_pitch];
+#pragma unroll
+        for (int u = 0; u < TD_BATCH; ++u) sample(n + u, (double)xb[u]);
     }
+    for (; n < nperseg; ++n) sample(n, (double)xs[(long)n * frame_pitch]);
     if (!live) return;
     const double mean = sum / (double)nperseg;
 #pragma unroll
