@@ -243,7 +243,9 @@ def main():
         "config": {"workload": f"{ {1024: 'c2', 2048: 'c3', 4096: 'c5'}.get(n, 'custom')}: {n}x{n} frames, {B} per GPU per step, full compute_height_map pipeline "
                                f"(demod + unwrap + integration), reference state cached",
                    "frame": n, "batch_per_gpu": B, "global_batch": B * world,
-                   "parallelism": f"frame-sharded x{world}, no collective in the compute"},
+                   "parallelism": f"frame-sharded x{world}, no collective in the compute",
+                   # each step's chunk runs as this many concurrent halves (engine FCD_STREAMS)
+                   "streams_per_chunk": 2 if int(os.environ.get("FCD_STREAMS", "2")) >= 2 else 1},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic_launch,

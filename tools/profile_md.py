@@ -2,7 +2,7 @@
 --kernel-trace --stats summary (engine kernels), the bench line of the same
 (profiled) command, the unprofiled bench line, and the PMC traffic table.
 
-    python tools/profile_md.py gpurun_out/<tag> profiles/<name>.md
+    python tools/profile_md.py gpurun_out/<tag> profiles/<name>.md [streams per chunk]
 """
 import csv
 import json
@@ -31,15 +31,38 @@ lines = [f"# {os.path.basename(dst)[:-3]} — rocprofv3 --kernel-trace --stats (
 # per-kernel averages over the bench's own launches only (the largest grid of each
 # kernel in the trace: full-chunk launch groups), so the one-frame reference-setup
 # launches of the same kernels do not dilute the figures
-trace = list(csv.DictReader(open(os.path.join(src, "prof", "run_kernel_trace.csv"))))
+trace = sorted((t for t in csv.DictReader(open(os.path.join(src, "prof", "run_kernel_trace.csv")))
+                if "fcdk::" in short(t["Kernel_Name"])), key=lambda t: int(t["Start_Timestamp"]))
+dur = [(int(t["End_Timestamp"]) - int(t["Start_Timestamp"])) / 1e3 for t in trace]
+names = [short(t["Kernel_Name"]) for t in trace]
+# The roofline pass (single stream, whole chunks): each k_band_phase<..., false> launch
+# with the k_demod_cols / k_demod_rows launches right before it.  Every other launch
+# belongs to the headline path, whose chunk runs as `streams` concurrent parts.
+groups, in_group = [], set()
+for i, k in enumerate(names):
+    if k == "fcdk::k_band_phase<1024, 128, false>":
+        j_cols = max(j for j in range(i) if names[j] == "fcdk::k_demod_cols<1024>")
+        j_rows = max(j for j in range(j_cols) if names[j] == "fcdk::k_demod_rows<1024>")
+        groups.append((dur[j_rows], dur[j_cols], dur[i]))
+        in_group.update((j_rows, j_cols, i))
+streams = int(sys.argv[3]) if len(sys.argv) > 3 else prof_bench["config"].get("streams_per_chunk", 1)
+part = chunk / streams
+# headline launches: the first (warmup + steps) x streams of each kernel in time order
+# (the profiled passes that follow run single-stream whole chunks)
+n_head = (prof_bench["warmup"] + prof_bench["steps"]) * streams
 full = {}
-for t in trace:
-    k = short(t["Kernel_Name"])
-    if "fcdk::" not in k:
+for i, t in enumerate(trace):
+    if i in in_group:
         continue
     g = int(t["Grid_Size_X"]) * int(t["Grid_Size_Y"]) * int(t["Grid_Size_Z"])
-    full.setdefault(k, {}).setdefault(g, []).append((int(t["End_Timestamp"]) - int(t["Start_Timestamp"])) / 1e3)
-demod = 0.0
+    full.setdefault(names[i], {}).setdefault(g, []).append(dur[i])
+for k in list(full):
+    g = max(full[k])
+    if len(full[k][g]) < n_head:
+        del full[k]  # reference setup / unfused-pass kernels
+    else:
+        full[k] = {g: full[k][g][:n_head]}
+demod = sum(sum(g) for g in groups) / max(len(groups), 1)
 for r in rows:
     if "fcdk::" not in r["Name"]:
         continue
@@ -47,18 +70,21 @@ for r in rows:
     k = short(r["Name"])
     lines.append(f"| `{k}` | {r['Calls']} | {avg:.2f} | {float(r['MinNs']) / 1e3:.2f} | "
                  f"{float(r['MaxNs']) / 1e3:.2f} | {avg / chunk:.3f} |")
-lines += ["", f"Full-chunk launches only ({chunk:g} frames each; from `run_kernel_trace.csv`, largest grid per kernel):", "",
+lines += ["", f"Headline-path launches ({part:g} frames each: every {chunk:g}-frame chunk runs as {streams} concurrent "
+          f"part(s) on separate streams, so with {streams} > 1 their durations overlap and the per-frame figures do not "
+          "add up to the wall time; from `run_kernel_trace.csv`, largest grid per kernel, the first (warmup + steps) x streams launches of each: the roofline pass "
+          "and the profiled passes excluded):", "",
           "| kernel | launches | avg us | us/frame |", "|---|---|---|---|"]
-for k, by_grid in sorted(full.items(), key=lambda kv: -max(kv[1]) ):
+for k, by_grid in sorted(full.items(), key=lambda kv: -max(kv[1])):
     g = max(by_grid)
     d = by_grid[g]
-    if len(by_grid) == 1 and len(d) < 4:
-        continue  # reference-setup kernels (one launch per set_reference)
     a = sum(d) / len(d)
-    if any(x in k for x in ("k_demod_rows", "k_demod_cols", "k_band_phase<1024, 128, false>")):
-        demod += a
-    lines.append(f"| `{k}` | {len(d)} | {a:.2f} | {a / chunk:.3f} |")
-lines += ["", f"Demod launch group (k_demod_rows + k_demod_cols + k_band_phase) from the full-chunk launches above: **{demod:.1f} us per "
+    lines.append(f"| `{k}` | {len(d)} | {a:.2f} | {a / part:.3f} |")
+lines += ["", f"Roofline pass (single stream, {chunk:g}-frame launch groups, {len(groups)} groups): k_demod_rows "
+          f"{sum(g[0] for g in groups) / max(len(groups), 1):.1f} + k_demod_cols "
+          f"{sum(g[1] for g in groups) / max(len(groups), 1):.1f} + k_band_phase "
+          f"{sum(g[2] for g in groups) / max(len(groups), 1):.1f} us.", "",
+          f"Demod launch group (k_demod_rows + k_demod_cols + k_band_phase) from the roofline-pass launches: **{demod:.1f} us per "
           f"launch**; the bench's HIP-event figure for the same group in this run: "
           f"**{prof_bench['roofline']['us_per_launch']} us per launch**.", "",
           "Bench line of the profiled command:", "", "```json", json.dumps(prof_bench), "```", "",
