@@ -211,25 +211,31 @@ def test_host_pipeline_follows_reference_change(df):
     assert rel_l2(b, want_b) < 1e-6
 
 
-def test_two_stream_split_equals_one_stream(df, monkeypatch):
+@pytest.mark.parametrize("case", ["real_1024_fused", "synthetic_512_unfused"])
+def test_two_stream_split_equals_one_stream(df, monkeypatch, case):
     """Device-pointer chunks run as two halves on two streams (FCD_STREAMS=2, the
-    default): heights bit-identical to the one-stream chain, with the exact MST pass
-    for the frames with residues running after the join (real frames, 7..1611
-    residues) and an odd frame count."""
+    default): heights bit-identical to the one-stream chain and to the host path, for
+    the fused 1024-wide chain (real frames, 7..1611 residues: the exact MST pass runs
+    after the join), with an odd frame count; the unfused chain (512^2) is not split
+    and must give the same heights under either setting."""
     import torch
-    from pyfcd import _lib
-    ref = df["ref_u16"].astype(np.float32)
-    frames = np.concatenate([df["frames_u16"], df["frames_u16"][:2]]).astype(np.float32)  # 5 frames
+    from bench_data import make_frames_numpy
+    if case.startswith("real"):
+        ref, sq = df["ref_u16"].astype(np.float32), float(df["square_size"])
+        frames = np.concatenate([df["frames_u16"], df["frames_u16"][:2]]).astype(np.float32)  # 5 frames
+    else:
+        ref, frames = make_frames_numpy(512, 5, seed=8, rotate_deg=5.0)
+        sq = 0.001
     dev = torch.device("cuda", 0)
     fd = torch.from_numpy(frames).to(dev)
     out = {}
     for ns in ("1", "2"):
         monkeypatch.setenv("FCD_STREAMS", ns)
-        eng = _engine(ref, float(df["square_size"]))
+        eng = _engine(ref, sq)
         hd = torch.empty_like(fd)
         eng.process_device(fd.data_ptr(), len(frames), 1.0, True, hd.data_ptr())
         torch.cuda.synchronize()
         out[ns] = hd.cpu().numpy()
     assert np.array_equal(out["1"], out["2"])
-    want, _, _ = _engine(ref, float(df["square_size"])).process(frames, 1.0, unwrap=True, want_phases=False)
+    want, _, _ = _engine(ref, sq).process(frames, 1.0, unwrap=True, want_phases=False)
     assert np.array_equal(out["2"], want)

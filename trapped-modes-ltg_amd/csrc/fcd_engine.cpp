@@ -671,17 +671,20 @@ fcdk::DemodTables demod_tables(fcd_ctx* c) {
 }
 
 // Fast path for nb frames (device pointer): band-pruned demod -> wrapped (c->wrapped).
-void fast_demod(fcd_ctx* c, const float* frames, int nb, hipStream_t s) {
+// fo: first workspace frame (as first_pass_chunk).
+void fast_demod(fcd_ctx* c, const float* frames, int nb, hipStream_t s, int fo = 0) {
     const fcdk::DemodTables T = demod_tables(c);
-    fcdk::demod_rows(c->W, frames, c->H, nb, T, c->Xb.as<float2>(), c->twp_row.as<float2>(), s);
-    fcdk::demod_cols(c->H, c->Xb.as<float2>(), nb, T, c->Ab.as<float2>(), c->NCA, c->twp_col.as<float2>(), s);
+    const long H = c->H;
+    float2* Xb = c->Xb.as<float2>() + fo * H * c->NC;
+    float2* Ab = c->Ab.as<float2>() + fo * 2 * H * c->NCA;
+    float* wrapped = c->wrapped.as<float>() + fo * 2 * c->hw();
+    fcdk::demod_rows(c->W, frames, c->H, nb, T, Xb, c->twp_row.as<float2>(), s);
+    fcdk::demod_cols(c->H, Xb, nb, T, Ab, c->NCA, c->twp_col.as<float2>(), s);
     if (c->band_B)
-        fcdk::band_phase(c->W, c->band_B, false, c->Ab.as<float2>(), c->H, nb, c->NCA, c->NCc[0], c->NCc[1],
-                         c->theta_p.as<float>(), c->wrapped.as<float>(), c->band_pre.as<float2>(),
-                         c->band_ptw.as<float2>(), s);
+        fcdk::band_phase(c->W, c->band_B, false, Ab, c->H, nb, c->NCA, c->NCc[0], c->NCc[1], c->theta_p.as<float>(),
+                         wrapped, c->band_pre.as<float2>(), c->band_ptw.as<float2>(), s);
     else
-        fcdk::demod_phase(c->W, c->Ab.as<float2>(), c->H, nb, c->NCA, T, c->theta.as<float>(), c->wrapped.as<float>(),
-                          c->twp_row.as<float2>(), s);
+        fcdk::demod_phase(c->W, Ab, c->H, nb, c->NCA, T, c->theta.as<float>(), wrapped, c->twp_row.as<float2>(), s);
 }
 
 // Reference angle of the band-pruned inverse: the same band pipeline run on
@@ -957,15 +960,20 @@ void first_pass_chunk(fcd_ctx* c, const float* fr, int nb, bool unwrap, bool fus
         fcdk::int_cols(c->H, Zt, c->W, nb, coef, Ht, c->twp_col.as<float2>(), s, unwrap ? colk : nullptr);
         fcdk::int_c2r(c->W, Ht, c->H, nb, hdst, c->twp_row.as<float2>(), s);
     } else {
+        const long H = c->H, W = c->W;
+        float* wrapped = c->wrapped.as<float>() + fo * 2 * H * W;
+        int* colk = c->colk.as<int>() + fo * 2 * H;
+        float2* Zt = c->Zt.as<float2>() + fo * H * W;
+        float2* Ht = c->Ht.as<float2>() + fo * H * (W / 2 + 1);
         if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
-        fast_demod(c, fr, nb, s);
+        fast_demod(c, fr, nb, s, fo);
         if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
-        if (unwrap) fcdk::unwrap_colk(c->wrapped.as<float>(), 2 * nb, c->H, c->W, c->colk.as<int>(), s);
+        if (unwrap) fcdk::unwrap_colk(wrapped, 2 * nb, c->H, c->W, colk, s);
         if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
-        fcdk::int_rows(c->W, unwrap ? 1 : 0, c->wrapped.as<float>(), c->colk.as<int>(), nullptr, kdst, res, c->H, nb,
-                       c->Zt.as<float2>(), c->twp_row.as<float2>(), s);
-        fcdk::int_cols(c->H, c->Zt.as<float2>(), c->W, nb, coef, c->Ht.as<float2>(), c->twp_col.as<float2>(), s);
-        fcdk::int_c2r(c->W, c->Ht.as<float2>(), c->H, nb, hdst, c->twp_row.as<float2>(), s);
+        fcdk::int_rows(c->W, unwrap ? 1 : 0, wrapped, colk, nullptr, kdst, res, c->H, nb, Zt, c->twp_row.as<float2>(),
+                       s);
+        fcdk::int_cols(c->H, Zt, c->W, nb, coef, Ht, c->twp_col.as<float2>(), s);
+        fcdk::int_c2r(c->W, Ht, c->H, nb, hdst, c->twp_row.as<float2>(), s);
     }
     if (c->profiling) {
         HIPCHK(hipEventRecord(c->next_event(), s));
@@ -1177,6 +1185,8 @@ int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int f
             float* hdst = (dev && height_out) ? height_out + (size_t)f0 * hw : c->out_h.as<float>();
             int32_t* kdst = k_out && unwrap ? (dev ? k_out + (size_t)f0 * 2 * hw : c->fk.as<int32_t>()) : nullptr;
             int* rs = res ? res + (size_t)f0 * 2 : nullptr;
+            // the fused (1024-wide) chain only: split, the unfused chain at 2048^2 / 4096^2
+            // measured 1-2 % slower (r01br), though its workspace offsets allow it
             const int nsplit = fused && !c->profiling && nb >= 2 ? c->nstreams : 1;
             if (nsplit == 2) {
                 // two halves of the chunk on two streams: kernels bound by different
@@ -1192,8 +1202,8 @@ int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int f
                 // second half after the first half's demod kernels instead: no gain)
                 HIPCHK(hipEventRecord(c->ev_fork, s));
                 HIPCHK(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
-                first_pass_chunk(c, fr, na, unwrap != 0, true, rs, hdst, nullptr, coef, s, 0);
-                first_pass_chunk(c, fr + (size_t)na * hw, nb2, unwrap != 0, true, rs ? rs + 2 * na : nullptr,
+                first_pass_chunk(c, fr, na, unwrap != 0, fused, rs, hdst, nullptr, coef, s, 0);
+                first_pass_chunk(c, fr + (size_t)na * hw, nb2, unwrap != 0, fused, rs ? rs + 2 * na : nullptr,
                                  hdst + (size_t)na * hw, nullptr, coef, c->aux, na);
                 HIPCHK(hipEventRecord(c->ev_join, c->aux));
                 HIPCHK(hipStreamWaitEvent(s, c->ev_join, 0));
