@@ -222,7 +222,7 @@ struct fcd_ctx {
     DevBuf cand_idx, cand_val;
     DevBuf fix_raw;  // raw samples of the frames redone by the exact pass
     // temporal analysis: staged block, exp table, bins, partial sums, output, window
-    DevBuf t_stage, t_tab, t_bins, t_part, t_out, t_win, t_wsum;
+    DevBuf t_stage, t_tab, t_bins, t_part, t_out, t_win, t_wsum, t_slices;
     HostPipe pipe;
     // MST workspace
     DevBuf mst_comp, mst_off, mst_rel, mst_cw, mst_ce, mst_bw, mst_be, mst_link, mst_hooks, mst_ids;
@@ -1482,7 +1482,7 @@ FCD_API int fcd_temporal_spectrum(fcd_ctx* c, const float* stack, int T, int row
         const int P = bh * bw, tiles = fcdk::temporal_dft_tiles(P);
         c->t_part.ensure((size_t)tiles * nf * 2 * sizeof(double));
         fcdk::temporal_dft(v.p, v.frame_pitch, v.row_pitch, bw, P, T, c->t_tab.as<double2>(), nullptr, nf, nullptr,
-                           c->t_part.as<double>(), s);
+                           c->t_part.as<double>(), nullptr, s);
         std::vector<double> part((size_t)tiles * nf * 2);
         HIPCHK(hipMemcpyAsync(part.data(), c->t_part.p, part.size() * sizeof(double), hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
@@ -1517,8 +1517,10 @@ FCD_API int fcd_temporal_bins(fcd_ctx* c, const float* stack, int T, int rows, i
             c->t_out.ensure((size_t)P * nbins * sizeof(double2));
             out = c->t_out.as<double2>();
         }
+        const int nz = fcdk::temporal_bins_slices(P, nbins, T);
+        if (nz > 1) c->t_slices.ensure((size_t)nz * P * nbins * sizeof(double2));
         fcdk::temporal_dft(v.p, v.frame_pitch, v.row_pitch, bw, P, T, c->t_tab.as<double2>(), c->t_bins.as<int>(),
-                           nbins, out, nullptr, s);
+                           nbins, out, nullptr, nz > 1 ? c->t_slices.as<double2>() : nullptr, s);
         if (!dev) {
             HIPCHK(hipMemcpyAsync(x_out, out, (size_t)P * nbins * sizeof(double2), hipMemcpyDeviceToHost, s));
             HIPCHK(hipStreamSynchronize(s));

@@ -134,8 +134,9 @@ void compose_phase(const float* w, const int32_t* k, float* out, long n, hipStre
 
 // temporal analysis of a map stack (kernels_temporal.hip)
 void temporal_dft(const float* stack, long frame_pitch, long row_pitch, int bw, int P, int T, const double2* tab,
-                  const int* freqs, int nf, double2* out, double* partial, hipStream_t s);
+                  const int* freqs, int nf, double2* out, double* partial, double2* slices, hipStream_t s);
 int temporal_dft_tiles(int P);
+int temporal_bins_slices(int P, int nf, int T);  // slices[slices][P][nf] workspace of a bins call
 int spectro_max_nperseg();
 void spectrogram(const float* stack, long frame_pitch, long row_pitch, int bw, int P, int nperseg, int step, int nseg,
                  const double* win, const double2* tab, const double2* wsum, int nf, double scale, double* out,

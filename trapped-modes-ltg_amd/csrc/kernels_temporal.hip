@@ -14,6 +14,7 @@
 // (f t) mod T, kept incrementally per frequency (exact argument reduction).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <stdexcept>
 #include <string>
 
@@ -45,8 +46,10 @@ template <bool REDUCE, bool LDS>
 __global__ __launch_bounds__(TD_THREADS) void k_tdft(const float* __restrict__ stack, long frame_pitch, long row_pitch,
                                                      int bw, int P, int T, const double2* __restrict__ tab,
                                                      const int* __restrict__ freqs, int nf, double2* __restrict__ out,
-                                                     double* __restrict__ partial) {
+                                                     double* __restrict__ partial, int tchunk) {
     constexpr int FT = TD_FT_DFT, PX = TD_PX;
+    // samples [t0, t1) of the series (blockIdx.z-th slice; one slice in REDUCE mode)
+    const int t0 = blockIdx.z * tchunk, t1 = min(T, t0 + tchunk);
     extern __shared__ double2 tab_lds[];
     const double2* tb = tab;
     if constexpr (LDS) {
@@ -72,7 +75,7 @@ __global__ __launch_bounds__(TD_THREADS) void k_tdft(const float* __restrict__ s
     for (int k = 0; k < FT; ++k) {
         const int j = blockIdx.y * FT + k;
         fk[k] = j < nf ? (freqs ? freqs[j] : j) : 0;
-        idx[k] = 0;
+        idx[k] = (int)(((long)fk[k] * t0) % T);
 #pragma unroll
         for (int u = 0; u < PX; ++u) re[u][k] = im[u][k] = 0.0;
     }
@@ -91,8 +94,8 @@ __global__ __launch_bounds__(TD_THREADS) void k_tdft(const float* __restrict__ s
     };
     // TD_BATCH samples loaded before any is used: that many loads in flight per
     // pixel and wave (few-bin calls have little arithmetic per sample to hide the latency)
-    int t = 0;
-    for (; t + TD_BATCH <= T; t += TD_BATCH) {
+    int t = t0;
+    for (; t + TD_BATCH <= t1; t += TD_BATCH) {
         float xb[TD_BATCH][PX];
 #pragma unroll
         for (int v = 0; v < TD_BATCH; ++v)
@@ -101,7 +104,7 @@ __global__ __launch_bounds__(TD_THREADS) void k_tdft(const float* __restrict__ s
 #pragma unroll
         for (int v = 0; v < TD_BATCH; ++v) step(xb[v]);
     }
-    for (; t < T; ++t) {
+    for (; t < t1; ++t) {
         float x1[PX];
 #pragma unroll
         for (int u = 0; u < PX; ++u) x1[u] = __builtin_nontemporal_load(xs[u] + (long)t * frame_pitch);
@@ -145,10 +148,24 @@ __global__ __launch_bounds__(TD_THREADS) void k_tdft(const float* __restrict__ s
 #pragma unroll
             for (int k = 0; k < FT; ++k) {
                 const int j = blockIdx.y * FT + k;
-                if (j < nf) out[(long)(p0 + u) * nf + j] = make_double2(re[u][k], im[u][k]);
+                if (j < nf) out[((long)blockIdx.z * P + p0 + u) * nf + j] = make_double2(re[u][k], im[u][k]);
             }
         }
     }
+}
+
+// out[i] = sum over the nz time slices of parts[z][i], in slice order (deterministic).
+__global__ __launch_bounds__(TD_THREADS) void k_tdft_sum(const double2* __restrict__ parts, int nz, long n,
+                                                         double2* __restrict__ out) {
+    const long i = (long)blockIdx.x * TD_THREADS + threadIdx.x;
+    if (i >= n) return;
+    double2 a = parts[i];
+    for (int z = 1; z < nz; ++z) {
+        const double2 b = parts[(long)z * n + i];
+        a.x += b.x;
+        a.y += b.y;
+    }
+    out[i] = a;
 }
 
 // One-sided PSD of every segment of every pixel (scipy.signal.spectrogram with
@@ -230,29 +247,46 @@ void check_launch(const char* what) {
 
 }  // namespace
 
+// Time slices of a few-bin (REDUCE = false) call: enough workgroups to fill the chip
+// (>= 1024), at least 256 samples per slice.
+int temporal_bins_slices(int P, int nf, int T) {
+    const long blocks = (long)temporal_dft_tiles(P) * ((nf + TD_FT_DFT - 1) / TD_FT_DFT);
+    const long want = (1024 + blocks - 1) / blocks;
+    return (int)std::max(1L, std::min(want, (long)T / 256));
+}
+
 void temporal_dft(const float* stack, long frame_pitch, long row_pitch, int bw, int P, int T, const double2* tab,
-                  const int* freqs, int nf, double2* out, double* partial, hipStream_t s) {
+                  const int* freqs, int nf, double2* out, double* partial, double2* slices, hipStream_t s) {
     if (P <= 0 || T <= 0 || nf <= 0) return;
-    const dim3 grid((unsigned)temporal_dft_tiles(P), (unsigned)((nf + TD_FT_DFT - 1) / TD_FT_DFT));
+    const int nz = partial ? 1 : temporal_bins_slices(P, nf, T);
+    const int tchunk = (T + nz - 1) / nz;
+    const dim3 grid((unsigned)temporal_dft_tiles(P), (unsigned)((nf + TD_FT_DFT - 1) / TD_FT_DFT), (unsigned)nz);
     const bool lds = T <= TD_LDS_TAB;
     const size_t lb = lds ? (size_t)T * sizeof(double2) : 0;
+    double2* dst = nz > 1 ? slices : out;
+    if (nz > 1 && !slices) throw std::runtime_error("temporal_dft: slice workspace missing");
     if (partial) {
         if (lds) {
             (void)hipFuncSetAttribute((const void*)k_tdft<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb);
             hipLaunchKernelGGL((k_tdft<true, true>), grid, dim3(TD_THREADS), lb, s, stack, frame_pitch, row_pitch, bw,
-                               P, T, tab, freqs, nf, out, partial);
+                               P, T, tab, freqs, nf, dst, partial, tchunk);
         } else {
             hipLaunchKernelGGL((k_tdft<true, false>), grid, dim3(TD_THREADS), 0, s, stack, frame_pitch, row_pitch, bw,
-                               P, T, tab, freqs, nf, out, partial);
+                               P, T, tab, freqs, nf, dst, partial, tchunk);
         }
     } else {
         if (lds) {
             (void)hipFuncSetAttribute((const void*)k_tdft<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb);
             hipLaunchKernelGGL((k_tdft<false, true>), grid, dim3(TD_THREADS), lb, s, stack, frame_pitch, row_pitch,
-                               bw, P, T, tab, freqs, nf, out, partial);
+                               bw, P, T, tab, freqs, nf, dst, partial, tchunk);
         } else {
             hipLaunchKernelGGL((k_tdft<false, false>), grid, dim3(TD_THREADS), 0, s, stack, frame_pitch, row_pitch,
-                               bw, P, T, tab, freqs, nf, out, partial);
+                               bw, P, T, tab, freqs, nf, dst, partial, tchunk);
+        }
+        if (nz > 1) {
+            const long n = (long)P * nf;
+            hipLaunchKernelGGL(k_tdft_sum, dim3((unsigned)((n + TD_THREADS - 1) / TD_THREADS)), dim3(TD_THREADS), 0, s,
+                               slices, nz, n, out);
         }
     }
     check_launch("temporal_dft");
