@@ -5,8 +5,8 @@
 //
 // The reference loops over pixels in Python; here each lane owns pixels of
 // the block and walks its time series (a coalesced row-run of every frame,
-// no transpose of the stack), 2 pixels x 8 frequencies per lane (k_tdft) or
-// 16 frequencies per lane (k_spectro) accumulated in f64.
+// no transpose of the stack), 2 pixels x 8 frequencies per lane accumulated
+// in f64.
 // The DFT is direct, not an FFT: T is any length (the number of maps), the
 // work is ~T x (T/2 + 1) complex MACs per pixel (1.3e11 flop for a 128 x 128
 // block of 2000 maps, ~2 ms of f64 VALU on the MI355X), and the exponentials
@@ -25,11 +25,10 @@ namespace fcdk {
 namespace {
 
 constexpr int TD_THREADS = 256;  // pixels per workgroup
-constexpr int TD_FT = 16;        // frequencies per lane
 constexpr int TD_LDS_TAB = 8192;  // table entries held in LDS (128 KiB of double2)
 constexpr int TD_BATCH = 8;       // samples per load batch
-constexpr int TD_PX = 2;          // pixels per lane of k_tdft (4 x 4 bins: 9.7 vs 4.6 ms, r01bq)
-constexpr int TD_FT_DFT = 8;      // frequencies per lane of k_tdft
+constexpr int TD_PX = 2;          // pixels per lane of k_tdft / k_spectro (4 x 4 bins: 9.7 vs 4.6 ms, r01bq)
+constexpr int TD_FT_DFT = 8;      // frequencies per lane of k_tdft / k_spectro
 
 // Pixel p of the block -> its element offset in frame 0.
 __device__ __forceinline__ long pix_off(int p, int bw, long row_pitch) { return (long)(p / bw) * row_pitch + p % bw; }
@@ -188,53 +187,78 @@ __global__ __launch_bounds__(TD_THREADS) void k_spectro(const float* __restrict_
         wl[i] = win[i];
     }
     __syncthreads();
-    const int p = blockIdx.x * TD_THREADS + threadIdx.x;
+    constexpr int FT = TD_FT_DFT, PX = TD_PX;  // as k_tdft: 4 f64 FMAs per table read
+    const int p0 = (blockIdx.x * TD_THREADS + threadIdx.x) * PX;
     const int seg = blockIdx.y;
-    const bool live = p < P;
-    const float* xs = stack + (live ? pix_off(p, bw, row_pitch) : 0) + (long)seg * step * frame_pitch;
-    int fk[TD_FT], idx[TD_FT];
-    double re[TD_FT], im[TD_FT];
+    bool live[PX];
+    const float* xs[PX];
 #pragma unroll
-    for (int k = 0; k < TD_FT; ++k) {
-        const int j = blockIdx.z * TD_FT + k;
+    for (int u = 0; u < PX; ++u) {
+        live[u] = p0 + u < P;
+        xs[u] = stack + (live[u] ? pix_off(p0 + u, bw, row_pitch) : 0) + (long)seg * step * frame_pitch;
+    }
+    int fk[FT], idx[FT];
+    double re[PX][FT], im[PX][FT], sum[PX];
+#pragma unroll
+    for (int k = 0; k < FT; ++k) {
+        const int j = blockIdx.z * FT + k;
         fk[k] = j < nf ? j : 0;
         idx[k] = 0;
-        re[k] = 0.0;
-        im[k] = 0.0;
-    }
-    double sum = 0.0;
-    auto sample = [&](int n, double x) {
-        sum += x;
-        const double xw = x * wl[n];
 #pragma unroll
-        for (int k = 0; k < TD_FT; ++k) {
+        for (int u = 0; u < PX; ++u) re[u][k] = im[u][k] = 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < PX; ++u) sum[u] = 0.0;
+    auto sample = [&](int n, const float (&x)[PX]) {
+        const double wn = wl[n];
+        double xw[PX];
+#pragma unroll
+        for (int u = 0; u < PX; ++u) {
+            sum[u] += (double)x[u];
+            xw[u] = (double)x[u] * wn;
+        }
+#pragma unroll
+        for (int k = 0; k < FT; ++k) {
             const double2 w = tb[idx[k]];
-            re[k] = fma(xw, w.x, re[k]);
-            im[k] = fma(xw, w.y, im[k]);
+#pragma unroll
+            for (int u = 0; u < PX; ++u) {
+                re[u][k] = fma(xw[u], w.x, re[u][k]);
+                im[u][k] = fma(xw[u], w.y, im[u][k]);
+            }
             idx[k] += fk[k];
             idx[k] -= idx[k] >= nperseg ? nperseg : 0;
         }
     };
     int n = 0;  // unconditional batched loads, as k_tdft
     for (; n + TD_BATCH <= nperseg; n += TD_BATCH) {
-        float xb[TD_BATCH];
+        float xb[TD_BATCH][PX];
 #pragma unroll
-        for (int u = 0; u < TD_BATCH; ++u) xb[u] = xs[(long)(n + u) * frame_pitch];
+        for (int v = 0; v < TD_BATCH; ++v)
 #pragma unroll
-        for (int u = 0; u < TD_BATCH; ++u) sample(n + u, (double)xb[u]);
+            for (int u = 0; u < PX; ++u) xb[v][u] = xs[u][(long)(n + v) * frame_pitch];
+#pragma unroll
+        for (int v = 0; v < TD_BATCH; ++v) sample(n + v, xb[v]);
     }
-    for (; n < nperseg; ++n) sample(n, (double)xs[(long)n * frame_pitch]);
-    if (!live) return;
-    const double mean = sum / (double)nperseg;
+    for (; n < nperseg; ++n) {
+        float x1[PX];
 #pragma unroll
-    for (int k = 0; k < TD_FT; ++k) {
-        const int j = blockIdx.z * TD_FT + k;
-        if (j >= nf) continue;
-        const double2 W = wsum[j];
-        const double xr = re[k] - mean * W.x, xi = im[k] - mean * W.y;
-        double s = (xr * xr + xi * xi) * scale;
-        if (j > 0 && !(nperseg % 2 == 0 && j == nperseg / 2)) s *= 2.0;
-        out[((long)p * nf + j) * nseg + seg] = s;
+        for (int u = 0; u < PX; ++u) x1[u] = xs[u][(long)n * frame_pitch];
+        sample(n, x1);
+    }
+#pragma unroll
+    for (int u = 0; u < PX; ++u) {
+        if (!live[u]) continue;
+        const double mean = sum[u] / (double)nperseg;
+#pragma unroll
+        for (int k = 0; k < FT; ++k) {
+            const int j = blockIdx.z * FT + k;
+            if (j >= nf) continue;
+            const double2 W = wsum[j];
+            const double xr = re[u][k] - mean * W.x, xi = im[u][k] - mean * W.y;
+            double sp = (xr * xr + xi * xi) * scale;
+            if (j > 0 && !(nperseg % 2 == 0 && j == nperseg / 2)) sp *= 2.0;
+            out[((long)(p0 + u) * nf + j) * nseg + seg] = sp;
+        }
     }
 }
 
@@ -300,7 +324,7 @@ void spectrogram(const float* stack, long frame_pitch, long row_pitch, int bw, i
                  const double* win, const double2* tab, const double2* wsum, int nf, double scale, double* out,
                  hipStream_t s) {
     if (P <= 0 || nseg <= 0) return;
-    const dim3 grid((unsigned)((P + TD_THREADS - 1) / TD_THREADS), (unsigned)nseg, (unsigned)((nf + TD_FT - 1) / TD_FT));
+    const dim3 grid((unsigned)temporal_dft_tiles(P), (unsigned)nseg, (unsigned)((nf + TD_FT_DFT - 1) / TD_FT_DFT));
     const size_t lb = (size_t)nperseg * (sizeof(double2) + sizeof(double));
     (void)hipFuncSetAttribute((const void*)k_spectro, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb);
     hipLaunchKernelGGL(k_spectro, grid, dim3(TD_THREADS), lb, s, stack, frame_pitch, row_pitch, bw, P, nperseg, step,
