@@ -164,3 +164,57 @@ def test_spectrogram_series():
     # and the reference's own float32 computation, to float32 accuracy
     t3, f3, S3 = ora.spectrogram_series(x, fs=TASA, nperseg=128)
     close_nan(S, S3, rtol=1e-5)
+
+
+@pytest.mark.gpu
+def test_device_pointer_block_equals_host():
+    """FCD_DEVICE_PTRS on a device-resident stack (the block addressed in place with the
+    stack's own pitches, no staging) gives the host-pointer results bit for bit."""
+    import ctypes
+    import torch
+    from pyfcd import _lib
+    eng = _lib.temporal_engine()
+    lib = _lib.load_library()
+    st = make_stack(300, n=96, seed=11, zero_corner=False)
+    T, rows, cols = st.shape
+    blk = (16, 40, 32, 24)  # r0, c0, bh, bw
+    dims = (T, rows, cols) + blk
+    sd = torch.from_numpy(st).cuda()
+    nf = 150
+    tot_h, cnt_h = eng.temporal_spectrum(st, nf, block=blk)
+    sc = np.empty((nf, 2))
+    _lib._check(lib.fcd_temporal_spectrum(eng.handle, ctypes.c_void_p(sd.data_ptr()), *dims, _lib.FCD_DEVICE_PTRS, nf,
+                                          sc.ctypes.data, None))
+    assert np.array_equal(sc[:, 0], tot_h) and np.array_equal(sc[:, 1], cnt_h)
+    bins = np.array([0, 6, 12, 149], np.int32)
+    X_h = eng.temporal_bins(st, bins, block=blk)
+    xd = torch.empty((blk[2] * blk[3], len(bins), 2), dtype=torch.float64, device="cuda")
+    _lib._check(lib.fcd_temporal_bins(eng.handle, ctypes.c_void_p(sd.data_ptr()), *dims, _lib.FCD_DEVICE_PTRS,
+                                      bins.ctypes.data, len(bins), ctypes.c_void_p(xd.data_ptr()), None))
+    Xd = xd.cpu().numpy()
+    assert np.array_equal(Xd[..., 0].reshape(X_h.shape), X_h.real)
+    assert np.array_equal(Xd[..., 1].reshape(X_h.shape), X_h.imag)
+    from scipy.signal import get_window
+    win = get_window(("tukey", 0.25), 64)
+    S_h = eng.spectrogram(st, 64, 8, win, TASA, block=blk)
+    sdv = torch.empty(S_h.shape, dtype=torch.float64, device="cuda")
+    _lib._check(lib.fcd_spectrogram(eng.handle, ctypes.c_void_p(sd.data_ptr()), *dims, _lib.FCD_DEVICE_PTRS, 64, 8,
+                                    win.ctypes.data, TASA, ctypes.c_void_p(sdv.data_ptr()), None))
+    torch.cuda.synchronize()
+    assert np.array_equal(sdv.cpu().numpy(), S_h)
+    # and the block itself against numpy's f64 FFT
+    ref = np.fft.fft(st[:, 16:48, 40:64].astype(np.float64), axis=0)
+    close_nan(np.transpose(ref[bins], (1, 2, 0)).real, X_h.real)
+
+
+@pytest.mark.gpu
+def test_temporal_bad_arguments():
+    from pyfcd import _lib
+    eng = _lib.temporal_engine()
+    st = make_stack(20, n=8, zero_corner=False)
+    with pytest.raises(_lib.FcdError):
+        eng.temporal_bins(st, [0, 20])  # bin out of range
+    with pytest.raises(_lib.FcdError):
+        eng.temporal_spectrum(st, 4, block=(4, 4, 8, 8))  # block outside the frame
+    with pytest.raises(_lib.FcdError):
+        eng.spectrogram(st, 32, 4, np.ones(32), TASA)  # nperseg > T
