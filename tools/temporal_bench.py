@@ -7,8 +7,9 @@ the reference's default) per call:
     1000 non-negative bins (fcd_temporal_spectrum), f64 accumulation;
   * the harmonic bins (fcd_temporal_bins, 3 bins);
   * spectrogram of every pixel (fcd_spectrogram, nperseg 256, noverlap 32, Tukey 0.25).
-Roofline: the DFT kernel is f64-VALU work, 4 flops per (pixel, sample, bin) (two f64
-FMAs), against the 78.6 TFLOP/s f64 vector peak (vendor spec).  CPU: the oracle's
+Roofline: 4 flops per (pixel, sample, bin) (two f64 FMAs) against 78.6 TFLOP/s, the
+f64 peak of both the matrix cores (the mean-spectrum GEMM, k_tdft_mfma) and the vector
+units (vendor spec).  CPU: the oracle's
 numpy / scipy calls (the reference's own, analyze.py:497, :521, :574) on a sample of the block's series, 1 core.
 
     python tools/temporal_bench.py [--T 2000] [--reps 5]
@@ -103,7 +104,7 @@ def main():
         "metric": "temporal post-analysis of a map stack (block_amplitude / spectrogram), pixel series per second",
         "workload": f"{T} maps of {n}x{n} float32 in HBM, one {b}x{b} block per call (num_blocks=64)",
         "block_amplitude_spectrum": {"ms": t_spec * 1e3, "series_per_s": P / t_spec, "bins": nf,
-                                     "roofline": {"bound": "f64 valu", "achieved_tflops": flops_spec / t_spec / 1e12,
+                                     "roofline": {"bound": "f64 (matrix cores; FCD_TDFT_VALU=1: vector)", "achieved_tflops": flops_spec / t_spec / 1e12,
                                                   "peak_tflops": F64_PEAK / 1e12,
                                                   "frac": flops_spec / t_spec / F64_PEAK}},
         "block_amplitude_harmonics": {"ms": t_harm * 1e3, "bins": len(bins)},

@@ -1479,7 +1479,7 @@ FCD_API int fcd_temporal_spectrum(fcd_ctx* c, const float* stack, int T, int row
         hipStream_t s = c->pick(stream);
         const BlockView v = stage_block(c, stack, T, rows, cols, r0, c0, bh, bw, flags == FCD_DEVICE_PTRS, s);
         upload_exp_table(c, c->t_tab, T, s);
-        const int P = bh * bw, tiles = fcdk::temporal_dft_tiles(P);
+        const int P = bh * bw, tiles = fcdk::temporal_spectrum_tiles(P, T);
         c->t_part.ensure((size_t)tiles * nf * 2 * sizeof(double));
         fcdk::temporal_dft(v.p, v.frame_pitch, v.row_pitch, bw, P, T, c->t_tab.as<double2>(), nullptr, nf, nullptr,
                            c->t_part.as<double>(), nullptr, s);

@@ -136,6 +136,7 @@ void compose_phase(const float* w, const int32_t* k, float* out, long n, hipStre
 void temporal_dft(const float* stack, long frame_pitch, long row_pitch, int bw, int P, int T, const double2* tab,
                   const int* freqs, int nf, double2* out, double* partial, double2* slices, hipStream_t s);
 int temporal_dft_tiles(int P);
+int temporal_spectrum_tiles(int P, int T);  // partial-sum rows of a mean-spectrum call
 int temporal_bins_slices(int P, int nf, int T);  // slices[slices][P][nf] workspace of a bins call
 int spectro_max_nperseg();
 void spectrogram(const float* stack, long frame_pitch, long row_pitch, int bw, int P, int nperseg, int step, int nseg,

@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -153,6 +154,120 @@ __global__ __launch_bounds__(TD_THREADS) void k_tdft(const float* __restrict__ s
     }
 }
 
+// The mean-spectrum call as a GEMM on the f64 matrix cores: X[p][c] = sum_t
+// x_p(t) E[t][c], E[t][2 f + e] = (cos, -sin)(2 pi f t / T)[e], with
+// v_mfma_f64_16x16x4_f64 (A: lane l holds x[pixel l & 15][t + (l >> 4)], B: lane l
+// holds E[t + (l >> 4)][column l & 15], C: column l & 15, row (l >> 4) + 4 r).  A
+// wave owns 32 pixels x 32 bins (2 x 4 tiles of 16 x 16), so each A fragment feeds
+// 4 MFMAs and each B fragment 2; B comes from the LDS table at a per-lane index
+// (f t) mod T kept incrementally.  Same partial-sum output as k_tdft<true, true>.
+typedef double dv4 __attribute__((ext_vector_type(4)));
+constexpr int TM_PIX = 128;  // pixels per workgroup (4 waves x 32)
+constexpr int TM_BINS = 32;  // bins per workgroup
+
+__global__ __launch_bounds__(TD_THREADS) void k_tdft_mfma(const float* __restrict__ stack, long frame_pitch,
+                                                          long row_pitch, int bw, int P, int T,
+                                                          const double2* __restrict__ tab, int nf,
+                                                          double* __restrict__ partial) {
+    extern __shared__ double2 tm_lds[];
+    for (int i = threadIdx.x; i < T; i += TD_THREADS) tm_lds[i] = tab[i];
+    __syncthreads();
+    const double* tl = reinterpret_cast<const double*>(tm_lds);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int kq = lane >> 4, col = lane & 15;
+    const int pbase = blockIdx.x * TM_PIX + wave * 32;
+    const int fbase = blockIdx.y * TM_BINS;
+    // A rows of this lane: pixels pbase + 16 m + col
+    const float* xs[2];
+    bool live[2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+        const int p = pbase + 16 * m + col;
+        live[m] = p < P;
+        xs[m] = stack + (live[m] ? pix_off(p, bw, row_pitch) : 0);
+    }
+    // B columns of this lane: bin fbase + 8 n + col / 2, component col & 1
+    int fq[4], idx[4], step4[4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+        const int f = fbase + 8 * n + (col >> 1);
+        fq[n] = f < nf ? f : 0;
+        idx[n] = (int)(((long)fq[n] * kq) % T);
+        step4[n] = (int)(((long)fq[n] * 4) % T);
+    }
+    const int comp = col & 1;
+    dv4 acc[2][4];
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n) acc[m][n] = dv4{0.0, 0.0, 0.0, 0.0};
+    auto kstep = [&](const float (&xa)[2], int t) {
+        double a[2], b[4];
+#pragma unroll
+        for (int m = 0; m < 2; ++m) a[m] = t + kq < T ? (double)xa[m] : 0.0;
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+            b[n] = tl[2 * idx[n] + comp];
+            idx[n] += step4[n];
+            idx[n] -= idx[n] >= T ? T : 0;
+        }
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+            for (int n = 0; n < 4; ++n) acc[m][n] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[m], b[n], acc[m][n], 0, 0, 0);
+    };
+    // batches of TM_B K-steps: their A loads are in flight together
+    constexpr int TM_B = 4;
+    int t = 0;
+    for (; t < T; t += 4 * TM_B) {
+        float xa[TM_B][2];
+#pragma unroll
+        for (int q = 0; q < TM_B; ++q) {
+            const int tt = min(t + 4 * q + kq, T - 1);  // clamped: samples past T are zeroed in kstep
+#pragma unroll
+            for (int m = 0; m < 2; ++m) xa[q][m] = __builtin_nontemporal_load(xs[m] + (long)tt * frame_pitch);
+        }
+#pragma unroll
+        for (int q = 0; q < TM_B; ++q)
+            if (t + 4 * q < T) kstep(xa[q], t + 4 * q);
+    }
+    // |X| per (pixel, bin): re in the even column lane, im in the odd one
+    __shared__ double red[TD_THREADS / 64][TM_BINS][2];
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+        double s = 0.0, c = 0.0;
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const double v = acc[m][n][r];
+                const double w = __shfl_xor(v, 1, 64);
+                const double mag = sqrt(v * v + w * w);
+                const int p = pbase + 16 * m + kq + 4 * r;
+                const bool ok = !comp && p < P && mag == mag;  // NaN samples make every bin NaN
+                s += ok ? mag : 0.0;
+                c += ok ? 1.0 : 0.0;
+            }
+        s += __shfl_xor(s, 16, 64);
+        c += __shfl_xor(c, 16, 64);
+        s += __shfl_xor(s, 32, 64);
+        c += __shfl_xor(c, 32, 64);
+        if (lane < 16 && !comp) {
+            red[wave][8 * n + (col >> 1)][0] = s;
+            red[wave][8 * n + (col >> 1)][1] = c;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < TM_BINS * 2) {
+        const int k = threadIdx.x >> 1, e = threadIdx.x & 1;
+        const int j = fbase + k;
+        double a = 0.0;
+#pragma unroll
+        for (int w = 0; w < TD_THREADS / 64; ++w) a += red[w][k][e];
+        if (j < nf) partial[((long)blockIdx.x * nf + j) * 2 + e] = a;
+    }
+}
+
 // out[i] = sum over the nz time slices of parts[z][i], in slice order (deterministic).
 __global__ __launch_bounds__(TD_THREADS) void k_tdft_sum(const double2* __restrict__ parts, int nz, long n,
                                                          double2* __restrict__ out) {
@@ -279,9 +394,30 @@ int temporal_bins_slices(int P, int nf, int T) {
     return (int)std::max(1L, std::min(want, (long)T / 256));
 }
 
+static bool spectrum_on_mfma(int T) {
+    static const bool off = [] {
+        const char* e = std::getenv("FCD_TDFT_VALU");
+        return e && e[0] == '1';
+    }();
+    return !off && T <= TD_LDS_TAB;
+}
+
+int temporal_spectrum_tiles(int P, int T) {
+    return spectrum_on_mfma(T) ? (P + TM_PIX - 1) / TM_PIX : temporal_dft_tiles(P);
+}
+
 void temporal_dft(const float* stack, long frame_pitch, long row_pitch, int bw, int P, int T, const double2* tab,
                   const int* freqs, int nf, double2* out, double* partial, double2* slices, hipStream_t s) {
     if (P <= 0 || T <= 0 || nf <= 0) return;
+    if (partial && !freqs && spectrum_on_mfma(T)) {
+        const dim3 g((unsigned)((P + TM_PIX - 1) / TM_PIX), (unsigned)((nf + TM_BINS - 1) / TM_BINS));
+        const size_t lb = (size_t)T * sizeof(double2);
+        (void)hipFuncSetAttribute((const void*)k_tdft_mfma, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb);
+        hipLaunchKernelGGL(k_tdft_mfma, g, dim3(TD_THREADS), lb, s, stack, frame_pitch, row_pitch, bw, P, T, tab, nf,
+                           partial);
+        check_launch("temporal_dft (mfma)");
+        return;
+    }
     const int nz = partial ? 1 : temporal_bins_slices(P, nf, T);
     const int tchunk = (T + nz - 1) / nz;
     const dim3 grid((unsigned)temporal_dft_tiles(P), (unsigned)((nf + TD_FT_DFT - 1) / TD_FT_DFT), (unsigned)nz);
