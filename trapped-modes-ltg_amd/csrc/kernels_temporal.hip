@@ -162,8 +162,15 @@ __global__ __launch_bounds__(TD_THREADS) void k_tdft(const float* __restrict__ s
 // 4 MFMAs and each B fragment 2; B comes from the LDS table at a per-lane index
 // (f t) mod T kept incrementally.  Same partial-sum output as k_tdft<true, true>.
 typedef double dv4 __attribute__((ext_vector_type(4)));
-constexpr int TM_PIX = 128;  // pixels per workgroup (4 waves x 32)
-constexpr int TM_BINS = 32;  // bins per workgroup
+#ifndef FCD_TM_WM
+#define FCD_TM_WM 2  // 16-pixel tiles per wave
+#endif
+#ifndef FCD_TM_WN
+#define FCD_TM_WN 4  // 8-bin (16-column) tiles per wave
+#endif
+constexpr int TM_WM = FCD_TM_WM, TM_WN = FCD_TM_WN;
+constexpr int TM_PIX = 4 * 16 * TM_WM;  // pixels per workgroup (4 waves)
+constexpr int TM_BINS = 8 * TM_WN;      // bins per workgroup
 
 __global__ __launch_bounds__(TD_THREADS) void k_tdft_mfma(const float* __restrict__ stack, long frame_pitch,
                                                           long row_pitch, int bw, int P, int T,
@@ -175,57 +182,58 @@ __global__ __launch_bounds__(TD_THREADS) void k_tdft_mfma(const float* __restric
     const double* tl = reinterpret_cast<const double*>(tm_lds);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int kq = lane >> 4, col = lane & 15;
-    const int pbase = blockIdx.x * TM_PIX + wave * 32;
+    const int pbase = blockIdx.x * TM_PIX + wave * 16 * TM_WM;
     const int fbase = blockIdx.y * TM_BINS;
     // A rows of this lane: pixels pbase + 16 m + col
-    const float* xs[2];
-    bool live[2];
+    const float* xs[TM_WM];
+    bool live[TM_WM];
 #pragma unroll
-    for (int m = 0; m < 2; ++m) {
+    for (int m = 0; m < TM_WM; ++m) {
         const int p = pbase + 16 * m + col;
         live[m] = p < P;
         xs[m] = stack + (live[m] ? pix_off(p, bw, row_pitch) : 0);
     }
     // B columns of this lane: bin fbase + 8 n + col / 2, component col & 1
-    int fq[4], idx[4], step4[4];
+    int fq[TM_WN], idx[TM_WN], step4[TM_WN];
 #pragma unroll
-    for (int n = 0; n < 4; ++n) {
+    for (int n = 0; n < TM_WN; ++n) {
         const int f = fbase + 8 * n + (col >> 1);
         fq[n] = f < nf ? f : 0;
         idx[n] = (int)(((long)fq[n] * kq) % T);
         step4[n] = (int)(((long)fq[n] * 4) % T);
     }
     const int comp = col & 1;
-    dv4 acc[2][4];
+    dv4 acc[TM_WM][TM_WN];
 #pragma unroll
-    for (int m = 0; m < 2; ++m)
+    for (int m = 0; m < TM_WM; ++m)
 #pragma unroll
-        for (int n = 0; n < 4; ++n) acc[m][n] = dv4{0.0, 0.0, 0.0, 0.0};
-    auto kstep = [&](const float (&xa)[2], int t) {
-        double a[2], b[4];
+        for (int n = 0; n < TM_WN; ++n) acc[m][n] = dv4{0.0, 0.0, 0.0, 0.0};
+    auto kstep = [&](const float (&xa)[TM_WM], int t) {
+        double a[TM_WM], b[TM_WN];
 #pragma unroll
-        for (int m = 0; m < 2; ++m) a[m] = t + kq < T ? (double)xa[m] : 0.0;
+        for (int m = 0; m < TM_WM; ++m) a[m] = t + kq < T ? (double)xa[m] : 0.0;
 #pragma unroll
-        for (int n = 0; n < 4; ++n) {
+        for (int n = 0; n < TM_WN; ++n) {
             b[n] = tl[2 * idx[n] + comp];
             idx[n] += step4[n];
             idx[n] -= idx[n] >= T ? T : 0;
         }
 #pragma unroll
-        for (int m = 0; m < 2; ++m)
+        for (int m = 0; m < TM_WM; ++m)
 #pragma unroll
-            for (int n = 0; n < 4; ++n) acc[m][n] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[m], b[n], acc[m][n], 0, 0, 0);
+            for (int n = 0; n < TM_WN; ++n)
+                acc[m][n] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[m], b[n], acc[m][n], 0, 0, 0);
     };
     // batches of TM_B K-steps: their A loads are in flight together
     constexpr int TM_B = 4;
     int t = 0;
     for (; t < T; t += 4 * TM_B) {
-        float xa[TM_B][2];
+        float xa[TM_B][TM_WM];
 #pragma unroll
         for (int q = 0; q < TM_B; ++q) {
             const int tt = min(t + 4 * q + kq, T - 1);  // clamped: samples past T are zeroed in kstep
 #pragma unroll
-            for (int m = 0; m < 2; ++m) xa[q][m] = __builtin_nontemporal_load(xs[m] + (long)tt * frame_pitch);
+            for (int m = 0; m < TM_WM; ++m) xa[q][m] = __builtin_nontemporal_load(xs[m] + (long)tt * frame_pitch);
         }
 #pragma unroll
         for (int q = 0; q < TM_B; ++q)
@@ -234,10 +242,10 @@ __global__ __launch_bounds__(TD_THREADS) void k_tdft_mfma(const float* __restric
     // |X| per (pixel, bin): re in the even column lane, im in the odd one
     __shared__ double red[TD_THREADS / 64][TM_BINS][2];
 #pragma unroll
-    for (int n = 0; n < 4; ++n) {
+    for (int n = 0; n < TM_WN; ++n) {
         double s = 0.0, c = 0.0;
 #pragma unroll
-        for (int m = 0; m < 2; ++m)
+        for (int m = 0; m < TM_WM; ++m)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const double v = acc[m][n][r];
