@@ -276,6 +276,115 @@ __global__ __launch_bounds__(TD_THREADS) void k_tdft_mfma(const float* __restric
     }
 }
 
+// Spectrogram segments on the matrix cores, as k_tdft_mfma: for segment blockIdx.y,
+// X[p][2f+e] = sum_n x_p(s0 + n) w_n E[n][2f+e] (B = window x table, gathered per
+// lane), the segment means from the A fragments (x_p summed over the lanes holding
+// pixel p's samples), then S = |X - mean W_f|^2 scale (x2 off DC / Nyquist).
+__global__ __launch_bounds__(TD_THREADS) void k_spectro_mfma(const float* __restrict__ stack, long frame_pitch,
+                                                             long row_pitch, int bw, int P, int nperseg, int step,
+                                                             int nseg, const double* __restrict__ win,
+                                                             const double2* __restrict__ tab,
+                                                             const double2* __restrict__ wsum, int nf, double scale,
+                                                             double* __restrict__ out) {
+    extern __shared__ double2 sm_lds[];
+    double2* const tb = sm_lds;                                     // [nperseg]
+    double* const wl = reinterpret_cast<double*>(sm_lds + nperseg);  // [nperseg]
+    for (int i = threadIdx.x; i < nperseg; i += TD_THREADS) {
+        tb[i] = tab[i];
+        wl[i] = win[i];
+    }
+    __syncthreads();
+    const double* tl = reinterpret_cast<const double*>(tb);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int kq = lane >> 4, col = lane & 15, comp = col & 1;
+    const int pbase = blockIdx.x * TM_PIX + wave * 16 * TM_WM;
+    const int seg = blockIdx.y;
+    const int fbase = blockIdx.z * TM_BINS;
+    const float* xs[TM_WM];
+#pragma unroll
+    for (int m = 0; m < TM_WM; ++m) {
+        const int p = pbase + 16 * m + col;
+        xs[m] = stack + (p < P ? pix_off(p, bw, row_pitch) : 0) + (long)seg * step * frame_pitch;
+    }
+    int fq[TM_WN], idx[TM_WN], step4[TM_WN];
+#pragma unroll
+    for (int n = 0; n < TM_WN; ++n) {
+        const int f = fbase + 8 * n + (col >> 1);
+        fq[n] = f < nf ? f : 0;
+        idx[n] = (fq[n] * kq) % nperseg;
+        step4[n] = (fq[n] * 4) % nperseg;
+    }
+    dv4 acc[TM_WM][TM_WN];
+    double sx[TM_WM];
+#pragma unroll
+    for (int m = 0; m < TM_WM; ++m) {
+        sx[m] = 0.0;
+#pragma unroll
+        for (int n = 0; n < TM_WN; ++n) acc[m][n] = dv4{0.0, 0.0, 0.0, 0.0};
+    }
+    constexpr int TM_B = 4;
+    for (int n0 = 0; n0 < nperseg; n0 += 4 * TM_B) {
+        float xa[TM_B][TM_WM];
+#pragma unroll
+        for (int q = 0; q < TM_B; ++q) {
+            const int nn = min(n0 + 4 * q + kq, nperseg - 1);  // clamped: samples past the segment are zeroed
+#pragma unroll
+            for (int m = 0; m < TM_WM; ++m) xa[q][m] = __builtin_nontemporal_load(xs[m] + (long)nn * frame_pitch);
+        }
+#pragma unroll
+        for (int q = 0; q < TM_B; ++q) {
+            const int nk = n0 + 4 * q;
+            if (nk >= nperseg) break;
+            const bool in = nk + kq < nperseg;
+            const double wn = in ? wl[nk + kq] : 0.0;
+            double a[TM_WM], b[TM_WN];
+#pragma unroll
+            for (int m = 0; m < TM_WM; ++m) {
+                a[m] = in ? (double)xa[q][m] : 0.0;
+                sx[m] += a[m];
+            }
+#pragma unroll
+            for (int n = 0; n < TM_WN; ++n) {
+                b[n] = wn * tl[2 * idx[n] + comp];
+                idx[n] += step4[n];
+                idx[n] -= idx[n] >= nperseg ? nperseg : 0;
+            }
+#pragma unroll
+            for (int m = 0; m < TM_WM; ++m)
+#pragma unroll
+                for (int n = 0; n < TM_WN; ++n)
+                    acc[m][n] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[m], b[n], acc[m][n], 0, 0, 0);
+        }
+    }
+    // segment sums per pixel: lanes with the same column hold its four sample phases
+#pragma unroll
+    for (int m = 0; m < TM_WM; ++m) {
+        sx[m] += __shfl_xor(sx[m], 16, 64);
+        sx[m] += __shfl_xor(sx[m], 32, 64);
+    }
+    const double inv_n = 1.0 / (double)nperseg;
+#pragma unroll
+    for (int m = 0; m < TM_WM; ++m)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int row = kq + 4 * r;  // pixel pbase + 16 m + row; its sum sits in lane `row`
+            const double mean = __shfl(sx[m], row, 64) * inv_n;
+            const int p = pbase + 16 * m + row;
+#pragma unroll
+            for (int n = 0; n < TM_WN; ++n) {
+                const int f = fbase + 8 * n + (col >> 1);
+                const double2 W = wsum[fq[n]];
+                const double v = acc[m][n][r] - mean * (comp ? W.y : W.x);
+                const double o = __shfl_xor(v, 1, 64);
+                if (!comp && p < P && f < nf) {
+                    double sp = (v * v + o * o) * scale;
+                    if (f > 0 && !(nperseg % 2 == 0 && f == nperseg / 2)) sp *= 2.0;
+                    out[((long)p * nf + f) * nseg + seg] = sp;
+                }
+            }
+        }
+}
+
 // out[i] = sum over the nz time slices of parts[z][i], in slice order (deterministic).
 __global__ __launch_bounds__(TD_THREADS) void k_tdft_sum(const double2* __restrict__ parts, int nz, long n,
                                                          double2* __restrict__ out) {
@@ -468,8 +577,16 @@ void spectrogram(const float* stack, long frame_pitch, long row_pitch, int bw, i
                  const double* win, const double2* tab, const double2* wsum, int nf, double scale, double* out,
                  hipStream_t s) {
     if (P <= 0 || nseg <= 0) return;
-    const dim3 grid((unsigned)temporal_dft_tiles(P), (unsigned)nseg, (unsigned)((nf + TD_FT_DFT - 1) / TD_FT_DFT));
     const size_t lb = (size_t)nperseg * (sizeof(double2) + sizeof(double));
+    if (spectrum_on_mfma(0)) {
+        const dim3 g((unsigned)((P + TM_PIX - 1) / TM_PIX), (unsigned)nseg, (unsigned)((nf + TM_BINS - 1) / TM_BINS));
+        (void)hipFuncSetAttribute((const void*)k_spectro_mfma, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb);
+        hipLaunchKernelGGL(k_spectro_mfma, g, dim3(TD_THREADS), lb, s, stack, frame_pitch, row_pitch, bw, P, nperseg,
+                           step, nseg, win, tab, wsum, nf, scale, out);
+        check_launch("spectrogram (mfma)");
+        return;
+    }
+    const dim3 grid((unsigned)temporal_dft_tiles(P), (unsigned)nseg, (unsigned)((nf + TD_FT_DFT - 1) / TD_FT_DFT));
     (void)hipFuncSetAttribute((const void*)k_spectro, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb);
     hipLaunchKernelGGL(k_spectro, grid, dim3(TD_THREADS), lb, s, stack, frame_pitch, row_pitch, bw, P, nperseg, step,
                        nseg, win, tab, wsum, nf, scale, out);
