@@ -91,6 +91,15 @@ struct KCfg {
 #ifndef FCD_INTCOLS_PREF_X
 #define FCD_INTCOLS_PREF_X 1
 #endif
+// Workgroup size of k_demod_cols up to 1024 points: 4 teams share one twiddle
+// table, 78 KB of LDS -> 2 workgroups = 16 waves per CU at 1024 (12 with 256
+// threads): 0.84 vs 0.89 us/frame (kbench r01cd).  Larger transforms keep 256.
+#ifndef FCD_DEMODCOLS_BLOCK
+#define FCD_DEMODCOLS_BLOCK 512
+#endif
+template <int N>
+struct DemodColsCfg : KCfg<N, (N <= 1024 ? FCD_DEMODCOLS_BLOCK : BLOCK)> {};
+
 template <int N>
 struct IntColsCfg : KCfg<N, FCD_INTCOLS_BLOCK> {
     static constexpr int V = N <= 1024 ? FCD_INTCOLS_WAVES : ColWaves<N>::V;
@@ -171,10 +180,10 @@ __global__ __launch_bounds__(KCfg<W>::THREADS, FCD_MIN_WAVES) void k_demod_rows(
 
 // ------------------------------------------------------------------ K2
 template <int H>
-__global__ __launch_bounds__(KCfg<H>::THREADS, ColWaves<H>::V) void k_demod_cols(const float2* __restrict__ Xb, int nb, DemodTables T,
+__global__ __launch_bounds__(DemodColsCfg<H>::THREADS, ColWaves<H>::V) void k_demod_cols(const float2* __restrict__ Xb, int nb, DemodTables T,
                                                       float2* __restrict__ Ab, int NCA,
                                                       const float2* __restrict__ tw) {
-    using C = KCfg<H>;
+    using C = DemodColsCfg<H>;
     constexpr int TT = C::TT, E = C::E, TEAMS = C::TEAMS;
     extern __shared__ __attribute__((aligned(16))) float2 lds_raw[];
     float2* const lds = lds_raw + C::NLEN;  // lds_raw[0, NLEN): the twiddle table
@@ -711,7 +720,7 @@ static void launch_demod_rows(const float* frames, int H, int nb, const DemodTab
 template <int H>
 static void launch_demod_cols(const float2* Xb, int nb, const DemodTables& T, float2* Ab, int NCA, const float2* tw,
                               hipStream_t s) {
-    using C = KCfg<H>;
+    using C = DemodColsCfg<H>;
     const size_t lds = (size_t)C::NLEN * 8 + (size_t)2 * C::TEAMS * C::ROW * 8;
     set_lds(k_demod_cols<H>, lds);
     const int grid = grid_for(((long)nb * T.NC + C::TEAMS - 1) / C::TEAMS, 4);
