@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define FCD_ABI_VERSION 4
+#define FCD_ABI_VERSION 5
 
 enum {
     FCD_OK = 0,
@@ -43,6 +43,12 @@ enum {
 };
 
 enum { FCD_HOST_PTRS = 0, FCD_DEVICE_PTRS = 1 };
+
+/* Flag bit of the temporal-analysis calls (OR-ed into flags): the stack holds
+ * float64 samples instead of float32.  The reference hands a float64 series to
+ * scipy / numpy unchanged (analyze.py:486-527), so it is not rounded to float32
+ * on the way in. */
+enum { FCD_STACK_F64 = 2 };
 
 /* Frame sample formats (fcd_process_raw).  The reference decodes every frame
  * to float32 on the host (analyze.load_image, analyze.py:25-40); these let the
@@ -147,7 +153,8 @@ int fcd_integrate(fcd_ctx* ctx, const float* gx, const float* gy, int n, double 
 int fcd_fft2(fcd_ctx* ctx, const float* in, int n, int flags, float* out, void* stream);
 
 /* Temporal analysis of a height-map stack.  `stack` is
- * float32 [T][rows][cols] (frame pitch rows*cols, row pitch cols; any shape,
+ * float32 [T][rows][cols], or float64 with FCD_STACK_F64 in flags (frame pitch
+ * rows*cols, row pitch cols, in elements; any shape,
  * not the context's); the block is [r0, r0 + bh) x [c0, c0 + bw), pixel
  * p = i * bw + j.  Host pointers: only the block is copied to the device.
  * All three accumulate in f64 and synchronise.
@@ -156,13 +163,13 @@ int fcd_fft2(fcd_ctx* ctx, const float* in, int n, int flags, float* out, void* 
  * (analyze.py:566-577: np.nanmean(|np.fft.fft(maps, axis=-1)|) over the
  * block's pixels, bins f < nf): sum_count (host) [nf][2] = sum of |X_p(f)|
  * over the pixels whose X_p(f) is not NaN, and their number. */
-int fcd_temporal_spectrum(fcd_ctx* ctx, const float* stack, int T, int rows, int cols, int r0, int c0, int bh, int bw,
+int fcd_temporal_spectrum(fcd_ctx* ctx, const void* stack, int T, int rows, int cols, int r0, int c0, int bh, int bw,
                           int flags, int nf, double* sum_count, void* stream);
 
 /* The harmonic bins of analyze.block_amplitude (analyze.py:579-587):
  * x_out [bh*bw][nbins] complex128 = sum_t x_p(t) exp(-2 pi i bins[k] t / T)
  * (bins host memory; x_out host or device per flags). */
-int fcd_temporal_bins(fcd_ctx* ctx, const float* stack, int T, int rows, int cols, int r0, int c0, int bh, int bw,
+int fcd_temporal_bins(fcd_ctx* ctx, const void* stack, int T, int rows, int cols, int r0, int c0, int bh, int bw,
                       int flags, const int* bins, int nbins, double* x_out, void* stream);
 
 /* analyze.spectrogram on a block (analyze.py:486-527: scipy.signal.spectrogram
@@ -170,7 +177,7 @@ int fcd_temporal_bins(fcd_ctx* ctx, const float* stack, int T, int rows, int col
  * one-sided): window float64 [nperseg] (host), segments start every
  * nperseg - noverlap samples, nseg = (T - nperseg) / (nperseg - noverlap) + 1,
  * nf = nperseg / 2 + 1; s_out float64 [bh*bw][nf][nseg]. */
-int fcd_spectrogram(fcd_ctx* ctx, const float* stack, int T, int rows, int cols, int r0, int c0, int bh, int bw,
+int fcd_spectrogram(fcd_ctx* ctx, const void* stack, int T, int rows, int cols, int r0, int c0, int bh, int bw,
                     int flags, int nperseg, int noverlap, const double* window, double fs, double* s_out,
                     void* stream);
 

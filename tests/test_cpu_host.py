@@ -28,13 +28,44 @@ def test_library_exports_every_header_symbol():
     lib = _lib.load_library()
     for name in header_symbols():
         assert hasattr(lib, name), name
-    assert lib.fcd_abi_version() == 4
+    assert lib.fcd_abi_version() == 5
 
 
 def test_library_is_gfx950_code_object():
     from pyfcd import _lib
     blob = open(_lib.LIB_PATH, "rb").read()
     assert b"amdgcn-amd-amdhsa--gfx950" in blob
+
+
+def kernel_resources(obj):
+    """{mangled kernel name: {"VGPRs": n, "Occupancy [waves/SIMD]": n, ...}} from the
+    compiler's resource report the build keeps next to each object (Makefile)."""
+    path = os.path.join(ROOT, "trapped-modes-ltg_amd", "build", obj + ".o.res")
+    out, cur = {}, None
+    for line in open(path):
+        m = re.search(r"remark: Function Name: (\S+)", line)
+        if m:
+            cur = out.setdefault(m.group(1), {})
+            continue
+        m = re.search(r"remark:\s+([^:]+): (\d+) \[", line)
+        if m and cur is not None:
+            cur[m.group(1).strip()] = int(m.group(2))
+    return out
+
+
+def test_kernel_register_budgets():
+    """The occupancy statements in the kernel comments hold for the compiled code:
+    k_demod_cols<1024> fits 128 VGPRs (two 512-thread workgroups = 16 waves per CU),
+    the fused k_phase_rows fits 256 (8 waves per CU), and no throughput kernel spills."""
+    res = kernel_resources("kernels_fast.hip")
+    dc = next(v for k, v in res.items() if k.startswith("_ZN4fcdk12k_demod_colsILi1024E"))
+    assert dc["VGPRs"] + dc["AGPRs"] <= 128 and dc["Occupancy [waves/SIMD]"] >= 4, dc
+    for name, v in res.items():
+        assert v.get("VGPRs Spill", 0) == 0 and v.get("SGPRs Spill", 0) == 0, name
+    pr = kernel_resources("kernels_phase_rows.hip")
+    for name, v in pr.items():
+        if "k_phase_rows" in name:
+            assert v["VGPRs"] + v["AGPRs"] <= 256 and v["VGPRs Spill"] == 0, (name, v)
 
 
 def test_no_silent_fallback_without_device():

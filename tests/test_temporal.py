@@ -158,12 +158,94 @@ def test_spectrogram_series():
     from pydata.analyze import analyze
     x = make_stack(1000, n=1, seed=1, zero_corner=False)[:, 0, 0]
     t, f, S = analyze.spectrogram(array=x, fs=TASA, nperseg=128)
+    assert S.dtype == np.float32  # scipy's dtype for a float32 series
     t2, f2, S2 = ora.spectrogram_series(x.astype(np.float64), fs=TASA, nperseg=128)
     assert np.array_equal(t, t2) and np.array_equal(f, f2)
-    close_nan(S, S2)
+    close_nan(S, S2, rtol=1e-6)  # f64 on the device, rounded once to float32
     # and the reference's own float32 computation, to float32 accuracy
     t3, f3, S3 = ora.spectrogram_series(x, fs=TASA, nperseg=128)
     close_nan(S, S3, rtol=1e-5)
+
+
+@pytest.fixture(params=["mfma", "valu"])
+def tdft_family(request, monkeypatch):
+    """Both kernel families: the f64 matrix-core kernels (default) and the vector-unit
+    ones (FCD_TDFT_VALU=1, read by the engine on every call)."""
+    if request.param == "valu":
+        monkeypatch.setenv("FCD_TDFT_VALU", "1")
+    else:
+        monkeypatch.delenv("FCD_TDFT_VALU", raising=False)
+    return request.param
+
+
+def offset_series(T, dtype, dc=1000.0, amp=1e-4, seed=2):
+    """A series whose mean is far larger than its fluctuation: the
+    constant detrend must not lose the fluctuation's digits."""
+    rng = np.random.default_rng(seed)
+    t = np.arange(T) / TASA
+    x = dc + amp * (np.sin(2 * np.pi * 31.0 * t) + 0.3 * rng.standard_normal(T))
+    return x.astype(dtype)
+
+
+@pytest.mark.gpu
+def test_spectrogram_series_f64_large_offset(tdft_family):
+    """A float64 series stays float64 on the device (the reference hands it to scipy
+    unchanged): equal to scipy's float64 spectrogram at 1e-9, returned as float64."""
+    from pydata.analyze import analyze
+    x = offset_series(1000, np.float64)
+    for kw in ({"nperseg": 128}, {}, {"nperseg": 100, "noverlap": 30, "window": "hann"}):
+        t, f, S = analyze.spectrogram(array=x, fs=TASA, **kw)
+        t2, f2, S2 = ora.spectrogram_series(x, fs=TASA, **kw)
+        assert S.dtype == S2.dtype == np.float64
+        assert np.array_equal(t, t2) and np.array_equal(f, f2)
+        # the samples themselves carry the fluctuation to ulp(1000) / 1e-4 ~ 1e-9
+        # relative, so two correct f64 detrends agree to a few 1e-9
+        close_nan(S, S2, rtol=1e-8)
+
+
+@pytest.mark.gpu
+def test_spectrogram_series_f32_large_offset(tdft_family):
+    """A float32 series with a large DC offset: the device detrends in f64, so it equals
+    scipy on the same samples widened to float64 (to the float32 rounding of the
+    result, which comes back float32 like scipy's)."""
+    from pydata.analyze import analyze
+    x = offset_series(1000, np.float32, amp=1e-2)
+    t, f, S = analyze.spectrogram(array=x, fs=TASA, nperseg=128)
+    assert S.dtype == np.float32
+    t2, f2, S2 = ora.spectrogram_series(x.astype(np.float64), fs=TASA, nperseg=128)
+    close_nan(S, S2, rtol=1e-6)
+
+
+@pytest.mark.gpu
+def test_spectrogram_block_large_offset(tmp_path, tdft_family):
+    """Maps far from zero (a float32 block with a 1000 offset) with NaN gaps: the gap
+    pixels are interpolated in float64 and the whole block runs as float64, as the
+    reference's per-pixel loop does."""
+    from pydata.analyze import analyze
+    st = make_stack(300, n=32, seed=4, nan_pixels=[(3, 5, 20, 30), (9, 1, 200, 202)])
+    st = st + np.float32(1000.0)
+    st[0, :5, :7] = 0.0
+    write_maps(str(tmp_path), st)
+    t, f, S, avg = analyze.spectrogram(map_folder=str(tmp_path), fs=TASA, num_blocks=4, block_index=0, nperseg=64)
+    t2, f2, S2, avg2 = ora.spectrogram_block(st.astype(np.float64), fs=TASA, num_blocks=4, block_index=0, nperseg=64)
+    close_nan(S, S2)
+    close_nan(avg, avg2)
+
+
+@pytest.mark.gpu
+def test_temporal_f64_stack_equals_widened_f32(tdft_family):
+    """FCD_STACK_F64: a float64 stack holding float32 values gives the float32 call's
+    results bit for bit (the arithmetic is f64 either way)."""
+    from pyfcd import _lib
+    eng = _lib.temporal_engine()
+    st = make_stack(257, n=24, seed=6, zero_corner=False)
+    st64 = st.astype(np.float64)
+    a = eng.temporal_spectrum(st, 129)
+    b = eng.temporal_spectrum(st64, 129)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+    assert np.array_equal(eng.temporal_bins(st, [0, 3, 128]), eng.temporal_bins(st64, [0, 3, 128]))
+    win = np.hanning(64)
+    assert np.array_equal(eng.spectrogram(st, 64, 8, win, TASA), eng.spectrogram(st64, 64, 8, win, TASA))
 
 
 @pytest.mark.gpu

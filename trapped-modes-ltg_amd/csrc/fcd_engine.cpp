@@ -1435,26 +1435,32 @@ FCD_API int fcd_fft2(fcd_ctx* c, const float* in, int n, int flags, float* out, 
 
 namespace {
 
-// The block [r0, r0 + bh) x [c0, c0 + bw) of a [T][rows][cols] float32 stack on
-// the device: the caller's own memory (device pointers) or a staged copy of
-// just the block (host pointers).  Returns the block origin and its pitches.
+// The block [r0, r0 + bh) x [c0, c0 + bw) of a [T][rows][cols] float32 (or, with
+// FCD_STACK_F64 in flags, float64) stack on the device: the caller's own memory
+// (device pointers) or a staged copy of just the block (host pointers).  Returns
+// the block origin and its pitches in elements.
 struct BlockView {
-    const float* p;
+    fcdk::Samples p;
     long frame_pitch, row_pitch;
 };
 
-BlockView stage_block(fcd_ctx* c, const float* stack, int T, int rows, int cols, int r0, int c0, int bh, int bw,
-                      bool dev, hipStream_t s) {
+BlockView stage_block(fcd_ctx* c, const void* stack, int T, int rows, int cols, int r0, int c0, int bh, int bw,
+                      int flags, hipStream_t s) {
     if (!stack || T <= 0 || rows <= 0 || cols <= 0 || bh <= 0 || bw <= 0 || r0 < 0 || c0 < 0 || r0 + bh > rows ||
         c0 + bw > cols)
         throw FcdError(FCD_E_INVALID, "bad stack / block arguments");
-    if (dev) return {stack + (long)r0 * cols + c0, (long)rows * cols, cols};
-    c->t_stage.ensure((size_t)T * bh * bw * sizeof(float));
-    float* d = c->t_stage.as<float>();
+    if (flags & ~(FCD_DEVICE_PTRS | FCD_STACK_F64)) throw FcdError(FCD_E_INVALID, "bad flags");
+    const bool dev = flags & FCD_DEVICE_PTRS, f64 = flags & FCD_STACK_F64;
+    const size_t es = f64 ? sizeof(double) : sizeof(float);
+    const char* src = static_cast<const char*>(stack);
+    if (dev) return {{src + ((size_t)r0 * cols + c0) * es, f64}, (long)rows * cols, cols};
+    c->t_stage.ensure((size_t)T * bh * bw * es);
+    char* d = static_cast<char*>(c->t_stage.p);
     for (int t = 0; t < T; ++t)
-        HIPCHK(hipMemcpy2DAsync(d + (size_t)t * bh * bw, (size_t)bw * 4, stack + ((size_t)t * rows + r0) * cols + c0,
-                                (size_t)cols * 4, (size_t)bw * 4, bh, hipMemcpyHostToDevice, s));
-    return {d, (long)bh * bw, bw};
+        HIPCHK(hipMemcpy2DAsync(d + (size_t)t * bh * bw * es, (size_t)bw * es,
+                                src + (((size_t)t * rows + r0) * cols + c0) * es, (size_t)cols * es, (size_t)bw * es,
+                                bh, hipMemcpyHostToDevice, s));
+    return {{d, f64}, (long)bh * bw, bw};
 }
 
 // exp(-2 pi i j / n), j < n, in f64 (the DFT kernels index it by (f t) mod n)
@@ -1471,13 +1477,13 @@ void upload_exp_table(fcd_ctx* c, DevBuf& buf, int n, hipStream_t s) {
 
 }  // namespace
 
-FCD_API int fcd_temporal_spectrum(fcd_ctx* c, const float* stack, int T, int rows, int cols, int r0, int c0, int bh,
+FCD_API int fcd_temporal_spectrum(fcd_ctx* c, const void* stack, int T, int rows, int cols, int r0, int c0, int bh,
                                   int bw, int flags, int nf, double* sum_count, void* stream) {
     FCD_TRY({
         check_ctx(c);
         if (!sum_count || nf <= 0 || nf > T) throw FcdError(FCD_E_INVALID, "bad spectrum arguments");
         hipStream_t s = c->pick(stream);
-        const BlockView v = stage_block(c, stack, T, rows, cols, r0, c0, bh, bw, flags == FCD_DEVICE_PTRS, s);
+        const BlockView v = stage_block(c, stack, T, rows, cols, r0, c0, bh, bw, flags, s);
         upload_exp_table(c, c->t_tab, T, s);
         const int P = bh * bw, tiles = fcdk::temporal_spectrum_tiles(P, T);
         c->t_part.ensure((size_t)tiles * nf * 2 * sizeof(double));
@@ -1498,7 +1504,7 @@ FCD_API int fcd_temporal_spectrum(fcd_ctx* c, const float* stack, int T, int row
     })
 }
 
-FCD_API int fcd_temporal_bins(fcd_ctx* c, const float* stack, int T, int rows, int cols, int r0, int c0, int bh,
+FCD_API int fcd_temporal_bins(fcd_ctx* c, const void* stack, int T, int rows, int cols, int r0, int c0, int bh,
                               int bw, int flags, const int* bins, int nbins, double* x_out, void* stream) {
     FCD_TRY({
         check_ctx(c);
@@ -1506,8 +1512,8 @@ FCD_API int fcd_temporal_bins(fcd_ctx* c, const float* stack, int T, int rows, i
         for (int i = 0; i < nbins; ++i)
             if (bins[i] < 0 || bins[i] >= T) throw FcdError(FCD_E_INVALID, "bin out of range");
         hipStream_t s = c->pick(stream);
-        const bool dev = flags == FCD_DEVICE_PTRS;
-        const BlockView v = stage_block(c, stack, T, rows, cols, r0, c0, bh, bw, dev, s);
+        const bool dev = flags & FCD_DEVICE_PTRS;
+        const BlockView v = stage_block(c, stack, T, rows, cols, r0, c0, bh, bw, flags, s);
         upload_exp_table(c, c->t_tab, T, s);
         c->t_bins.ensure((size_t)nbins * sizeof(int));
         upload(c->t_bins.p, bins, (size_t)nbins * sizeof(int), s);
@@ -1530,7 +1536,7 @@ FCD_API int fcd_temporal_bins(fcd_ctx* c, const float* stack, int T, int rows, i
     })
 }
 
-FCD_API int fcd_spectrogram(fcd_ctx* c, const float* stack, int T, int rows, int cols, int r0, int c0, int bh, int bw,
+FCD_API int fcd_spectrogram(fcd_ctx* c, const void* stack, int T, int rows, int cols, int r0, int c0, int bh, int bw,
                             int flags, int nperseg, int noverlap, const double* window, double fs, double* s_out,
                             void* stream) {
     FCD_TRY({
@@ -1539,8 +1545,8 @@ FCD_API int fcd_spectrogram(fcd_ctx* c, const float* stack, int T, int rows, int
             throw FcdError(FCD_E_INVALID, "bad spectrogram arguments");
         if (nperseg > fcdk::spectro_max_nperseg()) throw FcdError(FCD_E_UNSUPPORTED, "nperseg too large");
         hipStream_t s = c->pick(stream);
-        const bool dev = flags == FCD_DEVICE_PTRS;
-        const BlockView v = stage_block(c, stack, T, rows, cols, r0, c0, bh, bw, dev, s);
+        const bool dev = flags & FCD_DEVICE_PTRS;
+        const BlockView v = stage_block(c, stack, T, rows, cols, r0, c0, bh, bw, flags, s);
         const int step = nperseg - noverlap, nseg = (T - nperseg) / step + 1, nf = nperseg / 2 + 1;
         // window, its DFT W_f (the mean-removal term) and the density scale, in f64
         std::vector<double2> tab(nperseg), wsum(nf);

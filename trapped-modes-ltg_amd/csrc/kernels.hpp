@@ -132,14 +132,19 @@ void integ_multiply(const float2* Z, float2* Hh, int nbatch, int H, int W, Integ
 // phases f32 = w + 2pi k
 void compose_phase(const float* w, const int32_t* k, float* out, long n, hipStream_t s);
 
-// temporal analysis of a map stack (kernels_temporal.hip)
-void temporal_dft(const float* stack, long frame_pitch, long row_pitch, int bw, int P, int T, const double2* tab,
+// temporal analysis of a map stack (kernels_temporal.hip): samples float32 or
+// float64 (the reference keeps a float64 series in float64)
+struct Samples {
+    const void* p;
+    bool f64;
+};
+void temporal_dft(Samples stack, long frame_pitch, long row_pitch, int bw, int P, int T, const double2* tab,
                   const int* freqs, int nf, double2* out, double* partial, double2* slices, hipStream_t s);
 int temporal_dft_tiles(int P);
 int temporal_spectrum_tiles(int P, int T);  // partial-sum rows of a mean-spectrum call
 int temporal_bins_slices(int P, int nf, int T);  // slices[slices][P][nf] workspace of a bins call
 int spectro_max_nperseg();
-void spectrogram(const float* stack, long frame_pitch, long row_pitch, int bw, int P, int nperseg, int step, int nseg,
+void spectrogram(Samples stack, long frame_pitch, long row_pitch, int bw, int P, int nperseg, int step, int nseg,
                  const double* win, const double2* tab, const double2* wsum, int nf, double scale, double* out,
                  hipStream_t s);
 

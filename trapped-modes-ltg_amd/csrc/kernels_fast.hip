@@ -46,8 +46,10 @@ constexpr int BLOCK = 256;
 #ifndef FCD_MIN_WAVES
 #define FCD_MIN_WAVES 4
 #endif
-// The column kernels hold two transforms' worth of state (130-186 VGPRs
-// unconstrained): 3 waves/SIMD (168 VGPRs) up to 2048 points, 2 at 4096.
+// Minimum waves per SIMD of k_demod_cols above 1024 points (its 1024-point
+// form has its own, DemodColsCfg::V); 4096 points always 2.  The register
+// counts each kernel compiles to are in build/*.res (-Rpass-analysis), and
+// tests/test_cpu_host.py checks the ones the occupancy statements here rely on.
 #ifndef FCD_COL_WAVES
 #define FCD_COL_WAVES 2
 #endif
@@ -92,13 +94,17 @@ struct KCfg {
 #define FCD_INTCOLS_PREF_X 1
 #endif
 // Workgroup size of k_demod_cols up to 1024 points: 4 teams share one twiddle
-// table, 78 KB of LDS -> 2 workgroups = 16 waves per CU at 1024 (12 with 256
-// threads): 0.84 vs 0.89 us/frame (kbench r01cd).  Larger transforms keep 256.
+// table, 78 KB of LDS -> 2 workgroups = 16 waves per CU at 1024, which needs
+// <= 128 VGPRs, i.e. launch bounds of 4 waves per SIMD (compiles to 122):
+// 0.84 vs 0.89 us/frame in isolation (kbench r01cd; 12 waves per CU with 256
+// threads).  Larger transforms keep 256-thread workgroups.
 #ifndef FCD_DEMODCOLS_BLOCK
 #define FCD_DEMODCOLS_BLOCK 512
 #endif
 template <int N>
-struct DemodColsCfg : KCfg<N, (N <= 1024 ? FCD_DEMODCOLS_BLOCK : BLOCK)> {};
+struct DemodColsCfg : KCfg<N, (N <= 1024 ? FCD_DEMODCOLS_BLOCK : BLOCK)> {
+    static constexpr int V = N <= 1024 ? 4 : ColWaves<N>::V;
+};
 
 template <int N>
 struct IntColsCfg : KCfg<N, FCD_INTCOLS_BLOCK> {
@@ -180,7 +186,7 @@ __global__ __launch_bounds__(KCfg<W>::THREADS, FCD_MIN_WAVES) void k_demod_rows(
 
 // ------------------------------------------------------------------ K2
 template <int H>
-__global__ __launch_bounds__(DemodColsCfg<H>::THREADS, ColWaves<H>::V) void k_demod_cols(const float2* __restrict__ Xb, int nb, DemodTables T,
+__global__ __launch_bounds__(DemodColsCfg<H>::THREADS, DemodColsCfg<H>::V) void k_demod_cols(const float2* __restrict__ Xb, int nb, DemodTables T,
                                                       float2* __restrict__ Ab, int NCA,
                                                       const float2* __restrict__ tw) {
     using C = DemodColsCfg<H>;

@@ -1,5 +1,6 @@
 // Temporal analysis of a height-map stack: per-pixel
-// DFTs along time for a spatial block of a [T][rows][cols] float32 stack, as
+// DFTs along time for a spatial block of a [T][rows][cols] float32 or float64
+// stack (the sample type is a template parameter; arithmetic is f64 either way), as
 // analyze.block_amplitude (analyze.py:543-587: np.fft.fft over time, f64) and
 // analyze.spectrogram (analyze.py:419-531: scipy.signal.spectrogram per pixel).
 //
@@ -42,8 +43,8 @@ __device__ __forceinline__ long pix_off(int p, int bw, long row_pitch) { return 
 //           their count (np.nanmean's numerator / denominator) -> partial
 //           [gridDim.x][nf][2]; X itself is not stored.
 //   else:   X -> out [P][nf] (complex f64).
-template <bool REDUCE, bool LDS>
-__global__ __launch_bounds__(TD_THREADS) void k_tdft(const float* __restrict__ stack, long frame_pitch, long row_pitch,
+template <bool REDUCE, bool LDS, typename S>
+__global__ __launch_bounds__(TD_THREADS) void k_tdft(const S* __restrict__ stack, long frame_pitch, long row_pitch,
                                                      int bw, int P, int T, const double2* __restrict__ tab,
                                                      const int* __restrict__ freqs, int nf, double2* __restrict__ out,
                                                      double* __restrict__ partial, int tchunk) {
@@ -61,7 +62,7 @@ __global__ __launch_bounds__(TD_THREADS) void k_tdft(const float* __restrict__ s
     // LDS broadcast instead of 2)
     const int p0 = (blockIdx.x * TD_THREADS + threadIdx.x) * PX;
     bool live[PX];
-    const float* xs[PX];
+    const S* xs[PX];
 #pragma unroll
     for (int u = 0; u < PX; ++u) {
         live[u] = p0 + u < P;
@@ -79,7 +80,7 @@ __global__ __launch_bounds__(TD_THREADS) void k_tdft(const float* __restrict__ s
 #pragma unroll
         for (int u = 0; u < PX; ++u) re[u][k] = im[u][k] = 0.0;
     }
-    auto step = [&](const float (&x)[PX]) {
+    auto step = [&](const S (&x)[PX]) {
 #pragma unroll
         for (int k = 0; k < FT; ++k) {
             const double2 w = tb[idx[k]];  // wave-uniform index: an LDS broadcast
@@ -96,7 +97,7 @@ __global__ __launch_bounds__(TD_THREADS) void k_tdft(const float* __restrict__ s
     // pixel and wave (few-bin calls have little arithmetic per sample to hide the latency)
     int t = t0;
     for (; t + TD_BATCH <= t1; t += TD_BATCH) {
-        float xb[TD_BATCH][PX];
+        S xb[TD_BATCH][PX];
 #pragma unroll
         for (int v = 0; v < TD_BATCH; ++v)
 #pragma unroll
@@ -105,7 +106,7 @@ __global__ __launch_bounds__(TD_THREADS) void k_tdft(const float* __restrict__ s
         for (int v = 0; v < TD_BATCH; ++v) step(xb[v]);
     }
     for (; t < t1; ++t) {
-        float x1[PX];
+        S x1[PX];
 #pragma unroll
         for (int u = 0; u < PX; ++u) x1[u] = __builtin_nontemporal_load(xs[u] + (long)t * frame_pitch);
         step(x1);
@@ -172,7 +173,8 @@ constexpr int TM_WM = FCD_TM_WM, TM_WN = FCD_TM_WN;
 constexpr int TM_PIX = 4 * 16 * TM_WM;  // pixels per workgroup (4 waves)
 constexpr int TM_BINS = 8 * TM_WN;      // bins per workgroup
 
-__global__ __launch_bounds__(TD_THREADS) void k_tdft_mfma(const float* __restrict__ stack, long frame_pitch,
+template <typename S>
+__global__ __launch_bounds__(TD_THREADS) void k_tdft_mfma(const S* __restrict__ stack, long frame_pitch,
                                                           long row_pitch, int bw, int P, int T,
                                                           const double2* __restrict__ tab, int nf,
                                                           double* __restrict__ partial) {
@@ -185,7 +187,7 @@ __global__ __launch_bounds__(TD_THREADS) void k_tdft_mfma(const float* __restric
     const int pbase = blockIdx.x * TM_PIX + wave * 16 * TM_WM;
     const int fbase = blockIdx.y * TM_BINS;
     // A rows of this lane: pixels pbase + 16 m + col
-    const float* xs[TM_WM];
+    const S* xs[TM_WM];
     bool live[TM_WM];
 #pragma unroll
     for (int m = 0; m < TM_WM; ++m) {
@@ -208,7 +210,7 @@ __global__ __launch_bounds__(TD_THREADS) void k_tdft_mfma(const float* __restric
     for (int m = 0; m < TM_WM; ++m)
 #pragma unroll
         for (int n = 0; n < TM_WN; ++n) acc[m][n] = dv4{0.0, 0.0, 0.0, 0.0};
-    auto kstep = [&](const float (&xa)[TM_WM], int t) {
+    auto kstep = [&](const S (&xa)[TM_WM], int t) {
         double a[TM_WM], b[TM_WN];
 #pragma unroll
         for (int m = 0; m < TM_WM; ++m) a[m] = t + kq < T ? (double)xa[m] : 0.0;
@@ -228,7 +230,7 @@ __global__ __launch_bounds__(TD_THREADS) void k_tdft_mfma(const float* __restric
     constexpr int TM_B = 4;
     int t = 0;
     for (; t < T; t += 4 * TM_B) {
-        float xa[TM_B][TM_WM];
+        S xa[TM_B][TM_WM];
 #pragma unroll
         for (int q = 0; q < TM_B; ++q) {
             const int tt = min(t + 4 * q + kq, T - 1);  // clamped: samples past T are zeroed in kstep
@@ -280,7 +282,8 @@ __global__ __launch_bounds__(TD_THREADS) void k_tdft_mfma(const float* __restric
 // X[p][2f+e] = sum_n x_p(s0 + n) w_n E[n][2f+e] (B = window x table, gathered per
 // lane), the segment means from the A fragments (x_p summed over the lanes holding
 // pixel p's samples), then S = |X - mean W_f|^2 scale (x2 off DC / Nyquist).
-__global__ __launch_bounds__(TD_THREADS) void k_spectro_mfma(const float* __restrict__ stack, long frame_pitch,
+template <typename S>
+__global__ __launch_bounds__(TD_THREADS) void k_spectro_mfma(const S* __restrict__ stack, long frame_pitch,
                                                              long row_pitch, int bw, int P, int nperseg, int step,
                                                              int nseg, const double* __restrict__ win,
                                                              const double2* __restrict__ tab,
@@ -300,7 +303,7 @@ __global__ __launch_bounds__(TD_THREADS) void k_spectro_mfma(const float* __rest
     const int pbase = blockIdx.x * TM_PIX + wave * 16 * TM_WM;
     const int seg = blockIdx.y;
     const int fbase = blockIdx.z * TM_BINS;
-    const float* xs[TM_WM];
+    const S* xs[TM_WM];
 #pragma unroll
     for (int m = 0; m < TM_WM; ++m) {
         const int p = pbase + 16 * m + col;
@@ -324,7 +327,7 @@ __global__ __launch_bounds__(TD_THREADS) void k_spectro_mfma(const float* __rest
     }
     constexpr int TM_B = 4;
     for (int n0 = 0; n0 < nperseg; n0 += 4 * TM_B) {
-        float xa[TM_B][TM_WM];
+        S xa[TM_B][TM_WM];
 #pragma unroll
         for (int q = 0; q < TM_B; ++q) {
             const int nn = min(n0 + 4 * q + kq, nperseg - 1);  // clamped: samples past the segment are zeroed
@@ -405,7 +408,8 @@ __global__ __launch_bounds__(TD_THREADS) void k_tdft_sum(const double2* __restri
 //   W_f = sum_n w_n e_fn (host, f64), so the segment is read once;
 //   S_f = |X_f|^2 * scale, doubled except at DC and (even nperseg) Nyquist.
 // out [P][nf][nseg]; grid (pixel tiles, segments, frequency tiles).
-__global__ __launch_bounds__(TD_THREADS) void k_spectro(const float* __restrict__ stack, long frame_pitch,
+template <typename S>
+__global__ __launch_bounds__(TD_THREADS) void k_spectro(const S* __restrict__ stack, long frame_pitch,
                                                         long row_pitch, int bw, int P, int nperseg, int step,
                                                         int nseg, const double* __restrict__ win,
                                                         const double2* __restrict__ tab,
@@ -423,7 +427,7 @@ __global__ __launch_bounds__(TD_THREADS) void k_spectro(const float* __restrict_
     const int p0 = (blockIdx.x * TD_THREADS + threadIdx.x) * PX;
     const int seg = blockIdx.y;
     bool live[PX];
-    const float* xs[PX];
+    const S* xs[PX];
 #pragma unroll
     for (int u = 0; u < PX; ++u) {
         live[u] = p0 + u < P;
@@ -441,7 +445,7 @@ __global__ __launch_bounds__(TD_THREADS) void k_spectro(const float* __restrict_
     }
 #pragma unroll
     for (int u = 0; u < PX; ++u) sum[u] = 0.0;
-    auto sample = [&](int n, const float (&x)[PX]) {
+    auto sample = [&](int n, const S (&x)[PX]) {
         const double wn = wl[n];
         double xw[PX];
 #pragma unroll
@@ -463,7 +467,7 @@ __global__ __launch_bounds__(TD_THREADS) void k_spectro(const float* __restrict_
     };
     int n = 0;  // unconditional batched loads, as k_tdft
     for (; n + TD_BATCH <= nperseg; n += TD_BATCH) {
-        float xb[TD_BATCH][PX];
+        S xb[TD_BATCH][PX];
 #pragma unroll
         for (int v = 0; v < TD_BATCH; ++v)
 #pragma unroll
@@ -472,7 +476,7 @@ __global__ __launch_bounds__(TD_THREADS) void k_spectro(const float* __restrict_
         for (int v = 0; v < TD_BATCH; ++v) sample(n + v, xb[v]);
     }
     for (; n < nperseg; ++n) {
-        float x1[PX];
+        S x1[PX];
 #pragma unroll
         for (int u = 0; u < PX; ++u) x1[u] = xs[u][(long)n * frame_pitch];
         sample(n, x1);
@@ -511,26 +515,27 @@ int temporal_bins_slices(int P, int nf, int T) {
     return (int)std::max(1L, std::min(want, (long)T / 256));
 }
 
+// FCD_TDFT_VALU=1 selects the vector-unit kernels (read per call, so one process
+// can test both families)
 static bool spectrum_on_mfma(int T) {
-    static const bool off = [] {
-        const char* e = std::getenv("FCD_TDFT_VALU");
-        return e && e[0] == '1';
-    }();
-    return !off && T <= TD_LDS_TAB;
+    const char* e = std::getenv("FCD_TDFT_VALU");
+    return !(e && e[0] == '1') && T <= TD_LDS_TAB;
 }
 
 int temporal_spectrum_tiles(int P, int T) {
     return spectrum_on_mfma(T) ? (P + TM_PIX - 1) / TM_PIX : temporal_dft_tiles(P);
 }
 
-void temporal_dft(const float* stack, long frame_pitch, long row_pitch, int bw, int P, int T, const double2* tab,
-                  const int* freqs, int nf, double2* out, double* partial, double2* slices, hipStream_t s) {
-    if (P <= 0 || T <= 0 || nf <= 0) return;
+namespace {
+
+template <typename S>
+void temporal_dft_t(const S* stack, long frame_pitch, long row_pitch, int bw, int P, int T, const double2* tab,
+                    const int* freqs, int nf, double2* out, double* partial, double2* slices, hipStream_t s) {
     if (partial && !freqs && spectrum_on_mfma(T)) {
         const dim3 g((unsigned)((P + TM_PIX - 1) / TM_PIX), (unsigned)((nf + TM_BINS - 1) / TM_BINS));
         const size_t lb = (size_t)T * sizeof(double2);
-        (void)hipFuncSetAttribute((const void*)k_tdft_mfma, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb);
-        hipLaunchKernelGGL(k_tdft_mfma, g, dim3(TD_THREADS), lb, s, stack, frame_pitch, row_pitch, bw, P, T, tab, nf,
+        (void)hipFuncSetAttribute((const void*)k_tdft_mfma<S>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb);
+        hipLaunchKernelGGL(k_tdft_mfma<S>, g, dim3(TD_THREADS), lb, s, stack, frame_pitch, row_pitch, bw, P, T, tab, nf,
                            partial);
         check_launch("temporal_dft (mfma)");
         return;
@@ -544,20 +549,22 @@ void temporal_dft(const float* stack, long frame_pitch, long row_pitch, int bw, 
     if (nz > 1 && !slices) throw std::runtime_error("temporal_dft: slice workspace missing");
     if (partial) {
         if (lds) {
-            (void)hipFuncSetAttribute((const void*)k_tdft<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb);
-            hipLaunchKernelGGL((k_tdft<true, true>), grid, dim3(TD_THREADS), lb, s, stack, frame_pitch, row_pitch, bw,
-                               P, T, tab, freqs, nf, dst, partial, tchunk);
+            (void)hipFuncSetAttribute((const void*)k_tdft<true, true, S>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)lb);
+            hipLaunchKernelGGL((k_tdft<true, true, S>), grid, dim3(TD_THREADS), lb, s, stack, frame_pitch, row_pitch,
+                               bw, P, T, tab, freqs, nf, dst, partial, tchunk);
         } else {
-            hipLaunchKernelGGL((k_tdft<true, false>), grid, dim3(TD_THREADS), 0, s, stack, frame_pitch, row_pitch, bw,
-                               P, T, tab, freqs, nf, dst, partial, tchunk);
+            hipLaunchKernelGGL((k_tdft<true, false, S>), grid, dim3(TD_THREADS), 0, s, stack, frame_pitch, row_pitch,
+                               bw, P, T, tab, freqs, nf, dst, partial, tchunk);
         }
     } else {
         if (lds) {
-            (void)hipFuncSetAttribute((const void*)k_tdft<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb);
-            hipLaunchKernelGGL((k_tdft<false, true>), grid, dim3(TD_THREADS), lb, s, stack, frame_pitch, row_pitch,
+            (void)hipFuncSetAttribute((const void*)k_tdft<false, true, S>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)lb);
+            hipLaunchKernelGGL((k_tdft<false, true, S>), grid, dim3(TD_THREADS), lb, s, stack, frame_pitch, row_pitch,
                                bw, P, T, tab, freqs, nf, dst, partial, tchunk);
         } else {
-            hipLaunchKernelGGL((k_tdft<false, false>), grid, dim3(TD_THREADS), 0, s, stack, frame_pitch, row_pitch,
+            hipLaunchKernelGGL((k_tdft<false, false, S>), grid, dim3(TD_THREADS), 0, s, stack, frame_pitch, row_pitch,
                                bw, P, T, tab, freqs, nf, dst, partial, tchunk);
         }
         if (nz > 1) {
@@ -569,28 +576,53 @@ void temporal_dft(const float* stack, long frame_pitch, long row_pitch, int bw, 
     check_launch("temporal_dft");
 }
 
-int temporal_dft_tiles(int P) { return (P + TD_THREADS * TD_PX - 1) / (TD_THREADS * TD_PX); }
-
-int spectro_max_nperseg() { return 160 * 1024 / 24; }
-
-void spectrogram(const float* stack, long frame_pitch, long row_pitch, int bw, int P, int nperseg, int step, int nseg,
-                 const double* win, const double2* tab, const double2* wsum, int nf, double scale, double* out,
-                 hipStream_t s) {
-    if (P <= 0 || nseg <= 0) return;
+template <typename S>
+void spectrogram_t(const S* stack, long frame_pitch, long row_pitch, int bw, int P, int nperseg, int step, int nseg,
+                   const double* win, const double2* tab, const double2* wsum, int nf, double scale, double* out,
+                   hipStream_t s) {
     const size_t lb = (size_t)nperseg * (sizeof(double2) + sizeof(double));
     if (spectrum_on_mfma(0)) {
         const dim3 g((unsigned)((P + TM_PIX - 1) / TM_PIX), (unsigned)nseg, (unsigned)((nf + TM_BINS - 1) / TM_BINS));
-        (void)hipFuncSetAttribute((const void*)k_spectro_mfma, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb);
-        hipLaunchKernelGGL(k_spectro_mfma, g, dim3(TD_THREADS), lb, s, stack, frame_pitch, row_pitch, bw, P, nperseg,
+        (void)hipFuncSetAttribute((const void*)k_spectro_mfma<S>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb);
+        hipLaunchKernelGGL(k_spectro_mfma<S>, g, dim3(TD_THREADS), lb, s, stack, frame_pitch, row_pitch, bw, P, nperseg,
                            step, nseg, win, tab, wsum, nf, scale, out);
         check_launch("spectrogram (mfma)");
         return;
     }
     const dim3 grid((unsigned)temporal_dft_tiles(P), (unsigned)nseg, (unsigned)((nf + TD_FT_DFT - 1) / TD_FT_DFT));
-    (void)hipFuncSetAttribute((const void*)k_spectro, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb);
-    hipLaunchKernelGGL(k_spectro, grid, dim3(TD_THREADS), lb, s, stack, frame_pitch, row_pitch, bw, P, nperseg, step,
+    (void)hipFuncSetAttribute((const void*)k_spectro<S>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb);
+    hipLaunchKernelGGL(k_spectro<S>, grid, dim3(TD_THREADS), lb, s, stack, frame_pitch, row_pitch, bw, P, nperseg, step,
                        nseg, win, tab, wsum, nf, scale, out);
     check_launch("spectrogram");
+}
+
+}  // namespace
+
+void temporal_dft(Samples stack, long frame_pitch, long row_pitch, int bw, int P, int T, const double2* tab,
+                  const int* freqs, int nf, double2* out, double* partial, double2* slices, hipStream_t s) {
+    if (P <= 0 || T <= 0 || nf <= 0) return;
+    if (stack.f64)
+        temporal_dft_t(static_cast<const double*>(stack.p), frame_pitch, row_pitch, bw, P, T, tab, freqs, nf, out,
+                       partial, slices, s);
+    else
+        temporal_dft_t(static_cast<const float*>(stack.p), frame_pitch, row_pitch, bw, P, T, tab, freqs, nf, out,
+                       partial, slices, s);
+}
+
+int temporal_dft_tiles(int P) { return (P + TD_THREADS * TD_PX - 1) / (TD_THREADS * TD_PX); }
+
+int spectro_max_nperseg() { return 160 * 1024 / 24; }
+
+void spectrogram(Samples stack, long frame_pitch, long row_pitch, int bw, int P, int nperseg, int step, int nseg,
+                 const double* win, const double2* tab, const double2* wsum, int nf, double scale, double* out,
+                 hipStream_t s) {
+    if (P <= 0 || nseg <= 0) return;
+    if (stack.f64)
+        spectrogram_t(static_cast<const double*>(stack.p), frame_pitch, row_pitch, bw, P, nperseg, step, nseg, win, tab,
+                      wsum, nf, scale, out, s);
+    else
+        spectrogram_t(static_cast<const float*>(stack.p), frame_pitch, row_pitch, bw, P, nperseg, step, nseg, win, tab,
+                      wsum, nf, scale, out, s);
 }
 
 }  // namespace fcdk

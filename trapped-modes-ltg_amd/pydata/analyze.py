@@ -312,7 +312,11 @@ class analyze:
                 raise ValueError("Any map_folder or array is needed")
             x = np.asarray(array)
             nperseg, noverlap, win, f, t = cls._spectro_params(len(x), fs, kwargs)
-            S = eng.spectrogram(x.astype(np.float32).reshape(-1, 1, 1), nperseg, noverlap, win, fs)[0, 0]
+            # scipy keeps a float32 series in float32 and computes everything else in
+            # float64: the series goes to the device in its own precision (float64 is
+            # not rounded to float32 first) and S comes back in scipy's dtype
+            dt = np.float32 if x.dtype == np.float32 else np.float64
+            S = eng.spectrogram(x.astype(dt).reshape(-1, 1, 1), nperseg, noverlap, win, fs)[0, 0].astype(dt)
             if show:
                 cls._show_spectrogram(t, f, S, "Spectrogram of some point")
             return t, f, S
@@ -324,6 +328,9 @@ class analyze:
         bad = np.isnan(stack)
         part = bad.any(axis=0) & ~bad.all(axis=0)
         if part.any():  # NaN gaps inside a pixel's series: linear fill (analyze.py:512-517)
+            # np.interp returns float64 and the reference keeps those pixels in float64:
+            # the whole stack goes to the device as float64 (exact for the float32 pixels)
+            stack = stack.astype(np.float64)
             ar = np.arange(N)
             for iy, ix in zip(*np.nonzero(part)):
                 ts = stack[:, iy, ix]

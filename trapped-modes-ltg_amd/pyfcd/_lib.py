@@ -22,6 +22,7 @@ FCD_E_NOPEAKS = -5
 FCD_E_INTERNAL = -6
 FCD_HOST_PTRS = 0
 FCD_DEVICE_PTRS = 1
+FCD_STACK_F64 = 2  # temporal calls: float64 samples
 # frame sample formats (fcd_process_raw)
 FCD_FMT_F32 = 0
 FCD_FMT_U8 = 1
@@ -292,42 +293,46 @@ class Engine:
     # ---- temporal analysis of a [T][rows][cols] float32 map stack
     @staticmethod
     def _stack(stack, block):
+        """(contiguous stack, dims, flags): float64 stacks stay float64 (FCD_STACK_F64),
+        as the reference hands them to numpy / scipy unchanged; everything else goes
+        as float32."""
         st = np.asarray(stack)
         if st.ndim != 3:
             raise ValueError("stack must be [T, rows, cols]")
-        if st.dtype != np.float32 or not st.flags.c_contiguous:
-            st = np.ascontiguousarray(st, dtype=np.float32)
+        dt = np.float64 if st.dtype == np.float64 else np.float32
+        if st.dtype != dt or not st.flags.c_contiguous:
+            st = np.ascontiguousarray(st, dtype=dt)
         T, rows, cols = st.shape
         r0, c0, bh, bw = block if block is not None else (0, 0, rows, cols)
-        return st, (int(T), int(rows), int(cols), int(r0), int(c0), int(bh), int(bw))
+        flags = FCD_HOST_PTRS | (FCD_STACK_F64 if dt == np.float64 else 0)
+        return st, (int(T), int(rows), int(cols), int(r0), int(c0), int(bh), int(bw)), flags
 
     def temporal_spectrum(self, stack, nf, block=None):
         """(sum of |X(f)| over non-NaN pixels, their count) for bins f < nf of the
         temporal DFT of every pixel of the block (r0, c0, bh, bw)."""
-        st, dims = self._stack(stack, block)
+        st, dims, flags = self._stack(stack, block)
         sc = np.empty((int(nf), 2), np.float64)
-        _check(self._lib.fcd_temporal_spectrum(self._h, st.ctypes.data, *dims, FCD_HOST_PTRS, int(nf), sc.ctypes.data,
-                                               None))
+        _check(self._lib.fcd_temporal_spectrum(self._h, st.ctypes.data, *dims, flags, int(nf), sc.ctypes.data, None))
         return sc[:, 0], sc[:, 1]
 
     def temporal_bins(self, stack, bins, block=None):
         """complex128 [bh, bw, len(bins)]: the temporal DFT of every pixel at `bins`."""
-        st, dims = self._stack(stack, block)
+        st, dims, flags = self._stack(stack, block)
         b = np.ascontiguousarray(bins, dtype=np.int32)
         out = np.empty((dims[5], dims[6], len(b)), np.complex128)
-        _check(self._lib.fcd_temporal_bins(self._h, st.ctypes.data, *dims, FCD_HOST_PTRS, b.ctypes.data, len(b),
+        _check(self._lib.fcd_temporal_bins(self._h, st.ctypes.data, *dims, flags, b.ctypes.data, len(b),
                                            out.ctypes.data, None))
         return out
 
     def spectrogram(self, stack, nperseg, noverlap, window, fs, block=None):
         """float64 [bh, bw, nperseg // 2 + 1, nseg] one-sided PSD of every pixel's series."""
-        st, dims = self._stack(stack, block)
+        st, dims, flags = self._stack(stack, block)
         w = np.ascontiguousarray(window, dtype=np.float64)
         if w.shape != (int(nperseg),):
             raise ValueError("window length must equal nperseg")
         nseg = (dims[0] - nperseg) // (nperseg - noverlap) + 1
         out = np.empty((dims[5], dims[6], nperseg // 2 + 1, max(nseg, 0)), np.float64)
-        _check(self._lib.fcd_spectrogram(self._h, st.ctypes.data, *dims, FCD_HOST_PTRS, int(nperseg), int(noverlap),
+        _check(self._lib.fcd_spectrogram(self._h, st.ctypes.data, *dims, flags, int(nperseg), int(noverlap),
                                          w.ctypes.data, float(fs), out.ctypes.data, None))
         return out
 
