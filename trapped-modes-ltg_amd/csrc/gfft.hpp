@@ -390,4 +390,46 @@ __device__ __forceinline__ fv2 wrapped_phase_pk(fv2 theta, float2 u0, float2 u1)
     return fv2{rintf(q.x), rintf(q.y)} * -6.28318530717959f + d;
 }
 
+// wrapped_phase_pk for NP pixel pairs at once, written stage by stage so that
+// the NP independent chains interleave: back-to-back dependent packed-FP32 ops
+// (the Horner steps) and a v_cndmask right behind the v_cmp that writes its mask
+// each cost the issuing wave an s_nop on gfx950; NP chains side by side fill
+// those slots with the other pairs' work.  Same operations, order and result per
+// pixel as wrapped_phase_pk.
+template <int NP>
+__device__ __forceinline__ void wrapped_phase_pkn(const fv2 (&theta)[NP], const float2 (&u)[2 * NP], fv2 (&out)[NP]) {
+    fv2 r[NP], s[NP], p[NP];
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+        const float2 u0 = u[2 * k], u1 = u[2 * k + 1];
+        const float mx0 = fmaxf(fmaxf(fabsf(u0.x), fabsf(u0.y)), 1.17549435e-38f);
+        const float mx1 = fmaxf(fmaxf(fabsf(u1.x), fabsf(u1.y)), 1.17549435e-38f);
+        const fv2 mn = {fminf(fabsf(u0.x), fabsf(u0.y)), fminf(fabsf(u1.x), fabsf(u1.y))};
+        r[k] = mn * fv2{__builtin_amdgcn_rcpf(mx0), __builtin_amdgcn_rcpf(mx1)};
+    }
+#pragma unroll
+    for (int k = 0; k < NP; ++k) s[k] = r[k] * r[k];
+    constexpr float C[9] = {0.0024567286018282175f, -0.014401371590793133f, 0.03978124260902405f,
+                            -0.07234858721494675f,  0.10498946160078049f,   -0.14161229133605957f,
+                            0.19985906779766083f,   -0.33332598209381104f,  0.9999998807907104f};
+#pragma unroll
+    for (int k = 0; k < NP; ++k) p[k] = s[k] * C[0] + C[1];
+#pragma unroll
+    for (int c = 2; c < 9; ++c)
+#pragma unroll
+        for (int k = 0; k < NP; ++k) p[k] = p[k] * s[k] + C[c];
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+        const float2 u0 = u[2 * k], u1 = u[2 * k + 1];
+        fv2 a = r[k] * p[k];
+        a.x = fabsf(u0.y) > fabsf(u0.x) ? 1.57079632679489662f - a.x : a.x;
+        a.y = fabsf(u1.y) > fabsf(u1.x) ? 1.57079632679489662f - a.y : a.y;
+        a.x = u0.x < 0.f ? 3.14159265358979324f - a.x : a.x;
+        a.y = u1.x < 0.f ? 3.14159265358979324f - a.y : a.y;
+        const fv2 d = theta[k] - fv2{copysignf(a.x, u0.y), copysignf(a.y, u1.y)};
+        const fv2 q = d * 0.159154943091895f;
+        out[k] = fv2{rintf(q.x), rintf(q.y)} * -6.28318530717959f + d;
+    }
+}
+
 }  // namespace fcdk

@@ -55,6 +55,10 @@ namespace {
 #define FCD_BAND_NOSTORE 0  // diagnostic ablation only (no output): phase stores suppressed
 #endif
 
+#ifndef FCD_ATAN_N
+#define FCD_ATAN_N 2  // pixel pairs per interleaved atan2 group (wrapped_phase_pkn); 0: the per-pair form
+#endif
+
 #ifndef FCD_ATAN_GROUP
 #define FCD_ATAN_GROUP 4  // atan2 chains interleaved per scheduling group (0: unbounded)
 #endif
@@ -197,6 +201,33 @@ __global__ __launch_bounds__((BPCfg<W, B>::THREADS), FCD_BAND_WAVES) void k_band
             if constexpr (!(FCD_BAND_ABL & 1)) fft.template run_half<true>(x, s, t);  // 1: no transform
             STAMP(st++);
             float* o = out + row * W;
+#if FCD_ATAN_N > 0
+            if constexpr (!REF && !FCD_BAND_ABL) {
+                // FCD_ATAN_N pixel pairs per interleaved group (wrapped_phase_pkn)
+#pragma unroll
+                for (int q0 = 0; q0 < E; q0 += 2 * FCD_ATAN_N) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    fv2 tq[FCD_ATAN_N], wq[FCD_ATAN_N];
+                    float2 uq[2 * FCD_ATAN_N];
+#pragma unroll
+                    for (int k = 0; k < FCD_ATAN_N; ++k) {
+                        tq[k] = fv2{thc[q0 + 2 * k], thc[q0 + 2 * k + 1]};
+                        uq[2 * k] = x[q0 + 2 * k];
+                        uq[2 * k + 1] = x[q0 + 2 * k + 1];
+                    }
+                    wrapped_phase_pkn<FCD_ATAN_N>(tq, uq, wq);
+#pragma unroll
+                    for (int k = 0; k < FCD_ATAN_N; ++k) {
+                        const int n = g + L * t + RL * (q0 + 2 * k);
+                        if (!FCD_BAND_NOSTORE || wq[k].x == 1234.5f) {
+                            st_stream(o + n, wq[k].x);
+                            st_stream(o + n + RL, wq[k].y);
+                        }
+                    }
+                }
+            } else
+#endif
+            {
 #pragma unroll
             for (int q = 0; q < E; q += 2) {  // pixel pairs: packed atan2 / wrap
                 if (FCD_ATAN_GROUP && q % FCD_ATAN_GROUP == 0) __builtin_amdgcn_sched_barrier(0);  // bound the atan2 chains in flight
@@ -216,6 +247,7 @@ __global__ __launch_bounds__((BPCfg<W, B>::THREADS), FCD_BAND_WAVES) void k_band
                         st_stream(o + n + RL, w.y);
                     }
                 }
+            }
             }
             STAMP(st++);
         }

@@ -51,6 +51,15 @@ constexpr int PR_ROWS = FCD_PR_ROWS;  // rows per tile (one wave each)
 #ifndef FCD_PR_THETA_LATE
 #define FCD_PR_THETA_LATE 1  // paired path: reference angles loaded after the transforms (register pressure)
 #endif
+#ifndef FCD_PR_PKUNWRAP
+#define FCD_PR_PKUNWRAP 1  // unwrap / census on packed pairs of both maps (0: the integer-code form)
+#endif
+#ifndef FCD_PR_ABL
+#define FCD_PR_ABL 0  // diagnostic ablations only (wrong results): 1 no reference-angle loads, 2 no Zt stores
+#endif
+#ifndef FCD_PR_ATAN_N
+#define FCD_PR_ATAN_N 2  // pixel pairs per carrier in one interleaved atan2 group (0: the per-pair form)
+#endif
 #ifndef FCD_PR_ATAN_GROUP
 #define FCD_PR_ATAN_GROUP 4  // atan2 chains per scheduling group (0: unbounded)
 #endif
@@ -180,6 +189,13 @@ __global__ __launch_bounds__(PR_THREADS, FCD_PR_MINB) void k_phase_rows(
             // before the transforms: lane-contiguous in the permuted copy
             float4 th4[2][4];
             auto load_theta = [&]() {
+                if constexpr (FCD_PR_ABL & 1) {  // diagnostic: no reference-angle loads
+#pragma unroll
+                    for (int c = 0; c < 2; ++c)
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) th4[c][k] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    return;
+                }
 #pragma unroll
                 for (int c = 0; c < 2; ++c) {
                     const float4* tp = reinterpret_cast<const float4*>(theta + ((long)c * H + r) * PR_W) + lane * 4;
@@ -208,6 +224,36 @@ __global__ __launch_bounds__(PR_THREADS, FCD_PR_MINB) void k_phase_rows(
 #if FCD_PR_THETA_LATE
             load_theta();
 #endif
+#if FCD_PR_ATAN_N > 0
+            // FCD_PR_ATAN_N pixel pairs of each carrier per interleaved group
+            // (wrapped_phase_pkn: 2 * FCD_PR_ATAN_N independent chains)
+#pragma unroll
+            for (int q0 = 0; q0 < 16; q0 += 2 * FCD_PR_ATAN_N) {
+                __builtin_amdgcn_sched_barrier(0);
+                constexpr int NPG = 2 * FCD_PR_ATAN_N;
+                fv2 tq[NPG], wq[NPG];
+                float2 uq[2 * NPG];
+#pragma unroll
+                for (int m = 0; m < FCD_PR_ATAN_N; ++m) {
+                    const int q = q0 + 2 * m, k = q / 4, e = q % 4;
+                    tq[2 * m] = e == 0 ? fv2{th4[0][k].x, th4[0][k].y} : fv2{th4[0][k].z, th4[0][k].w};
+                    tq[2 * m + 1] = e == 0 ? fv2{th4[1][k].x, th4[1][k].y} : fv2{th4[1][k].z, th4[1][k].w};
+                    uq[4 * m] = x0[q];
+                    uq[4 * m + 1] = x0[q + 1];
+                    uq[4 * m + 2] = x1[q];
+                    uq[4 * m + 3] = x1[q + 1];
+                }
+                wrapped_phase_pkn<NPG>(tq, uq, wq);
+#pragma unroll
+                for (int m = 0; m < FCD_PR_ATAN_N; ++m) {
+                    const int q = q0 + 2 * m;
+                    w0[q] = wq[2 * m].x;
+                    w0[q + 1] = wq[2 * m].y;
+                    w1[q] = wq[2 * m + 1].x;
+                    w1[q + 1] = wq[2 * m + 1].y;
+                }
+            }
+#else
 #pragma unroll
             for (int q = 0; q < 16; q += 2) {  // pixel pairs: packed atan2 / wrap
                 if (FCD_PR_ATAN_GROUP && q % FCD_PR_ATAN_GROUP == 0) __builtin_amdgcn_sched_barrier(0);
@@ -221,6 +267,7 @@ __global__ __launch_bounds__(PR_THREADS, FCD_PR_MINB) void k_phase_rows(
                 w1[q] = a1.x;
                 w1[q + 1] = a1.y;
             }
+#endif
             PR_STAMP(4);
 #else
 #pragma unroll
@@ -276,6 +323,38 @@ __global__ __launch_bounds__(PR_THREADS, FCD_PR_MINB) void k_phase_rows(
                 col0[((long)f * 2 + 1) * H + r] = v[0].y;
             }
             if constexpr (UNWRAP) {
+#if FCD_PR_PKUNWRAP
+                // both maps as packed pairs: dd = -find_wrap(w(j), w(j+1)) = rint((w(j) -
+                // w(j+1)) / 2 pi) for every f32 difference except +-fl(pi) (exhaustively
+                // checked against the comparison form; +-fl(pi) is flagged ambiguous as
+                // before), so k'(c) = sum_{c' < c} dd(c') accumulates in f32 (exact
+                // small integers) and phi' = w + 2 pi k' is the same fma as before.
+                if (lane == 63) v[16] = v[15];  // no edge past the row end: dd = 0
+                fv2 dd[16];
+                fv2 run = {0.f, 0.f};
+                bool amb = false;
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    const fv2 d = pv(v[j]) - pv(v[j + 1]);
+                    amb |= (fabsf(d.x) == 3.14159274f) | (fabsf(d.y) == 3.14159274f);
+                    const fv2 q = d * 0.159154943091895f;
+                    dd[j] = fv2{rintf(q.x), rintf(q.y)};
+                    run += dd[j];
+                }
+                // one wave scan of both maps' segment sums, biased by 16 per lane into
+                // 16-bit halves (|run| <= 16, prefix <= 64 * 32 < 2^16)
+                const int packed = ((int)run.x + 16) | (((int)run.y + 16) << 16);
+                const int incl = team_scan_incl_dpp<64>(packed);
+                const int excl = incl - packed;
+                fv2 acc = {(float)((excl & 0xffff) - 16 * lane), (float)((excl >> 16) - 16 * lane)};
+                wave_sync();  // every lane has read its neighbour's first value
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    slot[pad(j0 + j)] = vp(acc * kTwoPiF + pv(v[j]));
+                    acc += dd[j];
+                }
+                bad |= amb;
+#else
                 int amb = 0, hb0 = 0, hb1 = 0;  // 2-bit codes of h + 1
 #pragma unroll
                 for (int j = 0; j < 16; ++j) {
@@ -302,6 +381,7 @@ __global__ __launch_bounds__(PR_THREADS, FCD_PR_MINB) void k_phase_rows(
                     acc1 -= ((hb1 >> (2 * j)) & 3) - 1;
                 }
                 bad |= amb;
+#endif
             }
         }
         if constexpr (UNWRAP) {  // first and last unwrapped rows of the tile -> seam buffer (k_seam_check)
@@ -328,11 +408,22 @@ __global__ __launch_bounds__(PR_THREADS, FCD_PR_MINB) void k_phase_rows(
                 const float2 a0 = a_row[0], b0 = nx[0];  // phi'(r, 0) = w(r, 0)
                 const float d0 = kTwoPiF * (float)(-fw_exact(a0.x, b0.x));
                 const float d1 = kTwoPiF * (float)(-fw_exact(a0.y, b0.y));
+#if FCD_PR_PKUNWRAP
+                // largest |b - a + d| of both maps (packed differences, one max3 per pixel)
+                float m = 0.f;
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    const fv2 e = (pv(nx[pad(j0 + j)]) - pv(a_row[pad(j0 + j)])) + fv2{d0, d1};
+                    m = fmaxf(m, fmaxf(fabsf(e.x), fabsf(e.y)));
+                }
+                bad |= (int)(m > kPR_VLim);
+#else
 #pragma unroll
                 for (int j = 0; j < 16; ++j) {
                     const float2 a = a_row[pad(j0 + j)], b = nx[pad(j0 + j)];
                     bad |= (int)(fabsf(b.x - a.x + d0) > kPR_VLim) | (int)(fabsf(b.y - a.y + d1) > kPR_VLim);
                 }
+#endif
             }
             if (__any(bad) && lane == 0) atomicOr(flags + f * 2, 1);
             PR_STAMP(7);
@@ -363,7 +454,10 @@ __global__ __launch_bounds__(PR_THREADS, FCD_PR_MINB) void k_phase_rows(
             const int c0 = threadIdx.x / PR_ROWS, rl = threadIdx.x % PR_ROWS;
             const float2* src = row_slot(rl, par ^ 1);
 #pragma unroll 4
-            for (int k = 0; k < PR_W / 64; ++k) st_stream(dst + (c0 + 64 * k) * PR_ZT + rl, src[pad(c0 + 64 * k)]);
+            for (int k = 0; k < PR_W / 64; ++k) {
+                const float2 v = src[pad(c0 + 64 * k)];
+                if (!(FCD_PR_ABL & 2) || v.x == 1234.5f) st_stream(dst + (c0 + 64 * k) * PR_ZT + rl, v);  // 2: no Zt stores
+            }
         }
         PR_STAMP(11);
         __syncthreads();
