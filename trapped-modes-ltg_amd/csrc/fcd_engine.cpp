@@ -226,6 +226,7 @@ struct fcd_ctx {
     HostPipe pipe;
     // MST workspace
     DevBuf mst_comp, mst_off, mst_rel, mst_cw, mst_ce, mst_bw, mst_be, mst_link, mst_hooks, mst_ids;
+    DevBuf mst_rootof, mst_offk, mst_lb0, mst_lb1, mst_lr0, mst_lr1, mst_ll0, mst_cnt;  // two-level rounds
     size_t mst_cap = 0;
 
     // stage timing: 4 events per chunk (start, after demod, after unwrap, after integrate)
@@ -273,6 +274,9 @@ void ensure_mst(fcd_ctx* c, int nact) {
     c->mst_be.ensure(nv * 4);
     c->mst_link.ensure(nv * 8);
     c->mst_hooks.ensure(sizeof(int));
+    for (DevBuf* b : {&c->mst_rootof, &c->mst_offk, &c->mst_lb0, &c->mst_lb1, &c->mst_lr0, &c->mst_lr1, &c->mst_ll0})
+        b->ensure(nv * 4);
+    c->mst_cnt.ensure((size_t)fcdk::mst_level_counts() * sizeof(int));
     c->mst_ids.ensure(sizeof(int) * 2 * (size_t)std::max(c->chunk, c->fchunk) + 64);
     c->mst_cap = nv;
 }
@@ -288,6 +292,14 @@ fcdk::MstWork mst_work(fcd_ctx* c) {
     m.best_e = c->mst_be.as<int>();
     m.link = c->mst_link.as<unsigned long long>();
     m.nhooks = c->mst_hooks.as<int>();
+    m.rootof = c->mst_rootof.as<int>();
+    m.offk = c->mst_offk.as<int>();
+    m.listB[0] = c->mst_lb0.as<int>();
+    m.listB[1] = c->mst_lb1.as<int>();
+    m.listR[0] = c->mst_lr0.as<int>();
+    m.listR[1] = c->mst_lr1.as<int>();
+    m.listL0 = c->mst_ll0.as<int>();
+    m.cnt = c->mst_cnt.as<int>();
     return m;
 }
 
@@ -311,11 +323,17 @@ void demod_phases(fcd_ctx* c, const float2* spec, int nb, float* wrapped, hipStr
     }
 }
 
+// The exact pass runs one pixel round and then the two-level rounds
+// (kernels_unwrap.hip); FCD_MST_LEVEL=0 keeps every round at pixel level.
+bool mst_two_level() {
+    const char* e = std::getenv("FCD_MST_LEVEL");
+    return !(e && e[0] == '0');
+}
+
 // k-fields of nmaps wrapped maps (skimage unwrap_phase, fcd.py:119).  Synchronises.
 void unwrap_maps(fcd_ctx* c, const float* w, int nmaps, int32_t* k, int* res_host, hipStream_t s) {
     int* res = c->rescnt.as<int>();
     fcdk::residues(w, nmaps, c->H, c->W, res, s);
-    fcdk::unwrap_scan(w, nmaps, c->H, c->W, c->colk.as<int>(), k, s);
     std::vector<int> counts(nmaps);
     HIPCHK(hipMemcpyAsync(counts.data(), res, sizeof(int) * nmaps, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
@@ -323,6 +341,9 @@ void unwrap_maps(fcd_ctx* c, const float* w, int nmaps, int32_t* k, int* res_hos
     std::vector<int> active;
     for (int i = 0; i < nmaps; ++i)
         if (counts[i] > 0) active.push_back(i);
+    // the scan unwrap for the residue-free maps (the MST pass overwrites the others);
+    // skipped when every map has residues (the fix-up groups of camera frames)
+    if ((int)active.size() < nmaps) fcdk::unwrap_scan(w, nmaps, c->H, c->W, c->colk.as<int>(), k, s);
     if (active.empty()) return;
     ensure_mst(c, (int)active.size());
     fcdk::MstWork m = mst_work(c);
@@ -333,6 +354,21 @@ void unwrap_maps(fcd_ctx* c, const float* w, int nmaps, int32_t* k, int* res_hos
     int rounds = 0;
     // Boruvka halves the component count every round; check convergence every
     // third round (a round after convergence hooks nothing and changes nothing).
+    if (mst_two_level()) {
+        // one pixel round, then rounds over the boundary / root lists only
+        fcdk::mst_round(w, c->mst_ids.as<int>(), nact, c->H, c->W, m, s, true);
+        fcdk::mst_level_setup(nact, c->H, c->W, m, s);
+        for (; rounds < max_rounds; rounds += 3) {
+            for (int g = 0; g < 3; ++g) fcdk::mst_level_round(w, c->mst_ids.as<int>(), nact, c->H, c->W, m, rounds + g, s);
+            int hooks = 0;
+            HIPCHK(hipMemcpyAsync(&hooks, m.nhooks, sizeof(int), hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+            if (hooks == 0) break;
+        }
+        if (rounds >= max_rounds) throw FcdError(FCD_E_INTERNAL, "unwrap: Boruvka did not converge");
+        fcdk::mst_level_finalize(c->mst_ids.as<int>(), nact, c->H, c->W, m, k, s);
+        return;
+    }
     for (; rounds < max_rounds; rounds += 3) {
         for (int g = 0; g < 3; ++g)
             fcdk::mst_round(w, c->mst_ids.as<int>(), nact, c->H, c->W, m, s, rounds + g == 0);

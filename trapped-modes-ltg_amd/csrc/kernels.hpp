@@ -116,12 +116,24 @@ void unwrap_scan(const float* w, int nmaps, int H, int W, int* colk, int32_t* k,
 struct MstWork {
     int* comp; int* off; double* rel; double* cand_w; int* cand_e;
     unsigned long long* best_w; int* best_e; unsigned long long* link; int* nhooks;
+    // two-level rounds (mst_level_*): per level-0 root its current root and
+    // offset; boundary-pixel lists (ping-pong), current-root lists (ping-pong),
+    // the level-0 root list, all segmented by block; cnt: mst_level_counts() ints
+    int* rootof; int* offk; int* listB[2]; int* listR[2]; int* listL0; int* cnt;
 };
 // Maps listed in map_ids (device int[nact]) of the wrapped stack w.
 void mst_init(const float* w, const int* map_ids, int nact, int H, int W, MstWork m, hipStream_t s);
 // first: the round right after mst_init (every component a single vertex)
 void mst_round(const float* w, const int* map_ids, int nact, int H, int W, MstWork m, hipStream_t s, bool first = false);
 void mst_finalize(const int* map_ids, int nact, int H, int W, MstWork m, int32_t* k, hipStream_t s);
+// Two-level Boruvka: after mst_init + one mst_round(first) every pixel has a
+// level-0 component; mst_level_setup lists the level-0 roots and the pixels on
+// a component boundary, and every later round walks only those lists
+// (round r reads list parity r & 1).  mst_level_finalize writes k.
+int mst_level_counts();
+void mst_level_setup(int nact, int H, int W, MstWork m, hipStream_t s);
+void mst_level_round(const float* w, const int* map_ids, int nact, int H, int W, MstWork m, int r, hipStream_t s);
+void mst_level_finalize(const int* map_ids, int nact, int H, int W, MstWork m, int32_t* k, hipStream_t s);
 
 // ---- integration ----
 // z = (w0 + 2pi k0) + i (w1 + 2pi k1)   (k may be null)

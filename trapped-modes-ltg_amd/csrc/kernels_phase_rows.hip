@@ -55,7 +55,8 @@ constexpr int PR_ROWS = FCD_PR_ROWS;  // rows per tile (one wave each)
 #define FCD_PR_PKUNWRAP 1  // unwrap / census on packed pairs of both maps (0: the integer-code form)
 #endif
 #ifndef FCD_PR_ABL
-#define FCD_PR_ABL 0  // diagnostic ablations only (wrong results): 1 no reference-angle loads, 2 no Zt stores
+#define FCD_PR_ABL 0  // diagnostic ablations only (wrong results): 1 no reference-angle loads, 2 no Zt stores,
+                      // 4 no band transforms, 8 no atan2 / wrap, 16 no z-row FFT
 #endif
 #ifndef FCD_PR_ATAN_N
 #define FCD_PR_ATAN_N 2  // pixel pairs per carrier in one interleaved atan2 group (0: the per-pair form)
@@ -218,6 +219,7 @@ __global__ __launch_bounds__(PR_THREADS, FCD_PR_MINB) void k_phase_rows(
                 x1[q] = cmul(stage[(PR_B + t + PR_G * q) * PR_SROW + wave], p);
             }
             float* const sx = reinterpret_cast<float*>(slot);
+            if (!(FCD_PR_ABL & 4))  // 4: no band transforms
             GroupFFTTab2<PR_B>::template run_half<true>(x0, x1, sx + g * GSched<PR_B>::REGION,
                                                        sx + (PR_L + g) * GSched<PR_B>::REGION, t, btab);
             PR_STAMP(3);
@@ -243,7 +245,12 @@ __global__ __launch_bounds__(PR_THREADS, FCD_PR_MINB) void k_phase_rows(
                     uq[4 * m + 2] = x1[q];
                     uq[4 * m + 3] = x1[q + 1];
                 }
-                wrapped_phase_pkn<NPG>(tq, uq, wq);
+                if constexpr (FCD_PR_ABL & 8) {  // 8: no atan2 / wrap
+#pragma unroll
+                    for (int k = 0; k < NPG; ++k) wq[k] = tq[k] - fv2{uq[2 * k].x, uq[2 * k + 1].x};
+                } else {
+                    wrapped_phase_pkn<NPG>(tq, uq, wq);
+                }
 #pragma unroll
                 for (int m = 0; m < FCD_PR_ATAN_N; ++m) {
                     const int q = q0 + 2 * m;
@@ -439,6 +446,7 @@ __global__ __launch_bounds__(PR_THREADS, FCD_PR_MINB) void k_phase_rows(
             // the last row transforms in its other slot (the previous tile's row,
             // no longer needed): its unwrapped row stays for the next census
             float2* const zs = row_slot(wave, par ^ 1);
+            if (!(FCD_PR_ABL & 16))  // 16: no z-row FFT
             GroupFFTTab<PR_W>::template run<false>(x, zs, lane, ztab);
             wave_sync();
 #pragma unroll

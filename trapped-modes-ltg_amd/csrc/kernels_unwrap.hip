@@ -20,6 +20,7 @@
 // history).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <stdexcept>
 #include <string>
 
@@ -420,6 +421,308 @@ __global__ void k_mst_finalize(const int* __restrict__ map_ids, int nact, int H,
 void mst_finalize(const int* map_ids, int nact, int H, int W, MstWork m, int32_t* k, hipStream_t s) {
     const long n = (long)nact * H * W;
     hipLaunchKernelGGL(k_mst_finalize, dim3(nblk(n)), dim3(256), 0, s, map_ids, nact, H, W, m, k);
+    FCD_CHECK_LAUNCH();
+}
+
+// ------------------------------------------------------------------ two-level Boruvka
+// After the first pixel round (mst_round first = true) every pixel v belongs to a
+// level-0 component comp[v] with k(v) = K[comp[v]] + off[v].  The later rounds
+// never touch every pixel again: each level-0 root c carries its current root
+// rootof[c] and offk[c] = K[c] - K[rootof[c]], so
+//   k(v) = K[root] + offk[comp[v]] + off[v],
+// candidates come from the pixels on a component boundary (a list that only
+// shrinks: a pixel whose four neighbours share its component never gets an
+// outgoing edge again), hooks and pointer jumps run over the list of current
+// roots, and the per-round relabelling over the level-0 roots (about a third of
+// the pixels after the first round).  Same edges, weights, tie-break and hook rule
+// as the pixel rounds, so the same unique MST and k-field.
+
+// The lists are SEGMENTED: block g of the fixed LVL_BLOCKS grid owns the pixel
+// range [g * seg, (g + 1) * seg) and segment g of every list (capacity seg, count
+// cnt[g]), appends through a workgroup counter in LDS and never touches a global
+// counter (one word would serialise millions of appends per round).  Within a
+// wave the appended entries keep lane order, so the boundary list stays in pixel
+// order run by run, which the per-root segmented minimum of k_lvl_cand uses.
+constexpr int LVL_BLOCKS = 4096;
+
+__device__ __forceinline__ int block_append(bool pred, int* lds_counter) {
+    const unsigned long long b = __ballot(pred);
+    if (!b) return -1;
+    const int lane = threadIdx.x & 63;
+    const int leader = __ffsll((long long)b) - 1;
+    int base = 0;
+    if (lane == leader) base = atomicAdd(lds_counter, __popcll(b));
+    base = __shfl(base, leader, 64);
+    return pred ? base + __popcll(b & ((1ull << lane) - 1)) : -1;
+}
+
+// cnt layout: [list][LVL_BLOCKS] for list = B0, B1, R0, R1, L0
+__device__ __forceinline__ int* lvl_cnt(int* cnt, int list) { return cnt + (long)list * LVL_BLOCKS; }
+
+__global__ __launch_bounds__(256) void k_lvl_setup(int nact, int H, int W, MstWork m, long seg) {
+    __shared__ int nroot, nbnd;
+    if (threadIdx.x == 0) nroot = nbnd = 0;
+    __syncthreads();
+    const long hw = (long)H * W, nv = nact * hw;
+    const long s0 = (long)blockIdx.x * seg, s1 = std::min(nv, s0 + seg);
+    for (long base = s0; base < s1; base += blockDim.x) {
+        const long v = base + threadIdx.x;
+        const bool in = v < s1;
+        bool root = false, bnd = false;
+        if (in) {
+            const long p = v % hw;
+            const int i = (int)(p / W), j = (int)(p % W);
+            const int c = m.comp[v];
+            root = c == (int)v;
+            bnd = (j + 1 < W && m.comp[v + 1] != c) || (j > 0 && m.comp[v - 1] != c) ||
+                  (i + 1 < H && m.comp[v + W] != c) || (i > 0 && m.comp[v - W] != c);
+            if (root) {
+                m.rootof[v] = (int)v;
+                m.offk[v] = 0;
+            }
+        }
+        const int pl = block_append(root, &nroot);
+        if (pl >= 0) {
+            m.listL0[s0 + pl] = (int)v;
+            m.listR[0][s0 + pl] = (int)v;
+        }
+        const int pb = block_append(bnd, &nbnd);
+        if (pb >= 0) m.listB[0][s0 + pb] = (int)v;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        lvl_cnt(m.cnt, 0)[blockIdx.x] = nbnd;
+        lvl_cnt(m.cnt, 2)[blockIdx.x] = nroot;
+        lvl_cnt(m.cnt, 4)[blockIdx.x] = nroot;
+    }
+}
+
+// Candidates over segment g of the boundary list B[par]; survivors (pixels that
+// still have an outgoing edge) go to segment g of B[par ^ 1] with their candidate
+// edge; per-root minimum weight by one atomicMin per run of consecutive lanes with
+// the same root.
+__global__ __launch_bounds__(256) void k_lvl_cand(int H, int W, MstWork m, int par, long seg) {
+    __shared__ int nout;
+    if (threadIdx.x == 0) nout = 0;
+    __syncthreads();
+    const long hw = (long)H * W;
+    const int nh = H * (W - 1);
+    const long s0 = (long)blockIdx.x * seg;
+    const int n = lvl_cnt(m.cnt, par)[blockIdx.x];
+    const int* B = m.listB[par] + s0;
+    int* B2 = m.listB[par ^ 1] + s0;
+    double* cw = m.cand_w + s0;
+    int* ce = m.cand_e + s0;
+    int* cr = m.listB[par] + s0;  // the candidates' roots overwrite the consumed entries of B[par]
+    const int lane = threadIdx.x & 63;
+    for (int base = 0; base < n; base += blockDim.x) {
+        const int i = base + threadIdx.x;
+        const bool in = i < n;
+        long v = 0;
+        int cv = -1 - lane;  // distinct per idle lane: never part of a run
+        double bw = __longlong_as_double(0x7ff0000000000000ll);
+        int be = 0x7fffffff;
+        if (in) {
+            v = B[i];
+            const long p = v % hw;
+            const int pi = (int)(p / W), pj = (int)(p % W);
+            cv = m.rootof[m.comp[v]];
+            const double rv = m.rel[v];
+            auto consider = [&](long u, int eidx) {
+                if (m.rootof[m.comp[u]] == cv) return;
+                const double we = __dadd_rn(rv, m.rel[u]);
+                if (we < bw || (we == bw && eidx < be)) {
+                    bw = we;
+                    be = eidx;
+                }
+            };
+            if (pj + 1 < W) consider(v + 1, pi * (W - 1) + pj);
+            if (pj > 0) consider(v - 1, pi * (W - 1) + pj - 1);
+            if (pi + 1 < H) consider(v + W, nh + pi * W + pj);
+            if (pi > 0) consider(v - W, nh + (pi - 1) * W + pj);
+        }
+        const bool has = be != 0x7fffffff;
+        // every lane has read its B entry before any is overwritten (survivors never
+        // outnumber the entries read: pos < base + blockDim.x after this iteration's
+        // reads, which the barrier orders)
+        __syncthreads();
+        const int pos = block_append(has, &nout);
+        if (pos >= 0) {
+            B2[pos] = (int)v;
+            ce[pos] = be;
+            cw[pos] = bw;
+            cr[pos] = cv;
+        }
+        const int cprev = __shfl_up(cv, 1, 64);
+        const unsigned long long heads = __ballot(lane == 0 || cprev != cv);
+        unsigned long long key = has ? (unsigned long long)__double_as_longlong(bw) : ~0ull;
+#pragma unroll
+        for (int sft = 1; sft < 64; sft <<= 1) {
+            const unsigned lo = __shfl_down((unsigned)key, sft, 64), hi = __shfl_down((unsigned)(key >> 32), sft, 64);
+            const unsigned long long other = ((unsigned long long)hi << 32) | lo;
+            const unsigned long long between = (lane + sft < 64) ? (heads >> (lane + 1)) & ((1ull << sft) - 1) : 1ull;
+            if (between == 0 && other < key) key = other;
+        }
+        if (((heads >> lane) & 1) && key != ~0ull) atomicMin(m.best_w + cv, key);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) lvl_cnt(m.cnt, par ^ 1)[blockIdx.x] = nout;
+}
+
+// Edge-index tie-break among the candidates of minimum weight (B[par ^ 1]).
+__global__ __launch_bounds__(256) void k_lvl_cand2(MstWork m, int par, long seg) {
+    const long s0 = (long)blockIdx.x * seg;
+    const int n = lvl_cnt(m.cnt, par ^ 1)[blockIdx.x];
+    const int* cr = m.listB[par] + s0;  // roots stored by k_lvl_cand
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const int cv = cr[i];
+        if ((unsigned long long)__double_as_longlong(m.cand_w[s0 + i]) == m.best_w[cv])
+            atomicMin(m.best_e + cv, m.cand_e[s0 + i]);
+    }
+}
+
+// Hooks of the current roots (R[par]); the roots that stay roots go to R[par ^ 1].
+__global__ __launch_bounds__(256) void k_lvl_hook(const float* __restrict__ w, const int* __restrict__ map_ids, int H,
+                                                  int W, MstWork m, int par, long seg) {
+    __shared__ int nout;
+    if (threadIdx.x == 0) nout = 0;
+    __syncthreads();
+    const long hw = (long)H * W;
+    const int nh = H * (W - 1);
+    const long s0 = (long)blockIdx.x * seg;
+    const int n = lvl_cnt(m.cnt, 2 + par)[blockIdx.x];
+    const int* R = m.listR[par] + s0;
+    int* R2 = m.listR[par ^ 1] + s0;
+    for (int base = 0; base < n; base += blockDim.x) {
+        const int i = base + threadIdx.x;
+        bool hooked = false, stays = false;
+        int c = 0;
+        if (i < n) {
+            c = R[i];
+            const int e = m.best_e[c];
+            if (e == 0x7fffffff) {
+                stays = true;
+            } else {
+                const long mb = ((long)c / hw) * hw;
+                long p1, p2;
+                if (e < nh) {
+                    p1 = mb + (long)(e / (W - 1)) * W + (e % (W - 1));
+                    p2 = p1 + 1;
+                } else {
+                    p1 = mb + (e - nh);
+                    p2 = p1 + W;
+                }
+                const float* mw = w + (long)map_ids[c / hw] * hw;
+                const int inc = find_wrap(mw[p1 - mb], mw[p2 - mb]);
+                long x, y;
+                int delta;  // k(y) - k(x) across the edge
+                if (m.rootof[m.comp[p1]] == c) {
+                    x = p1; y = p2; delta = -inc;
+                } else {
+                    x = p2; y = p1; delta = inc;
+                }
+                const int d = m.rootof[m.comp[y]];
+                if (m.best_e[d] == e && c < d) {
+                    stays = true;  // mutual pair: the smaller root stays a root
+                } else {
+                    const int kx = m.offk[m.comp[x]] + m.off[x], ky = m.offk[m.comp[y]] + m.off[y];
+                    m.link[c] = pack_link(d, ky - kx - delta);  // K_c - K_d
+                    hooked = true;
+                }
+            }
+            if (stays) m.link[c] = pack_link(c, 0);
+        }
+        const int pos = block_append(stays, &nout);
+        if (pos >= 0) R2[pos] = c;
+        count_hook(hooked, m.nhooks);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) lvl_cnt(m.cnt, 2 + (par ^ 1))[blockIdx.x] = nout;
+}
+
+// Pointer jumping over this round's roots (as k_mst_jump).
+__global__ __launch_bounds__(256) void k_lvl_jump(MstWork m, int par, long seg) {
+    const long s0 = (long)blockIdx.x * seg;
+    const int n = lvl_cnt(m.cnt, 2 + par)[blockIdx.x];
+    const int* R = m.listR[par] + s0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const int c = R[i];
+        unsigned long long l = __hip_atomic_load(m.link + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        int p = link_parent(l), o = link_off(l);
+        if (p == c) continue;
+        for (;;) {
+            const unsigned long long l2 = __hip_atomic_load(m.link + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const int pp = link_parent(l2);
+            if (pp == p) break;
+            o += link_off(l2);
+            p = pp;
+            __hip_atomic_store(m.link + c, pack_link(p, o), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+}
+
+// Relabel the level-0 roots; reset the candidate slots of this round's roots.
+__global__ __launch_bounds__(256) void k_lvl_update(MstWork m, long seg) {
+    const long s0 = (long)blockIdx.x * seg;
+    const int n = lvl_cnt(m.cnt, 4)[blockIdx.x];
+    const int* L0 = m.listL0 + s0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const int c = L0[i];
+        const int r = m.rootof[c];
+        const unsigned long long l = m.link[r];
+        const int p = link_parent(l);
+        if (p != r) {
+            m.rootof[c] = p;
+            m.offk[c] += link_off(l);
+        }
+        if (c == r) {
+            m.best_w[c] = 0x7ff0000000000000ull;
+            m.best_e[c] = 0x7fffffff;
+        }
+    }
+}
+
+__global__ void k_lvl_finalize(const int* __restrict__ map_ids, int nact, int H, int W, MstWork m, int32_t* k) {
+    const long hw = (long)H * W;
+    const long v = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= nact * hw) return;
+    const int slot = (int)(v / hw);
+    const long base = slot * hw;
+    const int kv = m.offk[m.comp[v]] + m.off[v];
+    const int kb = m.offk[m.comp[base]] + m.off[base];
+    k[(long)map_ids[slot] * hw + (v - base)] = kv - kb;
+}
+
+static long lvl_seg(long n) { return (n + LVL_BLOCKS - 1) / LVL_BLOCKS; }
+
+int mst_level_counts() { return 5 * LVL_BLOCKS; }
+
+void mst_level_setup(int nact, int H, int W, MstWork m, hipStream_t s) {
+    const long n = (long)nact * H * W, seg = lvl_seg(n);
+    hipLaunchKernelGGL(k_lvl_setup, dim3(LVL_BLOCKS), dim3(256), 0, s, nact, H, W, m, seg);
+    FCD_CHECK_LAUNCH();
+}
+
+void mst_level_round(const float* w, const int* map_ids, int nact, int H, int W, MstWork m, int r, hipStream_t s) {
+    const long n = (long)nact * H * W, seg = lvl_seg(n);
+    const int par = r & 1;
+    FCD_HIPCHK(hipMemsetAsync(m.nhooks, 0, sizeof(int), s));
+    const dim3 g(LVL_BLOCKS), b(256);
+    hipLaunchKernelGGL(k_lvl_cand, g, b, 0, s, H, W, m, par, seg);
+    FCD_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_lvl_cand2, g, b, 0, s, m, par, seg);
+    FCD_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_lvl_hook, g, b, 0, s, w, map_ids, H, W, m, par, seg);
+    FCD_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_lvl_jump, g, b, 0, s, m, par, seg);
+    FCD_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_lvl_update, g, b, 0, s, m, seg);
+    FCD_CHECK_LAUNCH();
+}
+
+void mst_level_finalize(const int* map_ids, int nact, int H, int W, MstWork m, int32_t* k, hipStream_t s) {
+    const long n = (long)nact * H * W;
+    hipLaunchKernelGGL(k_lvl_finalize, dim3(nblk(n)), dim3(256), 0, s, map_ids, nact, H, W, m, k);
     FCD_CHECK_LAUNCH();
 }
 
