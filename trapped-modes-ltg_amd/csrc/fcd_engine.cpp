@@ -10,6 +10,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -226,7 +227,7 @@ struct fcd_ctx {
     HostPipe pipe;
     // MST workspace
     DevBuf mst_comp, mst_off, mst_rel, mst_cw, mst_ce, mst_bw, mst_be, mst_link, mst_hooks, mst_ids;
-    DevBuf mst_rootof, mst_offk, mst_lb0, mst_lb1, mst_lr0, mst_lr1, mst_ll0, mst_cnt;  // two-level rounds
+    DevBuf mst_rootof, mst_offk, mst_lb0, mst_lb1, mst_lr0, mst_lr1, mst_ll0, mst_cnt, mst_mb0, mst_mb1;  // two-level rounds
     size_t mst_cap = 0;
 
     // stage timing: 4 events per chunk (start, after demod, after unwrap, after integrate)
@@ -277,6 +278,8 @@ void ensure_mst(fcd_ctx* c, int nact) {
     for (DevBuf* b : {&c->mst_rootof, &c->mst_offk, &c->mst_lb0, &c->mst_lb1, &c->mst_lr0, &c->mst_lr1, &c->mst_ll0})
         b->ensure(nv * 4);
     c->mst_cnt.ensure((size_t)fcdk::mst_level_counts() * sizeof(int));
+    c->mst_mb0.ensure(nv);
+    c->mst_mb1.ensure(nv);
     c->mst_ids.ensure(sizeof(int) * 2 * (size_t)std::max(c->chunk, c->fchunk) + 64);
     c->mst_cap = nv;
 }
@@ -300,6 +303,8 @@ fcdk::MstWork mst_work(fcd_ctx* c) {
     m.listR[1] = c->mst_lr1.as<int>();
     m.listL0 = c->mst_ll0.as<int>();
     m.cnt = c->mst_cnt.as<int>();
+    m.maskB[0] = c->mst_mb0.as<unsigned char>();
+    m.maskB[1] = c->mst_mb1.as<unsigned char>();
     return m;
 }
 
@@ -358,8 +363,23 @@ void unwrap_maps(fcd_ctx* c, const float* w, int nmaps, int32_t* k, int* res_hos
         // one pixel round, then rounds over the boundary / root lists only
         fcdk::mst_round(w, c->mst_ids.as<int>(), nact, c->H, c->W, m, s, true);
         fcdk::mst_level_setup(nact, c->H, c->W, m, s);
+        static const bool dbg = std::getenv("FCD_MST_DEBUG") != nullptr;
+        auto dump = [&](int r) {  // diagnostic: list sizes (B, R) entering round r
+            std::vector<int> cnt((size_t)fcdk::mst_level_counts());
+            HIPCHK(hipMemcpyAsync(cnt.data(), m.cnt, cnt.size() * 4, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+            const size_t nb = cnt.size() / 5;
+            long tot[5] = {0, 0, 0, 0, 0};
+            for (int l = 0; l < 5; ++l)
+                for (size_t g = 0; g < nb; ++g) tot[l] += cnt[l * nb + g];
+            std::fprintf(stderr, "[mst] nv %ld round %d: B %ld R %ld L0 %ld\n", (long)nact * c->hw(), r,
+                         tot[r & 1], tot[2 + (r & 1)], tot[4]);
+        };
         for (; rounds < max_rounds; rounds += 3) {
-            for (int g = 0; g < 3; ++g) fcdk::mst_level_round(w, c->mst_ids.as<int>(), nact, c->H, c->W, m, rounds + g, s);
+            for (int g = 0; g < 3; ++g) {
+                if (dbg) dump(rounds + g);
+                fcdk::mst_level_round(w, c->mst_ids.as<int>(), nact, c->H, c->W, m, rounds + g, s);
+            }
             int hooks = 0;
             HIPCHK(hipMemcpyAsync(&hooks, m.nhooks, sizeof(int), hipMemcpyDeviceToHost, s));
             HIPCHK(hipStreamSynchronize(s));

@@ -120,6 +120,7 @@ struct MstWork {
     // offset; boundary-pixel lists (ping-pong), current-root lists (ping-pong),
     // the level-0 root list, all segmented by block; cnt: mst_level_counts() ints
     int* rootof; int* offk; int* listB[2]; int* listR[2]; int* listL0; int* cnt;
+    unsigned char* maskB[2];  // per boundary entry: its neighbours still outside its component
 };
 // Maps listed in map_ids (device int[nact]) of the wrapped stack w.
 void mst_init(const float* w, const int* map_ids, int nact, int H, int W, MstWork m, hipStream_t s);

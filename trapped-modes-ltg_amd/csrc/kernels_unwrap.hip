@@ -372,21 +372,14 @@ __global__ void k_mst_update(int nact, int H, int W, MstWork m) {
     }
 }
 
-__global__ void k_mst_reset(int nact, int H, int W, MstWork m) {
-    const long v = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (v >= nact * (long)H * W) return;
-    m.best_w[v] = 0x7ff0000000000000ull;
-    m.best_e[v] = 0x7fffffff;
-}
-
 static inline unsigned nblk(long n) { return (unsigned)((n + 255) / 256); }
 
 void mst_init(const float* w, const int* map_ids, int nact, int H, int W, MstWork m, hipStream_t s) {
     const long n = (long)nact * H * W;
     hipLaunchKernelGGL(k_mst_rel, dim3(nblk(n)), dim3(256), 0, s, w, map_ids, nact, H, W, m.rel, m.comp, m.off);
     FCD_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_mst_reset, dim3(nblk(n)), dim3(256), 0, s, nact, H, W, m);
-    FCD_CHECK_LAUNCH();
+    // no reset of best_w / best_e: the first round (k_mst_cand<true>) writes every
+    // vertex's entry before anything reads it
 }
 
 void mst_round(const float* w, const int* map_ids, int nact, int H, int W, MstWork m, hipStream_t s, bool first) {
@@ -469,13 +462,15 @@ __global__ __launch_bounds__(256) void k_lvl_setup(int nact, int H, int W, MstWo
         const long v = base + threadIdx.x;
         const bool in = v < s1;
         bool root = false, bnd = false;
+        unsigned mask = 0;
         if (in) {
             const long p = v % hw;
             const int i = (int)(p / W), j = (int)(p % W);
             const int c = m.comp[v];
             root = c == (int)v;
-            bnd = (j + 1 < W && m.comp[v + 1] != c) || (j > 0 && m.comp[v - 1] != c) ||
-                  (i + 1 < H && m.comp[v + W] != c) || (i > 0 && m.comp[v - W] != c);
+            mask = (unsigned)(j + 1 < W && m.comp[v + 1] != c) | ((unsigned)(j > 0 && m.comp[v - 1] != c) << 1) |
+                   ((unsigned)(i + 1 < H && m.comp[v + W] != c) << 2) | ((unsigned)(i > 0 && m.comp[v - W] != c) << 3);
+            bnd = mask != 0;
             if (root) {
                 m.rootof[v] = (int)v;
                 m.offk[v] = 0;
@@ -487,7 +482,10 @@ __global__ __launch_bounds__(256) void k_lvl_setup(int nact, int H, int W, MstWo
             m.listR[0][s0 + pl] = (int)v;
         }
         const int pb = block_append(bnd, &nbnd);
-        if (pb >= 0) m.listB[0][s0 + pb] = (int)v;
+        if (pb >= 0) {
+            m.listB[0][s0 + pb] = (int)v;
+            m.maskB[0][s0 + pb] = (unsigned char)mask;
+        }
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -499,13 +497,17 @@ __global__ __launch_bounds__(256) void k_lvl_setup(int nact, int H, int W, MstWo
 
 // Candidates over segment g of the boundary list B[par]; survivors (pixels that
 // still have an outgoing edge) go to segment g of B[par ^ 1] with their candidate
-// edge; per-root minimum weight by one atomicMin per run of consecutive lanes with
-// the same root.
-__global__ __launch_bounds__(256) void k_lvl_cand(int H, int W, MstWork m, int par, long seg) {
+// edge and root; per-root minimum weight by one atomicMin per run of consecutive
+// lanes with the same root.  LVL_U entries per thread per iteration, their gathers
+// (B -> comp -> rootof, four neighbours each) issued together: the chain of
+// dependent loads, not bandwidth, bounds this kernel.
+constexpr int LVL_U = 4;
+
+__global__ __launch_bounds__(256) void k_lvl_cand(int lw, int lh, MstWork m, int par, long seg) {
     __shared__ int nout;
     if (threadIdx.x == 0) nout = 0;
     __syncthreads();
-    const long hw = (long)H * W;
+    const int W = 1 << lw, H = 1 << lh;
     const int nh = H * (W - 1);
     const long s0 = (long)blockIdx.x * seg;
     const int n = lvl_cnt(m.cnt, par)[blockIdx.x];
@@ -514,56 +516,96 @@ __global__ __launch_bounds__(256) void k_lvl_cand(int H, int W, MstWork m, int p
     double* cw = m.cand_w + s0;
     int* ce = m.cand_e + s0;
     int* cr = m.listB[par] + s0;  // the candidates' roots overwrite the consumed entries of B[par]
+    const unsigned char* M = m.maskB[par] + s0;
+    unsigned char* M2 = m.maskB[par ^ 1] + s0;
     const int lane = threadIdx.x & 63;
-    for (int base = 0; base < n; base += blockDim.x) {
-        const int i = base + threadIdx.x;
-        const bool in = i < n;
-        long v = 0;
-        int cv = -1 - lane;  // distinct per idle lane: never part of a run
-        double bw = __longlong_as_double(0x7ff0000000000000ll);
-        int be = 0x7fffffff;
-        if (in) {
-            v = B[i];
-            const long p = v % hw;
-            const int pi = (int)(p / W), pj = (int)(p % W);
-            cv = m.rootof[m.comp[v]];
-            const double rv = m.rel[v];
-            auto consider = [&](long u, int eidx) {
-                if (m.rootof[m.comp[u]] == cv) return;
-                const double we = __dadd_rn(rv, m.rel[u]);
-                if (we < bw || (we == bw && eidx < be)) {
-                    bw = we;
-                    be = eidx;
-                }
-            };
-            if (pj + 1 < W) consider(v + 1, pi * (W - 1) + pj);
-            if (pj > 0) consider(v - 1, pi * (W - 1) + pj - 1);
-            if (pi + 1 < H) consider(v + W, nh + pi * W + pj);
-            if (pi > 0) consider(v - W, nh + (pi - 1) * W + pj);
-        }
-        const bool has = be != 0x7fffffff;
-        // every lane has read its B entry before any is overwritten (survivors never
-        // outnumber the entries read: pos < base + blockDim.x after this iteration's
-        // reads, which the barrier orders)
-        __syncthreads();
-        const int pos = block_append(has, &nout);
-        if (pos >= 0) {
-            B2[pos] = (int)v;
-            ce[pos] = be;
-            cw[pos] = bw;
-            cr[pos] = cv;
-        }
-        const int cprev = __shfl_up(cv, 1, 64);
-        const unsigned long long heads = __ballot(lane == 0 || cprev != cv);
-        unsigned long long key = has ? (unsigned long long)__double_as_longlong(bw) : ~0ull;
+    for (int base = 0; base < n; base += 256 * LVL_U) {
+        int v[LVL_U], c0[LVL_U], cv[LVL_U], cn[LVL_U][4], rn[LVL_U][4], eix[LVL_U][4];
+        long nb[LVL_U][4];
+        bool in[LVL_U];
+        unsigned mk[LVL_U];
 #pragma unroll
-        for (int sft = 1; sft < 64; sft <<= 1) {
-            const unsigned lo = __shfl_down((unsigned)key, sft, 64), hi = __shfl_down((unsigned)(key >> 32), sft, 64);
-            const unsigned long long other = ((unsigned long long)hi << 32) | lo;
-            const unsigned long long between = (lane + sft < 64) ? (heads >> (lane + 1)) & ((1ull << sft) - 1) : 1ull;
-            if (between == 0 && other < key) key = other;
+        for (int u = 0; u < LVL_U; ++u) {
+            const int i = base + u * 256 + threadIdx.x;
+            in[u] = i < n;
+            v[u] = in[u] ? B[i] : 0;
+            mk[u] = in[u] ? M[i] : 0u;
         }
-        if (((heads >> lane) & 1) && key != ~0ull) atomicMin(m.best_w + cv, key);
+#pragma unroll
+        for (int u = 0; u < LVL_U; ++u) {
+            // only the neighbours outside v's component when it entered the list: a
+            // neighbour inside it stays inside (components only merge)
+            const int p = v[u] & ((1 << (lw + lh)) - 1);
+            const int pi = p >> lw, pj = p & (W - 1);
+            nb[u][0] = (mk[u] & 1) ? v[u] + 1 : -1;
+            nb[u][1] = (mk[u] & 2) ? v[u] - 1 : -1;
+            nb[u][2] = (mk[u] & 4) ? v[u] + W : -1;
+            nb[u][3] = (mk[u] & 8) ? v[u] - W : -1;
+            eix[u][0] = pi * (W - 1) + pj;
+            eix[u][1] = pi * (W - 1) + pj - 1;
+            eix[u][2] = nh + pi * W + pj;
+            eix[u][3] = nh + (pi - 1) * W + pj;
+            c0[u] = m.comp[v[u]];
+#pragma unroll
+            for (int d = 0; d < 4; ++d) cn[u][d] = nb[u][d] >= 0 ? m.comp[nb[u][d]] : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < LVL_U; ++u) {
+            cv[u] = m.rootof[c0[u]];
+#pragma unroll
+            for (int d = 0; d < 4; ++d) rn[u][d] = cn[u][d] >= 0 ? m.rootof[cn[u][d]] : -1;
+        }
+        double bw[LVL_U];
+        int be[LVL_U];
+#pragma unroll
+        for (int u = 0; u < LVL_U; ++u) {
+            bw[u] = __longlong_as_double(0x7ff0000000000000ll);
+            be[u] = 0x7fffffff;
+            if (!in[u]) {
+                cv[u] = -1 - lane;  // distinct per idle lane: never part of a run
+                continue;
+            }
+            const double rv = m.rel[v[u]];
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                if (rn[u][d] < 0 || rn[u][d] == cv[u]) {
+                    mk[u] &= ~(1u << d);
+                    continue;
+                }
+                const double we = __dadd_rn(rv, m.rel[nb[u][d]]);
+                if (we < bw[u] || (we == bw[u] && eix[u][d] < be[u])) {
+                    bw[u] = we;
+                    be[u] = eix[u][d];
+                }
+            }
+        }
+        // every lane has read its B entries before any is overwritten (survivors never
+        // outnumber the entries read so far; the barrier orders the reads first)
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < LVL_U; ++u) {
+            const bool has = be[u] != 0x7fffffff;
+            const int pos = block_append(has, &nout);
+            if (pos >= 0) {
+                B2[pos] = v[u];
+                M2[pos] = (unsigned char)mk[u];
+                ce[pos] = be[u];
+                cw[pos] = bw[u];
+                cr[pos] = cv[u];
+            }
+            const int cprev = __shfl_up(cv[u], 1, 64);
+            const unsigned long long heads = __ballot(lane == 0 || cprev != cv[u]);
+            unsigned long long key = has ? (unsigned long long)__double_as_longlong(bw[u]) : ~0ull;
+#pragma unroll
+            for (int sft = 1; sft < 64; sft <<= 1) {
+                const unsigned lo = __shfl_down((unsigned)key, sft, 64), hi = __shfl_down((unsigned)(key >> 32), sft, 64);
+                const unsigned long long other = ((unsigned long long)hi << 32) | lo;
+                const unsigned long long between =
+                    (lane + sft < 64) ? (heads >> (lane + 1)) & ((1ull << sft) - 1) : 1ull;
+                if (between == 0 && other < key) key = other;
+            }
+            if (((heads >> lane) & 1) && key != ~0ull) atomicMin(m.best_w + cv[u], key);
+        }
     }
     __syncthreads();
     if (threadIdx.x == 0) lvl_cnt(m.cnt, par ^ 1)[blockIdx.x] = nout;
@@ -708,7 +750,10 @@ void mst_level_round(const float* w, const int* map_ids, int nact, int H, int W,
     const int par = r & 1;
     FCD_HIPCHK(hipMemsetAsync(m.nhooks, 0, sizeof(int), s));
     const dim3 g(LVL_BLOCKS), b(256);
-    hipLaunchKernelGGL(k_lvl_cand, g, b, 0, s, H, W, m, par, seg);
+    int lw = 0, lh = 0;
+    while ((1 << lw) < W) ++lw;
+    while ((1 << lh) < H) ++lh;
+    hipLaunchKernelGGL(k_lvl_cand, g, b, 0, s, lw, lh, m, par, seg);
     FCD_CHECK_LAUNCH();
     hipLaunchKernelGGL(k_lvl_cand2, g, b, 0, s, m, par, seg);
     FCD_CHECK_LAUNCH();
