@@ -181,6 +181,32 @@ def test_unwrap_matches_oracle_random_residues(lib):
     assert np.all(d == d.flat[0])
 
 
+@pytest.mark.parametrize("shape", [(256, 256), (128, 512)])
+def test_unwrap_two_level_equals_pixel_rounds(lib, monkeypatch, shape):
+    """The two-level Boruvka (one pixel round, then block-segmented boundary / root
+    lists) and the all-pixel rounds (FCD_MST_LEVEL=0) build the same unique MST:
+    identical k-fields, bit for bit, over a batch of maps with thousands of residues
+    (several maps per list segment, segments spanning maps), and equal to the oracle."""
+    from oracle import fcd_oracle as O
+    rng = np.random.default_rng(11)
+    y, x = np.mgrid[0:shape[0], 0:shape[1]]
+    maps = []
+    for s in (0.6, 0.9, 1.3, 0.7, 1.1):
+        phi = 0.003 * (x - 60.0) ** 2 + 0.002 * (y - 30.0) ** 2 + rng.normal(0, s, x.shape)
+        maps.append(np.angle(np.exp(1j * phi)).astype(np.float32))
+    w = np.stack(maps)
+    eng = lib.Engine(shape)
+    k2, res = eng.unwrap(w)
+    assert (res > 0).all() and res.sum() > 5000
+    monkeypatch.setenv("FCD_MST_LEVEL", "0")
+    k1, _ = eng.unwrap(w)
+    assert np.array_equal(k1, k2)
+    for i in (0, 2):
+        _, ko = O.unwrap(w[i])
+        d = k2[i].astype(np.int64) - ko
+        assert np.all(d == d.flat[0])
+
+
 def test_unwrap_residue_free_scan(lib):
     from oracle import fcd_oracle as O
     y, x = np.mgrid[0:256, 0:512]

@@ -553,6 +553,9 @@ __global__ __launch_bounds__(IntColsCfg<H>::THREADS, IntColsCfg<H>::V) void k_in
                 if (col == 0) x[q] = make_float2(x[q].x + o.x, x[q].y + o.y);
             }
         }
+        // (both transforms in lockstep with a second LDS row per team measured slower:
+        // 3.94 vs 3.32 us/frame, kbench r02l; the next item's loads issued between them
+        // hide better.  Pairing k_demod_cols' two inverse transforms: no change, r02m)
         fft.template run<true>(y, s, t);
         if (base + TEAMS < i1) fetch(base + TEAMS + team < i1 ? base + TEAMS + team : items);
         fft.template run<false>(x, s, t);
