@@ -505,3 +505,29 @@ def test_reference_without_carriers_raises(lib):
     ref, frames = make_frames_numpy(256, 1, seed=2, rotate_deg=5.0)
     h, _, _ = fcd.compute_height_map(ref, frames[0], 0.001, height=1.0)
     assert np.isfinite(h).all()
+
+
+def _step(X, a=0.02, w=400):  # examples/val_example.py:16-18
+    x0 = len(X) // 2
+    return 1 / (1 + np.exp(-a * (X - x0 + w / 2))) * 1 / (1 + np.exp(a * (X - x0 - w / 2)))
+
+
+def _gauss_sin(X, Y, A=100, w=0.05):  # examples/val_example.py:19-20
+    return _step(X) * _step(Y) * A * np.sin(w * (X + Y))
+
+
+@pytest.mark.parametrize("k,bound", [(0, 0.52), (1, 0.57)])
+def test_val_known_answer(lib, golden, k, bound):
+    """pyval.val through the engine: the reference's only accuracy figure, "< 0.52 %"
+    (README.md:5-7; 0.518 % spectral / 0.558 % finite differences re-measured with the
+    reference), and the spectral run's height equals the reference's own (its f64 FFTs
+    against our f32 ones) on the golden 128 x 128 subsample."""
+    from pyval.val import val
+    X, Y, h, I, hmap, I0, cf = val(k, func=_gauss_sin, centrado_si=False)
+    assert cf == 1.0
+    err = np.max(np.abs(hmap - h)) * 100 / np.max(np.abs(hmap))
+    assert err < bound, err
+    if k == 0:
+        g = golden("val")
+        assert abs(err - float(g["err_percent"])) < 0.005, (err, float(g["err_percent"]))
+        assert rel_l2(hmap[::8, ::8], g["height_sub"]) < 1e-4
