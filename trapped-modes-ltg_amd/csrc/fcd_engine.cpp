@@ -328,11 +328,12 @@ void demod_phases(fcd_ctx* c, const float2* spec, int nb, float* wrapped, hipStr
     }
 }
 
-// The exact pass runs one pixel round and then the two-level rounds
-// (kernels_unwrap.hip); FCD_MST_LEVEL=0 keeps every round at pixel level.
-bool mst_two_level() {
+// The exact pass builds level-0 components inside 32 x 32 tiles and then runs the
+// two-level rounds (kernels_unwrap.hip).  FCD_MST_LEVEL=1: one pixel round instead of
+// the tiles; 0: every round at pixel level (both for A/B checks).
+int mst_level() {
     const char* e = std::getenv("FCD_MST_LEVEL");
-    return !(e && e[0] == '0');
+    return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : 2;
 }
 
 // k-fields of nmaps wrapped maps (skimage unwrap_phase, fcd.py:119).  Synchronises.
@@ -354,14 +355,21 @@ void unwrap_maps(fcd_ctx* c, const float* w, int nmaps, int32_t* k, int* res_hos
     fcdk::MstWork m = mst_work(c);
     const int nact = (int)active.size();
     upload(c->mst_ids.p, active.data(), sizeof(int) * nact, s);
-    fcdk::mst_init(w, c->mst_ids.as<int>(), nact, c->H, c->W, m, s);
     const int max_rounds = 64;
     int rounds = 0;
     // Boruvka halves the component count every round; check convergence every
     // third round (a round after convergence hooks nothing and changes nothing).
-    if (mst_two_level()) {
-        // one pixel round, then rounds over the boundary / root lists only
-        fcdk::mst_round(w, c->mst_ids.as<int>(), nact, c->H, c->W, m, s, true);
+    const int level = mst_level();
+    if (level >= 1) {
+        if (level >= 2 && c->H % 32 == 0 && c->W % 32 == 0) {
+            // level-0 components from Boruvka inside 32 x 32 tiles (LDS)
+            fcdk::mst_tile_level0(w, c->mst_ids.as<int>(), nact, c->H, c->W, m, s);
+        } else {
+            // one pixel round
+            fcdk::mst_init(w, c->mst_ids.as<int>(), nact, c->H, c->W, m, s);
+            fcdk::mst_round(w, c->mst_ids.as<int>(), nact, c->H, c->W, m, s, true);
+        }
+        // then rounds over the boundary / root lists only
         fcdk::mst_level_setup(nact, c->H, c->W, m, s);
         static const bool dbg = std::getenv("FCD_MST_DEBUG") != nullptr;
         auto dump = [&](int r) {  // diagnostic: list sizes (B, R) entering round r
@@ -389,6 +397,7 @@ void unwrap_maps(fcd_ctx* c, const float* w, int nmaps, int32_t* k, int* res_hos
         fcdk::mst_level_finalize(c->mst_ids.as<int>(), nact, c->H, c->W, m, k, s);
         return;
     }
+    fcdk::mst_init(w, c->mst_ids.as<int>(), nact, c->H, c->W, m, s);
     for (; rounds < max_rounds; rounds += 3) {
         for (int g = 0; g < 3; ++g)
             fcdk::mst_round(w, c->mst_ids.as<int>(), nact, c->H, c->W, m, s, rounds + g == 0);

@@ -132,6 +132,9 @@ void mst_finalize(const int* map_ids, int nact, int H, int W, MstWork m, int32_t
 // a component boundary, and every later round walks only those lists
 // (round r reads list parity r & 1).  mst_level_finalize writes k.
 int mst_level_counts();
+// Level-0 components from Boruvka inside each 32 x 32 tile (LDS), with the
+// reliabilities; replaces mst_init + the first pixel round before mst_level_setup.
+void mst_tile_level0(const float* w, const int* map_ids, int nact, int H, int W, MstWork m, hipStream_t s);
 void mst_level_setup(int nact, int H, int W, MstWork m, hipStream_t s);
 void mst_level_round(const float* w, const int* map_ids, int nact, int H, int W, MstWork m, int r, hipStream_t s);
 void mst_level_finalize(const int* map_ids, int nact, int H, int W, MstWork m, int32_t* k, hipStream_t s);

@@ -771,4 +771,208 @@ void mst_level_finalize(const int* map_ids, int nact, int H, int W, MstWork m, i
     FCD_CHECK_LAUNCH();
 }
 
+// ------------------------------------------------------------------ tile-local first level
+// Level-0 components from a Boruvka run inside each 32 x 32 tile, in LDS: by the
+// cut property, the lightest edge (under the total order (weight, edge index)) leaving
+// ANY vertex set is an edge of the unique MST, so a tile component whose lightest
+// outgoing edge -- over all its edges, the ones leaving the tile included -- ends
+// inside the tile may hook along it; a component whose lightest edge leaves the tile
+// waits (another component may still hook into it, and then the union's lightest
+// edge can be inside again).  The rounds stop when no component hooks.  Every hook
+// is an MST edge, so the components are subtrees of the MST and the two-level rounds
+// finish the same tree (same k-field as the all-pixel rounds).  The tile also
+// writes the f64 reliabilities (k_mst_rel's arithmetic) the later rounds read.
+constexpr int T0 = 32;                 // tile side
+constexpr int T0N = T0 * T0;           // pixels per tile
+constexpr int T0W = T0 + 4;            // wrapped-phase image with a 2-pixel halo
+constexpr int T0R = T0 + 2;            // reliabilities with a 1-pixel halo
+
+__global__ __launch_bounds__(256) void k_mst_tile0(const float* __restrict__ w, const int* __restrict__ map_ids,
+                                                   int nact, int H, int W, MstWork m) {
+    __shared__ float ws[T0W * T0W];
+    __shared__ double rs[T0R * T0R];
+    __shared__ unsigned long long bw[T0N];
+    __shared__ int lc[T0N], lo[T0N], be[T0N], lk[T0N], lko[T0N];
+    __shared__ int hooked;
+    const long hw = (long)H * W;
+    const int tiles_x = W / T0, tiles = (H / T0) * tiles_x;
+    const int slot = blockIdx.x / tiles, tile = blockIdx.x % tiles;
+    const int gi0 = (tile / tiles_x) * T0, gj0 = (tile % tiles_x) * T0;
+    const float* mw = w + (long)map_ids[slot] * hw;
+    const long vbase = (long)slot * hw;
+    const int nh = H * (W - 1);
+    // wrapped phases, 2-pixel halo (outside the map: never read for an existing edge)
+    for (int i = threadIdx.x; i < T0W * T0W; i += 256) {
+        const int gi = gi0 - 2 + i / T0W, gj = gj0 - 2 + i % T0W;
+        ws[i] = (gi >= 0 && gi < H && gj >= 0 && gj < W) ? mw[(long)gi * W + gj] : 0.f;
+    }
+    __syncthreads();
+    // reliabilities of the tile and its 1-pixel halo (k_mst_rel's operation order)
+    for (int i = threadIdx.x; i < T0R * T0R; i += 256) {
+        const int li = i / T0R, lj = i % T0R;  // ws index (li + 1, lj + 1)
+        const int gi = gi0 - 1 + li, gj = gj0 - 1 + lj;
+        double r = kBorderRel;
+        if (gi > 0 && gj > 0 && gi < H - 1 && gj < W - 1) {
+            const float* q = ws + (li + 1) * T0W + (lj + 1);
+            const double c = q[0];
+            const double h = __dsub_rn(wrapd(__dsub_rn((double)q[-1], c)), wrapd(__dsub_rn(c, (double)q[1])));
+            const double vv = __dsub_rn(wrapd(__dsub_rn((double)q[-T0W], c)), wrapd(__dsub_rn(c, (double)q[T0W])));
+            const double d1 =
+                __dsub_rn(wrapd(__dsub_rn((double)q[-T0W - 1], c)), wrapd(__dsub_rn(c, (double)q[T0W + 1])));
+            const double d2 =
+                __dsub_rn(wrapd(__dsub_rn((double)q[-T0W + 1], c)), wrapd(__dsub_rn(c, (double)q[T0W - 1])));
+            double s = __dadd_rn(__dmul_rn(h, h), __dmul_rn(vv, vv));
+            s = __dadd_rn(s, __dmul_rn(d1, d1));
+            s = __dadd_rn(s, __dmul_rn(d2, d2));
+            r = s;
+        }
+        rs[i] = r;
+        if (li >= 1 && li <= T0 && lj >= 1 && lj <= T0) m.rel[vbase + (long)gi * W + gj] = r;
+    }
+    for (int i = threadIdx.x; i < T0N; i += 256) {
+        lc[i] = i;
+        lo[i] = 0;
+        bw[i] = 0x7ff0000000000000ull;
+        be[i] = 0x7fffffff;
+    }
+    __syncthreads();
+    auto relat = [&](int li, int lj) { return rs[(li + 1) * T0R + (lj + 1)]; };  // li, lj in [-1, T0]
+    for (;;) {
+        // (a) each pixel's lightest edge to another tile component or out of the tile
+        unsigned long long key[4];
+        int ke[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int i = threadIdx.x + 256 * k;
+            const int li = i / T0, lj = i % T0, gi = gi0 + li, gj = gj0 + lj;
+            const int c = lc[i];
+            const double rv = relat(li, lj);
+            double bwv = __longlong_as_double(0x7ff0000000000000ll);
+            int bev = 0x7fffffff;
+            auto consider = [&](int ni, int nj, int eidx) {
+                const bool inside = ni >= 0 && ni < T0 && nj >= 0 && nj < T0;
+                if (inside && lc[ni * T0 + nj] == c) return;
+                const double we = __dadd_rn(rv, relat(ni, nj));
+                if (we < bwv || (we == bwv && eidx < bev)) {
+                    bwv = we;
+                    bev = eidx;
+                }
+            };
+            if (gj + 1 < W) consider(li, lj + 1, gi * (W - 1) + gj);
+            if (gj > 0) consider(li, lj - 1, gi * (W - 1) + gj - 1);
+            if (gi + 1 < H) consider(li + 1, lj, nh + gi * W + gj);
+            if (gi > 0) consider(li - 1, lj, nh + (gi - 1) * W + gj);
+            key[k] = bev != 0x7fffffff ? (unsigned long long)__double_as_longlong(bwv) : ~0ull;
+            ke[k] = bev;
+            if (key[k] != ~0ull) atomicMin(bw + c, key[k]);
+        }
+        if (threadIdx.x == 0) hooked = 0;
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int i = threadIdx.x + 256 * k;
+            if (key[k] != ~0ull && key[k] == bw[lc[i]]) atomicMin(be + lc[i], ke[k]);
+        }
+        __syncthreads();
+        // (c) hooks of the tile roots whose lightest edge ends inside the tile
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int c = threadIdx.x + 256 * k;
+            lk[c] = -1;
+            if (lc[c] != c) continue;
+            const int e = be[c];
+            if (e == 0x7fffffff) continue;
+            int a1i, a1j, a2i, a2j;  // edge endpoints (global), p1 = left / top
+            if (e < nh) {
+                a1i = e / (W - 1); a1j = e % (W - 1); a2i = a1i; a2j = a1j + 1;
+            } else {
+                a1i = (e - nh) / W; a1j = (e - nh) % W; a2i = a1i + 1; a2j = a1j;
+            }
+            const int l1i = a1i - gi0, l1j = a1j - gj0, l2i = a2i - gi0, l2j = a2j - gj0;
+            const bool in1 = l1i >= 0 && l1i < T0 && l1j >= 0 && l1j < T0;
+            const bool in2 = l2i >= 0 && l2i < T0 && l2j >= 0 && l2j < T0;
+            if (!in1 || !in2) continue;  // leaves the tile: the level rounds take it
+            const int x1 = l1i * T0 + l1j, x2 = l2i * T0 + l2j;
+            const int inc = find_wrap(ws[(l1i + 2) * T0W + l1j + 2], ws[(l2i + 2) * T0W + l2j + 2]);
+            int x, y, delta;  // k(y) - k(x) across the edge, x in c
+            if (lc[x1] == c) {
+                x = x1; y = x2; delta = -inc;
+            } else {
+                x = x2; y = x1; delta = inc;
+            }
+            const int d = lc[y];
+            if (be[d] == e && c < d) continue;  // mutual pair: the smaller root stays
+            lk[c] = d;
+            lko[c] = lo[y] - lo[x] - delta;  // K_c - K_d
+            hooked = 1;
+        }
+        __syncthreads();
+        if (!hooked) break;
+        // (d) resolve every hooked root to its final root (chains inside the tile)
+        int rf[4], ro[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int c = threadIdx.x + 256 * k;
+            int r = c, o = 0;
+            if (lc[c] == c) {
+                while (lk[r] >= 0) {
+                    o += lko[r];
+                    r = lk[r];
+                }
+            }
+            rf[k] = r;
+            ro[k] = o;
+        }
+        __syncthreads();
+        // publish the roots' results in lk / lko, then relabel every pixel
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int c = threadIdx.x + 256 * k;
+            if (lc[c] == c) {
+                lk[c] = rf[k];
+                lko[c] = ro[k];
+            }
+        }
+        __syncthreads();
+        int nc[4], no[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int i = threadIdx.x + 256 * k;
+            const int c = lc[i];
+            nc[k] = lk[c];
+            no[k] = lo[i] + lko[c];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int i = threadIdx.x + 256 * k;
+            lc[i] = nc[k];
+            lo[i] = no[k];
+            bw[i] = 0x7ff0000000000000ull;
+            be[i] = 0x7fffffff;
+        }
+        __syncthreads();
+    }
+    // level-0 components: global ids of the tile roots, offsets to them; candidate
+    // slots of every pixel reset for the level rounds
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int i = threadIdx.x + 256 * k;
+        const int li = i / T0, lj = i % T0;
+        const long v = vbase + (long)(gi0 + li) * W + (gj0 + lj);
+        const int c = lc[i];
+        m.comp[v] = (int)(vbase + (long)(gi0 + c / T0) * W + (gj0 + c % T0));
+        m.off[v] = lo[i];
+        m.best_w[v] = 0x7ff0000000000000ull;
+        m.best_e[v] = 0x7fffffff;
+    }
+}
+
+void mst_tile_level0(const float* w, const int* map_ids, int nact, int H, int W, MstWork m, hipStream_t s) {
+    if (H % T0 || W % T0) throw std::runtime_error("mst_tile_level0: frame not a multiple of the tile");
+    const long nblocks = (long)nact * (H / T0) * (W / T0);
+    hipLaunchKernelGGL(k_mst_tile0, dim3((unsigned)nblocks), dim3(256), 0, s, w, map_ids, nact, H, W, m);
+    FCD_CHECK_LAUNCH();
+}
+
 }  // namespace fcdk
