@@ -77,8 +77,9 @@ def test_spectro_params_match_scipy():
 
 # ---------------------------------------------------------------- GPU: device vs oracle
 @pytest.mark.gpu
-@pytest.mark.parametrize("T,block", [(400, 0), (301, 3)])
+@pytest.mark.parametrize("T,block", [(400, 0), (301, 3), (2000, 1)])
 def test_block_amplitude_matches_oracle(tmp_path, T, block):
+    """(2000 maps: the mean spectrum takes the FFT path by the engine's cost model.)"""
     from pydata.analyze import analyze
     st = make_stack(T, n=64, seed=T)
     write_maps(str(tmp_path), st)
@@ -111,7 +112,8 @@ def test_block_amplitude_no_peak(tmp_path):
 
 @pytest.mark.gpu
 def test_temporal_engine_long_series():
-    """T above the LDS table (the global-table kernel), odd T, a sub-block."""
+    """T above the LDS table (the FFT path for the spectrum, the global-table kernel
+    for the bins), odd T, a sub-block."""
     from pyfcd import _lib
     eng = _lib.temporal_engine()
     st = make_stack(9001, n=16, seed=5, zero_corner=False)
@@ -124,6 +126,67 @@ def test_temporal_engine_long_series():
     X = eng.temporal_bins(st, bins, block=(4, 2, 8, 8))
     close_nan(X.real, np.transpose(spec[bins, 4:12, 2:10], (1, 2, 0)).real)
     close_nan(X.imag, np.transpose(spec[bins, 4:12, 2:10], (1, 2, 0)).imag)
+
+
+def nan_spectrum(st, nf):
+    """np.nanmean's numerator and denominator over the pixels of |np.fft.fft| (f64):
+    a pixel with a NaN sample has every bin NaN and drops out."""
+    spec = np.abs(np.fft.fft(st.astype(np.float64), axis=0)[:nf])
+    ok = ~np.isnan(spec)
+    return np.where(ok, spec, 0.0).sum(axis=(1, 2)), ok.sum(axis=(1, 2)).astype(np.float64)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T", [1, 2, 3, 5, 100, 257, 2000])
+def test_temporal_fft_path_short_series(monkeypatch, T):
+    """The Bluestein / four-step FFT path (FCD_TDFT_FFT=1 forces it at any T): every
+    sub-transform length from 2 up, odd and prime T, NaN pixels excluded as np.nanmean
+    does, a sub-block addressed in place, against numpy's f64 FFT."""
+    from pyfcd import _lib
+    monkeypatch.setenv("FCD_TDFT_FFT", "1")
+    eng = _lib.temporal_engine()
+    st = make_stack(T, n=20, seed=T, zero_corner=False, nan_pixels=[(3, 4, T // 2, T // 2 + 1)])
+    nf = T // 2 + 1
+    tot, cnt = eng.temporal_spectrum(st, nf)
+    want_t, want_c = nan_spectrum(st, nf)
+    assert np.array_equal(cnt, want_c) and cnt[0] == 399
+    np.testing.assert_allclose(tot, want_t, rtol=1e-12)
+    blk = (2, 5, 11, 13)
+    tot, cnt = eng.temporal_spectrum(st, nf, block=blk)
+    want_t, want_c = nan_spectrum(st[:, 2:13, 5:18], nf)
+    assert np.array_equal(cnt, want_c)
+    np.testing.assert_allclose(tot, want_t, rtol=1e-12)
+
+
+@pytest.mark.gpu
+def test_temporal_fft_equals_direct_dft(monkeypatch, tdft_family):
+    """The FFT path and both direct-DFT kernel families agree to f64 rounding."""
+    from pyfcd import _lib
+    eng = _lib.temporal_engine()
+    st = make_stack(1500, n=40, seed=8, zero_corner=False)
+    monkeypatch.setenv("FCD_TDFT_FFT", "0")
+    direct = eng.temporal_spectrum(st, 751)
+    monkeypatch.setenv("FCD_TDFT_FFT", "1")
+    fft = eng.temporal_spectrum(st, 751)
+    assert np.array_equal(direct[1], fft[1])
+    np.testing.assert_allclose(fft[0], direct[0], rtol=1e-12)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T,n", [(40000, 24), (300001, 8)])
+def test_temporal_fft_long_series(T, n):
+    """Long series (the default FFT range, T > 8192): 40000 maps of 576 pixels need two
+    pixel batches of the work array; 300001 maps use the longest sub-transforms
+    (M = 2^20 = 1024 x 1024).  Against numpy's f64 FFT, per bin."""
+    from pyfcd import _lib
+    eng = _lib.temporal_engine()
+    rng = np.random.default_rng(T)
+    st = (rng.standard_normal((T, n, n)) + 3.0).astype(np.float32)
+    nf = T // 2 + 1
+    tot, cnt = eng.temporal_spectrum(st, nf)
+    want_t, want_c = nan_spectrum(st, nf)
+    assert np.array_equal(cnt, want_c)
+    np.testing.assert_allclose(tot, want_t, rtol=1e-10)
 
 
 @pytest.mark.gpu

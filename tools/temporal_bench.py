@@ -12,6 +12,10 @@ f64 peak of both the matrix cores (the mean-spectrum GEMM, k_tdft_mfma) and the 
 units (vendor spec).  CPU: the oracle's
 numpy / scipy calls (the reference's own, analyze.py:497, :521, :574) on a sample of the block's series, 1 core.
 
+The mean spectrum is timed on both paths (FCD_TDFT_FFT=0: the direct DFT, =1: the
+Bluestein / four-step FFT of kernels_tfft.hip, HBM-bound: 4 B x T + 4 x 16 B x M per
+series, M = 2^ceil(log2(2T - 1))).
+
     python tools/temporal_bench.py [--T 2000] [--reps 5]
 """
 import argparse
@@ -81,10 +85,25 @@ def main():
         torch.cuda.synchronize()
         return (time.perf_counter() - t0) / a.reps
 
+    def with_env(val, fn):
+        old = os.environ.get("FCD_TDFT_FFT")
+        os.environ["FCD_TDFT_FFT"] = val
+        try:
+            return timed(fn)
+        finally:
+            if old is None:
+                del os.environ["FCD_TDFT_FFT"]
+            else:
+                os.environ["FCD_TDFT_FFT"] = old
+
     t_spec = timed(spectrum)
+    t_fft = with_env("1", spectrum)
+    t_direct = with_env("0", spectrum)
+    M = 1 << max(2, (2 * T - 2).bit_length())
+    fft_bytes = P * (4.0 * T + 4 * 16.0 * M)  # stack read + 4 passes of the [M] f64 complex work
     t_harm = timed(harmonics)
     t_spg = timed(spectro)
-    flops_spec = 4.0 * P * T * nf
+    flops_spec = 4.0 * P * T * nf  # the direct DFT's count (the default path when T <= 8192)
     flops_spg = 4.0 * P * nseg * nperseg * nfs
 
     # CPU: the reference's calls on a sample of the block's series (1 core)
@@ -103,10 +122,15 @@ def main():
     print(json.dumps({
         "metric": "temporal post-analysis of a map stack (block_amplitude / spectrogram), pixel series per second",
         "workload": f"{T} maps of {n}x{n} float32 in HBM, one {b}x{b} block per call (num_blocks=64)",
-        "block_amplitude_spectrum": {"ms": t_spec * 1e3, "series_per_s": P / t_spec, "bins": nf,
-                                     "roofline": {"bound": "f64 (matrix cores; FCD_TDFT_VALU=1: vector)", "achieved_tflops": flops_spec / t_spec / 1e12,
-                                                  "peak_tflops": F64_PEAK / 1e12,
-                                                  "frac": flops_spec / t_spec / F64_PEAK}},
+        "block_amplitude_spectrum": {"ms": t_spec * 1e3, "series_per_s": P / t_spec, "bins": nf},
+        "direct_dft_roofline": {"bound": "f64 (matrix cores; FCD_TDFT_VALU=1 or T > 8192: vector)",
+                                "achieved_tflops": flops_spec / t_direct / 1e12, "peak_tflops": F64_PEAK / 1e12,
+                                "frac": flops_spec / t_direct / F64_PEAK},
+        "block_amplitude_spectrum_paths": {
+            "default": os.environ.get("FCD_TDFT_FFT_DEFAULT", "see kernels_tfft.hip"), "direct_ms": t_direct * 1e3, "fft_ms": t_fft * 1e3,
+            "fft_roofline": {"bound": "hbm", "M": M, "bytes_per_series": fft_bytes / P,
+                             "achieved_gbs": fft_bytes / t_fft / 1e9, "peak_gbs": 8000.0,
+                             "frac": fft_bytes / t_fft / 8e12}},
         "block_amplitude_harmonics": {"ms": t_harm * 1e3, "bins": len(bins)},
         "spectrogram": {"ms": t_spg * 1e3, "series_per_s": P / t_spg, "nperseg": nperseg, "segments": nseg,
                         "achieved_tflops": flops_spg / t_spg / 1e12, "frac": flops_spg / t_spg / F64_PEAK},

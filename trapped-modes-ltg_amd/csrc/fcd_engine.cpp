@@ -224,6 +224,7 @@ struct fcd_ctx {
     DevBuf fix_raw;  // raw samples of the frames redone by the exact pass
     // temporal analysis: staged block, exp table, bins, partial sums, output, window
     DevBuf t_stage, t_tab, t_bins, t_part, t_out, t_win, t_wsum, t_slices;
+    DevBuf t_chirp, t_bhat, t_work, t_gpart;  // the FFT path of the mean spectrum
     HostPipe pipe;
     // MST workspace
     DevBuf mst_comp, mst_off, mst_rel, mst_cw, mst_ce, mst_bw, mst_be, mst_link, mst_hooks, mst_ids;
@@ -1549,11 +1550,33 @@ FCD_API int fcd_temporal_spectrum(fcd_ctx* c, const void* stack, int T, int rows
         if (!sum_count || nf <= 0 || nf > T) throw FcdError(FCD_E_INVALID, "bad spectrum arguments");
         hipStream_t s = c->pick(stream);
         const BlockView v = stage_block(c, stack, T, rows, cols, r0, c0, bh, bw, flags, s);
-        upload_exp_table(c, c->t_tab, T, s);
-        const int P = bh * bw, tiles = fcdk::temporal_spectrum_tiles(P, T);
-        c->t_part.ensure((size_t)tiles * nf * 2 * sizeof(double));
-        fcdk::temporal_dft(v.p, v.frame_pitch, v.row_pitch, bw, P, T, c->t_tab.as<double2>(), nullptr, nf, nullptr,
-                           c->t_part.as<double>(), nullptr, s);
+        const int P = bh * bw;
+        fcdk::TfftPlan pl;
+        int tiles = 1;
+        if (fcdk::temporal_spectrum_uses_fft(T, nf) && fcdk::temporal_fft_plan(T, P, &pl)) {
+            // Bluestein + four-step FFT: chirp, twiddles and B = FFT(b) / M from the host in f64
+            std::vector<double2> chirp, tw, bhat;
+            fcdk::temporal_fft_tables(T, pl, chirp, tw, bhat);
+            c->t_tab.ensure(tw.size() * sizeof(double2));
+            c->t_chirp.ensure(chirp.size() * sizeof(double2));
+            c->t_bhat.ensure(bhat.size() * sizeof(double2));
+            c->t_work.ensure((size_t)pl.Pb * pl.M * sizeof(double2));
+            c->t_gpart.ensure((size_t)pl.ngroups * nf * sizeof(double2));
+            c->t_part.ensure((size_t)nf * 2 * sizeof(double));
+            upload(c->t_tab.p, tw.data(), tw.size() * sizeof(double2), s);
+            upload(c->t_chirp.p, chirp.data(), chirp.size() * sizeof(double2), s);
+            upload(c->t_bhat.p, bhat.data(), bhat.size() * sizeof(double2), s);
+            fcdk::temporal_spectrum_fft(v.p, v.frame_pitch, v.row_pitch, bw, P, T, nf, pl, c->t_chirp.as<double2>(),
+                                        c->t_tab.as<double2>(), c->t_bhat.as<double2>(), c->t_work.as<double2>(),
+                                        c->t_gpart.as<double2>(), c->t_part.as<double>(), s);
+            HIPCHK(hipStreamSynchronize(s));  // the host tables die here
+        } else {
+            upload_exp_table(c, c->t_tab, T, s);
+            tiles = fcdk::temporal_spectrum_tiles(P, T);
+            c->t_part.ensure((size_t)tiles * nf * 2 * sizeof(double));
+            fcdk::temporal_dft(v.p, v.frame_pitch, v.row_pitch, bw, P, T, c->t_tab.as<double2>(), nullptr, nf,
+                               nullptr, c->t_part.as<double>(), nullptr, s);
+        }
         std::vector<double> part((size_t)tiles * nf * 2);
         HIPCHK(hipMemcpyAsync(part.data(), c->t_part.p, part.size() * sizeof(double), hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));

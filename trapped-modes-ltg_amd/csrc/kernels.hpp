@@ -4,6 +4,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <vector>
 
 namespace fcdk {
 
@@ -160,6 +161,19 @@ int temporal_dft_tiles(int P);
 int temporal_spectrum_tiles(int P, int T);  // partial-sum rows of a mean-spectrum call
 int temporal_bins_slices(int P, int nf, int T);  // slices[slices][P][nf] workspace of a bins call
 int spectro_max_nperseg();
+// mean spectrum of a long series by Bluestein + four-step FFT (kernels_tfft.hip)
+struct TfftPlan {
+    int logM, M, log1, log2, M1, M2;  // M = 2^logM >= 2T - 1 = M1 x M2
+    int Pb, ngroups;                  // pixels per batch, 64-pixel partial groups
+};
+bool temporal_spectrum_uses_fft(int T, int nf);
+bool temporal_fft_plan(int T, int P, TfftPlan* pl);  // false: T too long for the LDS sub-transforms
+void temporal_fft_tables(int T, const TfftPlan& pl, std::vector<double2>& chirp, std::vector<double2>& tw,
+                         std::vector<double2>& bhat);
+// partial [nf][2] (sum of |X|, count) over the block; work [Pb x M] double2, gpart [ngroups x nf] double2
+void temporal_spectrum_fft(Samples stack, long frame_pitch, long row_pitch, int bw, int P, int T, int nf,
+                           const TfftPlan& pl, const double2* chirp, const double2* tw, const double2* bhat,
+                           double2* work, double2* gpart, double* partial, hipStream_t s);
 void spectrogram(Samples stack, long frame_pitch, long row_pitch, int bw, int P, int nperseg, int step, int nseg,
                  const double* win, const double2* tab, const double2* wsum, int nf, double scale, double* out,
                  hipStream_t s);

@@ -343,7 +343,7 @@ __global__ __launch_bounds__(PR_THREADS, FCD_PR_MINB) void k_phase_rows(
 #pragma unroll
                 for (int j = 0; j < 16; ++j) {
                     const fv2 d = pv(v[j]) - pv(v[j + 1]);
-                    amb |= (fabsf(d.x) == 3.14159274f) | (fabsf(d.y) == 3.14159274f);
+                    amb |= (fabsf(d.x) == 3.14159274f) || (fabsf(d.y) == 3.14159274f);
                     const fv2 q = d * 0.159154943091895f;
                     dd[j] = fv2{rintf(q.x), rintf(q.y)};
                     run += dd[j];
