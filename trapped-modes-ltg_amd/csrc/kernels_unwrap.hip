@@ -790,8 +790,12 @@ constexpr int T0R = T0 + 2;            // reliabilities with a 1-pixel halo
 __global__ __launch_bounds__(256) void k_mst_tile0(const float* __restrict__ w, const int* __restrict__ map_ids,
                                                    int nact, int H, int W, MstWork m) {
     __shared__ float ws[T0W * T0W];
-    __shared__ double rs[T0R * T0R];
-    __shared__ unsigned long long bw[T0N];
+    // reliabilities (before the rounds) and the components' lightest weights (during
+    // them) share one array: 35 KB per workgroup, 4 workgroups per CU
+    __shared__ double rs_bw[T0R * T0R];
+    static_assert(T0R * T0R * sizeof(double) >= T0N * sizeof(unsigned long long), "bw fits the rs array");
+    double* const rs = rs_bw;
+    unsigned long long* const bw = reinterpret_cast<unsigned long long*>(rs_bw);
     __shared__ int lc[T0N], lo[T0N], be[T0N], lk[T0N], lko[T0N];
     __shared__ int hooked;
     const long hw = (long)H * W;
@@ -829,6 +833,29 @@ __global__ __launch_bounds__(256) void k_mst_tile0(const float* __restrict__ w, 
         rs[i] = r;
         if (li >= 1 && li <= T0 && lj >= 1 && lj <= T0) m.rel[vbase + (long)gi * W + gj] = r;
     }
+    __syncthreads();
+    auto relat = [&](int li, int lj) { return rs[(li + 1) * T0R + (lj + 1)]; };  // li, lj in [-1, T0]
+    // the 4 incident edges of each of this thread's pixels, once: weight rel(p) + rel(q)
+    // (f64, as k_mst_rel / k_mst_round) as its bit pattern (non-negative doubles order
+    // as unsigned integers), ~0 for an edge past the map border, and its edge index;
+    // the rounds then only compare integers
+    unsigned long long ekey[4][4];
+    int eid[4][4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int i = threadIdx.x + 256 * k;
+        const int li = i / T0, lj = i % T0, gi = gi0 + li, gj = gj0 + lj;
+        const double rv = relat(li, lj);
+        auto edge = [&](int d, bool exists, int ni, int nj, int eidx) {
+            ekey[k][d] = exists ? (unsigned long long)__double_as_longlong(__dadd_rn(rv, relat(ni, nj))) : ~0ull;
+            eid[k][d] = eidx;
+        };
+        edge(0, gj + 1 < W, li, lj + 1, gi * (W - 1) + gj);
+        edge(1, gj > 0, li, lj - 1, gi * (W - 1) + gj - 1);
+        edge(2, gi + 1 < H, li + 1, lj, nh + gi * W + gj);
+        edge(3, gi > 0, li - 1, lj, nh + (gi - 1) * W + gj);
+    }
+    __syncthreads();  // every reliability read before bw overwrites them
     for (int i = threadIdx.x; i < T0N; i += 256) {
         lc[i] = i;
         lo[i] = 0;
@@ -836,7 +863,6 @@ __global__ __launch_bounds__(256) void k_mst_tile0(const float* __restrict__ w, 
         be[i] = 0x7fffffff;
     }
     __syncthreads();
-    auto relat = [&](int li, int lj) { return rs[(li + 1) * T0R + (lj + 1)]; };  // li, lj in [-1, T0]
     for (;;) {
         // (a) each pixel's lightest edge to another tile component or out of the tile
         unsigned long long key[4];
@@ -844,25 +870,22 @@ __global__ __launch_bounds__(256) void k_mst_tile0(const float* __restrict__ w, 
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int i = threadIdx.x + 256 * k;
-            const int li = i / T0, lj = i % T0, gi = gi0 + li, gj = gj0 + lj;
+            const int li = i / T0, lj = i % T0;
             const int c = lc[i];
-            const double rv = relat(li, lj);
-            double bwv = __longlong_as_double(0x7ff0000000000000ll);
+            unsigned long long bk = ~0ull;
             int bev = 0x7fffffff;
-            auto consider = [&](int ni, int nj, int eidx) {
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                const int ni = li + (d == 2) - (d == 3), nj = lj + (d == 0) - (d == 1);
                 const bool inside = ni >= 0 && ni < T0 && nj >= 0 && nj < T0;
-                if (inside && lc[ni * T0 + nj] == c) return;
-                const double we = __dadd_rn(rv, relat(ni, nj));
-                if (we < bwv || (we == bwv && eidx < bev)) {
-                    bwv = we;
-                    bev = eidx;
+                if (inside && lc[ni * T0 + nj] == c) continue;
+                const unsigned long long kk = ekey[k][d];
+                if (kk < bk || (kk == bk && kk != ~0ull && eid[k][d] < bev)) {
+                    bk = kk;
+                    bev = eid[k][d];
                 }
-            };
-            if (gj + 1 < W) consider(li, lj + 1, gi * (W - 1) + gj);
-            if (gj > 0) consider(li, lj - 1, gi * (W - 1) + gj - 1);
-            if (gi + 1 < H) consider(li + 1, lj, nh + gi * W + gj);
-            if (gi > 0) consider(li - 1, lj, nh + (gi - 1) * W + gj);
-            key[k] = bev != 0x7fffffff ? (unsigned long long)__double_as_longlong(bwv) : ~0ull;
+            }
+            key[k] = bk;
             ke[k] = bev;
             if (key[k] != ~0ull) atomicMin(bw + c, key[k]);
         }
