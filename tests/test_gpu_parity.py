@@ -183,8 +183,9 @@ def test_unwrap_matches_oracle_random_residues(lib):
 
 @pytest.mark.parametrize("shape", [(256, 256), (128, 512)])
 def test_unwrap_two_level_equals_pixel_rounds(lib, monkeypatch, shape):
-    """The two-level Boruvka (level-0 components from 32 x 32 tiles, or one pixel round
-    with FCD_MST_LEVEL=1, then block-segmented boundary / root lists) and the all-pixel
+    """The two-level Boruvka (level-0 components from 64 x 64 tiles, 32 x 32 with
+    FCD_MST_TILE=32, or one pixel round with FCD_MST_LEVEL=1, then block-segmented
+    boundary / root lists) and the all-pixel
     rounds (FCD_MST_LEVEL=0) build the same unique MST:
     identical k-fields, bit for bit, over a batch of maps with thousands of residues
     (several maps per list segment, segments spanning maps), and equal to the oracle."""
@@ -199,6 +200,10 @@ def test_unwrap_two_level_equals_pixel_rounds(lib, monkeypatch, shape):
     eng = lib.Engine(shape)
     k2, res = eng.unwrap(w)
     assert (res > 0).all() and res.sum() > 5000
+    monkeypatch.setenv("FCD_MST_TILE", "32")
+    k1, _ = eng.unwrap(w)
+    assert np.array_equal(k1, k2), "32 x 32 tiles"
+    monkeypatch.delenv("FCD_MST_TILE")
     for level in ("0", "1"):  # all-pixel rounds; one pixel round before the list rounds
         monkeypatch.setenv("FCD_MST_LEVEL", level)
         k1, _ = eng.unwrap(w)

@@ -362,7 +362,7 @@ void unwrap_maps(fcd_ctx* c, const float* w, int nmaps, int32_t* k, int* res_hos
     // third round (a round after convergence hooks nothing and changes nothing).
     const int level = mst_level();
     if (level >= 1) {
-        if (level >= 2 && c->H % 32 == 0 && c->W % 32 == 0) {
+        if (level >= 2 && fcdk::mst_tile_side(c->H, c->W) > 0) {
             // level-0 components from Boruvka inside 32 x 32 tiles (LDS)
             fcdk::mst_tile_level0(w, c->mst_ids.as<int>(), nact, c->H, c->W, m, s);
         } else {

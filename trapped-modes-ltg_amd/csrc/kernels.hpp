@@ -135,6 +135,7 @@ void mst_finalize(const int* map_ids, int nact, int H, int W, MstWork m, int32_t
 int mst_level_counts();
 // Level-0 components from Boruvka inside each 32 x 32 tile (LDS), with the
 // reliabilities; replaces mst_init + the first pixel round before mst_level_setup.
+int mst_tile_side(int H, int W);  // 64, 32, or 0: no tile pass
 void mst_tile_level0(const float* w, const int* map_ids, int nact, int H, int W, MstWork m, hipStream_t s);
 void mst_level_setup(int nact, int H, int W, MstWork m, hipStream_t s);
 void mst_level_round(const float* w, const int* map_ids, int nact, int H, int W, MstWork m, int r, hipStream_t s);

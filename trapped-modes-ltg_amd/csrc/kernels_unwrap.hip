@@ -20,6 +20,8 @@
 // history).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include <algorithm>
 #include <stdexcept>
 #include <string>
@@ -782,16 +784,18 @@ void mst_level_finalize(const int* map_ids, int nact, int H, int W, MstWork m, i
 // is an MST edge, so the components are subtrees of the MST and the two-level rounds
 // finish the same tree (same k-field as the all-pixel rounds).  The tile also
 // writes the f64 reliabilities (k_mst_rel's arithmetic) the later rounds read.
-constexpr int T0 = 32;                 // tile side
-constexpr int T0N = T0 * T0;           // pixels per tile
-constexpr int T0W = T0 + 4;            // wrapped-phase image with a 2-pixel halo
-constexpr int T0R = T0 + 2;            // reliabilities with a 1-pixel halo
-
-__global__ __launch_bounds__(256) void k_mst_tile0(const float* __restrict__ w, const int* __restrict__ map_ids,
-                                                   int nact, int H, int W, MstWork m) {
+// Tile side T0 = 32 (1024 pixels, 256 threads, 35 KB of LDS: 4 workgroups per CU) or
+// 64 (4096 pixels, 1024 threads, 133 KB: one per CU); 4 pixels per thread either way.
+template <int T0>
+__global__ __launch_bounds__(T0 * T0 / 4) void k_mst_tile0(const float* __restrict__ w, const int* __restrict__ map_ids,
+                                                          int nact, int H, int W, MstWork m) {
+    constexpr int T0N = T0 * T0;  // pixels per tile
+    constexpr int T0W = T0 + 4;   // wrapped-phase image with a 2-pixel halo
+    constexpr int T0R = T0 + 2;   // reliabilities with a 1-pixel halo
+    constexpr int NT = T0N / 4;   // threads
     __shared__ float ws[T0W * T0W];
     // reliabilities (before the rounds) and the components' lightest weights (during
-    // them) share one array: 35 KB per workgroup, 4 workgroups per CU
+    // them) share one array
     __shared__ double rs_bw[T0R * T0R];
     static_assert(T0R * T0R * sizeof(double) >= T0N * sizeof(unsigned long long), "bw fits the rs array");
     double* const rs = rs_bw;
@@ -806,13 +810,13 @@ __global__ __launch_bounds__(256) void k_mst_tile0(const float* __restrict__ w, 
     const long vbase = (long)slot * hw;
     const int nh = H * (W - 1);
     // wrapped phases, 2-pixel halo (outside the map: never read for an existing edge)
-    for (int i = threadIdx.x; i < T0W * T0W; i += 256) {
+    for (int i = threadIdx.x; i < T0W * T0W; i += NT) {
         const int gi = gi0 - 2 + i / T0W, gj = gj0 - 2 + i % T0W;
         ws[i] = (gi >= 0 && gi < H && gj >= 0 && gj < W) ? mw[(long)gi * W + gj] : 0.f;
     }
     __syncthreads();
     // reliabilities of the tile and its 1-pixel halo (k_mst_rel's operation order)
-    for (int i = threadIdx.x; i < T0R * T0R; i += 256) {
+    for (int i = threadIdx.x; i < T0R * T0R; i += NT) {
         const int li = i / T0R, lj = i % T0R;  // ws index (li + 1, lj + 1)
         const int gi = gi0 - 1 + li, gj = gj0 - 1 + lj;
         double r = kBorderRel;
@@ -843,7 +847,7 @@ __global__ __launch_bounds__(256) void k_mst_tile0(const float* __restrict__ w, 
     int eid[4][4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        const int i = threadIdx.x + 256 * k;
+        const int i = threadIdx.x + NT * k;
         const int li = i / T0, lj = i % T0, gi = gi0 + li, gj = gj0 + lj;
         const double rv = relat(li, lj);
         auto edge = [&](int d, bool exists, int ni, int nj, int eidx) {
@@ -856,7 +860,7 @@ __global__ __launch_bounds__(256) void k_mst_tile0(const float* __restrict__ w, 
         edge(3, gi > 0, li - 1, lj, nh + (gi - 1) * W + gj);
     }
     __syncthreads();  // every reliability read before bw overwrites them
-    for (int i = threadIdx.x; i < T0N; i += 256) {
+    for (int i = threadIdx.x; i < T0N; i += NT) {
         lc[i] = i;
         lo[i] = 0;
         bw[i] = 0x7ff0000000000000ull;
@@ -869,7 +873,7 @@ __global__ __launch_bounds__(256) void k_mst_tile0(const float* __restrict__ w, 
         int ke[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const int i = threadIdx.x + 256 * k;
+            const int i = threadIdx.x + NT * k;
             const int li = i / T0, lj = i % T0;
             const int c = lc[i];
             unsigned long long bk = ~0ull;
@@ -893,14 +897,14 @@ __global__ __launch_bounds__(256) void k_mst_tile0(const float* __restrict__ w, 
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const int i = threadIdx.x + 256 * k;
+            const int i = threadIdx.x + NT * k;
             if (key[k] != ~0ull && key[k] == bw[lc[i]]) atomicMin(be + lc[i], ke[k]);
         }
         __syncthreads();
         // (c) hooks of the tile roots whose lightest edge ends inside the tile
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const int c = threadIdx.x + 256 * k;
+            const int c = threadIdx.x + NT * k;
             lk[c] = -1;
             if (lc[c] != c) continue;
             const int e = be[c];
@@ -935,7 +939,7 @@ __global__ __launch_bounds__(256) void k_mst_tile0(const float* __restrict__ w, 
         int rf[4], ro[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const int c = threadIdx.x + 256 * k;
+            const int c = threadIdx.x + NT * k;
             int r = c, o = 0;
             if (lc[c] == c) {
                 while (lk[r] >= 0) {
@@ -950,7 +954,7 @@ __global__ __launch_bounds__(256) void k_mst_tile0(const float* __restrict__ w, 
         // publish the roots' results in lk / lko, then relabel every pixel
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const int c = threadIdx.x + 256 * k;
+            const int c = threadIdx.x + NT * k;
             if (lc[c] == c) {
                 lk[c] = rf[k];
                 lko[c] = ro[k];
@@ -960,7 +964,7 @@ __global__ __launch_bounds__(256) void k_mst_tile0(const float* __restrict__ w, 
         int nc[4], no[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const int i = threadIdx.x + 256 * k;
+            const int i = threadIdx.x + NT * k;
             const int c = lc[i];
             nc[k] = lk[c];
             no[k] = lo[i] + lko[c];
@@ -968,7 +972,7 @@ __global__ __launch_bounds__(256) void k_mst_tile0(const float* __restrict__ w, 
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const int i = threadIdx.x + 256 * k;
+            const int i = threadIdx.x + NT * k;
             lc[i] = nc[k];
             lo[i] = no[k];
             bw[i] = 0x7ff0000000000000ull;
@@ -980,7 +984,7 @@ __global__ __launch_bounds__(256) void k_mst_tile0(const float* __restrict__ w, 
     // slots of every pixel reset for the level rounds
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        const int i = threadIdx.x + 256 * k;
+        const int i = threadIdx.x + NT * k;
         const int li = i / T0, lj = i % T0;
         const long v = vbase + (long)(gi0 + li) * W + (gj0 + lj);
         const int c = lc[i];
@@ -991,10 +995,22 @@ __global__ __launch_bounds__(256) void k_mst_tile0(const float* __restrict__ w, 
     }
 }
 
+int mst_tile_side(int H, int W) {
+    const char* e = std::getenv("FCD_MST_TILE");  // diagnostic override (32 / 64), read per call
+    const int want = e ? std::atoi(e) : 64;
+    if (want == 64 && H % 64 == 0 && W % 64 == 0) return 64;
+    if (H % 32 == 0 && W % 32 == 0) return 32;
+    return 0;
+}
+
 void mst_tile_level0(const float* w, const int* map_ids, int nact, int H, int W, MstWork m, hipStream_t s) {
-    if (H % T0 || W % T0) throw std::runtime_error("mst_tile_level0: frame not a multiple of the tile");
-    const long nblocks = (long)nact * (H / T0) * (W / T0);
-    hipLaunchKernelGGL(k_mst_tile0, dim3((unsigned)nblocks), dim3(256), 0, s, w, map_ids, nact, H, W, m);
+    const int t = mst_tile_side(H, W);
+    if (!t) throw std::runtime_error("mst_tile_level0: frame not a multiple of the tile");
+    const long nblocks = (long)nact * (H / t) * (W / t);
+    if (t == 64)
+        hipLaunchKernelGGL(k_mst_tile0<64>, dim3((unsigned)nblocks), dim3(1024), 0, s, w, map_ids, nact, H, W, m);
+    else
+        hipLaunchKernelGGL(k_mst_tile0<32>, dim3((unsigned)nblocks), dim3(256), 0, s, w, map_ids, nact, H, W, m);
     FCD_CHECK_LAUNCH();
 }
 
