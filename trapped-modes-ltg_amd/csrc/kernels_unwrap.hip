@@ -786,29 +786,63 @@ void mst_level_finalize(const int* map_ids, int nact, int H, int W, MstWork m, i
 // writes the f64 reliabilities (k_mst_rel's arithmetic) the later rounds read.
 // Tile side T0 = 32 (1024 pixels, 256 threads, 35 KB of LDS: 4 workgroups per CU) or
 // 64 (4096 pixels, 1024 threads, 133 KB: one per CU); 4 pixels per thread either way.
+#ifdef FCD_T0_STAMPS
+// diagnostic: per-phase cycles of the first 256 tiles (thread 0) and their round counts
+__device__ unsigned long long g_t0_stamps[256 * 9];
+extern "C" __attribute__((visibility("default"))) int fcd_debug_t0_stamps(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_t0_stamps), sizeof(g_t0_stamps)) == hipSuccess ? 0 : -1;
+}
+#endif
+// Edges of a tile by a local code that keeps the global edge order (horizontal edges
+// first, each kind row-major; li, lj in [-1, T0] relative to the tile origin):
+// horizontal (li, lj)-(li, lj + 1) -> (li + 1) << 7 | (lj + 1), vertical (li, lj)-(li + 1, lj)
+// -> 1 << 14 | (li + 1) << 7 | (lj + 1).  Decoding is shifts and masks.
+__device__ __forceinline__ int t0_hcode(int li, int lj) { return ((li + 1) << 7) | (lj + 1); }
+__device__ __forceinline__ int t0_vcode(int li, int lj) { return (1 << 14) | ((li + 1) << 7) | (lj + 1); }
+// a root's link: parent (local index) in the high half, K_c - K_parent (|.| <= T0N) low
+__device__ __forceinline__ unsigned t0_link(int parent, int off) { return ((unsigned)parent << 16) | (unsigned short)off; }
+__device__ __forceinline__ int t0_parent(unsigned l) { return (int)(l >> 16); }
+__device__ __forceinline__ int t0_off(unsigned l) { return (int)(short)(l & 0xffffu); }
+
 template <int T0>
 __global__ __launch_bounds__(T0 * T0 / 4) void k_mst_tile0(const float* __restrict__ w, const int* __restrict__ map_ids,
                                                           int nact, int H, int W, MstWork m) {
     constexpr int T0N = T0 * T0;  // pixels per tile
     constexpr int T0W = T0 + 4;   // wrapped-phase image with a 2-pixel halo
     constexpr int T0R = T0 + 2;   // reliabilities with a 1-pixel halo
-    constexpr int NT = T0N / 4;   // threads
-    __shared__ float ws[T0W * T0W];
-    // reliabilities (before the rounds) and the components' lightest weights (during
-    // them) share one array
-    __shared__ double rs_bw[T0R * T0R];
-    static_assert(T0R * T0R * sizeof(double) >= T0N * sizeof(unsigned long long), "bw fits the rs array");
-    double* const rs = rs_bw;
-    unsigned long long* const bw = reinterpret_cast<unsigned long long*>(rs_bw);
-    __shared__ int lc[T0N], lo[T0N], be[T0N], lk[T0N], lko[T0N];
-    __shared__ int hooked;
+    constexpr int NT = T0N / 4;   // threads, 4 pixels each
+    static_assert(T0 <= 64, "16-bit local indices and 7-bit edge-code fields");
+    // 16 bytes per pixel (64 KB at 64 x 64: two workgroups per CU): the rounds' arrays;
+    // before them the same bytes hold the wrapped phases and reliabilities.  A root's
+    // link replaces its edge code once every hook decision is made (step (c)).
+    __shared__ __attribute__((aligned(16))) unsigned char pool[16 * T0N];
+    unsigned long long* const bw = reinterpret_cast<unsigned long long*>(pool);  // component minima (f64 bits)
+    int* const be = reinterpret_cast<int*>(pool + 8 * T0N);                      // their edge codes
+    unsigned* const lnk = reinterpret_cast<unsigned*>(pool + 8 * T0N);           // then the roots' links
+    short* const lc = reinterpret_cast<short*>(pool + 12 * T0N);                 // component of each pixel
+    short* const lo = reinterpret_cast<short*>(pool + 14 * T0N);                 // K(pixel) - K(component)
+    float* const ws = reinterpret_cast<float*>(pool);
+    double* const rs = reinterpret_cast<double*>(pool + ((T0W * T0W * 4 + 15) & ~15));
+    static_assert(((T0W * T0W * 4 + 15) & ~15) + T0R * T0R * 8 <= 16 * T0N, "phases + reliabilities fit the pool");
+#ifdef FCD_T0_STAMPS
+    unsigned long long tprev = __builtin_readcyclecounter(), ph[8] = {};
+#define T0_STAMP(i)                                                \
+    do {                                                           \
+        const unsigned long long t_ = __builtin_readcyclecounter(); \
+        ph[(i)] += t_ - tprev;                                     \
+        tprev = t_;                                                \
+    } while (0)
+#else
+#define T0_STAMP(i) \
+    do {            \
+    } while (0)
+#endif
     const long hw = (long)H * W;
     const int tiles_x = W / T0, tiles = (H / T0) * tiles_x;
     const int slot = blockIdx.x / tiles, tile = blockIdx.x % tiles;
     const int gi0 = (tile / tiles_x) * T0, gj0 = (tile % tiles_x) * T0;
     const float* mw = w + (long)map_ids[slot] * hw;
     const long vbase = (long)slot * hw;
-    const int nh = H * (W - 1);
     // wrapped phases, 2-pixel halo (outside the map: never read for an existing edge)
     for (int i = threadIdx.x; i < T0W * T0W; i += NT) {
         const int gi = gi0 - 2 + i / T0W, gj = gj0 - 2 + i % T0W;
@@ -838,36 +872,38 @@ __global__ __launch_bounds__(T0 * T0 / 4) void k_mst_tile0(const float* __restri
         if (li >= 1 && li <= T0 && lj >= 1 && lj <= T0) m.rel[vbase + (long)gi * W + gj] = r;
     }
     __syncthreads();
+    T0_STAMP(0);
     auto relat = [&](int li, int lj) { return rs[(li + 1) * T0R + (lj + 1)]; };  // li, lj in [-1, T0]
     // the 4 incident edges of each of this thread's pixels, once: weight rel(p) + rel(q)
     // (f64, as k_mst_rel / k_mst_round) as its bit pattern (non-negative doubles order
-    // as unsigned integers), ~0 for an edge past the map border, and its edge index;
-    // the rounds then only compare integers
+    // as unsigned integers), ~0 for an edge past the map border; the rounds then only
+    // compare integers (weight, then edge code)
     unsigned long long ekey[4][4];
-    int eid[4][4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int i = threadIdx.x + NT * k;
         const int li = i / T0, lj = i % T0, gi = gi0 + li, gj = gj0 + lj;
         const double rv = relat(li, lj);
-        auto edge = [&](int d, bool exists, int ni, int nj, int eidx) {
+        auto edge = [&](int d, bool exists, int ni, int nj) {
             ekey[k][d] = exists ? (unsigned long long)__double_as_longlong(__dadd_rn(rv, relat(ni, nj))) : ~0ull;
-            eid[k][d] = eidx;
         };
-        edge(0, gj + 1 < W, li, lj + 1, gi * (W - 1) + gj);
-        edge(1, gj > 0, li, lj - 1, gi * (W - 1) + gj - 1);
-        edge(2, gi + 1 < H, li + 1, lj, nh + gi * W + gj);
-        edge(3, gi > 0, li - 1, lj, nh + (gi - 1) * W + gj);
+        edge(0, gj + 1 < W, li, lj + 1);
+        edge(1, gj > 0, li, lj - 1);
+        edge(2, gi + 1 < H, li + 1, lj);
+        edge(3, gi > 0, li - 1, lj);
     }
-    __syncthreads();  // every reliability read before bw overwrites them
+    __syncthreads();  // every phase / reliability read before the rounds' arrays overwrite them
     for (int i = threadIdx.x; i < T0N; i += NT) {
-        lc[i] = i;
+        lc[i] = (short)i;
         lo[i] = 0;
         bw[i] = 0x7ff0000000000000ull;
         be[i] = 0x7fffffff;
     }
     __syncthreads();
+    T0_STAMP(1);
+    [[maybe_unused]] int nrounds = 0;
     for (;;) {
+        ++nrounds;
         // (a) each pixel's lightest edge to another tile component or out of the tile
         unsigned long long key[4];
         int ke[4];
@@ -884,43 +920,45 @@ __global__ __launch_bounds__(T0 * T0 / 4) void k_mst_tile0(const float* __restri
                 const bool inside = ni >= 0 && ni < T0 && nj >= 0 && nj < T0;
                 if (inside && lc[ni * T0 + nj] == c) continue;
                 const unsigned long long kk = ekey[k][d];
-                if (kk < bk || (kk == bk && kk != ~0ull && eid[k][d] < bev)) {
+                const int code = d == 0 ? t0_hcode(li, lj)
+                                        : (d == 1 ? t0_hcode(li, lj - 1) : (d == 2 ? t0_vcode(li, lj) : t0_vcode(li - 1, lj)));
+                if (kk < bk || (kk == bk && kk != ~0ull && code < bev)) {
                     bk = kk;
-                    bev = eid[k][d];
+                    bev = code;
                 }
             }
             key[k] = bk;
             ke[k] = bev;
-            if (key[k] != ~0ull) atomicMin(bw + c, key[k]);
+            if (bk != ~0ull) atomicMin(bw + c, bk);
         }
-        if (threadIdx.x == 0) hooked = 0;
         __syncthreads();
+        T0_STAMP(2);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int i = threadIdx.x + NT * k;
             if (key[k] != ~0ull && key[k] == bw[lc[i]]) atomicMin(be + lc[i], ke[k]);
         }
         __syncthreads();
-        // (c) hooks of the tile roots whose lightest edge ends inside the tile
+        T0_STAMP(3);
+        // (c) hooks of the tile roots whose lightest edge ends inside the tile: decided
+        // from the edge codes, then published as links over them
+        int hooked = 0;
+        unsigned nl[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int c = threadIdx.x + NT * k;
-            lk[c] = -1;
+            nl[k] = t0_link(c, 0);
             if (lc[c] != c) continue;
             const int e = be[c];
             if (e == 0x7fffffff) continue;
-            int a1i, a1j, a2i, a2j;  // edge endpoints (global), p1 = left / top
-            if (e < nh) {
-                a1i = e / (W - 1); a1j = e % (W - 1); a2i = a1i; a2j = a1j + 1;
-            } else {
-                a1i = (e - nh) / W; a1j = (e - nh) % W; a2i = a1i + 1; a2j = a1j;
-            }
-            const int l1i = a1i - gi0, l1j = a1j - gj0, l2i = a2i - gi0, l2j = a2j - gj0;
+            const int l1i = ((e >> 7) & 127) - 1, l1j = (e & 127) - 1;
+            const bool vert = e >> 14;
+            const int l2i = l1i + vert, l2j = l1j + !vert;
             const bool in1 = l1i >= 0 && l1i < T0 && l1j >= 0 && l1j < T0;
             const bool in2 = l2i >= 0 && l2i < T0 && l2j >= 0 && l2j < T0;
             if (!in1 || !in2) continue;  // leaves the tile: the level rounds take it
             const int x1 = l1i * T0 + l1j, x2 = l2i * T0 + l2j;
-            const int inc = find_wrap(ws[(l1i + 2) * T0W + l1j + 2], ws[(l2i + 2) * T0W + l2j + 2]);
+            const int inc = find_wrap(mw[(long)(gi0 + l1i) * W + gj0 + l1j], mw[(long)(gi0 + l2i) * W + gj0 + l2j]);
             int x, y, delta;  // k(y) - k(x) across the edge, x in c
             if (lc[x1] == c) {
                 x = x1; y = x2; delta = -inc;
@@ -929,56 +967,57 @@ __global__ __launch_bounds__(T0 * T0 / 4) void k_mst_tile0(const float* __restri
             }
             const int d = lc[y];
             if (be[d] == e && c < d) continue;  // mutual pair: the smaller root stays
-            lk[c] = d;
-            lko[c] = lo[y] - lo[x] - delta;  // K_c - K_d
+            nl[k] = t0_link(d, lo[y] - lo[x] - delta);  // K_c - K_d
             hooked = 1;
         }
-        __syncthreads();
-        if (!hooked) break;
-        // (d) resolve every hooked root to its final root (chains inside the tile)
-        int rf[4], ro[4];
+        const int any = __syncthreads_or(hooked);
+        if (!any) break;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int c = threadIdx.x + NT * k;
-            int r = c, o = 0;
-            if (lc[c] == c) {
-                while (lk[r] >= 0) {
-                    o += lko[r];
-                    r = lk[r];
-                }
-            }
-            rf[k] = r;
-            ro[k] = o;
+            if (lc[c] == c) lnk[c] = nl[k];
         }
         __syncthreads();
-        // publish the roots' results in lk / lko, then relabel every pixel
+        T0_STAMP(4);
+        // (d) every hooked root to its final root, publishing the shortcuts as it walks
+        // (a root's link is one 32-bit word, so parent and offset are read together)
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int c = threadIdx.x + NT * k;
-            if (lc[c] == c) {
-                lk[c] = rf[k];
-                lko[c] = ro[k];
+            if (lc[c] != c) continue;
+            const unsigned l = __hip_atomic_load(lnk + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            int p = t0_parent(l), o = t0_off(l);
+            if (p == c) continue;
+            for (;;) {
+                const unsigned l2 = __hip_atomic_load(lnk + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                const int pp = t0_parent(l2);
+                if (pp == p) break;
+                o += t0_off(l2);
+                p = pp;
+                __hip_atomic_store(lnk + c, t0_link(p, o), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
         }
         __syncthreads();
+        T0_STAMP(5);
         int nc[4], no[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int i = threadIdx.x + NT * k;
-            const int c = lc[i];
-            nc[k] = lk[c];
-            no[k] = lo[i] + lko[c];
+            const unsigned l = lnk[lc[i]];
+            nc[k] = t0_parent(l);
+            no[k] = lo[i] + t0_off(l);
         }
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int i = threadIdx.x + NT * k;
-            lc[i] = nc[k];
-            lo[i] = no[k];
+            lc[i] = (short)nc[k];
+            lo[i] = (short)no[k];
             bw[i] = 0x7ff0000000000000ull;
             be[i] = 0x7fffffff;
         }
         __syncthreads();
+        T0_STAMP(6);
     }
     // level-0 components: global ids of the tile roots, offsets to them; candidate
     // slots of every pixel reset for the level rounds
@@ -993,6 +1032,13 @@ __global__ __launch_bounds__(T0 * T0 / 4) void k_mst_tile0(const float* __restri
         m.best_w[v] = 0x7ff0000000000000ull;
         m.best_e[v] = 0x7fffffff;
     }
+#ifdef FCD_T0_STAMPS
+    T0_STAMP(7);
+    if (blockIdx.x < 256 && threadIdx.x == 0) {
+        for (int i = 0; i < 8; ++i) g_t0_stamps[blockIdx.x * 9 + i] = ph[i];
+        g_t0_stamps[blockIdx.x * 9 + 8] = nrounds;
+    }
+#endif
 }
 
 int mst_tile_side(int H, int W) {
