@@ -877,13 +877,21 @@ __global__ __launch_bounds__(T0 * T0 / 4) void k_mst_tile0(const float* __restri
     // the 4 incident edges of each of this thread's pixels, once: weight rel(p) + rel(q)
     // (f64, as k_mst_rel / k_mst_round) as its bit pattern (non-negative doubles order
     // as unsigned integers), ~0 for an edge past the map border; the rounds then only
-    // compare integers (weight, then edge code)
+    // compare integers (weight, then edge code).  With them the edges' find_wrap values
+    // (2 bits each, + 1), so a hook needs no phase reads.
     unsigned long long ekey[4][4];
+    unsigned incs = 0;
+    auto wat = [&](int li, int lj) { return ws[(li + 2) * T0W + (lj + 2)]; };
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int i = threadIdx.x + NT * k;
         const int li = i / T0, lj = i % T0, gi = gi0 + li, gj = gj0 + lj;
         const double rv = relat(li, lj);
+        const float wc = wat(li, lj);
+        incs |= (unsigned)(find_wrap(wc, wat(li, lj + 1)) + 1) << (8 * k);
+        incs |= (unsigned)(find_wrap(wat(li, lj - 1), wc) + 1) << (8 * k + 2);
+        incs |= (unsigned)(find_wrap(wc, wat(li + 1, lj)) + 1) << (8 * k + 4);
+        incs |= (unsigned)(find_wrap(wat(li - 1, lj), wc) + 1) << (8 * k + 6);
         auto edge = [&](int d, bool exists, int ni, int nj) {
             ekey[k][d] = exists ? (unsigned long long)__double_as_longlong(__dadd_rn(rv, relat(ni, nj))) : ~0ull;
         };
@@ -905,69 +913,65 @@ __global__ __launch_bounds__(T0 * T0 / 4) void k_mst_tile0(const float* __restri
     for (;;) {
         ++nrounds;
         // (a) each pixel's lightest edge to another tile component or out of the tile
+        // (the five component labels loaded unconditionally, then selects)
         unsigned long long key[4];
-        int ke[4];
+        int ke[4], kd[4], cs[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int i = threadIdx.x + NT * k;
             const int li = i / T0, lj = i % T0;
-            const int c = lc[i];
-            unsigned long long bk = ~0ull;
-            int bev = 0x7fffffff;
+            int nbc[4];
+            bool in[4];
 #pragma unroll
             for (int d = 0; d < 4; ++d) {
                 const int ni = li + (d == 2) - (d == 3), nj = lj + (d == 0) - (d == 1);
-                const bool inside = ni >= 0 && ni < T0 && nj >= 0 && nj < T0;
-                if (inside && lc[ni * T0 + nj] == c) continue;
-                const unsigned long long kk = ekey[k][d];
+                in[d] = ni >= 0 && ni < T0 && nj >= 0 && nj < T0;
+                nbc[d] = lc[in[d] ? ni * T0 + nj : i];
+            }
+            const int c = lc[i];
+            cs[k] = c;
+            unsigned long long bk = ~0ull;
+            int bev = 0x7fffffff, bd = 0;
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                const unsigned long long kk = (in[d] && nbc[d] == c) ? ~0ull : ekey[k][d];
                 const int code = d == 0 ? t0_hcode(li, lj)
                                         : (d == 1 ? t0_hcode(li, lj - 1) : (d == 2 ? t0_vcode(li, lj) : t0_vcode(li - 1, lj)));
-                if (kk < bk || (kk == bk && kk != ~0ull && code < bev)) {
-                    bk = kk;
-                    bev = code;
-                }
+                const bool better = kk < bk || (kk == bk && kk != ~0ull && code < bev);
+                bk = better ? kk : bk;
+                bev = better ? code : bev;
+                bd = better ? d : bd;
             }
             key[k] = bk;
             ke[k] = bev;
+            kd[k] = bd;
             if (bk != ~0ull) atomicMin(bw + c, bk);
         }
         __syncthreads();
         T0_STAMP(2);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int i = threadIdx.x + NT * k;
-            if (key[k] != ~0ull && key[k] == bw[lc[i]]) atomicMin(be + lc[i], ke[k]);
-        }
+        for (int k = 0; k < 4; ++k)
+            if (key[k] != ~0ull && key[k] == bw[cs[k]]) atomicMin(be + cs[k], ke[k]);
         __syncthreads();
         T0_STAMP(3);
-        // (c) hooks of the tile roots whose lightest edge ends inside the tile: decided
-        // from the edge codes, then published as links over them
+        // (c) hooks: the pixel holding its component's lightest edge (unique: weight,
+        // then edge code) decides, if that edge ends inside the tile, and leaves the link
+        // in the component's (no longer needed) minimum slot, marked by bit 63 (a weight's
+        // bits never have it); the roots then move the links over their edge codes
         int hooked = 0;
-        unsigned nl[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const int c = threadIdx.x + NT * k;
-            nl[k] = t0_link(c, 0);
-            if (lc[c] != c) continue;
-            const int e = be[c];
-            if (e == 0x7fffffff) continue;
-            const int l1i = ((e >> 7) & 127) - 1, l1j = (e & 127) - 1;
-            const bool vert = e >> 14;
-            const int l2i = l1i + vert, l2j = l1j + !vert;
-            const bool in1 = l1i >= 0 && l1i < T0 && l1j >= 0 && l1j < T0;
-            const bool in2 = l2i >= 0 && l2i < T0 && l2j >= 0 && l2j < T0;
-            if (!in1 || !in2) continue;  // leaves the tile: the level rounds take it
-            const int x1 = l1i * T0 + l1j, x2 = l2i * T0 + l2j;
-            const int inc = find_wrap(mw[(long)(gi0 + l1i) * W + gj0 + l1j], mw[(long)(gi0 + l2i) * W + gj0 + l2j]);
-            int x, y, delta;  // k(y) - k(x) across the edge, x in c
-            if (lc[x1] == c) {
-                x = x1; y = x2; delta = -inc;
-            } else {
-                x = x2; y = x1; delta = inc;
-            }
-            const int d = lc[y];
-            if (be[d] == e && c < d) continue;  // mutual pair: the smaller root stays
-            nl[k] = t0_link(d, lo[y] - lo[x] - delta);  // K_c - K_d
+            const int i = threadIdx.x + NT * k, c = cs[k];
+            if (key[k] == ~0ull || key[k] != bw[c] || ke[k] != be[c]) continue;
+            const int li = i / T0, lj = i % T0, d = kd[k];
+            const int ni = li + (d == 2) - (d == 3), nj = lj + (d == 0) - (d == 1);
+            if (!(ni >= 0 && ni < T0 && nj >= 0 && nj < T0)) continue;  // leaves the tile: the level rounds take it
+            const int y = ni * T0 + nj;
+            const int inc = (int)((incs >> (8 * k + 2 * d)) & 3u) - 1;
+            const int delta = (d == 0 || d == 2) ? -inc : inc;  // k(y) - k(i) across the edge
+            const int dr = lc[y];
+            if (be[dr] == ke[k] && c < dr) continue;  // mutual pair: the smaller root stays
+            bw[c] = (1ull << 63) | t0_link(dr, lo[y] - lo[i] - delta);  // K_c - K_dr
             hooked = 1;
         }
         const int any = __syncthreads_or(hooked);
@@ -975,7 +979,9 @@ __global__ __launch_bounds__(T0 * T0 / 4) void k_mst_tile0(const float* __restri
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int c = threadIdx.x + NT * k;
-            if (lc[c] == c) lnk[c] = nl[k];
+            if (lc[c] != c) continue;
+            const unsigned long long v = bw[c];
+            lnk[c] = (v >> 63) ? (unsigned)v : t0_link(c, 0);
         }
         __syncthreads();
         T0_STAMP(4);
