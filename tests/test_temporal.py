@@ -137,13 +137,16 @@ def nan_spectrum(st, nf):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("pair", ["1", "0"])
 @pytest.mark.parametrize("T", [1, 2, 3, 5, 100, 257, 2000])
-def test_temporal_fft_path_short_series(monkeypatch, T):
+def test_temporal_fft_path_short_series(monkeypatch, T, pair):
     """The Bluestein / four-step FFT path (FCD_TDFT_FFT=1 forces it at any T): every
     sub-transform length from 2 up, odd and prime T, NaN pixels excluded as np.nanmean
-    does, a sub-block addressed in place, against numpy's f64 FFT."""
+    does, a sub-block addressed in place, against numpy's f64 FFT; two real series per
+    transform (default) and one (FCD_TDFT_PAIR=0)."""
     from pyfcd import _lib
     monkeypatch.setenv("FCD_TDFT_FFT", "1")
+    monkeypatch.setenv("FCD_TDFT_PAIR", pair)
     eng = _lib.temporal_engine()
     st = make_stack(T, n=20, seed=T, zero_corner=False, nan_pixels=[(3, 4, T // 2, T // 2 + 1)])
     nf = T // 2 + 1
@@ -309,6 +312,33 @@ def test_temporal_f64_stack_equals_widened_f32(tdft_family):
     assert np.array_equal(eng.temporal_bins(st, [0, 3, 128]), eng.temporal_bins(st64, [0, 3, 128]))
     win = np.hanning(64)
     assert np.array_equal(eng.spectrogram(st, 64, 8, win, TASA), eng.spectrogram(st64, 64, 8, win, TASA))
+
+
+@pytest.mark.gpu
+def test_fft_path_device_pointer_block(monkeypatch):
+    """The FFT path on a device-resident stack, the block addressed in place through the
+    stack's own pitches (float32 and float64 stacks), equals the host-pointer call and
+    numpy."""
+    import ctypes
+    import torch
+    from pyfcd import _lib
+    monkeypatch.setenv("FCD_TDFT_FFT", "1")
+    eng = _lib.temporal_engine()
+    lib = _lib.load_library()
+    st = make_stack(700, n=72, seed=12, zero_corner=False, nan_pixels=[(20, 30, 100, 101)])
+    T, rows, cols = st.shape
+    blk = (8, 20, 30, 40)  # r0, c0, bh, bw
+    nf = 351
+    want_t, want_c = nan_spectrum(st[:, 8:38, 20:60], nf)
+    for arr, flag in ((st, 0), (st.astype(np.float64), _lib.FCD_STACK_F64)):
+        sd = torch.from_numpy(arr).cuda()
+        sc = np.empty((nf, 2))
+        _lib._check(lib.fcd_temporal_spectrum(eng.handle, ctypes.c_void_p(sd.data_ptr()), T, rows, cols, *blk,
+                                              _lib.FCD_DEVICE_PTRS | flag, nf, sc.ctypes.data, None))
+        tot_h, cnt_h = eng.temporal_spectrum(arr, nf, block=blk)
+        assert np.array_equal(sc[:, 0], tot_h) and np.array_equal(sc[:, 1], cnt_h)
+        assert np.array_equal(cnt_h, want_c) and cnt_h[0] == 1199
+        np.testing.assert_allclose(tot_h, want_t, rtol=1e-12)
 
 
 @pytest.mark.gpu

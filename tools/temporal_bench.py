@@ -13,8 +13,8 @@ units (vendor spec).  CPU: the oracle's
 numpy / scipy calls (the reference's own, analyze.py:497, :521, :574) on a sample of the block's series, 1 core.
 
 The mean spectrum is timed on both paths (FCD_TDFT_FFT=0: the direct DFT, =1: the
-Bluestein / four-step FFT of kernels_tfft.hip, HBM-bound: 4 B x T + 4 x 16 B x M per
-series, M = 2^ceil(log2(2T - 1))).
+Bluestein / four-step FFT of kernels_tfft.hip, two real series per transform, HBM-bound:
+4 B x T + 2 x 16 B x M + 16 B x T per series, M = 2^ceil(log2(2T - 1))).
 
     python tools/temporal_bench.py [--T 2000] [--reps 5]
 """
@@ -100,7 +100,9 @@ def main():
     t_fft = with_env("1", spectrum)
     t_direct = with_env("0", spectrum)
     M = 1 << max(2, (2 * T - 2).bit_length())
-    fft_bytes = P * (4.0 * T + 4 * 16.0 * M)  # stack read + 4 passes of the [M] f64 complex work
+    # stack read + 4 passes of the [M] f64 complex work per pixel pair + the pair's spectrum
+    # written and read back (16 B x T per pixel pair each way)
+    fft_bytes = P * (4.0 * T + 2 * 16.0 * M + 16.0 * T)
     t_harm = timed(harmonics)
     t_spg = timed(spectro)
     flops_spec = 4.0 * P * T * nf  # the direct DFT's count (the default path when T <= 8192)

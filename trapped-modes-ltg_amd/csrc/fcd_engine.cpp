@@ -224,7 +224,7 @@ struct fcd_ctx {
     DevBuf fix_raw;  // raw samples of the frames redone by the exact pass
     // temporal analysis: staged block, exp table, bins, partial sums, output, window
     DevBuf t_stage, t_tab, t_bins, t_part, t_out, t_win, t_wsum, t_slices;
-    DevBuf t_chirp, t_bhat, t_work, t_gpart;  // the FFT path of the mean spectrum
+    DevBuf t_chirp, t_bhat, t_work, t_gpart, t_zo, t_bad;  // the FFT path of the mean spectrum
     HostPipe pipe;
     // MST workspace
     DevBuf mst_comp, mst_off, mst_rel, mst_cw, mst_ce, mst_bw, mst_be, mst_link, mst_hooks, mst_ids;
@@ -1560,15 +1560,20 @@ FCD_API int fcd_temporal_spectrum(fcd_ctx* c, const void* stack, int T, int rows
             c->t_tab.ensure(tw.size() * sizeof(double2));
             c->t_chirp.ensure(chirp.size() * sizeof(double2));
             c->t_bhat.ensure(bhat.size() * sizeof(double2));
-            c->t_work.ensure((size_t)pl.Pb * pl.M * sizeof(double2));
+            c->t_work.ensure((size_t)pl.work_elems * sizeof(double2));
             c->t_gpart.ensure((size_t)pl.ngroups * nf * sizeof(double2));
+            if (pl.pair) {
+                c->t_zo.ensure((size_t)pl.zo_elems * sizeof(double2));
+                c->t_bad.ensure((size_t)P * sizeof(int));
+            }
             c->t_part.ensure((size_t)nf * 2 * sizeof(double));
             upload(c->t_tab.p, tw.data(), tw.size() * sizeof(double2), s);
             upload(c->t_chirp.p, chirp.data(), chirp.size() * sizeof(double2), s);
             upload(c->t_bhat.p, bhat.data(), bhat.size() * sizeof(double2), s);
+            const fcdk::TfftWork wk{c->t_work.as<double2>(), pl.pair ? c->t_zo.as<double2>() : nullptr,
+                                    c->t_gpart.as<double2>(), pl.pair ? c->t_bad.as<int>() : nullptr};
             fcdk::temporal_spectrum_fft(v.p, v.frame_pitch, v.row_pitch, bw, P, T, nf, pl, c->t_chirp.as<double2>(),
-                                        c->t_tab.as<double2>(), c->t_bhat.as<double2>(), c->t_work.as<double2>(),
-                                        c->t_gpart.as<double2>(), c->t_part.as<double>(), s);
+                                        c->t_tab.as<double2>(), c->t_bhat.as<double2>(), wk, c->t_part.as<double>(), s);
             HIPCHK(hipStreamSynchronize(s));  // the host tables die here
         } else {
             upload_exp_table(c, c->t_tab, T, s);

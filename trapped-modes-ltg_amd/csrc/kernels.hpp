@@ -165,16 +165,24 @@ int spectro_max_nperseg();
 // mean spectrum of a long series by Bluestein + four-step FFT (kernels_tfft.hip)
 struct TfftPlan {
     int logM, M, log1, log2, M1, M2;  // M = 2^logM >= 2T - 1 = M1 x M2
-    int Pb, ngroups;                  // pixels per batch, 64-pixel partial groups
+    int Pb, ngroups;                  // pixels per batch, partial-sum rows (64 or 128 pixels each)
+    bool pair;                        // two real series per transform (x_p + i x_q)
+    long work_elems, zo_elems;        // double2 workspace sizes
+};
+struct TfftWork {
+    double2* work;   // [work_elems]
+    double2* zo;     // [zo_elems] (pair)
+    double2* gpart;  // [ngroups][nf]
+    int* bad;        // [P] (pair): pixel has a non-finite sample
 };
 bool temporal_spectrum_uses_fft(int T, int nf);
 bool temporal_fft_plan(int T, int P, TfftPlan* pl);  // false: T too long for the LDS sub-transforms
 void temporal_fft_tables(int T, const TfftPlan& pl, std::vector<double2>& chirp, std::vector<double2>& tw,
                          std::vector<double2>& bhat);
-// partial [nf][2] (sum of |X|, count) over the block; work [Pb x M] double2, gpart [ngroups x nf] double2
+// partial [nf][2] (sum of |X|, count) over the block
 void temporal_spectrum_fft(Samples stack, long frame_pitch, long row_pitch, int bw, int P, int T, int nf,
                            const TfftPlan& pl, const double2* chirp, const double2* tw, const double2* bhat,
-                           double2* work, double2* gpart, double* partial, hipStream_t s);
+                           const TfftWork& wk, double* partial, hipStream_t s);
 void spectrogram(Samples stack, long frame_pitch, long row_pitch, int bw, int P, int nperseg, int step, int nseg,
                  const double* win, const double2* tab, const double2* wsum, int nf, double scale, double* out,
                  hipStream_t s);

@@ -185,29 +185,52 @@ __device__ __forceinline__ void load_twl(double2* twl, const double2* __restrict
 
 }  // namespace
 
-// Step 1: pixels [pbase + 8 bx, +8) of the batch, column n2 = by.
-template <int LOG1, typename S>
+// Step 1: column n2 = bx of group by: pixels [pbase + 8 by, +8), or with PAIR the 8
+// pixel pairs (p, p + 8), p in [pbase + 16 by, +8), as x_p + i x_{p+8} (a pixel with a
+// non-finite sample, bad[p], enters as zeros: np.nanmean drops it anyway).
+template <int LOG1, typename S, bool PAIR>
 __global__ __launch_bounds__(TF_NT) void k_tfft_cols_fwd(const S* __restrict__ stack, long frame_pitch,
                                                          long row_pitch, int bw, int P, int T, int pbase,
+                                                         const int* __restrict__ bad,
                                                          const double2* __restrict__ chirp,
                                                          const double2* __restrict__ tw, int logM, int M2,
                                                          double2* __restrict__ work) {
     constexpr int M1 = 1 << LOG1;
     extern __shared__ double2 tf_buf[];
     double2* const twl = tf_buf + lds_slots<LOG1>();
-    const int n2 = blockIdx.x, grp = blockIdx.y, g0 = grp * TF_G;
+    const int n2 = blockIdx.x, grp = blockIdx.y;
     const long M = 1L << logM;
     load_twl<LOG1>(twl, tw, logM);
-    for (int e = threadIdx.x; e < M1 * TF_G; e += TF_NT) {
-        const int n1 = e / TF_G, g = e % TF_G, p = pbase + g0 + g;
-        const long t = (long)M2 * n1 + n2;
-        double2 v = make_double2(0.0, 0.0);
-        if (t < T && p < P) {
-            const double x = (double)stack[tf_pix_off(p, bw, row_pitch) + t * frame_pitch];
-            const double2 c = chirp[t];
-            v = make_double2(x * c.x, x * c.y);
+    if constexpr (PAIR) {
+        const int g = threadIdx.x % TF_G;  // fixed per thread (TF_NT % TF_G == 0)
+        const int pa = pbase + grp * 2 * TF_G + g, pb = pa + TF_G;
+        const bool oka = pa < P && !bad[pa], okb = pb < P && !bad[pb];
+        const S* xa = stack + (oka ? tf_pix_off(pa, bw, row_pitch) : 0);
+        const S* xb = stack + (okb ? tf_pix_off(pb, bw, row_pitch) : 0);
+        for (int e = threadIdx.x; e < M1 * TF_G; e += TF_NT) {
+            const long t = (long)M2 * (e / TF_G) + n2;
+            double2 v = make_double2(0.0, 0.0);
+            if (t < T) {
+                const double a = oka ? (double)xa[t * frame_pitch] : 0.0;
+                const double b = okb ? (double)xb[t * frame_pitch] : 0.0;
+                const double2 c = chirp[t];
+                v = make_double2(a * c.x - b * c.y, a * c.y + b * c.x);
+            }
+            tf_buf[lp(e)] = v;
         }
-        tf_buf[lp(e)] = v;
+    } else {
+        const int g0 = grp * TF_G;
+        for (int e = threadIdx.x; e < M1 * TF_G; e += TF_NT) {
+            const int n1 = e / TF_G, g = e % TF_G, p = pbase + g0 + g;
+            const long t = (long)M2 * n1 + n2;
+            double2 v = make_double2(0.0, 0.0);
+            if (t < T && p < P) {
+                const double x = (double)stack[tf_pix_off(p, bw, row_pitch) + t * frame_pitch];
+                const double2 c = chirp[t];
+                v = make_double2(x * c.x, x * c.y);
+            }
+            tf_buf[lp(e)] = v;
+        }
     }
     __syncthreads();
     lds_fft<LOG1, false>(tf_buf, twl);
@@ -292,6 +315,79 @@ __global__ __launch_bounds__(TF_NT) void k_tfft_cols_inv(const double2* __restri
     }
 }
 
+// Pixels of the block with a non-finite sample (any t): bad[p] = 1 (zeroed beforehand).
+template <typename S>
+__global__ __launch_bounds__(TF_NT) void k_tfft_flags(const S* __restrict__ stack, long frame_pitch, long row_pitch,
+                                                      int bw, int P, int T, int* __restrict__ bad) {
+    const int p = blockIdx.x * TF_NT + threadIdx.x;
+    if (p >= P) return;
+    const S* x = stack + tf_pix_off(p, bw, row_pitch);
+    const int t0 = blockIdx.y * TF_NT, t1 = min(T, t0 + TF_NT);
+    bool ok = true;
+    int t = t0;
+    for (; t + 8 <= t1; t += 8) {  // 8 loads in flight per lane
+        S v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = x[(long)(t + u) * frame_pitch];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) ok &= isfinite((double)v[u]);
+    }
+    for (; t < t1; ++t) ok &= isfinite((double)x[(long)t * frame_pitch]);
+    if (!ok) atomicOr(bad + p, 1);
+}
+
+// Step 3 of the paired path: column n2 = bx of pair group by: inverse FFT over k1, then
+// Z[k] = c[k] conv[k] (the DFT of x_p + i x_{p+8}) for k = M2 n1 + n2 < T -> zo[by][k][8].
+template <int LOG1>
+__global__ __launch_bounds__(TF_NT) void k_tfft_cols_inv_pair(const double2* __restrict__ work, int M2,
+                                                              const double2* __restrict__ tw, int logM, int T,
+                                                              const double2* __restrict__ chirp,
+                                                              double2* __restrict__ zo) {
+    constexpr int M1 = 1 << LOG1;
+    extern __shared__ double2 tf_buf[];
+    double2* const twl = tf_buf + lds_slots<LOG1>();
+    const int n2 = blockIdx.x, grp = blockIdx.y;
+    const long M = 1L << logM;
+    load_twl<LOG1>(twl, tw, logM);
+    for (int e = threadIdx.x; e < M1 * TF_G; e += TF_NT)
+        tf_buf[lp(e)] = work[((long)grp * M + (long)(e / TF_G) * M2 + n2) * TF_G + e % TF_G];
+    __syncthreads();
+    lds_fft<LOG1, true>(tf_buf, twl);
+    for (int e = threadIdx.x; e < M1 * TF_G; e += TF_NT) {
+        const long k = (long)M2 * (e / TF_G) + n2;
+        if (k < T) zo[((long)grp * T + k) * TF_G + e % TF_G] = zmul(tf_buf[lp(e)], chirp[k]);
+    }
+}
+
+// Both pixels' spectra from Z (real inputs): X_p[k] = (Z[k] + conj Z[-k]) / 2,
+// X_{p+8}[k] = (Z[k] - conj Z[-k]) / 2i; per bin k < nf the sum of |X| over the
+// 128 pixels of pair groups [8 by, +8) and their count -> gpart[(pbase / 128 + by) nf + k].
+// A thread is (bin, slot): 8 slots of a bin in adjacent lanes, summed by shuffles.
+constexpr int TF_PS = 128;  // pixels per partial row of the paired path
+__global__ __launch_bounds__(TF_NT) void k_tfft_split(const double2* __restrict__ zo, int T, int nf, int pbase, int P,
+                                                      const int* __restrict__ bad, double2* __restrict__ gpart) {
+    const int g = threadIdx.x % TF_G;
+    const int k = blockIdx.x * (TF_NT / TF_G) + threadIdx.x / TF_G;
+    const int kk = min(k, nf - 1), km = kk == 0 ? 0 : T - kk;
+    double s = 0.0, c = 0.0;
+    for (int j = 0; j < TF_PS / (2 * TF_G); ++j) {
+        const int q = blockIdx.y * (TF_PS / (2 * TF_G)) + j;
+        const int pa = pbase + q * 2 * TF_G + g, pb = pa + TF_G;
+        const bool oka = pa < P && !bad[pa], okb = pb < P && !bad[pb];
+        const double2 z = zo[((long)q * T + kk) * TF_G + g], zm = zo[((long)q * T + km) * TF_G + g];
+        const double ar = z.x + zm.x, ai = z.y - zm.y, br = z.x - zm.x, bi = z.y + zm.y;
+        const double ma = 0.5 * sqrt(ar * ar + ai * ai), mb = 0.5 * sqrt(br * br + bi * bi);
+        s += (oka ? ma : 0.0) + (okb ? mb : 0.0);
+        c += (oka ? 1.0 : 0.0) + (okb ? 1.0 : 0.0);
+    }
+#pragma unroll
+    for (int o = 1; o < TF_G; o <<= 1) {
+        s += __shfl_xor(s, o, 64);
+        c += __shfl_xor(c, o, 64);
+    }
+    if (g == 0 && k < nf) gpart[((long)(pbase / TF_PS) + blockIdx.y) * nf + k] = make_double2(s, c);
+}
+
 __global__ __launch_bounds__(TF_NT) void k_tfft_sum(const double2* __restrict__ gpart, int ngroups, int nf,
                                                     double* __restrict__ partial) {
     const int n = blockIdx.x * TF_NT + threadIdx.x;
@@ -314,23 +410,39 @@ void tf_check(const char* what) {
     if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
 }
 
+#define FCD_TF_HIPCHK(x)                                                                         \
+    do {                                                                                         \
+        const hipError_t e_ = (x);                                                               \
+        if (e_ != hipSuccess) throw std::runtime_error(std::string(#x) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
 constexpr int TF_MAXLOG = 10;  // longest sub-transform: 1024 x 8 x 16 B (+ pads, + table) = 152 KiB of LDS
 
-template <int L1, typename S>
-void launch_cols_fwd(const S* stack, long fp, long rp, int bw, int P, int T, int pbase, int nb,
-                     const double2* chirp,
-                     const double2* tw, int logM, int M2, double2* work, hipStream_t s) {
+template <int L1, typename S, bool PAIR>
+void launch_cols_fwd(const S* stack, long fp, long rp, int bw, int P, int T, int pbase, int ngrp, const int* bad,
+                     const double2* chirp, const double2* tw, int logM, int M2, double2* work, hipStream_t s) {
     const size_t lb = (size_t)(lds_slots<L1>() + (1 << L1)) * sizeof(double2);
-    (void)hipFuncSetAttribute((const void*)k_tfft_cols_fwd<L1, S>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb);
-    hipLaunchKernelGGL((k_tfft_cols_fwd<L1, S>), dim3((unsigned)M2, (unsigned)(nb / TF_G)), dim3(TF_NT), lb, s, stack,
-                       fp, rp, bw, P, T, pbase, chirp, tw, logM, M2, work);
+    (void)hipFuncSetAttribute((const void*)k_tfft_cols_fwd<L1, S, PAIR>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lb);
+    hipLaunchKernelGGL((k_tfft_cols_fwd<L1, S, PAIR>), dim3((unsigned)M2, (unsigned)ngrp), dim3(TF_NT), lb, s, stack,
+                       fp, rp, bw, P, T, pbase, bad, chirp, tw, logM, M2, work);
+}
+
+template <int L1>
+void launch_cols_inv_pair(const double2* work, int ngrp, int M2, const double2* tw, int logM, int T,
+                          const double2* chirp, double2* zo, hipStream_t s) {
+    const size_t lb = (size_t)(lds_slots<L1>() + (1 << L1)) * sizeof(double2);
+    (void)hipFuncSetAttribute((const void*)k_tfft_cols_inv_pair<L1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lb);
+    hipLaunchKernelGGL(k_tfft_cols_inv_pair<L1>, dim3((unsigned)M2, (unsigned)ngrp), dim3(TF_NT), lb, s, work, M2, tw,
+                       logM, T, chirp, zo);
 }
 
 template <int L2>
-void launch_rows(double2* work, int nb, int M1, const double2* bhat, const double2* tw, int logM, hipStream_t s) {
+void launch_rows(double2* work, int ngrp, int M1, const double2* bhat, const double2* tw, int logM, hipStream_t s) {
     const size_t lb = (size_t)(lds_slots<L2>() + (1 << L2)) * sizeof(double2);
     (void)hipFuncSetAttribute((const void*)k_tfft_rows<L2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb);
-    hipLaunchKernelGGL(k_tfft_rows<L2>, dim3((unsigned)M1, (unsigned)(nb / TF_G)), dim3(TF_NT), lb, s, work, bhat,
+    hipLaunchKernelGGL(k_tfft_rows<L2>, dim3((unsigned)M1, (unsigned)ngrp), dim3(TF_NT), lb, s, work, bhat,
                        tw, logM);
 }
 
@@ -361,32 +473,52 @@ void launch_cols_inv(const double2* work, int nb, int M2, const double2* tw, int
 
 template <typename S>
 void spectrum_fft_t(const S* stack, long fp, long rp, int bw, int P, int T, int nf, const TfftPlan& pl,
-                    const double2* chirp, const double2* tw, const double2* bhat, double2* work, double2* gpart,
-                    double* partial, hipStream_t s) {
-    for (int pbase = 0; pbase < P; pbase += pl.Pb) {
-        // pixels of this batch, rounded up to whole 64-pixel groups
-        const int nb = std::min(pl.Pb, (P - pbase + TF_GS - 1) / TF_GS * TF_GS);
-        TF_SWITCH(pl.log1, (launch_cols_fwd<LG, S>(stack, fp, rp, bw, P, T, pbase, nb, chirp, tw, pl.logM,
-                                                    pl.M2, work, s)));
-        tf_check("temporal fft (columns)");
-        TF_SWITCH(pl.log2, (launch_rows<LG>(work, nb, pl.M1, bhat, tw, pl.logM, s)));
-        tf_check("temporal fft (rows)");
-        TF_SWITCH(pl.log1, (launch_cols_inv<LG>(work, nb, pl.M2, tw, pl.logM, nf, pbase, P, gpart, s)));
-        tf_check("temporal fft (inverse columns)");
+                    const double2* chirp, const double2* tw, const double2* bhat, const TfftWork& wk, double* partial,
+                    hipStream_t s) {
+    if (pl.pair) {
+        FCD_TF_HIPCHK(hipMemsetAsync(wk.bad, 0, (size_t)P * sizeof(int), s));
+        hipLaunchKernelGGL(k_tfft_flags<S>, dim3((unsigned)((P + TF_NT - 1) / TF_NT), (unsigned)((T + TF_NT - 1) / TF_NT)),
+                           dim3(TF_NT), 0, s, stack, fp, rp, bw, P, T, wk.bad);
+        tf_check("temporal fft (finite flags)");
     }
-    hipLaunchKernelGGL(k_tfft_sum, dim3((unsigned)((nf + TF_NT - 1) / TF_NT)), dim3(TF_NT), 0, s, gpart,
-                       (P + TF_GS - 1) / TF_GS, nf, partial);
+    for (int pbase = 0; pbase < P; pbase += pl.Pb) {
+        if (pl.pair) {
+            // pixels of this batch, rounded up to whole 128-pixel partial rows; 16 per pair group
+            const int nb = std::min(pl.Pb, (P - pbase + TF_PS - 1) / TF_PS * TF_PS), ngrp = nb / (2 * TF_G);
+            TF_SWITCH(pl.log1, (launch_cols_fwd<LG, S, true>(stack, fp, rp, bw, P, T, pbase, ngrp, wk.bad, chirp, tw,
+                                                              pl.logM, pl.M2, wk.work, s)));
+            tf_check("temporal fft (columns)");
+            TF_SWITCH(pl.log2, (launch_rows<LG>(wk.work, ngrp, pl.M1, bhat, tw, pl.logM, s)));
+            tf_check("temporal fft (rows)");
+            TF_SWITCH(pl.log1, (launch_cols_inv_pair<LG>(wk.work, ngrp, pl.M2, tw, pl.logM, T, chirp, wk.zo, s)));
+            tf_check("temporal fft (inverse columns)");
+            hipLaunchKernelGGL(k_tfft_split, dim3((unsigned)((nf + TF_NT / TF_G - 1) / (TF_NT / TF_G)), (unsigned)(nb / TF_PS)),
+                               dim3(TF_NT), 0, s, wk.zo, T, nf, pbase, P, wk.bad, wk.gpart);
+            tf_check("temporal fft (split)");
+        } else {
+            // pixels of this batch, rounded up to whole 64-pixel groups
+            const int nb = std::min(pl.Pb, (P - pbase + TF_GS - 1) / TF_GS * TF_GS);
+            TF_SWITCH(pl.log1, (launch_cols_fwd<LG, S, false>(stack, fp, rp, bw, P, T, pbase, nb / TF_G, nullptr, chirp,
+                                                               tw, pl.logM, pl.M2, wk.work, s)));
+            tf_check("temporal fft (columns)");
+            TF_SWITCH(pl.log2, (launch_rows<LG>(wk.work, nb / TF_G, pl.M1, bhat, tw, pl.logM, s)));
+            tf_check("temporal fft (rows)");
+            TF_SWITCH(pl.log1, (launch_cols_inv<LG>(wk.work, nb, pl.M2, tw, pl.logM, nf, pbase, P, wk.gpart, s)));
+            tf_check("temporal fft (inverse columns)");
+        }
+    }
+    hipLaunchKernelGGL(k_tfft_sum, dim3((unsigned)((nf + TF_NT - 1) / TF_NT)), dim3(TF_NT), 0, s, wk.gpart,
+                       pl.ngroups, nf, partial);
     tf_check("temporal fft (sum)");
 }
 
 }  // namespace
 
 // FCD_TDFT_FFT=1 / =0 forces / forbids this path (read per call, so one process can
-// test both).  By default the cheaper of the two by their measured rates (r02w, 128 x 128
+// test both).  By default the cheaper of the two by their measured rates (128 x 128
 // block): the direct DFT at 4 T nf flops per series and ~40 TFLOP/s on the matrix cores
-// (T <= 8192; ~27 on the vector units above), the FFT at 4 T + 64 M bytes per series and
-// ~2.5 TB/s.  For all T / 2 + 1 bins that is T > ~1550 (T = 1500: 1.83 vs 1.88 ms,
-// T = 2000: 3.07 vs 1.96, T = 20000: 483 vs 26).
+// (T <= 8192; ~27 on the vector units above), the paired FFT at 4 T + 32 M + 16 T bytes
+// per series and ~2.5 TB/s (r02aj: T = 2000 3.02 vs 1.12 ms, T = 20000 475 vs 14.1).
 bool temporal_spectrum_uses_fft(int T, int nf) {
     const char* e = std::getenv("FCD_TDFT_FFT");
     if (e && e[0] == '1') return true;
@@ -394,7 +526,7 @@ bool temporal_spectrum_uses_fft(int T, int nf) {
     long M = 4;
     while (M < 2L * T - 1) M <<= 1;
     const double direct = 4.0 * T * (double)nf / (T <= 8192 ? 40e12 : 27e12);
-    const double fft = (4.0 * T + 64.0 * (double)M) / 2.5e12;
+    const double fft = (20.0 * T + 32.0 * (double)M) / 2.5e12;
     return fft < direct;
 }
 
@@ -408,11 +540,18 @@ bool temporal_fft_plan(int T, int P, TfftPlan* pl) {
     pl->log1 = logM - pl->log2;
     pl->M1 = 1 << pl->log1;
     pl->M2 = 1 << pl->log2;
-    // pixels per batch: a work array of <= 1 GiB, a multiple of 64 pixels, <= 2^16 (grid y)
-    const long cap = std::min(1L << 16, std::max(1L, (1L << 30) / ((long)pl->M * (long)sizeof(double2)) / TF_GS) * TF_GS);
-    const long need = ((long)P + TF_GS - 1) / TF_GS * TF_GS;
+    // FCD_TDFT_PAIR=0: one pixel per transform (diagnostic); default two (x_p + i x_q)
+    const char* e = std::getenv("FCD_TDFT_PAIR");
+    pl->pair = !(e && e[0] == '0');
+    // pixels per batch: a work array of <= 1 GiB, a multiple of 128 pixels, <= 2^16 (grid y)
+    const long cap =
+        std::min(1L << 16, std::max(1L, (1L << 30) / ((long)pl->M * (long)sizeof(double2)) / TF_PS) * TF_PS);
+    const long need = ((long)P + TF_PS - 1) / TF_PS * TF_PS;
     pl->Pb = (int)std::min(cap, need);
-    pl->ngroups = (P + TF_GS - 1) / TF_GS;
+    const int per_row = pl->pair ? TF_PS : TF_GS;
+    pl->ngroups = (P + per_row - 1) / per_row;
+    pl->work_elems = (long)pl->Pb * pl->M / (pl->pair ? 2 : 1);
+    pl->zo_elems = pl->pair ? (long)pl->Pb / 2 * T : 0;
     return true;
 }
 
@@ -468,14 +607,14 @@ void temporal_fft_tables(int T, const TfftPlan& pl, std::vector<double2>& chirp,
 
 void temporal_spectrum_fft(Samples stack, long frame_pitch, long row_pitch, int bw, int P, int T, int nf,
                            const TfftPlan& pl, const double2* chirp, const double2* tw, const double2* bhat,
-                           double2* work, double2* gpart, double* partial, hipStream_t s) {
+                           const TfftWork& wk, double* partial, hipStream_t s) {
     if (nf <= 0 || nf > T) throw std::runtime_error("temporal fft: bad bin count");
     if (stack.f64)
         spectrum_fft_t(static_cast<const double*>(stack.p), frame_pitch, row_pitch, bw, P, T, nf, pl, chirp, tw, bhat,
-                       work, gpart, partial, s);
+                       wk, partial, s);
     else
         spectrum_fft_t(static_cast<const float*>(stack.p), frame_pitch, row_pitch, bw, P, T, nf, pl, chirp, tw, bhat,
-                       work, gpart, partial, s);
+                       wk, partial, s);
 }
 
 }  // namespace fcdk
