@@ -40,7 +40,7 @@ names = [short(t["Kernel_Name"]) for t in trace]
 # belongs to the headline path, whose chunk runs as `streams` concurrent parts.
 groups, in_group = [], set()
 for i, k in enumerate(names):
-    if k == "fcdk::k_band_phase<1024, 128, false>":
+    if k in ("fcdk::k_band_phase<1024, 128, false>", "fcdk::k_band_phase_res<1024, 128, 16>"):
         j_cols = max(j for j in range(i) if names[j] == "fcdk::k_demod_cols<1024>")
         j_rows = max(j for j in range(j_cols) if names[j] == "fcdk::k_demod_rows<1024>")
         groups.append((dur[j_rows], dur[j_cols], dur[i]))

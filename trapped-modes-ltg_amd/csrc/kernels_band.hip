@@ -21,6 +21,8 @@
 // exactly as fcd.py:118 up to float rounding.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -256,6 +258,163 @@ __global__ __launch_bounds__((BPCfg<W, B>::THREADS), FCD_BAND_WAVES) void k_band
     STAMP(st++);
 }
 
+// ------------------------------------------------------------------ theta-resident form
+// The same transform and phase step with the reference angles held in registers:
+// one 1024-thread workgroup per CU, one wave per row of a 16-row tile, and an item
+// = (carrier, row tile, slice of the frames).  The wave loads its row of theta once
+// per item and reuses it for every frame of the slice, so the per-frame reference
+// reads (8 MB per 1024^2 frame through L2 in k_band_phase) disappear; the tile of
+// the next frame is prefetched into registers while the current one is
+// transformed, and the two staging buffers alternate so one barrier per frame
+// suffices.  The 16 waves of a frame write 16 consecutive rows (64 KB) of a
+// phase plane.
+#ifndef FCD_BAND_RESIDENT
+#define FCD_BAND_RESIDENT 1  // 0: k_band_phase for every launch
+#endif
+#ifndef FCD_BAND_RES_ITEMS
+#define FCD_BAND_RES_ITEMS 4  // target items per CU (frame slices = items * CUs / (2 * row tiles))
+#endif
+#ifndef FCD_BAND_RES_ROWS
+#define FCD_BAND_RES_ROWS 16  // rows per item (waves per workgroup): 16 = one Ab tile; 8 = half a tile, two workgroups per CU (same speed, kbench r02ap)
+#endif
+
+template <int W, int B, int ROWS>
+struct BRCfg {
+    static constexpr int G = B / 16, L = W / B, RL = W / 16;
+    static_assert(RL == 64, "one wave per row");
+    static_assert(BTILE % ROWS == 0, "items cover whole or half Ab tiles");
+    static constexpr int THREADS = ROWS * RL;
+    static constexpr int SR = ROWS + 1;     // staged row pitch (complex)
+    static constexpr int REGION = GSched<B>::REGION;
+    static constexpr int STAGE = B * SR;    // float2 per staging buffer
+    static constexpr int TN = B * ROWS;     // staged slots per item tile
+    static constexpr int SPT = (TN + THREADS - 1) / THREADS;
+    static constexpr size_t LDS = (size_t)(2 * STAGE + RL * 16) * 8 + (size_t)ROWS * L * REGION * 4;
+};
+
+template <int W, int B, int ROWS>
+__global__ __launch_bounds__((BRCfg<W, B, ROWS>::THREADS), 1) void k_band_phase_res(
+    const float2* __restrict__ Ab, int H, int nb, int NCA, int ncc0, int ncc1, const float* __restrict__ theta,
+    float* __restrict__ out, const float2* __restrict__ pre, const float2* __restrict__ ptw, int slices) {
+    using C = BRCfg<W, B, ROWS>;
+    constexpr int G = C::G, L = C::L, RL = C::RL, E = 16, SPT = C::SPT, TN = C::TN, SR = C::SR;
+    constexpr int HALVES = BTILE / ROWS;  // item tiles per Ab tile
+    extern __shared__ __attribute__((aligned(16))) float2 lds_b[];
+    float2* const stage0 = lds_b;                // [2][B][SROW]
+    float2* const ptl = lds_b + 2 * C::STAGE;    // pre-twiddles [q][RL]
+    const int rl = threadIdx.x / RL;             // this wave's row of the tile
+    const int l = threadIdx.x % RL, g = l / G, t = l % G;
+    float* const s = reinterpret_cast<float*>(ptl + RL * E) + (size_t)(rl * L + g) * C::REGION;
+    GroupFFT<B> fft;
+    fft.load(ptw, t);
+    for (int i = threadIdx.x; i < RL * E; i += C::THREADS) ptl[(i % E) * RL + i / E] = pre[i];
+    const int rbs = H / BTILE, rts = H / ROWS;
+    const int per = (nb + slices - 1) / slices;
+    const int items = 2 * rts * slices;
+    const int tile_n = NCA * BTILE;
+    // item -> (slice fastest, carrier, row tile); frames [f0, f1) of the slice
+    auto first_f = [&](int it) { return (it % slices) * per; };
+    auto last_f = [&](int it) { return min(nb, (it % slices + 1) * per); };
+    // the item's rows of Ab tile rb: slot (j, r) at j * BTILE + hb * ROWS + r
+    auto src_of = [&](int it, int f) {
+        const int c = (it / slices) % 2, rt = it / (2 * slices);
+        return Ab + (((long)f * 2 + c) * rbs + rt / HALVES) * (long)tile_n + (rt % HALVES) * ROWS;
+    };
+    float2 pf[SPT];
+    auto fetch = [&](int it, int f) {
+        const float2* src = src_of(it, f);
+#pragma unroll
+        for (int i = 0; i < SPT; ++i) {
+            const int idx = min((int)threadIdx.x + i * C::THREADS, TN - 1);
+            pf[i] = src[min(idx / ROWS, NCA - 1) * BTILE + idx % ROWS];  // past the band: zeroed at staging
+        }
+    };
+    // advance (it, f) to the block's next non-empty (item, frame)
+    auto next = [&](int& it, int& f) {
+        if (f + 1 < last_f(it)) {
+            ++f;
+            return;
+        }
+        for (it += gridDim.x; it < items && first_f(it) >= last_f(it); it += gridDim.x) {
+        }
+        f = it < items ? first_f(it) : 0;
+    };
+    int it = blockIdx.x, f = 0;
+    for (; it < items && first_f(it) >= last_f(it); it += gridDim.x) {
+    }
+    if (it >= items) return;
+    f = first_f(it);
+    fetch(it, f);
+    int cur_it = -1, buf = 0;
+    float th[E];
+    while (it < items) {
+        const int c = (it / slices) % 2, row = (it / (2 * slices)) * ROWS + rl;
+        const int ncc = c ? ncc1 : ncc0;
+        if (it != cur_it) {  // this wave's row of theta (lane-contiguous copy), kept for the item
+            const float4* tr = reinterpret_cast<const float4*>(theta + ((long)c * H + row) * W) + l * 4;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float4 v = tr[k];
+                th[4 * k] = v.x;
+                th[4 * k + 1] = v.y;
+                th[4 * k + 2] = v.z;
+                th[4 * k + 3] = v.w;
+            }
+            cur_it = it;
+        }
+        // slots [ncc, B) are staged as zeros.  Buffer `buf` was last read two
+        // frames ago, before the previous barrier, by every wave.
+        float2* const st = stage0 + buf * C::STAGE;
+#pragma unroll
+        for (int i = 0; i < SPT; ++i) {
+            const int idx = threadIdx.x + i * C::THREADS;
+            if (idx < TN) st[(idx / ROWS) * SR + idx % ROWS] = idx < ncc * ROWS ? pf[i] : make_float2(0.f, 0.f);
+        }
+        __syncthreads();
+        const int fcur = f;
+        next(it, f);
+        if (it < items) fetch(it, f);
+        float2 x[E];
+#pragma unroll
+        for (int q = 0; q < E; ++q) x[q] = cmul(st[(t + G * q) * SR + rl], ptl[q * RL + l]);
+        fft.template run_half<true>(x, s, t);
+        float* o = out + (((long)fcur * 2 + c) * H + row) * W;
+#pragma unroll
+        for (int q0 = 0; q0 < E; q0 += 2 * FCD_ATAN_N) {
+            __builtin_amdgcn_sched_barrier(0);
+            fv2 tq[FCD_ATAN_N], wq[FCD_ATAN_N];
+            float2 uq[2 * FCD_ATAN_N];
+#pragma unroll
+            for (int k = 0; k < FCD_ATAN_N; ++k) {
+                tq[k] = fv2{th[q0 + 2 * k], th[q0 + 2 * k + 1]};
+                uq[2 * k] = x[q0 + 2 * k];
+                uq[2 * k + 1] = x[q0 + 2 * k + 1];
+            }
+            wrapped_phase_pkn<FCD_ATAN_N>(tq, uq, wq);
+#pragma unroll
+            for (int k = 0; k < FCD_ATAN_N; ++k) {
+                const int n = g + L * t + RL * (q0 + 2 * k);
+                st_stream(o + n, wq[k].x);
+                st_stream(o + n + RL, wq[k].y);
+            }
+        }
+        buf ^= 1;
+    }
+}
+
+static int band_res_slices(int H, int nb, int rows) {
+    static int ncu = 0;
+    if (!ncu) {
+        int dev = 0;
+        hipDeviceProp_t p;
+        if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&p, dev) == hipSuccess) ncu = p.multiProcessorCount;
+        if (!ncu) ncu = 256;
+    }
+    const int tiles = 2 * (H / rows);
+    const int want = (FCD_BAND_RES_ITEMS * ncu + tiles - 1) / tiles;
+    return std::max(1, std::min(nb, want));
+}
+
 #ifdef FCD_STAMPS
 extern "C" int fcd_debug_band_stamps(unsigned long long* out) {
     return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_band_stamps), sizeof(g_band_stamps));
@@ -309,6 +468,26 @@ static void launch_band(bool ref, const float2* Ab, int H, int nb, int NCA, int 
         hipLaunchKernelGGL((k_band_phase<W, B, true>), dim3(grid), dim3(C::THREADS), lds, s, Ab, H, nb, NCA, ncc0,
                            ncc1, theta, out, pre, ptw);
     } else {
+        if constexpr (W / 16 == 64 && FCD_BAND_RESIDENT && FCD_ATAN_N > 0 && !FCD_BAND_ABL && !FCD_BAND_NOSTORE &&
+                      !FCD_BAND_NOTHETA) {
+            // FCD_BAND_RES=0 in the environment selects k_band_phase (equality tests)
+            const char* env = std::getenv("FCD_BAND_RES");
+            if (B <= 128 && !(env && env[0] == '0')) {
+                constexpr int ROWS = FCD_BAND_RES_ROWS;
+                using R = BRCfg<W, B, ROWS>;
+                const int slices = band_res_slices(H, nb, ROWS);
+                const int items = 2 * (H / ROWS) * slices;
+                static_assert(R::LDS <= 160 * 1024, "resident band kernel LDS");
+                (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_band_phase_res<W, B, ROWS>),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)R::LDS);
+                hipLaunchKernelGGL((k_band_phase_res<W, B, ROWS>), dim3(band_grid(items, (int)std::max<size_t>(1, (160 * 1024) / R::LDS))),
+                                   dim3(R::THREADS), R::LDS, s, Ab,
+                                   H, nb, NCA, ncc0, ncc1, theta, out, pre, ptw, slices);
+                const hipError_t e = hipGetLastError();
+                if (e != hipSuccess) throw std::runtime_error(std::string("band_phase_res launch: ") + hipGetErrorString(e));
+                return;
+            }
+        }
         if (lds > 64 * 1024)
             (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_band_phase<W, B, false>),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
