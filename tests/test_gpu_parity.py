@@ -227,23 +227,25 @@ def test_unwrap_residue_free_scan(lib):
     assert np.all(d == d.flat[0])
 
 
-def test_band_phase_resident_equals_classic(lib, monkeypatch):
+@pytest.mark.parametrize("n,count", [(1024, 7), (2048, 3)])
+def test_band_phase_resident_equals_classic(lib, monkeypatch, n, count):
     """The theta-resident band kernel (k_band_phase_res: reference angles kept in
-    registers across the frames of an item, one wave per tile row) and k_band_phase
-    (FCD_BAND_RES=0) run the same transform and phase step: bit-identical wrapped
-    phases at 1024^2, over an odd frame count (uneven frame slices)."""
+    registers across the frames of an item, one wave (1024^2) or wave pair (2048^2)
+    per tile row) and k_band_phase (FCD_BAND_RES=0) run the same transform and phase
+    step: bit-identical wrapped phases, over odd frame counts (uneven frame slices)."""
     from bench_data import make_frames_numpy
     from oracle import fcd_oracle as O
-    ref, frames = make_frames_numpy(1024, 7, seed=21, rotate_deg=5.0)
+    ref, frames = make_frames_numpy(n, count, seed=21, rotate_deg=5.0)
     eng = lib.Engine(ref.shape)
     eng.set_reference(ref, 0.001)
     _, w_res, _ = eng.process(frames, 1.0, unwrap=False)
     monkeypatch.setenv("FCD_BAND_RES", "0")
     _, w_cls, _ = eng.process(frames, 1.0, unwrap=False)
     assert np.array_equal(w_res, w_cls)
-    _, _, _, ex = O.compute_height_map(ref, frames[3], 0.001, height=1.0, unwrap_phases=False)
-    for q in range(2):
-        assert wrap_diff(w_res[3][q], ex["wrapped"][q]).max() < 2e-4
+    if n == 1024:
+        _, _, _, ex = O.compute_height_map(ref, frames[3], 0.001, height=1.0, unwrap_phases=False)
+        for q in range(2):
+            assert wrap_diff(w_res[3][q], ex["wrapped"][q]).max() < 2e-4
 
 
 # ---------------------------------------------------------------- end to end

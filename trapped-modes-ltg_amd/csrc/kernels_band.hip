@@ -281,7 +281,7 @@ __global__ __launch_bounds__((BPCfg<W, B>::THREADS), FCD_BAND_WAVES) void k_band
 template <int W, int B, int ROWS>
 struct BRCfg {
     static constexpr int G = B / 16, L = W / B, RL = W / 16;
-    static_assert(RL == 64, "one wave per row");
+    static_assert(RL == 64 || RL == 128, "one or two waves per row");
     static_assert(BTILE % ROWS == 0, "items cover whole or half Ab tiles");
     static constexpr int THREADS = ROWS * RL;
     static constexpr int SR = ROWS + 1;     // staged row pitch (complex)
@@ -302,7 +302,7 @@ __global__ __launch_bounds__((BRCfg<W, B, ROWS>::THREADS), 1) void k_band_phase_
     extern __shared__ __attribute__((aligned(16))) float2 lds_b[];
     float2* const stage0 = lds_b;                // [2][B][SROW]
     float2* const ptl = lds_b + 2 * C::STAGE;    // pre-twiddles [q][RL]
-    const int rl = threadIdx.x / RL;             // this wave's row of the tile
+    const int rl = threadIdx.x / RL;             // this wave's (or wave pair's) row of the tile
     const int l = threadIdx.x % RL, g = l / G, t = l % G;
     float* const s = reinterpret_cast<float*>(ptl + RL * E) + (size_t)(rl * L + g) * C::REGION;
     GroupFFT<B> fft;
@@ -468,12 +468,13 @@ static void launch_band(bool ref, const float2* Ab, int H, int nb, int NCA, int 
         hipLaunchKernelGGL((k_band_phase<W, B, true>), dim3(grid), dim3(C::THREADS), lds, s, Ab, H, nb, NCA, ncc0,
                            ncc1, theta, out, pre, ptw);
     } else {
-        if constexpr (W / 16 == 64 && FCD_BAND_RESIDENT && FCD_ATAN_N > 0 && !FCD_BAND_ABL && !FCD_BAND_NOSTORE &&
-                      !FCD_BAND_NOTHETA) {
+        if constexpr ((W == 1024 || W == 2048) && B <= W / 8 && FCD_BAND_RESIDENT && FCD_ATAN_N > 0 && !FCD_BAND_ABL &&
+                      !FCD_BAND_NOSTORE && !FCD_BAND_NOTHETA) {
             // FCD_BAND_RES=0 in the environment selects k_band_phase (equality tests)
             const char* env = std::getenv("FCD_BAND_RES");
-            if (B <= 128 && !(env && env[0] == '0')) {
-                constexpr int ROWS = FCD_BAND_RES_ROWS;
+            if (!(env && env[0] == '0')) {
+                // rows per item: 1024 threads at most (2048-point rows take two waves)
+                constexpr int ROWS = FCD_BAND_RES_ROWS * (W / 16) <= 1024 ? FCD_BAND_RES_ROWS : 1024 / (W / 16);
                 using R = BRCfg<W, B, ROWS>;
                 const int slices = band_res_slices(H, nb, ROWS);
                 const int items = 2 * (H / ROWS) * slices;
