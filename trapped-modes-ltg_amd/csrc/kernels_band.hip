@@ -312,45 +312,52 @@ __global__ __launch_bounds__((BRCfg<W, B, ROWS>::THREADS), 1) void k_band_phase_
     const int per = (nb + slices - 1) / slices;
     const int items = 2 * rts * slices;
     const int tile_n = NCA * BTILE;
-    // item -> (slice fastest, carrier, row tile); frames [f0, f1) of the slice
-    auto first_f = [&](int it) { return (it % slices) * per; };
-    auto last_f = [&](int it) { return min(nb, (it % slices + 1) * per); };
-    // the item's rows of Ab tile rb: slot (j, r) at j * BTILE + hb * ROWS + r
-    auto src_of = [&](int it, int f) {
-        const int c = (it / slices) % 2, rt = it / (2 * slices);
-        return Ab + (((long)f * 2 + c) * rbs + rt / HALVES) * (long)tile_n + (rt % HALVES) * ROWS;
+    // item -> (slice fastest, carrier, row tile); frames [f0, f1) of the slice.
+    // Decoded once per item (the divisions by `slices` stay off the per-frame path).
+    struct Item {
+        int it, c, rt, f0, f1;
     };
+    auto decode = [&](int it) {
+        Item d;
+        const int q = it / slices;
+        d.it = it;
+        d.c = q % 2;
+        d.rt = q / 2;
+        d.f0 = (it - q * slices) * per;
+        d.f1 = min(nb, d.f0 + per);
+        return d;
+    };
+    // the block's first non-empty item at or after `it`
+    auto seek = [&](int it) {
+        Item d = decode(it < items ? it : 0);
+        for (; it < items; it += gridDim.x) {
+            d = decode(it);
+            if (d.f0 < d.f1) return d;
+        }
+        d.it = items;
+        return d;
+    };
+    // the item's rows of Ab tile rb: slot (j, r) at j * BTILE + hb * ROWS + r
     float2 pf[SPT];
-    auto fetch = [&](int it, int f) {
-        const float2* src = src_of(it, f);
+    auto fetch = [&](const Item& d, int f) {
+        const float2* src = Ab + (((long)f * 2 + d.c) * rbs + d.rt / HALVES) * (long)tile_n + (d.rt % HALVES) * ROWS;
 #pragma unroll
         for (int i = 0; i < SPT; ++i) {
             const int idx = min((int)threadIdx.x + i * C::THREADS, TN - 1);
             pf[i] = src[min(idx / ROWS, NCA - 1) * BTILE + idx % ROWS];  // past the band: zeroed at staging
         }
     };
-    // advance (it, f) to the block's next non-empty (item, frame)
-    auto next = [&](int& it, int& f) {
-        if (f + 1 < last_f(it)) {
-            ++f;
-            return;
-        }
-        for (it += gridDim.x; it < items && first_f(it) >= last_f(it); it += gridDim.x) {
-        }
-        f = it < items ? first_f(it) : 0;
-    };
-    int it = blockIdx.x, f = 0;
-    for (; it < items && first_f(it) >= last_f(it); it += gridDim.x) {
-    }
-    if (it >= items) return;
-    f = first_f(it);
-    fetch(it, f);
-    int cur_it = -1, buf = 0;
+    Item cur = seek(blockIdx.x);
+    if (cur.it >= items) return;
+    int f = cur.f0;
+    fetch(cur, f);
+    int buf = 0;
+    bool fresh = true;
     float th[E];
-    while (it < items) {
-        const int c = (it / slices) % 2, row = (it / (2 * slices)) * ROWS + rl;
+    while (cur.it < items) {
+        const int c = cur.c, row = cur.rt * ROWS + rl;
         const int ncc = c ? ncc1 : ncc0;
-        if (it != cur_it) {  // this wave's row of theta (lane-contiguous copy), kept for the item
+        if (fresh) {  // this wave's row of theta (lane-contiguous copy), kept for the item
             const float4* tr = reinterpret_cast<const float4*>(theta + ((long)c * H + row) * W) + l * 4;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -360,7 +367,6 @@ __global__ __launch_bounds__((BRCfg<W, B, ROWS>::THREADS), 1) void k_band_phase_
                 th[4 * k + 2] = v.z;
                 th[4 * k + 3] = v.w;
             }
-            cur_it = it;
         }
         // slots [ncc, B) are staged as zeros.  Buffer `buf` was last read two
         // frames ago, before the previous barrier, by every wave.
@@ -372,8 +378,14 @@ __global__ __launch_bounds__((BRCfg<W, B, ROWS>::THREADS), 1) void k_band_phase_
         }
         __syncthreads();
         const int fcur = f;
-        next(it, f);
-        if (it < items) fetch(it, f);
+        fresh = f + 1 >= cur.f1;
+        if (fresh) {
+            cur = seek(cur.it + gridDim.x);
+            f = cur.f0;
+        } else {
+            ++f;
+        }
+        if (cur.it < items) fetch(cur, f);
         float2 x[E];
 #pragma unroll
         for (int q = 0; q < E; ++q) x[q] = cmul(st[(t + G * q) * SR + rl], ptl[q * RL + l]);
