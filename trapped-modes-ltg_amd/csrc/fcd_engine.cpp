@@ -1296,7 +1296,12 @@ int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int f
     // ---- pass 2: frames whose maps have residues are redone with the Boruvka (MST) unwrap
     std::vector<int> counts((size_t)n_frames * 2);
     HIPCHK(hipMemcpyAsync(counts.data(), res, counts.size() * sizeof(int), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
+    // polled rather than a blocking wait: the caller's next batch is enqueued as soon
+    // as this one's census is back (a blocking wait's wake-up sat in every bench step)
+    hipError_t qe;
+    while ((qe = hipStreamQuery(s)) == hipErrorNotReady) {
+    }
+    HIPCHK(qe);
     std::vector<int> redo;
     for (int f = 0; f < n_frames; ++f)
         if (counts[2 * (size_t)f] || counts[2 * (size_t)f + 1]) redo.push_back(f);
@@ -1314,19 +1319,39 @@ int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int f
     } fix_timer{c, fix_t0, redo.size()};
     for (size_t g0 = 0; g0 < redo.size(); g0 += nbmax) {
         const int ng = (int)std::min<size_t>(nbmax, redo.size() - g0);
-        stage_frames(c, frames, format, dev, redo.data() + g0, ng, s);
-        fast_demod(c, c->frames_in.as<float>(), ng, s);
+        const int* gi = redo.data() + g0;
+        // a group of consecutive frames (every frame of a batch of camera frames has
+        // residues) is read in place and its heights are written in place: no
+        // per-frame staging copies, whose host-side enqueueing left the GPU idle
+        const bool run = gi[ng - 1] - gi[0] == ng - 1;
+        const float* fr;
+        if (run && dev && format == FCD_FMT_F32) {
+            fr = reinterpret_cast<const float*>(frames) + (size_t)gi[0] * hw;
+        } else {
+            stage_frames(c, frames, format, dev, gi, ng, s);
+            fr = c->frames_in.as<float>();
+        }
+        fast_demod(c, fr, ng, s);
         int32_t* kf = c->fk.as<int32_t>();
         unwrap_maps(c, c->wrapped.as<float>(), 2 * ng, kf, nullptr, s);
         fcdk::int_rows(c->W, 2, c->wrapped.as<float>(), nullptr, kf, nullptr, nullptr, c->H, ng, c->Zt.as<float2>(),
                        c->twp_row.as<float2>(), s);
         fcdk::int_cols(c->H, c->Zt.as<float2>(), c->W, ng, coef, c->Ht.as<float2>(), c->twp_col.as<float2>(), s);
-        fcdk::int_c2r(c->W, c->Ht.as<float2>(), c->H, ng, c->out_h.as<float>(), c->twp_row.as<float2>(), s);
-        for (int i = 0; i < ng; ++i) {
-            const size_t f = (size_t)redo[g0 + i];
-            if (height_out)
-                HIPCHK(hipMemcpyAsync(height_out + f * hw, c->out_h.as<float>() + (size_t)i * hw, hw * 4, out_kind, s));
-            if (k_out) HIPCHK(hipMemcpyAsync(k_out + f * 2 * hw, kf + (size_t)i * 2 * hw, 2 * hw * 4, out_kind, s));
+        const bool direct = run && dev && height_out;
+        float* hdst = direct ? height_out + (size_t)gi[0] * hw : c->out_h.as<float>();
+        fcdk::int_c2r(c->W, c->Ht.as<float2>(), c->H, ng, hdst, c->twp_row.as<float2>(), s);
+        if (run) {
+            if (height_out && !direct)
+                HIPCHK(hipMemcpyAsync(height_out + (size_t)gi[0] * hw, hdst, (size_t)ng * hw * 4, out_kind, s));
+            if (k_out)
+                HIPCHK(hipMemcpyAsync(k_out + (size_t)gi[0] * 2 * hw, kf, (size_t)ng * 2 * hw * 4, out_kind, s));
+        } else {
+            for (int i = 0; i < ng; ++i) {
+                const size_t f = (size_t)gi[i];
+                if (height_out)
+                    HIPCHK(hipMemcpyAsync(height_out + f * hw, hdst + (size_t)i * hw, hw * 4, out_kind, s));
+                if (k_out) HIPCHK(hipMemcpyAsync(k_out + f * 2 * hw, kf + (size_t)i * 2 * hw, 2 * hw * 4, out_kind, s));
+            }
         }
         HIPCHK(hipStreamSynchronize(s));
     }
