@@ -338,16 +338,24 @@ int mst_level() {
 }
 
 // k-fields of nmaps wrapped maps (skimage unwrap_phase, fcd.py:119).  Synchronises.
-void unwrap_maps(fcd_ctx* c, const float* w, int nmaps, int32_t* k, int* res_host, hipStream_t s) {
-    int* res = c->rescnt.as<int>();
-    fcdk::residues(w, nmaps, c->H, c->W, res, s);
-    std::vector<int> counts(nmaps);
-    HIPCHK(hipMemcpyAsync(counts.data(), res, sizeof(int) * nmaps, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    if (res_host) std::copy(counts.begin(), counts.end(), res_host);
+// all_mst: every map goes through the MST pass without a residue count (the
+// exact fix-up of frames already known to carry residues; on a residue-free map
+// the MST integration equals the scan, k(0, 0) = 0 in both).
+void unwrap_maps(fcd_ctx* c, const float* w, int nmaps, int32_t* k, int* res_host, hipStream_t s,
+                 bool all_mst = false) {
     std::vector<int> active;
-    for (int i = 0; i < nmaps; ++i)
-        if (counts[i] > 0) active.push_back(i);
+    if (all_mst) {
+        for (int i = 0; i < nmaps; ++i) active.push_back(i);
+    } else {
+        int* res = c->rescnt.as<int>();
+        fcdk::residues(w, nmaps, c->H, c->W, res, s);
+        std::vector<int> counts(nmaps);
+        HIPCHK(hipMemcpyAsync(counts.data(), res, sizeof(int) * nmaps, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        if (res_host) std::copy(counts.begin(), counts.end(), res_host);
+        for (int i = 0; i < nmaps; ++i)
+            if (counts[i] > 0) active.push_back(i);
+    }
     // the scan unwrap for the residue-free maps (the MST pass overwrites the others);
     // skipped when every map has residues (the fix-up groups of camera frames)
     if ((int)active.size() < nmaps) fcdk::unwrap_scan(w, nmaps, c->H, c->W, c->colk.as<int>(), k, s);
@@ -1333,7 +1341,7 @@ int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int f
         }
         fast_demod(c, fr, ng, s);
         int32_t* kf = c->fk.as<int32_t>();
-        unwrap_maps(c, c->wrapped.as<float>(), 2 * ng, kf, nullptr, s);
+        unwrap_maps(c, c->wrapped.as<float>(), 2 * ng, kf, nullptr, s, true);
         fcdk::int_rows(c->W, 2, c->wrapped.as<float>(), nullptr, kf, nullptr, nullptr, c->H, ng, c->Zt.as<float2>(),
                        c->twp_row.as<float2>(), s);
         fcdk::int_cols(c->H, c->Zt.as<float2>(), c->W, ng, coef, c->Ht.as<float2>(), c->twp_col.as<float2>(), s);
