@@ -289,7 +289,8 @@ struct BRCfg {
     static constexpr int STAGE = B * SR;    // float2 per staging buffer
     static constexpr int TN = B * ROWS;     // staged slots per item tile
     static constexpr int SPT = (TN + THREADS - 1) / THREADS;
-    static constexpr size_t LDS = (size_t)(2 * STAGE + RL * 16) * 8 + (size_t)ROWS * L * REGION * 4;
+    static constexpr int NBUF = 2;  // staging buffers
+    static constexpr size_t LDS = (size_t)(NBUF * STAGE + RL * 16) * 8 + (size_t)ROWS * L * REGION * 4;
 };
 
 template <int W, int B, int ROWS>
@@ -300,8 +301,8 @@ __global__ __launch_bounds__((BRCfg<W, B, ROWS>::THREADS), 1) void k_band_phase_
     constexpr int G = C::G, L = C::L, RL = C::RL, E = 16, SPT = C::SPT, TN = C::TN, SR = C::SR;
     constexpr int HALVES = BTILE / ROWS;  // item tiles per Ab tile
     extern __shared__ __attribute__((aligned(16))) float2 lds_b[];
-    float2* const stage0 = lds_b;                // [2][B][SROW]
-    float2* const ptl = lds_b + 2 * C::STAGE;    // pre-twiddles [q][RL]
+    float2* const stage0 = lds_b;                // [NBUF][B][SR]
+    float2* const ptl = lds_b + C::NBUF * C::STAGE;  // pre-twiddles [q][RL]
     const int rl = threadIdx.x / RL;             // this wave's (or wave pair's) row of the tile
     const int l = threadIdx.x % RL, g = l / G, t = l % G;
     float* const s = reinterpret_cast<float*>(ptl + RL * E) + (size_t)(rl * L + g) * C::REGION;
@@ -347,50 +348,13 @@ __global__ __launch_bounds__((BRCfg<W, B, ROWS>::THREADS), 1) void k_band_phase_
             pf[i] = src[min(idx / ROWS, NCA - 1) * BTILE + idx % ROWS];  // past the band: zeroed at staging
         }
     };
-    Item cur = seek(blockIdx.x);
-    if (cur.it >= items) return;
-    int f = cur.f0;
-    fetch(cur, f);
-    int buf = 0;
-    bool fresh = true;
-    float th[E];
-    while (cur.it < items) {
-        const int c = cur.c, row = cur.rt * ROWS + rl;
-        const int ncc = c ? ncc1 : ncc0;
-        if (fresh) {  // this wave's row of theta (lane-contiguous copy), kept for the item
-            const float4* tr = reinterpret_cast<const float4*>(theta + ((long)c * H + row) * W) + l * 4;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const float4 v = tr[k];
-                th[4 * k] = v.x;
-                th[4 * k + 1] = v.y;
-                th[4 * k + 2] = v.z;
-                th[4 * k + 3] = v.w;
-            }
-        }
-        // slots [ncc, B) are staged as zeros.  Buffer `buf` was last read two
-        // frames ago, before the previous barrier, by every wave.
-        float2* const st = stage0 + buf * C::STAGE;
-#pragma unroll
-        for (int i = 0; i < SPT; ++i) {
-            const int idx = threadIdx.x + i * C::THREADS;
-            if (idx < TN) st[(idx / ROWS) * SR + idx % ROWS] = idx < ncc * ROWS ? pf[i] : make_float2(0.f, 0.f);
-        }
-        __syncthreads();
-        const int fcur = f;
-        fresh = f + 1 >= cur.f1;
-        if (fresh) {
-            cur = seek(cur.it + gridDim.x);
-            f = cur.f0;
-        } else {
-            ++f;
-        }
-        if (cur.it < items) fetch(cur, f);
+    // one row of one (item, frame): this wave's transform, phase step and stores
+    auto row_step = [&](const float2* st, const float (&th)[E], int c, int row, int f) {
         float2 x[E];
 #pragma unroll
         for (int q = 0; q < E; ++q) x[q] = cmul(st[(t + G * q) * SR + rl], ptl[q * RL + l]);
         fft.template run_half<true>(x, s, t);
-        float* o = out + (((long)fcur * 2 + c) * H + row) * W;
+        float* o = out + (((long)f * 2 + c) * H + row) * W;
 #pragma unroll
         for (int q0 = 0; q0 < E; q0 += 2 * FCD_ATAN_N) {
             __builtin_amdgcn_sched_barrier(0);
@@ -410,6 +374,50 @@ __global__ __launch_bounds__((BRCfg<W, B, ROWS>::THREADS), 1) void k_band_phase_
                 st_stream(o + n + RL, wq[k].y);
             }
         }
+    };
+    auto load_theta = [&](float (&th)[E], int c, int row) {  // lane-contiguous copy
+        const float4* tr = reinterpret_cast<const float4*>(theta + ((long)c * H + row) * W) + l * 4;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float4 v = tr[k];
+            th[4 * k] = v.x;
+            th[4 * k + 1] = v.y;
+            th[4 * k + 2] = v.z;
+            th[4 * k + 3] = v.w;
+        }
+    };
+    auto stage_in = [&](float2* st, int ncc) {  // slots [ncc, B) staged as zeros
+#pragma unroll
+        for (int i = 0; i < SPT; ++i) {
+            const int idx = threadIdx.x + i * C::THREADS;
+            if (idx < TN) st[(idx / ROWS) * SR + idx % ROWS] = idx < ncc * ROWS ? pf[i] : make_float2(0.f, 0.f);
+        }
+    };
+    Item cur = seek(blockIdx.x);
+    if (cur.it >= items) return;
+    int f = cur.f0;
+    fetch(cur, f);
+    float th[E];
+    int buf = 0;
+    bool fresh = true;
+    while (cur.it < items) {
+        const int c = cur.c, row = cur.rt * ROWS + rl;
+        const int ncc = c ? ncc1 : ncc0;
+        if (fresh) load_theta(th, c, row);  // kept for the item's frames
+        // Buffer `buf` was last read two frames ago, before the previous barrier.
+        float2* const st = stage0 + buf * C::STAGE;
+        stage_in(st, ncc);
+        __syncthreads();
+        const int fcur = f;
+        fresh = f + 1 >= cur.f1;
+        if (fresh) {
+            cur = seek(cur.it + gridDim.x);
+            f = cur.f0;
+        } else {
+            ++f;
+        }
+        if (cur.it < items) fetch(cur, f);
+        row_step(st, th, c, row, fcur);
         buf ^= 1;
     }
 }
