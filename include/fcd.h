@@ -92,9 +92,12 @@ int fcd_set_reference(fcd_ctx* ctx, const float* reference, int flags, double sq
  * (fcd.py:72-101) for n images (many-reference workloads)
  * WITHOUT replacing the context's reference: infos[i] gets what
  * fcd_set_reference(images[i]) would report (peaks, radius, calibration factor,
- * carrier frequencies, disk pixel counts, blobs, threshold).  The |F| high-pass,
- * threshold and candidate extraction run on the device, the labelling of the
- * few above-threshold pixels on the host.  Synchronises. */
+ * carrier frequencies, disk pixel counts, blobs, threshold).  Batches of images
+ * run every image-sized stage on the device (means, FFTs, |F| high-pass and its
+ * maximum, thresholded candidates, 8-connected labelling, the 4 dimmest blobs'
+ * peaks); the host finishes each image from its <= 4 peaks (an image with more than
+ * 4096 above-threshold pixels is labelled on the host from its candidate list).
+ * Synchronises. */
 int fcd_find_peaks(fcd_ctx* ctx, const float* images, int n, int flags, double square_size, fcd_ref_info* infos);
 
 /* Carrier arrays for the Python mirror: ccsgn complex64 [2][rows][cols]

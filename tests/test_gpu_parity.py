@@ -502,6 +502,40 @@ def test_find_peaks_batch_matches_reference_setup(lib, golden):
     assert [p.tolist() for p in out[0][1]] == d["peaks"].tolist()
 
 
+def test_device_labelling_matches_host(lib, monkeypatch, golden):
+    """fourier.find_peak_locations on the device (k_label_peaks: candidates sorted by raster
+    index, 8-connected union-find whose roots are each blob's first pixel, per-blob maximum
+    with the first pixel on ties, blobs ordered by (maximum, label), 4 kept) reports the same
+    reference info as the host labelling (FCD_HOST_LABEL=1) for camera references, rotated and
+    unrotated boards (whose Hermitian-partner and 45-degree maxima tie to the bit), all in
+    one batched call; a noise image with more candidates than the device labels falls back
+    to the host labelling inside the same batch."""
+    from bench_data import make_frames_numpy
+    r = golden("real_pair")
+    d = golden("real_df")
+    rng = np.random.default_rng(5)
+    refs = [r["ref_u8"].astype(np.float32), d["ref_u16"].astype(np.float32),
+            make_frames_numpy(1024, 1, rotate_deg=5.0)[0], make_frames_numpy(1024, 1)[0],
+            rng.standard_normal((1024, 1024)).astype(np.float32)]
+    stack = np.stack(refs)
+    eng = lib.Engine(stack.shape[1:])
+    dev = eng.find_peaks(stack, 0.0022)
+    monkeypatch.setenv("FCD_HOST_LABEL", "1")
+    host = eng.find_peaks(stack, 0.0022)
+    monkeypatch.delenv("FCD_HOST_LABEL")
+    fields = ("radius", "calibration_factor", "threshold", "n_blobs")
+    arrays = ("peaks", "frequencies", "mask_count", "blob_peaks")
+    for a, b in zip(dev, host):
+        for k in fields:
+            assert getattr(a, k) == getattr(b, k), k
+        for k in arrays:
+            assert np.array_equal(np.ctypeslib.as_array(getattr(a, k)), np.ctypeslib.as_array(getattr(b, k))), k
+    assert dev[4].n_blobs == 4  # the noise image: thousands of candidates, labelled on the host
+    single = lib.Engine(stack.shape[1:]).set_reference(refs[1], 0.0022)
+    assert single.calibration_factor == dev[1].calibration_factor
+    assert np.array_equal(np.ctypeslib.as_array(single.peaks), np.ctypeslib.as_array(dev[1].peaks))
+
+
 @pytest.mark.parametrize("rows,cols", [(512, 1024), (1024, 512), (256, 128)])
 def test_non_square_frames_vs_oracle(lib, golden, rows, cols):
     """H != W (the reference takes any frame shape; the engine any power-of-two pair): a

@@ -220,7 +220,7 @@ struct fcd_ctx {
     // workspace
     int chunk = 1;
     DevBuf spec, work, wrapped, kbuf, colk, rescnt, frames_in, out_h, scalar;
-    DevBuf cand_idx, cand_val;
+    DevBuf cand_idx, cand_val, pk_small, pk_F, pk_work;  // reference setup: candidates, scalars, spectra
     DevBuf fix_raw;  // raw samples of the frames redone by the exact pass
     // temporal analysis: staged block, exp table, bins, partial sums, output, window
     DevBuf t_stage, t_tab, t_bins, t_part, t_out, t_win, t_wsum, t_slices;
@@ -479,9 +479,10 @@ void check_ctx(fcd_ctx* c) {
     HIPCHK(hipSetDevice(c->device));
 }
 
-void find_carriers_host(fcd_ctx* c, const std::vector<int>& idx_in, const std::vector<float>& val_in, float thr,
-                        double square_size) {
-    const int H = c->H, W = c->W;
+// fourier.find_peak_locations (fourier.py:139-168) on the host, from an image's
+// candidate list: the images whose above-threshold set exceeds the device labelling
+// kernel's capacity (fcdk::label_peaks).  Returns the 4 dimmest blobs in order.
+std::vector<Blob> label_candidates_host(int H, int W, const std::vector<int>& idx_in, const std::vector<float>& val_in) {
     const size_t n = idx_in.size();
     std::vector<size_t> order(n);
     std::iota(order.begin(), order.end(), 0);
@@ -537,6 +538,14 @@ void find_carriers_host(fcd_ctx* c, const std::vector<int>& idx_in, const std::v
     }
     std::stable_sort(blobs.begin(), blobs.end(), [](const Blob& a, const Blob& b) { return a.value < b.value; });
     if (blobs.size() > 4) blobs.resize(4);
+    return blobs;
+}
+
+// The rest of fourier.find_peaks + compute_calibration_factor + the carrier disks
+// from the 4 dimmest blobs (fourier.py:38-39, fcd.py:53-101): sets c->info and
+// c->disk_rows_host.
+void carriers_from_blobs(fcd_ctx* c, const std::vector<Blob>& blobs, float thr, double square_size) {
+    const int H = c->H, W = c->W;
     if (blobs.size() < 1) throw FcdError(FCD_E_NOPEAKS, "find_peaks: no spectral peaks above threshold");
 
     const std::vector<double> kr = wavenumber(H, 1.0, true), kc = wavenumber(W, 1.0, true);
@@ -773,50 +782,73 @@ void band_reference(fcd_ctx* c, const float* dref, hipStream_t s) {
     fcdk::band_theta_lanes(c->W, c->band_B, c->theta_b.as<float>(), 2 * c->H, c->theta_p.as<float>(), s);
 }
 
-// fourier.find_peaks + compute_calibration_factor + the carrier disks for one
-// device-resident image: sets c->info and c->disk_rows_host (fcd.py:53-101,
-// fourier.py:7-41).  Uses the chunk workspace (spec, wrapped, scalar, cand_*).
-void find_peaks_device(fcd_ctx* c, const float* dref, double square_size, hipStream_t s) {
+// fourier.find_peaks + compute_calibration_factor + the carrier disks for nb
+// device-resident images (fcd.py:53-101, fourier.py:7-41), every image-sized stage
+// batched on the device: means, centring, FFT, |F| * highpass and its maximum, the
+// above-threshold candidates, the 8-connected labelling and the 4-blob pick
+// (kernels_fft.hip); the host finishes each image from its <= 4 peaks.  c->info and
+// c->disk_rows_host end up describing the last image; infos[i] (nullable) gets each.
+// Workspace: pk_* (16 bytes per pixel per image).
+int find_peaks_batch_max(const fcd_ctx* c) { return (int)std::max(1L, (512L << 20) / (16L * c->hw())); }
+
+void find_peaks_batch(fcd_ctx* c, const float* dimgs, int nb, double square_size, fcd_ref_info* infos, hipStream_t s) {
     const long hw = c->hw();
-    // fourier.find_peaks: |fftshift(fft2(ref - mean))| * highpass  (fourier.py:18-34)
-    double* dmean = c->scalar.as<double>();
-    fcdk::mean_f64(dref, hw, dmean, s);
-    double mean = 0;
-    HIPCHK(hipMemcpyAsync(&mean, dmean, sizeof(double), hipMemcpyDeviceToHost, s));
+    const int H = c->H, W = c->W;
+    if (nb <= 0) return;
+    constexpr int cap = 1 << 16;  // candidates kept per image (the device labels up to 4096 of them)
+    c->pk_F.ensure((size_t)nb * hw * sizeof(float2));
+    c->pk_work.ensure((size_t)nb * hw * 2 * sizeof(float));
+    float2* F = c->pk_F.as<float2>();
+    float* centered = c->pk_work.as<float>();
+    float* mag = centered + (size_t)nb * hw;
+    c->pk_small.ensure((size_t)nb * (8 + 4 + 4 + 32) + (size_t)(H + W) * 8);
+    double* sums = c->pk_small.as<double>();
+    unsigned* maxbits = reinterpret_cast<unsigned*>(sums + nb);
+    int* counts = reinterpret_cast<int*>(maxbits + nb);
+    int* res = counts + nb;
+    double* ktab = reinterpret_cast<double*>(res + 8 * (size_t)nb);
+    const std::vector<double> krs = wavenumber(H, 1.0, true), kcs = wavenumber(W, 1.0, true);
+    upload(ktab, krs.data(), H * sizeof(double), s);
+    upload(ktab + H, kcs.data(), W * sizeof(double), s);
+    c->cand_idx.ensure((size_t)nb * cap * sizeof(int));
+    c->cand_val.ensure((size_t)nb * cap * sizeof(float));
+    const double kmin = 4 * kPi / (double)std::min(H, W);  // fourier.py:22
+    fcdk::center_images(dimgs, nb, hw, sums, centered, s);
+    fft2_real(c, centered, F, nb, 0.f, s);
+    fcdk::spectrum_candidates_b(F, nb, H, W, ktab, ktab + H, kmin * kmin, mag, maxbits, counts, c->cand_idx.as<int>(),
+                                c->cand_val.as<float>(), cap, s);
+    fcdk::label_peaks(counts, c->cand_idx.as<int>(), c->cand_val.as<float>(), cap, nb, H, W, res, s);
+    std::vector<unsigned> mb(nb);
+    std::vector<int> rs((size_t)nb * 8);
+    HIPCHK(hipMemcpyAsync(mb.data(), maxbits, nb * sizeof(unsigned), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(rs.data(), res, rs.size() * sizeof(int), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    const float meanf = (float)(mean / (double)hw);
-    float2* F = c->spec.as<float2>();
-    fft2_real(c, dref, F, 1, meanf, s);
-    const std::vector<double> krs = wavenumber(c->H, 1.0, true), kcs = wavenumber(c->W, 1.0, true);
-    DevBuf ktab;
-    ktab.ensure((c->H + c->W) * sizeof(double));
-    upload(ktab.p, krs.data(), c->H * sizeof(double), s);
-    upload(ktab.as<double>() + c->H, kcs.data(), c->W * sizeof(double), s);
-    const double kmin = 4 * kPi / (double)std::min(c->H, c->W);
-    float* mag = c->wrapped.as<float>();
-    unsigned* maxbits = reinterpret_cast<unsigned*>(c->scalar.as<char>() + 16);
-    int* count = reinterpret_cast<int*>(c->scalar.as<char>() + 32);
-    fcdk::spectrum_mag(F, mag, maxbits, c->H, c->W, ktab.as<double>(), ktab.as<double>() + c->H, kmin * kmin, s);
-    const int cap = 1 << 16;
-    c->cand_idx.ensure(cap * sizeof(int));
-    c->cand_val.ensure(cap * sizeof(float));
-    fcdk::spectrum_candidates(mag, maxbits, c->H, c->W, count, c->cand_idx.as<int>(), c->cand_val.as<float>(),
-                              cap, s);
-    int ncand = 0;
-    unsigned mb = 0;
-    HIPCHK(hipMemcpyAsync(&ncand, count, sizeof(int), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(&mb, maxbits, sizeof(unsigned), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    if (ncand > cap) throw FcdError(FCD_E_UNSUPPORTED, "find_peaks: too many pixels above threshold");
-    std::vector<int> cidx(ncand);
-    std::vector<float> cval(ncand);
-    if (ncand) {
-        HIPCHK(hipMemcpy(cidx.data(), c->cand_idx.p, ncand * sizeof(int), hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(cval.data(), c->cand_val.p, ncand * sizeof(float), hipMemcpyDeviceToHost));
+    const bool host_label = std::getenv("FCD_HOST_LABEL") != nullptr;  // A/B: the host labelling for all
+    for (int b = 0; b < nb; ++b) {
+        float mx;
+        std::memcpy(&mx, &mb[b], 4);
+        const int* r = rs.data() + (size_t)b * 8;
+        std::vector<Blob> blobs;
+        if (r[0] != 0 || host_label) {
+            const int ncand = r[0] != 0 ? r[1] : -1;
+            int n = ncand;
+            if (n < 0) HIPCHK(hipMemcpy(&n, counts + b, sizeof(int), hipMemcpyDeviceToHost));
+            if (n > cap) throw FcdError(FCD_E_UNSUPPORTED, "find_peaks: too many pixels above threshold");
+            std::vector<int> cidx(n);
+            std::vector<float> cval(n);
+            if (n) {
+                HIPCHK(hipMemcpy(cidx.data(), c->cand_idx.as<int>() + (size_t)b * cap, n * sizeof(int),
+                                 hipMemcpyDeviceToHost));
+                HIPCHK(hipMemcpy(cval.data(), c->cand_val.as<float>() + (size_t)b * cap, n * sizeof(float),
+                                 hipMemcpyDeviceToHost));
+            }
+            blobs = label_candidates_host(H, W, cidx, cval);
+        } else {
+            for (int e = 0; e < r[2]; ++e) blobs.push_back(Blob{r[3 + e], r[3 + e], 0.f});
+        }
+        carriers_from_blobs(c, blobs, 0.5f * mx, square_size);
+        if (infos) infos[b] = c->info;
     }
-    float mx;
-    std::memcpy(&mx, &mb, 4);
-    find_carriers_host(c, cidx, cval, 0.5f * mx, square_size);
 }
 
 }  // namespace
@@ -917,7 +949,7 @@ FCD_API int fcd_set_reference(fcd_ctx* c, const float* reference, int flags, dou
             upload(c->frames_in.p, reference, hw * sizeof(float), s);
             dref = c->frames_in.as<float>();
         }
-        find_peaks_device(c, dref, square_size, s);
+        find_peaks_batch(c, dref, 1, square_size, nullptr, s);
         float2* F = c->spec.as<float2>();
         c->disk_rows.ensure(c->disk_rows_host.size() * sizeof(int));
         upload(c->disk_rows.p, c->disk_rows_host.data(), c->disk_rows_host.size() * sizeof(int), s);
@@ -950,7 +982,7 @@ FCD_API int fcd_find_peaks(fcd_ctx* c, const float* images, int n, int flags, do
         hipStream_t s = c->own;
         const long hw = c->hw();
         // the context's reference (if any) is kept: its per-reference host state is
-        // restored afterwards; the device state find_peaks_device touches is workspace
+        // restored afterwards; the device state find_peaks_batch touches is workspace
         const fcd_ref_info keep_info = c->info;
         const std::vector<int> keep_rows = c->disk_rows_host;
         struct Restore {
@@ -962,15 +994,16 @@ FCD_API int fcd_find_peaks(fcd_ctx* c, const float* images, int n, int flags, do
                 c->disk_rows_host = rows;
             }
         } restore{c, keep_info, keep_rows};
-        for (int i = 0; i < n; ++i) {
-            const float* img = images + (size_t)i * hw;
+        const int bmax = find_peaks_batch_max(c);
+        for (int i0 = 0; i0 < n; i0 += bmax) {
+            const int nb = std::min(bmax, n - i0);
+            const float* img = images + (size_t)i0 * hw;
             if (flags != FCD_DEVICE_PTRS) {
-                c->frames_in.ensure(hw * sizeof(float));
-                upload(c->frames_in.p, img, hw * sizeof(float), s);
+                c->frames_in.ensure((size_t)nb * hw * sizeof(float));
+                upload(c->frames_in.p, img, (size_t)nb * hw * sizeof(float), s);
                 img = c->frames_in.as<float>();
             }
-            find_peaks_device(c, img, square_size, s);
-            infos[i] = c->info;
+            find_peaks_batch(c, img, nb, square_size, infos + i0, s);
         }
     })
 }

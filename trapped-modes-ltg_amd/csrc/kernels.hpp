@@ -101,14 +101,16 @@ void col_fft(int H, int W, bool inverse, float2* data, int nbatch, const float2*
 void disk_mask(const float2* in, float2* out, int nbatch, int H, int W, DiskTable t, hipStream_t s);
 // theta = atan2(R)  (reference carrier angle)
 void angle(const float2* in, float* out, long n, hipStream_t s);
-// Mean of an image (f64 accumulation) into *out_d (device double).
-void mean_f64(const float* img, long n, double* out_d, hipStream_t s);
-// Masked |F| in shifted layout + max (as uint bits) for peak finding.
-void spectrum_mag(const float2* F, float* mag, unsigned* maxbits, int H, int W, const double* krow_s,
-                  const double* kcol_s, double kmin2, hipStream_t s);
-// Candidate pixels of the thresholded spectrum (border excluded).
-void spectrum_candidates(const float* mag, const unsigned* maxbits, int H, int W, int* count, int* idx,
-                         float* val, int cap, hipStream_t s);
+// Batched reference setup (fourier.find_peaks for nb images): out[b] = img[b] - mean(img[b])
+// (f64 mean, f32 difference); |F| * highpass per image with its maximum and the
+// above-threshold candidates (cap per image, border excluded); 8-connected labelling and
+// the 4 dimmest blobs' peaks per image (res: 8 ints per image, see kernels_fft.hip).
+void center_images(const float* img, int nb, long hw, double* sums, float* out, hipStream_t s);
+void spectrum_candidates_b(const float2* F, int nb, int H, int W, const double* krow_s, const double* kcol_s,
+                           double kmin2, float* mag, unsigned* maxbits, int* count, int* idx, float* val, int cap,
+                           hipStream_t s);
+void label_peaks(const int* counts, const int* idx, const float* val, int cap, int nb, int H, int W, int* res,
+                 hipStream_t s);
 
 // ---- unwrap ----
 void residues(const float* w, int nmaps, int H, int W, int* counts, hipStream_t s);

@@ -244,92 +244,242 @@ void angle(const float2* in, float* out, long n, hipStream_t s) {
     FCD_CHECK_LAUNCH();
 }
 
-// ------------------------------------------------------------------ peak finding support
-// fourier.find_peaks (fourier.py:18-35): |fftshift(F)| * highpass, max, threshold.
-__global__ void k_mean(const float* __restrict__ img, long n, double* out) {
+// ------------------------------------------------------------------ batched reference setup
+// fourier.find_peaks (fourier.py:7-41) for nb images at once, every stage on the
+// device: f64 image means, (image - mean) in f32 (the row FFT's input), |F| * highpass
+// with a per-image maximum, the above-threshold candidates per image, and the
+// 8-connected labelling with the peak pick (k_label_peaks).
+__global__ void k_mean_b(const float* __restrict__ img, long hw, double* sums) {
     __shared__ double part[256];
+    const float* p = img + (long)blockIdx.y * hw;
     double acc = 0.0;
-    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
-        acc += (double)img[i];
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < hw; i += (long)gridDim.x * blockDim.x)
+        acc += (double)p[i];
     part[threadIdx.x] = acc;
     __syncthreads();
     for (int st = 128; st > 0; st >>= 1) {
         if ((int)threadIdx.x < st) part[threadIdx.x] += part[threadIdx.x + st];
         __syncthreads();
     }
-    if (threadIdx.x == 0) atomicAdd(out, part[0]);
+    if (threadIdx.x == 0) atomicAdd(sums + blockIdx.y, part[0]);
 }
 
-void mean_f64(const float* img, long n, double* out_d, hipStream_t s) {
-    FCD_HIPCHK(hipMemsetAsync(out_d, 0, sizeof(double), s));
-    hipLaunchKernelGGL(k_mean, dim3(256), dim3(256), 0, s, img, n, out_d);
+__global__ void k_center_b(const float* __restrict__ img, long hw, long n, const double* __restrict__ sums,
+                           float* __restrict__ out) {
+    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= n) return;
+    out[idx] = img[idx] - (float)(sums[idx / hw] / (double)hw);  // image - mean, fourier.py:18
+}
+
+void center_images(const float* img, int nb, long hw, double* sums, float* out, hipStream_t s) {
+    FCD_HIPCHK(hipMemsetAsync(sums, 0, sizeof(double) * nb, s));
+    hipLaunchKernelGGL(k_mean_b, dim3(256, nb), dim3(256), 0, s, img, hw, sums);
+    FCD_CHECK_LAUNCH();
+    const long n = (long)nb * hw;
+    hipLaunchKernelGGL(k_center_b, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, img, hw, n, sums, out);
     FCD_CHECK_LAUNCH();
 }
 
-__global__ void k_spectrum_mag(const float2* __restrict__ F, float* __restrict__ mag, unsigned* maxbits, int H, int W,
-                               const double* __restrict__ krow_s, const double* __restrict__ kcol_s, double kmin2) {
-    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+__global__ void k_spectrum_mag_b(const float2* __restrict__ F, float* __restrict__ mag, unsigned* maxbits, int H,
+                                 int W, long n, const double* __restrict__ krow_s, const double* __restrict__ kcol_s,
+                                 double kmin2) {
+    const long gidx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long hw = (long)H * W;
     float m = 0.f;
-    if (idx < (long)H * W) {
-        const int si = (int)(idx / W), sj = (int)(idx % W);           // shifted coordinates
-        int i = (si + H / 2) & (H - 1), j = (sj + W / 2) & (W - 1);  // unshifted source
-        // Read the Hermitian pair (k, -k) from ONE canonical bin so |F(k)| == |F(-k)|
-        // bit-for-bit, as the reference's real-input pocketfft guarantees; its peak
-        // picks rely on that tie (SURVEY.md §8a parity fact 1).
-        const int mi = (H - i) & (H - 1), mj = (W - j) & (W - 1);
+    const long b = gidx / hw;  // H * W is a multiple of 64: a wave stays in one image
+    if (gidx < n) {
+        const long idx = gidx - b * hw;
+        const int si = (int)(idx / W), sj = (int)(idx % W);
+        int i = (si + H / 2) & (H - 1), j = (sj + W / 2) & (W - 1);
+        const int mi = (H - i) & (H - 1), mj = (W - j) & (W - 1);  // one canonical bin per Hermitian pair
         if (mi < i || (mi == i && mj < j)) {
             i = mi;
             j = mj;
         }
-        const float2 f = F[(long)i * W + j];
+        const float2 f = F[b * hw + (long)i * W + j];
         m = hypotf(f.x, f.y);
         const double kr = krow_s[si], kc = kcol_s[sj];
         const double k2 = __dadd_rn(__dmul_rn(kr, kr), __dmul_rn(kc, kc));
         if (!(k2 > kmin2)) m = 0.f;
-        mag[idx] = m;
+        mag[gidx] = m;
     }
-    // wave max then one atomic per wave (non-negative floats order as uints)
     unsigned u = __float_as_uint(m);
     for (int o = 32; o > 0; o >>= 1) {
         const unsigned v = __shfl_xor(u, o, 64);
         u = v > u ? v : u;
     }
-    if ((threadIdx.x & 63) == 0) atomicMax(maxbits, u);
+    if ((threadIdx.x & 63) == 0 && b * hw < n) atomicMax(maxbits + b, u);
 }
 
-void spectrum_mag(const float2* F, float* mag, unsigned* maxbits, int H, int W, const double* krow_s,
-                  const double* kcol_s, double kmin2, hipStream_t s) {
-    const long n = (long)H * W;
-    FCD_HIPCHK(hipMemsetAsync(maxbits, 0, sizeof(unsigned), s));
-    hipLaunchKernelGGL(k_spectrum_mag, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, F, mag, maxbits, H, W,
-                       krow_s, kcol_s, kmin2);
-    FCD_CHECK_LAUNCH();
-}
-
-// find_peak_locations (fourier.py:152-158): pixels > threshold, 1-px border zeroed.
-__global__ void k_candidates(const float* __restrict__ mag, const unsigned* __restrict__ maxbits, int H, int W,
-                             int* count, int* idx_out, float* val_out, int cap) {
-    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= (long)H * W) return;
+__global__ void k_candidates_b(const float* __restrict__ mag, const unsigned* __restrict__ maxbits, int H, int W,
+                               long n, int* count, int* idx_out, float* val_out, int cap) {
+    const long gidx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gidx >= n) return;
+    const long hw = (long)H * W, b = gidx / hw, idx = gidx - b * hw;
     const int si = (int)(idx / W), sj = (int)(idx % W);
-    if (si == 0 || sj == 0 || si == H - 1 || sj == W - 1) return;
-    const float thr = 0.5f * __uint_as_float(*maxbits);
-    const float m = mag[idx];
+    if (si == 0 || sj == 0 || si == H - 1 || sj == W - 1) return;  // fourier.py:154-158
+    const float thr = 0.5f * __uint_as_float(maxbits[b]);           // fourier.py:35
+    const float m = mag[gidx];
     if (m > thr) {
-        const int slot = atomicAdd(count, 1);
+        const int slot = atomicAdd(count + b, 1);
         if (slot < cap) {
-            idx_out[slot] = (int)idx;
-            val_out[slot] = m;
+            idx_out[b * cap + slot] = (int)idx;
+            val_out[b * cap + slot] = m;
         }
     }
 }
 
-void spectrum_candidates(const float* mag, const unsigned* maxbits, int H, int W, int* count, int* idx, float* val,
-                         int cap, hipStream_t s) {
-    const long n = (long)H * W;
-    FCD_HIPCHK(hipMemsetAsync(count, 0, sizeof(int), s));
-    hipLaunchKernelGGL(k_candidates, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, mag, maxbits, H, W, count,
-                       idx, val, cap);
+void spectrum_candidates_b(const float2* F, int nb, int H, int W, const double* krow_s, const double* kcol_s,
+                           double kmin2, float* mag, unsigned* maxbits, int* count, int* idx, float* val, int cap,
+                           hipStream_t s) {
+    const long n = (long)nb * H * W;
+    FCD_HIPCHK(hipMemsetAsync(maxbits, 0, sizeof(unsigned) * nb, s));
+    FCD_HIPCHK(hipMemsetAsync(count, 0, sizeof(int) * nb, s));
+    hipLaunchKernelGGL(k_spectrum_mag_b, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, F, mag, maxbits, H, W, n,
+                       krow_s, kcol_s, kmin2);
+    FCD_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_candidates_b, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, mag, maxbits, H, W, n,
+                       count, idx, val, cap);
+    FCD_CHECK_LAUNCH();
+}
+
+// fourier.find_peak_locations (fourier.py:139-168) on one image's candidate list per
+// workgroup: sort by raster index, 8-connected union-find (roots hook under the
+// smaller root, so a component's root is its first pixel in raster order = its
+// skimage label order), per blob the maximum (first pixel on ties, regionprops'
+// row-major coords), then the blobs sorted by (maximum, label) and the first
+// LABEL_TOP kept: the stable ascending sort's 4 dimmest blobs.
+// res[b * 8]: {status (0 ok, 1: more candidates than LABEL_CAP), blobs, kept, peak raster index x 4}.
+constexpr int LABEL_CAP = 4096;
+constexpr int LABEL_TOP = 4;
+
+__device__ __forceinline__ int label_find(volatile int* par, int x) {
+    int p = par[x];
+    while (p != x) {
+        x = p;
+        p = par[x];
+    }
+    return x;
+}
+
+template <class T>
+__device__ __forceinline__ void bitonic_lds(T* key, int n2) {
+    for (int k = 2; k <= n2; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            __syncthreads();
+            for (int i = threadIdx.x; i < n2; i += blockDim.x) {
+                const int ixj = i ^ j;
+                if (ixj > i) {
+                    const bool asc = (i & k) == 0;
+                    const T a = key[i], b = key[ixj];
+                    if ((a > b) == asc) {
+                        key[i] = b;
+                        key[ixj] = a;
+                    }
+                }
+            }
+        }
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(1024) void k_label_peaks(const int* __restrict__ counts, const int* __restrict__ idxs,
+                                                      const float* __restrict__ vals, int cap, int H, int W,
+                                                      int* __restrict__ res) {
+    __shared__ unsigned long long sk[LABEL_CAP];  // (raster index, slot) for the first sort, (max, root) for the second
+    __shared__ unsigned long long cm[LABEL_CAP];  // per root: (value bits, ~position) maximum
+    __shared__ int key[LABEL_CAP];
+    __shared__ float val[LABEL_CAP];
+    __shared__ int par[LABEL_CAP];
+    __shared__ int nblob;
+    const int b = blockIdx.x;
+    const int n = counts[b];
+    int* out = res + b * 8;
+    if (n > cap || n > LABEL_CAP) {  // the host labels this image from its candidate list
+        if (threadIdx.x == 0) {
+            out[0] = 1;
+            out[1] = n;
+        }
+        return;
+    }
+    int n2 = 1;
+    while (n2 < n) n2 <<= 1;
+    const int* ci = idxs + (long)b * cap;
+    const float* cv = vals + (long)b * cap;
+    for (int i = threadIdx.x; i < n2; i += blockDim.x)
+        sk[i] = i < n ? ((unsigned long long)(unsigned)ci[i] << 32) | (unsigned)i : ~0ull;
+    if (threadIdx.x == 0) nblob = 0;
+    bitonic_lds(sk, n2);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const int slot = (int)(sk[i] & 0xffffffffu);
+        key[i] = (int)(sk[i] >> 32);
+        val[i] = cv[slot];
+        par[i] = i;
+        cm[i] = 0;
+    }
+    __syncthreads();
+    auto lookup = [&](int r, int c) -> int {  // position of pixel (r, c) in the sorted list, or -1
+        if (r < 0 || c < 0 || r >= H || c >= W) return -1;
+        const int want = r * W + c;
+        int lo = 0, hi = n;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (key[mid] < want) lo = mid + 1; else hi = mid;
+        }
+        return lo < n && key[lo] == want ? lo : -1;
+    };
+    volatile int* vpar = par;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const int r = key[i] / W, c = key[i] % W;
+        const int nb4[4][2] = {{r - 1, c - 1}, {r - 1, c}, {r - 1, c + 1}, {r, c - 1}};
+        for (int q = 0; q < 4; ++q) {
+            const int j = lookup(nb4[q][0], nb4[q][1]);
+            if (j < 0) continue;
+            int x = i, y = j;
+            for (;;) {  // unite: the larger root hooks under the smaller
+                x = label_find(vpar, x);
+                y = label_find(vpar, y);
+                if (x == y) break;
+                if (x < y) {
+                    const int t = x;
+                    x = y;
+                    y = t;
+                }
+                if (atomicCAS(&par[x], x, y) == x) break;
+            }
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const int rt = label_find(vpar, i);
+        atomicMax(&cm[rt], ((unsigned long long)__float_as_uint(val[i]) << 32) | (0xffffffffu - (unsigned)i));
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < n2; i += blockDim.x) {
+        const bool root = i < n && par[i] == i;
+        sk[i] = root ? ((cm[i] >> 32) << 32) | (unsigned)i : ~0ull;
+        if (root) atomicAdd(&nblob, 1);
+    }
+    bitonic_lds(sk, n2);
+    if (threadIdx.x == 0) {
+        const int kept = nblob < LABEL_TOP ? nblob : LABEL_TOP;
+        out[0] = 0;
+        out[1] = nblob;
+        out[2] = kept;
+        for (int e = 0; e < LABEL_TOP; ++e) {
+            int pk = -1;
+            if (e < kept) {
+                const int rt = (int)(sk[e] & 0xffffffffu);
+                pk = key[0xffffffffu - (unsigned)(cm[rt] & 0xffffffffu)];
+            }
+            out[3 + e] = pk;
+        }
+    }
+}
+
+void label_peaks(const int* counts, const int* idx, const float* val, int cap, int nb, int H, int W, int* res,
+                 hipStream_t s) {
+    hipLaunchKernelGGL(k_label_peaks, dim3(nb), dim3(1024), 0, s, counts, idx, val, cap, H, W, res);
     FCD_CHECK_LAUNCH();
 }
 
