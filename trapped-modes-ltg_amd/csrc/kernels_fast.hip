@@ -570,7 +570,9 @@ __global__ __launch_bounds__(IntColsCfg<H>::THREADS, IntColsCfg<H>::V) void k_in
             const float ky = c.kye[i];
             float k2 = kx2 + c.ky2[i];
             if (i == 0 && col == 0) k2 = 1.f;
-            const float sc = c.norm / k2;
+            // 1 / k^2 by the hardware reciprocal (1 ulp) instead of an IEEE division
+            // (a 10-instruction sequence per element)
+            const float sc = c.norm * __builtin_amdgcn_rcpf(k2);
             const float m0 = (kx * c.a0 + ky * c.b0) * sc;
             const float m1 = (kx * c.a1 + ky * c.b1) * sc;
             const float re = m0 * f0.x + m1 * f1.x;
