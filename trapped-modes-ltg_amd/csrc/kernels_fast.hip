@@ -90,6 +90,9 @@ struct KCfg {
 #ifndef FCD_INTCOLS_PREF_Y
 #define FCD_INTCOLS_PREF_Y 0
 #endif
+#ifndef FCD_INTCOLS_KY_LDS
+#define FCD_INTCOLS_KY_LDS 1  // k_int_cols reads ky_eff / ky^2 from LDS copies (0: from the global tables)
+#endif
 #ifndef FCD_INTCOLS_PREF_X
 #define FCD_INTCOLS_PREF_X 1
 #endif
@@ -495,6 +498,15 @@ __global__ __launch_bounds__(IntColsCfg<H>::THREADS, IntColsCfg<H>::V) void k_in
     float2* s = lds + team * C::ROW;
     RegFFT<H> fft;
     fft.init(tw, lds_raw, threadIdx.x, C::THREADS);
+    // the row wavenumber tables (ky_eff, ky^2) of every element, read per item: LDS copies
+    float* const lky = reinterpret_cast<float*>(lds + TEAMS * C::ROW);
+    float* const lky2 = lky + H;
+    if constexpr (FCD_INTCOLS_KY_LDS) {
+        for (int i = threadIdx.x; i < H; i += C::THREADS) {
+            lky[i] = c.kye[i];
+            lky2[i] = c.ky2[i];
+        }
+    }
     __syncthreads();
     const int NCH = W / 2 + 1;
     const int items = nb * NCH;
@@ -560,19 +572,21 @@ __global__ __launch_bounds__(IntColsCfg<H>::THREADS, IntColsCfg<H>::V) void k_in
         if (base + TEAMS < i1) fetch(base + TEAMS + team < i1 ? base + TEAMS + team : items);
         fft.template run<false>(x, s, t);
         const float kx = c.kxe[col], kx2 = c.kx2[col];
+        const float hnorm = 0.5f * c.norm;
 #pragma unroll
         for (int q = 0; q < E; ++q) {
             const int i = t + TT * q;
             const float2 z = x[q];
             const float2 zm = y[q];
-            const float2 f0 = make_float2(0.5f * (z.x + zm.x), 0.5f * (z.y - zm.y));
-            const float2 f1 = make_float2(0.5f * (z.y + zm.y), -0.5f * (z.x - zm.x));
-            const float ky = c.kye[i];
-            float k2 = kx2 + c.ky2[i];
+            // 2 Phi0 and 2 Phi1 (the halves go into the multiplier's scale)
+            const float2 f0 = make_float2(z.x + zm.x, z.y - zm.y);
+            const float2 f1 = make_float2(z.y + zm.y, zm.x - z.x);
+            const float ky = FCD_INTCOLS_KY_LDS ? lky[i] : c.kye[i];
+            float k2 = kx2 + (FCD_INTCOLS_KY_LDS ? lky2[i] : c.ky2[i]);
             if (i == 0 && col == 0) k2 = 1.f;
             // 1 / k^2 by the hardware reciprocal (1 ulp) instead of an IEEE division
             // (a 10-instruction sequence per element)
-            const float sc = c.norm * __builtin_amdgcn_rcpf(k2);
+            const float sc = hnorm * __builtin_amdgcn_rcpf(k2);
             const float m0 = (kx * c.a0 + ky * c.b0) * sc;
             const float m1 = (kx * c.a1 + ky * c.b1) * sc;
             const float re = m0 * f0.x + m1 * f1.x;
@@ -777,7 +791,7 @@ template <int H>
 static void launch_int_cols(const float2* Zt, int W, int nb, const IntegCoef& c, float2* Ht, const float2* tw,
                             hipStream_t s, const int* colk) {
     using C = IntColsCfg<H>;
-    const size_t lds = (size_t)C::NLEN * 8 + (size_t)C::TEAMS * C::ROW * 8;
+    const size_t lds = (size_t)C::NLEN * 8 + (size_t)C::TEAMS * C::ROW * 8 + (FCD_INTCOLS_KY_LDS ? (size_t)H * 8 : 0);
     set_lds(k_int_cols<H>, lds);
     const int grid = grid_for(((long)nb * (W / 2 + 1) + C::TEAMS - 1) / C::TEAMS, 4);
     const int zt = zt_rows(W);
