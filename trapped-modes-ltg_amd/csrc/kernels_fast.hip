@@ -511,19 +511,26 @@ __global__ __launch_bounds__(IntColsCfg<H>::THREADS, IntColsCfg<H>::V) void k_in
     const int NCH = W / 2 + 1;
     const int items = nb * NCH;
     const int zmask = (1 << zts) - 1;
+    // Element q of this lane is row t + TT q.  TT is a multiple of the Zt tile height,
+    // so its tile offset is this lane's offset plus q TT W (and in Ht q TT NCH): the
+    // addresses are one lane base and a uniform stride, computed once, instead of
+    // the tile arithmetic per load (which cost ~200 VALU instructions per item).
+    const long zt_lane = (((long)(t >> zts) * W) << zts) + (t & zmask);
+    const long zt_step = (long)TT * W;
+    const long ht_lane = (long)(t >> 4) * NCH * 16 + (t & 15);
+    const long ht_step = (long)TT * NCH;
     // Both columns of the NEXT item are loaded into registers while the current
     // item is transformed (loads issued before the current item's stores).
     float2 py[E], px[E];
+    auto fetch_fc = [&](int f, int col, bool mirror, float2 (&v)[E]) {
+        const int cc = mirror ? (W - col) & (W - 1) : col;
+        const float2* src = Zt + (long)f * H * W + ((long)cc << zts) + zt_lane;
+#pragma unroll
+        for (int q = 0; q < E; ++q) v[q] = src[q * zt_step];
+    };
     auto fetch_col = [&](int item, bool mirror, float2 (&v)[E]) {
         const bool valid = item < items;
-        const int f = valid ? item / NCH : 0, col = valid ? item % NCH : 0;
-        const int cc = mirror ? (W - col) & (W - 1) : col;
-        const float2* src = Zt + (long)f * H * W + ((long)cc << zts);
-#pragma unroll
-        for (int q = 0; q < E; ++q) {
-            const int rr = t + TT * q;
-            v[q] = src[(((long)(rr >> zts) * W) << zts) + (rr & zmask)];
-        }
+        fetch_fc(valid ? item / NCH : 0, valid ? item % NCH : 0, mirror, v);
     };
     auto fetch = [&](int item) {
         if constexpr (C::PREF_Y) fetch_col(item, true, py);
@@ -595,9 +602,9 @@ __global__ __launch_bounds__(IntColsCfg<H>::THREADS, IntColsCfg<H>::V) void k_in
         }
         fft.template run<true>(x, s, t);
         if (valid) {
-            float2* dst = Ht + (long)f * H * NCH;
+            float2* dst = Ht + (long)f * H * NCH + (long)col * 16 + ht_lane;
 #pragma unroll
-            for (int q = 0; q < E; ++q) dst[tix(t + TT * q, col, NCH)] = x[q];
+            for (int q = 0; q < E; ++q) dst[q * ht_step] = x[q];  // tix(t + TT q, col, NCH)
         }
     }
 }
