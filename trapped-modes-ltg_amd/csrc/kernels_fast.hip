@@ -204,14 +204,19 @@ __global__ __launch_bounds__(DemodColsCfg<H>::THREADS, DemodColsCfg<H>::V) void 
     __syncthreads();
     const int NC = T.NC;
     const int items = nb * NC;
+    // element q of this lane is row t + TT q (TT a multiple of the 16-row tile): its
+    // tile offset is this lane's offset plus q TT NC (q TT NCA in Ab)
+    static_assert(TT % TILE == 0, "row stride across whole tiles");
+    const long xb_lane = (long)(t >> 4) * NC * TILE + (t & 15), xb_step = (long)TT * NC;
+    const long ab_lane = (long)(t >> 4) * NCA * TILE + (t & 15), ab_step = (long)TT * NCA;
     for (int base = blockIdx.x * TEAMS; base < items; base += gridDim.x * TEAMS) {
         const int item = base + team;
         const bool valid = item < items;
         const int f = valid ? item / NC : 0, i = valid ? item % NC : 0;
         float2 x[E];
-        const float2* src = Xb + (long)f * H * NC;
+        const float2* src = Xb + (long)f * H * NC + (long)i * TILE + xb_lane;
 #pragma unroll
-        for (int q = 0; q < E; ++q) x[q] = src[tix(t + TT * q, i, NC)];
+        for (int q = 0; q < E; ++q) x[q] = src[q * xb_step];  // tix(t + TT q, i, NC)
         fft.template run<false>(x, s, t);
         if constexpr (!Sched<H>::WAVE_LOCAL) __syncthreads();
 #pragma unroll
@@ -252,9 +257,9 @@ __global__ __launch_bounds__(DemodColsCfg<H>::THREADS, DemodColsCfg<H>::V) void 
             }
             fft.template run<true>(y, s2, t);
             if (live) {
-                float2* dst = Ab + ((long)f * 2 + o.x) * H * NCA;
+                float2* dst = Ab + ((long)f * 2 + o.x) * H * NCA + (long)o.y * TILE + ab_lane;
 #pragma unroll
-                for (int q = 0; q < E; ++q) dst[tix(t + TT * q, o.y, NCA)] = y[q];
+                for (int q = 0; q < E; ++q) dst[q * ab_step] = y[q];  // tix(t + TT q, o.y, NCA)
             }
         }
     }
@@ -640,19 +645,27 @@ __global__ __launch_bounds__(C2RCfg<W>::THREADS) void k_int_c2r(const float2* __
     fft.init(tw, lds_raw, threadIdx.x, C::THREADS);
     __syncthreads();
     const int NCH = W / 2 + 1;
-    const int nblk = H / rpw;
-    // the next item's staged block (NCH x rpw values) is prefetched into registers
+    // rows per staged block: the launch passes C::RPW; as a constant the block's
+    // index arithmetic is shifts, and a 16-row block is one contiguous Ht tile row
+    (void)rpw;
+    constexpr int RPW = C::RPW;
+    const int nblk = H / RPW;
+    // the next item's staged block (NCH x RPW values) is prefetched into registers
     // while the current one is transformed (SPT values per thread, all in flight)
     constexpr int SPT = ((W / 2 + 1) * C::RPW + C::THREADS - 1) / C::THREADS;
     float2 pf[SPT];
     auto fetch = [&](int blk) {
-        const int f = blk / nblk, r0 = (blk % nblk) * rpw;
+        const int f = blk / nblk, r0 = (blk % nblk) * RPW;
         const float2* src = Ht + (long)f * H * NCH;
 #pragma unroll
         for (int i = 0; i < SPT; ++i) {
             const int idx = threadIdx.x + i * C::THREADS;
-            const int col = min(idx / rpw, NCH - 1), rl = idx % rpw;
-            pf[i] = src[tix(r0 + rl, col, NCH)];
+            if constexpr (RPW == TILE) {
+                pf[i] = src[(long)r0 * NCH + min(idx, NCH * TILE - 1)];  // tix(r0 + idx % 16, idx / 16, NCH)
+            } else {
+                const int col = min(idx / RPW, NCH - 1), rl = idx % RPW;
+                pf[i] = src[tix(r0 + rl, col, NCH)];
+            }
         }
     };
     // XCD-aware order: workgroups are dealt round-robin to the 8 XCDs, each with
@@ -664,26 +677,26 @@ __global__ __launch_bounds__(C2RCfg<W>::THREADS) void k_int_c2r(const float2* __
     const int vb = (G % 8 == 0) ? (int)(blockIdx.x % 8) * (G / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
     if (vb < nb * nblk) fetch(vb);
     for (int blk = vb; blk < nb * nblk; blk += G) {
-        const int f = blk / nblk, r0 = (blk % nblk) * rpw;
+        const int f = blk / nblk, r0 = (blk % nblk) * RPW;
 #pragma unroll
         for (int i = 0; i < SPT; ++i) {
             const int idx = threadIdx.x + i * C::THREADS;
-            if (idx < NCH * rpw) stage[(idx / rpw) * (rpw + 1) + idx % rpw] = pf[i];
+            if (idx < NCH * RPW) stage[(idx / RPW) * (RPW + 1) + idx % RPW] = pf[i];
         }
         __syncthreads();
         if (blk + G < nb * nblk) fetch(blk + G);
-        for (int pr = team; pr < rpw / 2; pr += TEAMS) {
+        for (int pr = team; pr < RPW / 2; pr += TEAMS) {
             float2 x[E];
 #pragma unroll
             for (int q = 0; q < E; ++q) {
                 const int col = t + TT * q;
                 float2 g1, g2;
                 if (col <= W / 2) {
-                    g1 = stage[col * (rpw + 1) + 2 * pr];
-                    g2 = stage[col * (rpw + 1) + 2 * pr + 1];
+                    g1 = stage[col * (RPW + 1) + 2 * pr];
+                    g2 = stage[col * (RPW + 1) + 2 * pr + 1];
                 } else {  // row-wise Hermitian: G(y, W - c) = conj G(y, c)
-                    g1 = stage[(W - col) * (rpw + 1) + 2 * pr];
-                    g2 = stage[(W - col) * (rpw + 1) + 2 * pr + 1];
+                    g1 = stage[(W - col) * (RPW + 1) + 2 * pr];
+                    g2 = stage[(W - col) * (RPW + 1) + 2 * pr + 1];
                     g1.y = -g1.y;
                     g2.y = -g2.y;
                 }
