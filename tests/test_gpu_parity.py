@@ -412,6 +412,72 @@ def test_fused_census_sends_residue_frames_to_exact_pass(lib, golden, fused):
     assert np.array_equal(hf, hu)
 
 
+def dislocation_frames(n, rows, x0s, length=200):
+    """Checkerboard frames each warped by an edge-dislocation pair on one row,
+    u_x = P / (2 pi) * (atan2(y - y0, x - x0) - atan2(y - y0, x - x0 - length))
+    (P = 20 px, the board's period, so the cut between the cores is invisible): both
+    carrier phases wind by +-2 pi around the two cores, a residue pair on row ~y0."""
+    from bench_data import checkerboard, warp_numpy
+    ref = checkerboard(n)
+    y, x = np.mgrid[0:n, 0:n].astype(np.float64)
+    frames = [warp_numpy(ref, np.zeros_like(x),
+                         (20.0 / TWOPI) * (np.arctan2(y - y0, x - x0) - np.arctan2(y - y0, x - x0 - length)))
+              for y0, x0 in zip(rows, x0s)]
+    return ref, np.stack(frames)
+
+
+def residue_rows(w):
+    """Plaquette rows (r: between pixel rows r and r + 1) of a wrapped map's residues."""
+    w = np.asarray(w, np.float64)
+    wr = lambda d: (d + np.pi) % TWOPI - np.pi  # noqa: E731
+    c = wr(w[:-1, 1:] - w[:-1, :-1]) + wr(w[1:, 1:] - w[:-1, 1:]) + wr(w[1:, :-1] - w[1:, 1:]) + wr(w[:-1, :-1] - w[1:, :-1])
+    return np.nonzero(np.abs(c) > 1)[0]
+
+
+# (y0, x0) of dislocation pairs whose residues all fall on plaquette rows 8k - 1,
+# i.e. between two 8-row unwrap tiles, in both carrier maps (found by running the
+# oracle over candidate placements; rechecked on the engine's own phases below)
+SEAM_PAIRS = {1024: [(206.75, 307.2), (207.0, 307.2), (319.5, 358.4), (319.75, 358.4), (487.0, 435.2)],
+              2048: [(487.0, 870.4)]}
+
+
+@pytest.mark.parametrize("n,count", [(1024, 16), (2048, 2), (2048, 4)])
+def test_census_flags_residues_on_tile_seams(lib, monkeypatch, n, count):
+    """Residue pairs between the last row of one 8-row unwrap tile and the first row of
+    the next, at tile edges inside a block's contiguous range and at range edges
+    (k_ir_seam_check; at 2048^2 x 2 frames every block owns one tile): the unfused
+    k_int_rows2 census and the fused kernel's census must flag every frame, so all
+    heights come from the exact MST pass, bit-identical between the two paths."""
+    from pyfcd import _lib
+    seam = SEAM_PAIRS[n]
+    fill = count - len(seam)
+    rows = [p[0] for p in seam] + [8 * (12 + 7 * i) - 0.5 for i in range(fill)]
+    x0s = [p[1] for p in seam] + [n * (0.25 + 0.3 * i / max(fill, 1)) for i in range(fill)]
+    ref, frames = dislocation_frames(n, rows, x0s)
+    _lib._engines.clear()
+    heights = {}
+    for unfused in ("1", "0"):
+        monkeypatch.setenv("FCD_UNFUSED", unfused)
+        eng = lib.Engine(ref.shape)
+        eng.set_reference(ref, 0.001)
+        eng.profile(True)
+        h, w, _ = eng.process(frames, 1.0, unwrap=True, want_phases=unfused == "1")
+        st, _ = eng.stage_times()
+        eng.profile(False)
+        assert int(st["fixup_frames"]) == count, (unfused, st)
+        if w is not None:
+            rr = [[residue_rows(w[f, m]) for m in range(2)] for f in range(count)]
+            assert all(len(r) > 0 for fr in rr for r in fr)
+            seam_only = [f for f in range(count) if all((r % 8 == 7).all() for r in rr[f])]
+            assert len(seam_only) >= 1, [[r.tolist() for r in fr] for fr in rr]
+        heights[unfused] = h
+        del eng
+    monkeypatch.delenv("FCD_UNFUSED")
+    _lib._engines.clear()
+    if n == 1024:  # the fused kernel is 1024-wide only
+        assert np.array_equal(heights["1"], heights["0"])
+
+
 def test_full_size_2048_vs_oracle(lib):
     """configs[2] geometry (2048^2, HBM-bound regime): one rotated-board frame against the
     oracle with unwrapping; peaks / cf bit-exact, phases up to one 2*pi*c, heights rel-L2."""

@@ -213,6 +213,7 @@ struct fcd_ctx {
     int nstreams = 2;                // FCD_STREAMS: device-path chunks split over 1 or 2 streams
     hipStream_t aux = nullptr;       // the second stream and its fork / join events
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    DevBuf ir_seam;                  // k_int_rows2's seam rows (tile-range edges), one region per stream
     DevBuf ztw, col0, seam;          // its 1024-point group-FFT twiddles; column-0 wrapped values [f][2][H];
                                      // first/last unwrapped rows of every tile [f][H/tile][2][W]
     size_t fres_cap = 0;
@@ -736,6 +737,7 @@ void build_demod_tables(fcd_ctx* c, hipStream_t s) {
     c->fk.ensure(nb * 2 * hw * sizeof(int32_t));
     c->col0.ensure(nb * 2 * (size_t)H * sizeof(float));
     if (c->fused_ok) c->seam.ensure(nb * (size_t)(H / fcdk::phase_rows_tile()) * 2 * W * sizeof(float2));
+    c->ir_seam.ensure(2 * fcdk::int_rows_seam_bytes(W, H, (int)nb));
     c->rescnt.ensure(std::max(nb, (size_t)c->chunk) * 2 * sizeof(int));
     c->mst_cap = 0;  // re-size the MST workspace for the new chunk on next use
 }
@@ -1077,8 +1079,11 @@ void first_pass_chunk(fcd_ctx* c, const float* fr, int nb, bool unwrap, bool fus
         if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
         if (unwrap) fcdk::unwrap_colk(wrapped, 2 * nb, c->H, c->W, colk, s);
         if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
+        // the second concurrent half (fo > 0) has its own seam region
+        float2* seam = c->ir_seam.as<float2>() +
+                       (fo ? fcdk::int_rows_seam_bytes(c->W, c->H, c->fchunk) / sizeof(float2) : 0);
         fcdk::int_rows(c->W, unwrap ? 1 : 0, wrapped, colk, nullptr, kdst, res, c->H, nb, Zt, c->twp_row.as<float2>(),
-                       s);
+                       seam, s);
         fcdk::int_cols(c->H, Zt, c->W, nb, coef, Ht, c->twp_col.as<float2>(), s);
         fcdk::int_c2r(c->W, Ht, c->H, nb, hdst, c->twp_row.as<float2>(), s);
     }
@@ -1376,7 +1381,7 @@ int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int f
         int32_t* kf = c->fk.as<int32_t>();
         unwrap_maps(c, c->wrapped.as<float>(), 2 * ng, kf, nullptr, s, true);
         fcdk::int_rows(c->W, 2, c->wrapped.as<float>(), nullptr, kf, nullptr, nullptr, c->H, ng, c->Zt.as<float2>(),
-                       c->twp_row.as<float2>(), s);
+                       c->twp_row.as<float2>(), nullptr, s);
         fcdk::int_cols(c->H, c->Zt.as<float2>(), c->W, ng, coef, c->Ht.as<float2>(), c->twp_col.as<float2>(), s);
         const bool direct = run && dev && height_out;
         float* hdst = direct ? height_out + (size_t)gi[0] * hw : c->out_h.as<float>();

@@ -63,8 +63,11 @@ void demod_cols(int H, const float2* Xb, int nb, const DemodTables& T, float2* A
                 hipStream_t s);
 void demod_phase(int W, const float2* Ab, int H, int nb, int NCA, const DemodTables& T, const float* theta,
                  float* wrapped, const float2* tw, hipStream_t s);
+// seam: kmode 1's buffer of the tile ranges' first / last unwrapped rows
+// (int_rows_seam_bytes(W, H, nb) bytes; may be null for kmodes 0 and 2)
 void int_rows(int W, int kmode, const float* w, const int* colk, const int32_t* kin, int32_t* kout, int* rescount,
-              int H, int nb, float2* Zt, const float2* tw, hipStream_t s);
+              int H, int nb, float2* Zt, const float2* tw, float2* seam, hipStream_t s);
+size_t int_rows_seam_bytes(int W, int H, int nb);
 struct IntegCoef;
 // colk (nullable): per (frame, map, row) column-0 unwrap offsets still to be
 // added (the fused path adds 2 pi W (colk0 + i colk1) to each row's DC bin).

@@ -104,6 +104,11 @@ struct KCfg {
 #ifndef FCD_DEMODCOLS_BLOCK
 #define FCD_DEMODCOLS_BLOCK 512
 #endif
+// k_demod_cols loads the next item's column during the current item's transforms
+// (1) or at the top of each item (0).
+#ifndef FCD_DEMODCOLS_PREF
+#define FCD_DEMODCOLS_PREF 1
+#endif
 template <int N>
 struct DemodColsCfg : KCfg<N, (N <= 1024 ? FCD_DEMODCOLS_BLOCK : BLOCK)> {
     static constexpr int V = N <= 1024 ? 4 : ColWaves<N>::V;
@@ -209,14 +214,31 @@ __global__ __launch_bounds__(DemodColsCfg<H>::THREADS, DemodColsCfg<H>::V) void 
     static_assert(TT % TILE == 0, "row stride across whole tiles");
     const long xb_lane = (long)(t >> 4) * NC * TILE + (t & 15), xb_step = (long)TT * NC;
     const long ab_lane = (long)(t >> 4) * NCA * TILE + (t & 15), ab_step = (long)TT * NCA;
+#if FCD_DEMODCOLS_PREF
+    // the next item's column is loaded while the current one is transformed
+    float2 xn[E];
+    auto fetch = [&](int it) {
+        const int fi = it < items ? it / NC : 0, ii = it < items ? it % NC : 0;
+        const float2* src = Xb + (long)fi * H * NC + (long)ii * TILE + xb_lane;
+#pragma unroll
+        for (int q = 0; q < E; ++q) xn[q] = src[q * xb_step];  // tix(t + TT q, ii, NC)
+    };
+    fetch(blockIdx.x * TEAMS + team);
+#endif
     for (int base = blockIdx.x * TEAMS; base < items; base += gridDim.x * TEAMS) {
         const int item = base + team;
         const bool valid = item < items;
         const int f = valid ? item / NC : 0, i = valid ? item % NC : 0;
         float2 x[E];
+#if FCD_DEMODCOLS_PREF
+#pragma unroll
+        for (int q = 0; q < E; ++q) x[q] = xn[q];
+        if (base + (int)gridDim.x * TEAMS < items) fetch(item + gridDim.x * TEAMS);
+#else
         const float2* src = Xb + (long)f * H * NC + (long)i * TILE + xb_lane;
 #pragma unroll
         for (int q = 0; q < E; ++q) x[q] = src[q * xb_step];  // tix(t + TT q, i, NC)
+#endif
         fft.template run<false>(x, s, t);
         if constexpr (!Sched<H>::WAVE_LOCAL) __syncthreads();
 #pragma unroll
@@ -785,26 +807,48 @@ static void launch_demod_phase(const float2* Ab, int H, int nb, int NCA, const D
 }
 
 template <int W>
+static int int_rows_grid(int H, int nb) {
+    using C = IRCfg<W>;
+    const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(2048 / C::THREADS, (160 * 1024) / C::LDS_BYTES));
+    return grid_for((long)nb * (H / C::ZT), per_cu);
+}
+
+template <int W>
 static void launch_int_rows(int kmode, const float* w, const int* colk, const int32_t* kin, int32_t* kout,
-                            int* rescount, int H, int nb, float2* Zt, const float2* tw, hipStream_t s) {
+                            int* rescount, int H, int nb, float2* Zt, const float2* tw, float2* seam, hipStream_t s) {
     using C = IRCfg<W>;
     const size_t lds = C::LDS_BYTES;
-    const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(2048 / C::THREADS, (160 * 1024) / lds));
-    const int grid = grid_for((long)nb * (H / C::ZT), per_cu);
+    int grid = int_rows_grid<W>(H, nb);
+    const long items = (long)nb * (H / C::ZT);
+    const int per = (int)((items + grid - 1) / grid);  // KMODE 1 with C::SEAM: tiles per block, a contiguous range
     if (kmode == 0) {
         set_lds(k_int_rows2<W, 0>, lds);
         hipLaunchKernelGGL((k_int_rows2<W, 0>), dim3(grid), dim3(C::THREADS), lds, s, w, colk, kin, kout, rescount, H,
-                           nb, Zt, tw);
+                           nb, Zt, tw, seam, per);
     } else if (kmode == 1) {
+        if (C::SEAM) {
+            if (!seam) throw std::runtime_error("int_rows: the seam census needs a seam buffer");
+            grid = (int)((items + per - 1) / per);
+        }
         set_lds(k_int_rows2<W, 1>, lds);
         hipLaunchKernelGGL((k_int_rows2<W, 1>), dim3(grid), dim3(C::THREADS), lds, s, w, colk, kin, kout, rescount, H,
-                           nb, Zt, tw);
+                           nb, Zt, tw, seam, per);
+        if (C::SEAM && grid > 1) {
+            FCD_CHECK_LAUNCH();
+            hipLaunchKernelGGL(k_ir_seam_check<W>, dim3((unsigned)((grid - 1 + 3) / 4)), dim3(256), 0, s, seam, H, nb,
+                               per, grid, rescount);
+        }
     } else {
         set_lds(k_int_rows2<W, 2>, lds);
         hipLaunchKernelGGL((k_int_rows2<W, 2>), dim3(grid), dim3(C::THREADS), lds, s, w, colk, kin, kout, rescount, H,
-                           nb, Zt, tw);
+                           nb, Zt, tw, seam, per);
     }
     FCD_CHECK_LAUNCH();
+}
+
+template <int W>
+static void int_rows_seam_bytes_t(int H, int nb, size_t* out) {
+    *out = (size_t)int_rows_grid<W>(H, nb) * 2 * W * sizeof(float2);
 }
 
 template <int H>
@@ -846,8 +890,13 @@ void demod_phase(int W, const float2* Ab, int H, int nb, int NCA, const DemodTab
     FCD_SIZE_SWITCH(W, launch_demod_phase, Ab, H, nb, NCA, T, theta, wrapped, tw, s);
 }
 void int_rows(int W, int kmode, const float* w, const int* colk, const int32_t* kin, int32_t* kout, int* rescount,
-              int H, int nb, float2* Zt, const float2* tw, hipStream_t s) {
-    FCD_SIZE_SWITCH(W, launch_int_rows, kmode, w, colk, kin, kout, rescount, H, nb, Zt, tw, s);
+              int H, int nb, float2* Zt, const float2* tw, float2* seam, hipStream_t s) {
+    FCD_SIZE_SWITCH(W, launch_int_rows, kmode, w, colk, kin, kout, rescount, H, nb, Zt, tw, seam, s);
+}
+size_t int_rows_seam_bytes(int W, int H, int nb) {
+    size_t b = 0;
+    FCD_SIZE_SWITCH(W, int_rows_seam_bytes_t, H, nb, &b);
+    return b;
 }
 void int_cols(int H, const float2* Zt, int W, int nb, const IntegCoef& c, float2* Ht, const float2* tw,
               hipStream_t s, const int* colk) {

@@ -103,6 +103,8 @@ int main(int argc, char** argv) {
     int32_t* kbuf = dalloc<int32_t>((size_t)nb * 2 * hw);
     float2* Zt = dalloc<float2>((size_t)nb * hw);
     float2* Ht = dalloc<float2>((size_t)nb * H * (W / 2 + 1));
+    const size_t irseam_bytes = fcdk::int_rows_seam_bytes(W, H, nb);  // one region per chain stream (<= 4)
+    float2* irseam = dalloc<float2>(4 * irseam_bytes / sizeof(float2));
     float* hout = dalloc<float>((size_t)nb * hw);
     float* ktab = dalloc<float>(2 * (W + H));
     fcdk::IntegCoef coef{ktab, ktab + W, ktab + W + H, ktab + 2 * W + H, 1.f, 0.5f, -0.5f, 1.f, 1e-6f};
@@ -191,10 +193,10 @@ int main(int argc, char** argv) {
     }
     timeit("colk", 8.0 * H, [&] { fcdk::unwrap_colk(wrapped, 2 * nb, H, W, colk, s); });
     timeit("int_rows k0", 2 * f + 2 * f, [&] {
-        fcdk::int_rows(W, 0, wrapped, colk, nullptr, nullptr, nullptr, H, nb, Zt, tw, s);
+        fcdk::int_rows(W, 0, wrapped, colk, nullptr, nullptr, nullptr, H, nb, Zt, tw, nullptr, s);
     });
     timeit("int_rows k1", 2 * f + 2 * f, [&] {
-        fcdk::int_rows(W, 1, wrapped, colk, nullptr, nullptr, res, H, nb, Zt, tw, s);
+        fcdk::int_rows(W, 1, wrapped, colk, nullptr, nullptr, res, H, nb, Zt, tw, irseam, s);
     });
     timeit("int_cols", 2 * f + 8.0 * H * (W / 2 + 1),
            [&] { fcdk::int_cols(H, Zt, W, nb, coef, Ht, tw, s); });
@@ -227,7 +229,7 @@ int main(int argc, char** argv) {
                                  pre, ptw, st);
                 fcdk::unwrap_colk(wrapped + o * 2 * hw, 2 * m, H, W, colk + o * 2 * H, st);
                 fcdk::int_rows(W, 1, wrapped + o * 2 * hw, colk + o * 2 * H, nullptr, nullptr, res + 2 * o, H, m,
-                               Zt + o * hw, tw, st);
+                               Zt + o * hw, tw, irseam + k * (irseam_bytes / sizeof(float2)), st);
                 fcdk::int_cols(H, Zt + o * hw, W, m, coef, Ht + o * H * (W / 2 + 1), tw, st);
                 fcdk::int_c2r(W, Ht + o * H * (W / 2 + 1), H, m, hout + o * hw, tw, st);
             };
