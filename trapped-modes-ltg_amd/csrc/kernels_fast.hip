@@ -135,6 +135,13 @@ __device__ __forceinline__ int fw_fast(float a, float b) {
 }
 
 // ------------------------------------------------------------------ K1
+// band columns per lane that k_demod_rows keeps in registers (the rest are read
+// from the table per row pair)
+#ifndef FCD_DR_HCREG
+#define FCD_DR_HCREG 2
+#endif
+constexpr int DR_HCR = FCD_DR_HCREG;
+
 template <int W>
 __global__ __launch_bounds__(KCfg<W>::THREADS, FCD_MIN_WAVES) void k_demod_rows(const float* __restrict__ frames, int H, int nb,
                                                       DemodTables T, float2* __restrict__ Xb,
@@ -151,6 +158,11 @@ __global__ __launch_bounds__(KCfg<W>::THREADS, FCD_MIN_WAVES) void k_demod_rows(
     __syncthreads();
     const int NC = T.NC;
     const int rbs = H / TILE;
+    // this lane's first DR_HCR band columns, held for the whole kernel (no dependent
+    // global load in front of every row pair's band extraction)
+    int hcr[DR_HCR > 0 ? DR_HCR : 1];
+#pragma unroll
+    for (int k = 0; k < DR_HCR; ++k) hcr[k] = t + k * TT < NC ? T.hc[t + k * TT] : 0;
     // the next row pair of this team is loaded while the current one is transformed
     float2 xn[E];
     auto fetch = [&](int blk, int pr) {
@@ -175,13 +187,16 @@ __global__ __launch_bounds__(KCfg<W>::THREADS, FCD_MIN_WAVES) void k_demod_rows(
 #pragma unroll
             for (int q = 0; q < E; ++q) s[pad(t + TT * q)] = x[q];
             team_sync<W>();
-            for (int i = t; i < NC; i += TT) {
-                const int hc = T.hc[i];
+            auto band = [&](int i, int hc) {
                 const float2 zk = s[pad(hc)], zm = s[pad((W - hc) & (W - 1))];
                 // X_a = (Z(k) + conj Z(-k)) / 2 ; X_b = (Z(k) - conj Z(-k)) / 2i
                 stage[i * (TILE + 1) + 2 * pr] = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y));
                 stage[i * (TILE + 1) + 2 * pr + 1] = make_float2(0.5f * (zk.y + zm.y), -0.5f * (zk.x - zm.x));
-            }
+            };
+#pragma unroll
+            for (int k = 0; k < DR_HCR; ++k)
+                if (t + k * TT < NC) band(t + k * TT, hcr[k]);
+            for (int i = t + DR_HCR * TT; i < NC; i += TT) band(i, T.hc[i]);
         }
         const int f = blk / rbs, rb = blk % rbs;
         __syncthreads();
@@ -239,12 +254,16 @@ __global__ __launch_bounds__(DemodColsCfg<H>::THREADS, DemodColsCfg<H>::V) void 
 #pragma unroll
         for (int q = 0; q < E; ++q) x[q] = src[q * xb_step];  // tix(t + TT q, i, NC)
 #endif
+        // the item's output count and first output (every column has 4 table slots),
+        // read before the forward transform so that it hides their latency
+        const int nout = valid ? T.nouts[i] : 0;
+        int4 on = T.outs[i * 4];     // carrier, cslot, mirror, uc
+        int2 rn = T.outrows[i * 4];  // shifted rows [lo, hi]
         fft.template run<false>(x, s, t);
         if constexpr (!Sched<H>::WAVE_LOCAL) __syncthreads();
 #pragma unroll
         for (int q = 0; q < E; ++q) s[pad(t + TT * q)] = x[q];
         team_sync<H>();
-        const int nout = valid ? T.nouts[i] : 0;
         // teams spanning waves share the workgroup barrier: every team loops to
         // the largest output count among the workgroup's items
         int nmax = nout;
@@ -259,8 +278,12 @@ __global__ __launch_bounds__(DemodColsCfg<H>::THREADS, DemodColsCfg<H>::V) void 
 #pragma unroll 1
         for (int e = 0; e < nmax; ++e) {
             const bool live = e < nout;
-            const int4 o = live ? T.outs[i * 4 + e] : make_int4(0, 0, 0, 0);  // carrier, cslot, mirror, uc
-            const int2 rr = live ? T.outrows[i * 4 + e] : make_int2(1, 0);   // shifted rows [lo, hi]
+            const int4 o = live ? on : make_int4(0, 0, 0, 0);
+            const int2 rr = live ? rn : make_int2(1, 0);
+            if (e + 1 < 4) {  // the next output's entries, during this inverse transform
+                on = T.outs[i * 4 + e + 1];
+                rn = T.outrows[i * 4 + e + 1];
+            }
             float2 y[E];
 #pragma unroll
             for (int q = 0; q < E; ++q) {
