@@ -329,30 +329,45 @@ struct GroupFFTTab2 {
     }
 };
 
-// atan2(y, x) in f32: |error| <= ~2.5e-7 rad (degree-8 odd minimax-fit
-// polynomial on [0, 1] after the octant reduction, v_rcp_f32 division);
+// atan(r) = r P(r^2) on [0, 1]: minimax-fit polynomials of FCD_ATAN_TERMS terms
+// (highest order first).  Max |error| evaluated in f32 with FMAs: 9 terms 1.0e-7
+// rad, 8 terms 1.4e-7, 7 terms 3.2e-7 (tools/atan_fit.py) -- all far below the
+// f32 transforms' own phase error against the f64 reference.
+#ifndef FCD_ATAN_TERMS
+#define FCD_ATAN_TERMS 9
+#endif
+constexpr int kAtanN = FCD_ATAN_TERMS;
+__host__ __device__ constexpr float atan_coef(int i) {
+    constexpr float C9[9] = {0.0024567286018282175f, -0.014401371590793133f, 0.03978124260902405f,
+                             -0.07234858721494675f,  0.10498946160078049f,   -0.14161229133605957f,
+                             0.19985906779766083f,   -0.33332598209381104f,  0.9999998807907104f};
+    constexpr float C8[8] = {-0.004054554738104343f, 0.02186291478574276f,  -0.05591226741671562f,
+                             0.09642193466424942f,   -0.1390862762928009f,  0.19946564733982086f,
+                             -0.33329859375953674f,  0.9999993443489075f};
+    constexpr float C7[7] = {0.006811772007495165f, -0.033604156225919724f, 0.07962360233068466f,
+                             -0.13233338296413422f, 0.19807814061641693f,   -0.3331736922264099f,
+                             0.9999961256980896f};
+    return kAtanN == 9 ? C9[i] : (kAtanN == 8 ? C8[i] : C7[i]);
+}
+static_assert(kAtanN >= 7 && kAtanN <= 9, "FCD_ATAN_TERMS: 7, 8 or 9");
+
+// atan2(y, x) in f32 (atan_coef after the octant reduction, v_rcp_f32 division);
 // atan2(0, 0) = 0, like atan2f.  About 20 VALU operations.
 __device__ __forceinline__ float fast_atan2(float y, float x) {
     const float ax = fabsf(x), ay = fabsf(y);
     const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
     const float r = mx > 0.f ? mn * __builtin_amdgcn_rcpf(mx) : 0.f;
     const float s = r * r;
-    float p = 0.0024567286018282175f;
-    p = fmaf(p, s, -0.014401371590793133f);
-    p = fmaf(p, s, 0.03978124260902405f);
-    p = fmaf(p, s, -0.07234858721494675f);
-    p = fmaf(p, s, 0.10498946160078049f);
-    p = fmaf(p, s, -0.14161229133605957f);
-    p = fmaf(p, s, 0.19985906779766083f);
-    p = fmaf(p, s, -0.33332598209381104f);
-    p = fmaf(p, s, 0.9999998807907104f);
+    float p = atan_coef(0);
+#pragma unroll
+    for (int c = 1; c < kAtanN; ++c) p = fmaf(p, s, atan_coef(c));
     float a = r * p;
     a = ay > ax ? 1.57079632679489662f - a : a;
     a = x < 0.f ? 3.14159265358979324f - a : a;
     return copysignf(a, y);
 }
 
-// fast_atan2 of two values at once: the reduction's divide, square, degree-8
+// fast_atan2 of two values at once: the reduction's divide, square,
 // polynomial and final product run as packed-FP32 ops (v_pk_mul / v_pk_fma: both
 // values per instruction), the octant fix-ups per value; the zero-magnitude
 // guard is a clamp of the divisor to FLT_MIN (0 * rcp(FLT_MIN) = 0) instead of
@@ -364,15 +379,9 @@ __device__ __forceinline__ fv2 fast_atan2_pk(fv2 y, fv2 x) {
     const fv2 mn = {fminf(fabsf(x.x), fabsf(y.x)), fminf(fabsf(x.y), fabsf(y.y))};
     const fv2 r = mn * fv2{__builtin_amdgcn_rcpf(mx0), __builtin_amdgcn_rcpf(mx1)};
     const fv2 s = r * r;
-    fv2 p = fv2{0.0024567286018282175f, 0.0024567286018282175f};
-    p = p * s + -0.014401371590793133f;
-    p = p * s + 0.03978124260902405f;
-    p = p * s + -0.07234858721494675f;
-    p = p * s + 0.10498946160078049f;
-    p = p * s + -0.14161229133605957f;
-    p = p * s + 0.19985906779766083f;
-    p = p * s + -0.33332598209381104f;
-    p = p * s + 0.9999998807907104f;
+    fv2 p = fv2{atan_coef(0), atan_coef(0)};
+#pragma unroll
+    for (int c = 1; c < kAtanN; ++c) p = p * s + atan_coef(c);
     fv2 a = r * p;
     a.x = fabsf(y.x) > fabsf(x.x) ? 1.57079632679489662f - a.x : a.x;
     a.y = fabsf(y.y) > fabsf(x.y) ? 1.57079632679489662f - a.y : a.y;
@@ -409,15 +418,12 @@ __device__ __forceinline__ void wrapped_phase_pkn(const fv2 (&theta)[NP], const 
     }
 #pragma unroll
     for (int k = 0; k < NP; ++k) s[k] = r[k] * r[k];
-    constexpr float C[9] = {0.0024567286018282175f, -0.014401371590793133f, 0.03978124260902405f,
-                            -0.07234858721494675f,  0.10498946160078049f,   -0.14161229133605957f,
-                            0.19985906779766083f,   -0.33332598209381104f,  0.9999998807907104f};
 #pragma unroll
-    for (int k = 0; k < NP; ++k) p[k] = s[k] * C[0] + C[1];
+    for (int k = 0; k < NP; ++k) p[k] = s[k] * atan_coef(0) + atan_coef(1);
 #pragma unroll
-    for (int c = 2; c < 9; ++c)
+    for (int c = 2; c < kAtanN; ++c)
 #pragma unroll
-        for (int k = 0; k < NP; ++k) p[k] = p[k] * s[k] + C[c];
+        for (int k = 0; k < NP; ++k) p[k] = p[k] * s[k] + atan_coef(c);
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
         const float2 u0 = u[2 * k], u1 = u[2 * k + 1];
