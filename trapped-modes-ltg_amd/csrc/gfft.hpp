@@ -330,11 +330,16 @@ struct GroupFFTTab2 {
 };
 
 // atan(r) = r P(r^2) on [0, 1]: minimax-fit polynomials of FCD_ATAN_TERMS terms
-// (highest order first).  Max |error| evaluated in f32 with FMAs: 9 terms 1.0e-7
-// rad, 8 terms 1.4e-7, 7 terms 3.2e-7 (tools/atan_fit.py) -- all far below the
-// f32 transforms' own phase error against the f64 reference.
+// (highest order first).  Max |error| evaluated in f32: 9 terms 1.0e-7 rad, 8
+// terms 1.4e-7, 7 terms 3.2e-7 (tools/atan_fit.py; in f64 the fits themselves are
+// 5.8e-9 / 3.7e-8 / 2.5e-7).  8 by default: one packed FMA per pixel pair less
+// than 9 at the same f32 error.  7 terms (two less, band kernel 3.17 -> 3.05
+// us/frame, kbench r02c8) leave the wrapped phases' tail error against the f64
+// oracle unchanged (99.99th percentile 2.7e-6 rad, tools/atan_accuracy.py) but
+// their systematic error integrates into the 4096^2 no-unwrap height: rel-L2
+// 1.13e-5 against the 1e-5 bound (test_full_size_4096_properties, r02c9).
 #ifndef FCD_ATAN_TERMS
-#define FCD_ATAN_TERMS 9
+#define FCD_ATAN_TERMS 8
 #endif
 constexpr int kAtanN = FCD_ATAN_TERMS;
 __host__ __device__ constexpr float atan_coef(int i) {
