@@ -56,12 +56,16 @@ def kernel_resources(obj):
 def test_kernel_register_budgets():
     """The occupancy statements in the kernel comments hold for the compiled code:
     k_demod_cols<1024> fits 128 VGPRs (two 512-thread workgroups = 16 waves per CU),
-    the fused k_phase_rows fits 256 (8 waves per CU), and no throughput kernel spills."""
+    the fused k_phase_rows fits 256 (8 waves per CU), and no throughput kernel spills
+    -- except k_int_rows2<4096, 1>'s seam census, whose at most 4 spilled VGPRs hold
+    loop invariants (stored at entry, reloaded once per tile; measured faster than the
+    spill-free halo form, int_rows.inc IRCfg::SEAM)."""
     res = kernel_resources("kernels_fast.hip")
     dc = next(v for k, v in res.items() if k.startswith("_ZN4fcdk12k_demod_colsILi1024E"))
     assert dc["VGPRs"] + dc["AGPRs"] <= 128 and dc["Occupancy [waves/SIMD]"] >= 4, dc
     for name, v in res.items():
-        assert v.get("VGPRs Spill", 0) == 0 and v.get("SGPRs Spill", 0) == 0, name
+        vlim = 4 if name.startswith("_ZN4fcdk11k_int_rows2ILi4096ELi1E") else 0
+        assert v.get("VGPRs Spill", 0) <= vlim and v.get("SGPRs Spill", 0) == 0, name
     pr = kernel_resources("kernels_phase_rows.hip")
     for name, v in pr.items():
         if "k_phase_rows" in name:

@@ -438,14 +438,15 @@ def residue_rows(w):
 # i.e. between two 8-row unwrap tiles, in both carrier maps (found by running the
 # oracle over candidate placements; rechecked on the engine's own phases below)
 SEAM_PAIRS = {1024: [(206.75, 307.2), (207.0, 307.2), (319.5, 358.4), (319.75, 358.4), (487.0, 435.2)],
-              2048: [(487.0, 870.4)]}
+              2048: [(487.0, 870.4)],
+              4096: [(487.0, 870.4), (607.0, 870.4)]}  # 4-row tiles at 4096: rows 4k - 1
 
 
-@pytest.mark.parametrize("n,count", [(1024, 16), (2048, 2), (2048, 4)])
+@pytest.mark.parametrize("n,count", [(1024, 16), (2048, 2), (2048, 4), (4096, 2)])
 def test_census_flags_residues_on_tile_seams(lib, monkeypatch, n, count):
-    """Residue pairs between the last row of one 8-row unwrap tile and the first row of
-    the next, at tile edges inside a block's contiguous range and at range edges
-    (k_ir_seam_check; at 2048^2 x 2 frames every block owns one tile): the unfused
+    """Residue pairs between the last row of one unwrap tile (8 rows; 4 at 4096) and the
+    first row of the next, at tile edges inside a block's contiguous range and at range
+    edges (k_ir_seam_check; at 2048^2 x 2 frames every block owns one tile): the unfused
     k_int_rows2 census and the fused kernel's census must flag every frame, so all
     heights come from the exact MST pass, bit-identical between the two paths."""
     from pyfcd import _lib
@@ -468,7 +469,8 @@ def test_census_flags_residues_on_tile_seams(lib, monkeypatch, n, count):
         if w is not None:
             rr = [[residue_rows(w[f, m]) for m in range(2)] for f in range(count)]
             assert all(len(r) > 0 for fr in rr for r in fr)
-            seam_only = [f for f in range(count) if all((r % 8 == 7).all() for r in rr[f])]
+            zt = 8 if n <= 2048 else 4  # unwrap tile rows (int_rows.inc zt_rows)
+            seam_only = [f for f in range(count) if all((r % zt == zt - 1).all() for r in rr[f])]
             assert len(seam_only) >= 1, [[r.tolist() for r in fr] for fr in rr]
         heights[unfused] = h
         del eng
