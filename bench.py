@@ -6,10 +6,16 @@ the same host.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--size 1024] [--batch 256]
 
-For N > 1 the driver launches one process per GPU with torch.distributed.run;
-each rank processes its own `--batch` frames (weak scaling, SURVEY.md §8e:
-frames are independent, no collective in the compute), the step time is the
-max over ranks, and rank 0 prints one JSON line.
+For N > 1 there is one process per GPU: either the caller launches the ranks
+(torch.distributed.run sets WORLD_SIZE), or a plain `python bench.py --gpus N`
+launches them itself through torch.distributed.run before anything touches the
+GPU (pyfcd/dist.py:spawn_ranks) and exits with the ranks' exit code.  Each rank
+checks WORLD_SIZE == N, processes its own `--batch` frames (weak scaling,
+SURVEY.md §8e: frames are independent, no collective in the compute), the step
+time is the max over ranks, and rank 0 prints one JSON line.  `--gather` then
+times a grouped send/recv gather of every rank's heights to rank 0, reported as
+`gather` beside (never inside) the frames/s.  `--dry-run` stops after the
+rendezvous (no GPU): rank 0 prints the world it saw (CPU test of the launcher).
 """
 import argparse
 import json
@@ -119,20 +125,44 @@ def main():
     ap.add_argument("--cpu-frames", type=int, default=12)
     ap.add_argument("--cpu-workers", type=int, default=16, help="processes of the all-cores CPU baseline")
     ap.add_argument("--gather", action="store_true", help="also time an RCCL gather of the heights to rank 0")
+    ap.add_argument("--dry-run", action="store_true", help="rendezvous only, no GPU (launcher test)")
     args = ap.parse_args()
+
+    from pyfcd.dist import dist_env, spawn_ranks
+    rank, world, local = dist_env()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher around us: start one rank per GPU as child processes (nothing
+        # has touched the GPU in this process) and report their exit status
+        sys.exit(spawn_ranks(args.gpus, os.path.abspath(__file__), sys.argv[1:]))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
 
     import torch
     import torch.distributed as dist
-    from pyfcd import _lib
-    from pyfcd.dist import dist_env, gather_stack, max_over_ranks
-    from bench_data import make_frames_torch, SQUARE_SIZE
-
-    rank, world, local = dist_env()
     if world > 1:
         # "nccl" is RCCL on ROCm (one process per GPU, xGMI); FCD_BENCH_BACKEND=gloo only
-        # to rehearse N ranks sharing the GPUs of a smaller box
-        dist.init_process_group(os.environ.get("FCD_BENCH_BACKEND", "nccl"), init_method="env://")
-    local = local % max(torch.cuda.device_count(), 1)
+        # to rehearse N ranks sharing the GPUs of a smaller box (and for --dry-run)
+        backend = "gloo" if args.dry_run else os.environ.get("FCD_BENCH_BACKEND", "nccl")
+        dist.init_process_group(backend, init_method="env://")
+        assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
+    if args.dry_run:
+        seen = torch.zeros(world, dtype=torch.int64)
+        seen[rank] = rank + 1
+        if world > 1:
+            dist.all_reduce(seen)
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_seen": seen.tolist()}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    from pyfcd import _lib
+    from pyfcd.dist import gather_stack, max_over_ranks
+    from bench_data import make_frames_torch, SQUARE_SIZE
+    ndev = torch.cuda.device_count()
+    if world > 1 and ndev < world and os.environ.get("FCD_BENCH_BACKEND", "nccl") == "nccl":
+        raise SystemExit(f"bench.py: {world} ranks over RCCL need {world} GPUs, {ndev} visible")
+    local = local % max(ndev, 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     n, B = args.size, args.batch
@@ -193,13 +223,19 @@ def main():
 
     gather_ms = None
     if args.gather and world > 1:
+        # heights of every rank's last step to rank 0 (one grouped send/recv batch);
+        # a first untimed gather sets up the point-to-point channels
+        stacked = gather_stack(heights, B * world)
+        del stacked
         torch.cuda.synchronize(dev)
         dist.barrier()
         g0 = time.perf_counter()
-        gather_stack(heights, B * world)
+        stacked = gather_stack(heights, B * world)
         torch.cuda.synchronize(dev)
-        dist.barrier()
         gather_ms = max_over_ranks((time.perf_counter() - g0) * 1e3, device=dev)
+        if rank == 0:  # rank 0's own shard sits first in the stack
+            assert torch.equal(stacked[:B], heights)
+        del stacked
 
     if rank != 0:
         if world > 1:
@@ -262,7 +298,11 @@ def main():
         "event_ms_per_step": round(ev0.elapsed_time(ev1) / args.steps, 3),
     }
     if gather_ms is not None:
-        out["gather_ms"] = round(gather_ms, 3)
+        gb = 4.0 * n * n * B * (world - 1) / 1e9
+        out["gather"] = {"ms": round(gather_ms, 3), "bytes_to_root_GB": round(gb, 3),
+                         "GB_per_s_into_root": round(gb / (gather_ms * 1e-3), 1),
+                         "how": "dist.batch_isend_irecv: every rank's last-step heights to rank 0, all links at once; "
+                                "not inside the frames/s"}
     if world == 1 and not args.no_cpu_baseline:
         log("CPU baseline (oracle, 1 core, then all cores)")
         single = cpu_baseline(n, args.cpu_frames)

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define FCD_ABI_VERSION 5
+#define FCD_ABI_VERSION 6
 
 enum {
     FCD_OK = 0,
@@ -87,6 +87,17 @@ int fcd_synchronize(fcd_ctx* ctx);
  * inside it, fcd.compute_calibration_factor (fcd.py:72-101), fourier.find_peaks
  * (fourier.py:7-41) and Carrier.__init__ (carriers.py:10-24).  Synchronises. */
 int fcd_set_reference(fcd_ctx* ctx, const float* reference, int flags, double square_size, fcd_ref_info* info);
+
+/* Replaces Carrier(reference_image, calibration_factor, peak, peak_radius)
+ * (carriers.py:10-24) for both carriers at once, with caller-chosen geometry
+ * instead of fourier.find_peaks: peaks int64 [2][2] fftshifted (row, col),
+ * radius double [2] (each carrier's own disk), the calibration factor of
+ * Carrier.frequencies (carriers.py:12).  Carrier q's ccsgn comes from image
+ * ref_q (ref1 may equal ref0 or be NULL: the same image).  Afterwards
+ * fcd_process / fcd_phases_from_spectrum demodulate against these carriers and
+ * info reports them (n_blobs = 0, threshold = 0).  Synchronises. */
+int fcd_set_carriers(fcd_ctx* ctx, const float* ref0, const float* ref1, int flags, double calibration_factor,
+                     const int64_t* peaks, const double* radius, fcd_ref_info* info);
 
 /* fourier.find_peaks (fourier.py:7-41) + fcd.compute_calibration_factor
  * (fcd.py:72-101) for n images (many-reference workloads)

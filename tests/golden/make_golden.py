@@ -22,6 +22,15 @@ Fixtures (all under tests/golden/):
   ingest.npz         analyze.load_image decodes of every example picture (sha256 of the
                      float32 image), analyze.mask / center of camera frames, and the
                      analyze.folder loop body's height maps with and without the mask
+  bench_board.npz    the benchmarked c2 board (bench_data.py: pattern.py geometry, 1024^2,
+                     unrotated and rotated 5 degrees): the reference's find_peaks picks,
+                     blobs, cf, radius, and compute_height_map of two warped frames
+  analyze_ref.npz    pydata/analyze.py ITSELF (imported with a placeholder `cv2` module
+                     whose every attribute access raises: cv2 is only used on the polar
+                     paths, analyze.py:237-241, 674-676, which are not run): analyze.mask /
+                     center on camera frames, analyze.folder on a directory of frames
+                     (with and without the mask), block_split / block_amplitude /
+                     spectrogram on synthetic float32 and float64 map folders
 """
 import os
 import sys
@@ -323,8 +332,165 @@ def make_ingest():
     print("ingest", len(files), "files; centers", centers, "cf", cf)
 
 
+def make_bench_board():
+    """Carrier picks of the reference on the exact board bench.py runs (configs[1]):
+    bench_data.checkerboard(1024) (pattern.py geometry, pattern.py:17-36), and the same
+    board rotated 5 degrees (SURVEY.md §8a parity fact 2)."""
+    import hashlib
+    sys.path.insert(0, os.path.dirname(os.path.dirname(OUT)))  # the repo root: bench_data.py (numpy only)
+    from bench_data import make_frames_numpy
+    out = {"versions": VERSIONS}
+    for tag, rot in (("flat", 0.0), ("rot5", 5.0)):
+        ref, frames = make_frames_numpy(1024, 2, seed=0, rotate_deg=rot)
+        sq = 0.001
+        locs, thr = peak_locations(ref)
+        image_fft = np.fft.fftshift(np.abs(fft2(ref - np.mean(ref))))
+        out[f"{tag}_blob_values"] = np.array([image_fft[p[0], p[1]] for p in locs], np.float32)
+        out[f"{tag}_blob_peaks"] = locs
+        out[f"{tag}_threshold"] = thr
+        out[f"{tag}_ref_sha"] = hashlib.sha256(ref.tobytes()).hexdigest()
+        out[f"{tag}_frames_sha"] = hashlib.sha256(frames.tobytes()).hexdigest()
+        for f in range(2):
+            r = run_pair(ref, frames[f], sq, height=1.0)
+            out[f"{tag}_height_sub{f}"] = r["height"][::4, ::4].astype(np.float32)
+            out[f"{tag}_height_stats{f}"] = stats(r["height"])
+            out[f"{tag}_wrapped_sub{f}"] = r["wrapped"][:, ::8, ::8]
+        for key in ("peaks", "cf", "radius", "freqs", "mask_count"):
+            out[f"{tag}_{key}"] = r[key]
+        print("bench_board", tag, r["peaks"].tolist(), locs.tolist(), out[f"{tag}_blob_values"].tolist(), r["cf"])
+    np.savez_compressed(os.path.join(OUT, "bench_board.npz"), **out)
+
+
+def import_reference_analyze():
+    """/root/reference/pydata/analyze.py, imported as the reference ships it.  Its module
+    top level does `import cv2` (analyze.py:21), absent here; cv2 is used only by the
+    polar paths (analyze.py:237-241, 674-676), which no fixture runs.  A placeholder
+    module stands in for the import and raises on any attribute access, so a fixture that
+    reached cv2 would fail instead of silently using a stand-in."""
+    import types
+
+    class _NoCv2(types.ModuleType):
+        def __getattr__(self, name):
+            raise RuntimeError(f"cv2.{name} used: the fixture reached a cv2 path of analyze.py")
+
+    sys.modules.setdefault("cv2", _NoCv2("cv2"))
+    import matplotlib
+    matplotlib.use("Agg")
+    from pydata.analyze import analyze  # reference, read-only
+    return analyze
+
+
+def synthetic_maps(T, n, dtype, seed):
+    """A map stack like analyze.folder's output: a standing oscillation at 5.2 Hz (500 Hz
+    sampling, block_amplitude's default `tasa`) and its second harmonic, plus noise;
+    some pixels are exactly 0 in the first map (the reference NaN-masks those)."""
+    rng = np.random.default_rng(seed)
+    t = np.arange(T) / 500.0
+    y, x = np.mgrid[0:n, 0:n] / n
+    a1 = 1e-3 * (1 + np.sin(2 * np.pi * x) * np.cos(np.pi * y))
+    a2 = 2e-4 * np.cos(3 * np.pi * x * y)
+    ph = 2 * np.pi * (x + 0.5 * y)
+    st = (a1[None] * np.cos(2 * np.pi * 5.2 * t[:, None, None] + ph[None])
+          + a2[None] * np.cos(2 * np.pi * 10.4 * t[:, None, None] - ph[None])
+          + 5e-5 * rng.standard_normal((T, n, n)))
+    st = st.astype(dtype)
+    holes = rng.random((n, n)) < 0.03
+    st[0][holes] = 0
+    return st
+
+
+def make_analyze_ref():
+    import shutil
+    import tempfile
+    analyze = import_reference_analyze()
+    out = {"versions": VERSIONS}
+    mask_dir = os.path.join(PICS, "mask")
+    mask_names = sorted(f for f in os.listdir(mask_dir) if f.endswith(".tif"))
+    # analyze.mask / center (analyze.py:43-140): full camera frames 4 and 5 (frame 4 is
+    # real_df.npz's frame 1; frame 5 is stored here), and 512^2 crops around the floater of
+    # frames 2, 5, 8 (stored), each with its own smoothing size
+    crop = (slice(150, 662), slice(380, 892))
+    out["frame5_u16"] = load_raw("mask/" + mask_names[5])
+    cases = [("full", 4, 15), ("full", 5, 14), ("crop", 2, 20), ("crop", 5, 15), ("crop", 8, 15)]
+    crops, mbits, cents = {}, [], []
+    for kind, idx, smoothed in cases:
+        raw = load_raw("mask/" + mask_names[idx])
+        if kind == "crop":
+            raw = np.ascontiguousarray(raw[crop])
+            crops[idx] = raw
+        m, c = analyze.mask(raw.astype(np.float32), smoothed=smoothed, find_center=True)
+        mbits.append(np.packbits(m))
+        cents.append(c)
+    out.update(mask_names=np.array(mask_names), mask_cases=np.array([(k, i, s) for k, i, s in cases]),
+               mask_bits=np.concatenate(mbits),
+               mask_bits_len=np.array([len(b) for b in mbits]), mask_centers=np.array(cents),
+               crop_rows=np.array([crop[0].start, crop[0].stop]), crop_cols=np.array([crop[1].start, crop[1].stop]))
+    for idx, raw in crops.items():
+        out[f"crop{idx}_u16"] = raw
+    # analyze.folder (analyze.py:143-286): real_df.npz's three frames plain, frames 4 + 5 masked
+    tmp = tempfile.mkdtemp(prefix="fcd_golden_")
+    try:
+        refp = os.path.join(PICS, "reference_df.tif")
+        runs = (("plain", None, ["prueba1_20250317_122608_C1S0001000001.tif", "mask/" + mask_names[4], "ellipse_10.tif"]),
+                ("masked", 15, ["mask/" + mask_names[4], "mask/" + mask_names[5]]))
+        for tag, smoothed, frames in runs:
+            ddir = os.path.join(tmp, "frames_" + tag)
+            os.makedirs(ddir)
+            for f in frames:
+                shutil.copy(os.path.join(PICS, f), os.path.join(ddir, os.path.basename(f)))
+            analyze.folder(refp, ddir, LAYERS, 0.002, smoothed=smoothed)
+            mdir = os.path.join(ddir, "maps")
+            names = sorted(f for f in os.listdir(mdir) if f.endswith("_map.npy"))
+            maps = [np.load(os.path.join(mdir, f)) for f in names]
+            out[f"folder_{tag}_frames"] = np.array([os.path.basename(f) for f in frames])
+            out[f"folder_{tag}_names"] = np.array(names)
+            out[f"folder_{tag}_h_sub"] = np.stack([m[::4, ::4] for m in maps])
+            out[f"folder_{tag}_h_stats"] = np.stack([stats(m) for m in maps])
+            out[f"folder_{tag}_zero_count"] = np.array([int((m == 0).sum()) for m in maps])
+            out[f"folder_{tag}_cf"] = np.load(os.path.join(mdir, "calibration_factor.npy"))
+            cp = os.path.join(mdir, "centers.txt")
+            out[f"folder_{tag}_centers_txt"] = open(cp).read() if os.path.exists(cp) else ""
+        # temporal post-analysis (analyze.py:365-641) on synthetic map folders
+        for dt in ("float32", "float64"):
+            T, n = (240, 32) if dt == "float32" else (150, 32)
+            st = synthetic_maps(T, n, np.dtype(dt), seed=11 if dt == "float32" else 12)
+            mdir = os.path.join(tmp, "maps_" + dt)
+            os.makedirs(mdir)
+            for t in range(T):
+                np.save(os.path.join(mdir, f"f{t:05d}_map.npy"), st[t])
+            np.save(os.path.join(mdir, "calibration_factor.npy"), np.array([0.001]))
+            out[f"{dt}_stack"] = st
+            bs = analyze.block_split(mdir, t_limit=T - 7, num_blocks=4, block_index=1)
+            out[f"{dt}_split"] = bs
+            for k, (mode, blk, zero) in enumerate(((3, 0, 0), (2, 3, 0), (1, 2, 1e-4))):
+                res = analyze.block_amplitude(mdir, mode=mode, num_blocks=4, block_index=blk, zero=zero)
+                harm, amps, phases, f0 = res
+                out[f"{dt}_amp{k}_args"] = np.array([mode, blk, zero])
+                out[f"{dt}_amp{k}_harm"] = np.array(harm, np.float64)
+                out[f"{dt}_amp{k}_amps"] = amps
+                out[f"{dt}_amp{k}_phases"] = phases
+                out[f"{dt}_amp{k}_f0"] = f0
+            f0_given = 5.0
+            harm, amps, phases, f0 = analyze.block_amplitude(mdir, f0=f0_given, mode=2, num_blocks=16, block_index=5)
+            out[f"{dt}_ampf_harm"] = np.array(harm, np.float64)
+            out[f"{dt}_ampf_amps"] = amps
+            out[f"{dt}_ampf_phases"] = phases
+            t_, f_, S_all, S_avg = analyze.spectrogram(map_folder=mdir, fs=125, nperseg=64, noverlap=32,
+                                                      num_blocks=4, block_index=0)
+            out[f"{dt}_spec_t"], out[f"{dt}_spec_f"] = t_, f_
+            out[f"{dt}_spec_all"], out[f"{dt}_spec_avg"] = S_all, S_avg
+            t_, f_, S = analyze.spectrogram(array=st[:, 5, 7], fs=125, nperseg=50, noverlap=10)
+            out[f"{dt}_spec1_t"], out[f"{dt}_spec1_f"], out[f"{dt}_spec1"] = t_, f_, S
+            print("analyze temporal", dt, [out[f"{dt}_amp{k}_f0"] for k in range(3)], S_all.shape)
+    finally:
+        shutil.rmtree(tmp)
+    np.savez_compressed(os.path.join(OUT, "analyze_ref.npz"), **out)
+    print("analyze_ref: centers", cents, "folder centers", repr(out["folder_masked_centers_txt"]))
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["real_pair", "real_df", "unwrap", "synthetic", "integrate", "val", "ingest"]
+    which = sys.argv[1:] or ["real_pair", "real_df", "unwrap", "synthetic", "integrate", "val", "ingest",
+                             "bench_board", "analyze_ref"]
     if "real_pair" in which:
         make_real_pair()
     if "real_df" in which:
@@ -339,3 +505,7 @@ if __name__ == "__main__":
         make_val()
     if "ingest" in which:
         make_ingest()
+    if "bench_board" in which:
+        make_bench_board()
+    if "analyze_ref" in which:
+        make_analyze_ref()

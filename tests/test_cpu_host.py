@@ -28,7 +28,7 @@ def test_library_exports_every_header_symbol():
     lib = _lib.load_library()
     for name in header_symbols():
         assert hasattr(lib, name), name
-    assert lib.fcd_abi_version() == 5
+    assert lib.fcd_abi_version() == 6
 
 
 def test_library_is_gfx950_code_object():
@@ -160,10 +160,14 @@ def _gloo_worker(rank, world, port, q):
         a, b = shard_range(total, rank, world)
         local = torch.arange(a, b, dtype=torch.float32)[:, None, None].expand(b - a, 2, 3).contiguous()
         out = gather_stack(local, total)
+        again = gather_stack(local, total)  # a second grouped batch on the same channels
         t = max_over_ranks(float(rank + 1))
         n = sum_over_ranks(float(b - a))
         if rank == 0:
+            assert torch.equal(out, again) and out.shape == (total, 2, 3)
             q.put((out[:, 0, 0].tolist(), t, n))
+        else:
+            assert out is None
     finally:
         dist.destroy_process_group()
 
@@ -187,3 +191,28 @@ def test_gloo_two_rank_shard_gather():
     frames, tmax, total = res
     assert frames == [float(i) for i in range(7)]
     assert tmax == 2.0 and total == 7.0
+
+
+def test_bench_launches_its_own_ranks():
+    """`python bench.py --gpus 2` with no launcher around it starts two rank
+    processes itself (torch.distributed.run, 127.0.0.1) before any GPU call; each
+    rank sees WORLD_SIZE 2 (--dry-run: rendezvous over gloo, then stop)."""
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=180, env=env, cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
+    out = json.loads(line)
+    assert out["n_gpus"] == 2 and out["ranks_seen"] == [1, 2]
+
+
+def test_bench_refuses_world_mismatch():
+    import subprocess
+    import sys
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=180, env=env, cwd="/tmp")
+    assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr

@@ -1,0 +1,57 @@
+"""The frame-sharded multi-rank path driving the engine: two rank
+processes share the box's one GPU (gloo for the process group, as the CPU tests;
+on an 8-GPU node the same code runs one rank per GPU over RCCL), each demodulates
+its contiguous shard of the batch, the heights are gathered to rank 0 with the
+grouped send/recv of pyfcd.dist.gather_stack, and rank 0 checks the stack
+bit-for-bit against one process running the whole batch (frames are independent,
+the reference state is deterministic)."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _rank(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "trapped-modes-ltg_amd")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import torch  # noqa: F401  (torch's HIP runtime first, conftest.py)
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from bench_data import make_frames_numpy
+        from pyfcd import _lib
+        from pyfcd.dist import gather_stack, shard_range
+        ref, frames = make_frames_numpy(256, 7, seed=2, rotate_deg=5.0)
+        a, b = shard_range(len(frames), rank, world)
+        eng = _lib.Engine(ref.shape, device=0)
+        eng.set_reference(ref, 0.001)
+        h, _, _ = eng.process(frames[a:b], 1.0, unwrap=True, want_phases=False)
+        out = gather_stack(torch.from_numpy(h), len(frames))
+        if rank == 0:
+            full, _, _ = eng.process(frames, 1.0, unwrap=True, want_phases=False)
+            q.put(bool(np.array_equal(out.numpy(), full)))
+        eng.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_ranks_shard_and_gather_equal_one_process():
+    import multiprocessing as mp
+    from pyfcd.dist import free_port
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    ok = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert ok

@@ -542,6 +542,64 @@ std::vector<Blob> label_candidates_host(int H, int W, const std::vector<int>& id
     return blobs;
 }
 
+// Carrier geometry of both carriers (Carrier.__init__, carriers.py:10-20): peak
+// pixels (fftshifted row, col), calibration factor, physical wavenumbers
+// (pixel_to_wavenumber, carriers.py:12) and the disk band-pass raster per carrier
+// with its own radius (skimage.draw.disk: strict < 1 in f64, clipped to the image,
+// carriers.py:17-20).  Sets c->info's geometry fields and c->disk_rows_host.
+void carrier_geometry(fcd_ctx* c, const long prow[2], const long pcol[2], double cf, const double R[2]) {
+    const int H = c->H, W = c->W;
+    fcd_ref_info& info = c->info;
+    for (int q = 0; q < 2; ++q) {
+        info.peaks[q][0] = prow[q];
+        info.peaks[q][1] = pcol[q];
+    }
+    info.calibration_factor = cf;
+    info.radius = R[0];
+    const std::vector<double> krc = wavenumber(H, cf, true), kcc = wavenumber(W, cf, true);
+    for (int q = 0; q < 2; ++q) {
+        info.frequencies[q][0] = krc[info.peaks[q][0]];
+        info.frequencies[q][1] = kcc[info.peaks[q][1]];
+    }
+    // disk raster (skimage.draw.disk -> ellipse, rotation 0), per shifted column the row range
+    c->disk_rows_host.assign((size_t)4 * W, 0);
+    for (int q = 0; q < 2; ++q) {
+        const double Rq = R[q];
+        int* rows = c->disk_rows_host.data() + (size_t)q * 2 * W;
+        for (int j = 0; j < W; ++j) {
+            rows[2 * j] = 1;
+            rows[2 * j + 1] = 0;
+        }
+        const long pr = info.peaks[q][0], pc = info.peaks[q][1];
+        const long lo_r = std::max<long>((long)std::ceil((double)pr - Rq), 0);
+        const long hi_r = std::min<long>((long)std::floor((double)pr + Rq), H - 1);
+        const long lo_c = std::max<long>((long)std::ceil((double)pc - Rq), 0);
+        const long hi_c = std::min<long>((long)std::floor((double)pc + Rq), W - 1);
+        int count = 0;
+        for (long sc = lo_c; sc <= hi_c; ++sc) {
+            const double cc = (double)(sc - lo_c) - (double)(pc - lo_c);
+            const double cq = cc / Rq;
+            const double c2 = cq * cq;
+            int first = -1, last = -2;
+            for (long sr = lo_r; sr <= hi_r; ++sr) {
+                const double rr = (double)(sr - lo_r) - (double)(pr - lo_r);
+                const double rq = rr / Rq;
+                const double d = rq * rq + c2;
+                if (d < 1.0) {
+                    if (first < 0) first = (int)sr;
+                    last = (int)sr;
+                    ++count;
+                }
+            }
+            if (first >= 0) {
+                rows[2 * sc] = first;
+                rows[2 * sc + 1] = last;
+            }
+        }
+        info.mask_count[q] = count;
+    }
+}
+
 // The rest of fourier.find_peaks + compute_calibration_factor + the carrier disks
 // from the 4 dimmest blobs (fourier.py:38-39, fcd.py:53-101): sets c->info and
 // c->disk_rows_host.
@@ -582,62 +640,18 @@ void carriers_from_blobs(fcd_ctx* c, const std::vector<Blob>& blobs, float thr, 
     }
     info.threshold = thr;
     const int pk[2] = {blobs[ir].peak, blobs[ip].peak};
-    for (int q = 0; q < 2; ++q) {
-        info.peaks[q][0] = pk[q] / W;
-        info.peaks[q][1] = pk[q] % W;
-    }
+    const long prow[2] = {pk[0] / W, pk[1] / W}, pcol[2] = {pk[0] % W, pk[1] % W};
     // calibration factor (fcd.py:85-101): 2*sq / (2*pi / mean(|k_pix|))
-    const double ak[4] = {std::fabs(kr[pk[0] / W]), std::fabs(kc[pk[0] % W]), std::fabs(kr[pk[1] / W]),
-                          std::fabs(kc[pk[1] % W])};
+    const double ak[4] = {std::fabs(kr[prow[0]]), std::fabs(kc[pcol[0]]), std::fabs(kr[prow[1]]),
+                          std::fabs(kc[pcol[1]])};
     const double mean = (((ak[0] + ak[1]) + ak[2]) + ak[3]) / 4.0;
     const double pixel_wavelength = (2 * kPi) / mean;
     const double cf = (2 * square_size) / pixel_wavelength;
-    info.calibration_factor = cf;
-    const double dr = (double)(info.peaks[0][0] - info.peaks[1][0]);
-    const double dc = (double)(info.peaks[0][1] - info.peaks[1][1]);
-    info.radius = std::sqrt(dr * dr + dc * dc) / 2;
-    const std::vector<double> krc = wavenumber(H, cf, true), kcc = wavenumber(W, cf, true);
-    for (int q = 0; q < 2; ++q) {
-        info.frequencies[q][0] = krc[info.peaks[q][0]];
-        info.frequencies[q][1] = kcc[info.peaks[q][1]];
-    }
-    // disk raster (skimage.draw.disk -> ellipse, rotation 0), per shifted column the row range
-    c->disk_rows_host.assign((size_t)4 * W, 0);
-    const double R = info.radius;
-    for (int q = 0; q < 2; ++q) {
-        int* rows = c->disk_rows_host.data() + (size_t)q * 2 * W;
-        for (int j = 0; j < W; ++j) {
-            rows[2 * j] = 1;
-            rows[2 * j + 1] = 0;
-        }
-        const long pr = info.peaks[q][0], pc = info.peaks[q][1];
-        const long lo_r = std::max<long>((long)std::ceil((double)pr - R), 0);
-        const long hi_r = std::min<long>((long)std::floor((double)pr + R), H - 1);
-        const long lo_c = std::max<long>((long)std::ceil((double)pc - R), 0);
-        const long hi_c = std::min<long>((long)std::floor((double)pc + R), W - 1);
-        int count = 0;
-        for (long sc = lo_c; sc <= hi_c; ++sc) {
-            const double cc = (double)(sc - lo_c) - (double)(pc - lo_c);
-            const double cq = cc / R;
-            const double c2 = cq * cq;
-            int first = -1, last = -2;
-            for (long sr = lo_r; sr <= hi_r; ++sr) {
-                const double rr = (double)(sr - lo_r) - (double)(pr - lo_r);
-                const double rq = rr / R;
-                const double d = rq * rq + c2;
-                if (d < 1.0) {
-                    if (first < 0) first = (int)sr;
-                    last = (int)sr;
-                    ++count;
-                }
-            }
-            if (first >= 0) {
-                rows[2 * sc] = first;
-                rows[2 * sc + 1] = last;
-            }
-        }
-        info.mask_count[q] = count;
-    }
+    const double dr = (double)(prow[0] - prow[1]);
+    const double dc = (double)(pcol[0] - pcol[1]);
+    const double radius = std::sqrt(dr * dr + dc * dc) / 2;  // fcd.py:68
+    const double R[2] = {radius, radius};
+    carrier_geometry(c, prow, pcol, cf, R);
 }
 
 // Band-pruned demodulation tables: which unshifted columns each carrier disk
@@ -782,6 +796,61 @@ void band_reference(fcd_ctx* c, const float* dref, hipStream_t s) {
     fcdk::band_phase(c->W, c->band_B, true, c->Ab.as<float2>(), c->H, 1, c->NCA, c->NCc[0], c->NCc[1], nullptr,
                      c->theta_b.as<float>(), c->band_pre.as<float2>(), c->band_ptw.as<float2>(), s);
     fcdk::band_theta_lanes(c->W, c->band_B, c->theta_b.as<float>(), 2 * c->H, c->theta_p.as<float>(), s);
+}
+
+// Everything the per-frame path needs from the reference once c->info and
+// c->disk_rows_host hold the carrier geometry: the disk tables, the band-pruned
+// demodulation tables, and per carrier q the reference signal ifft2(fft2(ref_q) *
+// mask_q) (Carrier._ccsgn, carriers.py:22-24, kept as its angle theta and as the
+// band kernels' theta_b / theta_p).  Carrier q's signal comes from image dref[q]
+// (both usually the same reference; distinct Carrier objects may carry distinct
+// ones).  Synchronises.
+void reference_state(fcd_ctx* c, const float* dref0, const float* dref1, hipStream_t s) {
+    const long hw = c->hw();
+    c->disk_rows.ensure(c->disk_rows_host.size() * sizeof(int));
+    upload(c->disk_rows.p, c->disk_rows_host.data(), c->disk_rows_host.size() * sizeof(int), s);
+    build_demod_tables(c, s);
+    c->refsig.ensure(2 * hw * sizeof(float2));
+    c->theta.ensure(2 * hw * sizeof(float));
+    float2* F = c->spec.as<float2>();
+    const float* drefs[2] = {dref0, dref1};
+    const int passes = dref1 == dref0 ? 1 : 2;
+    DevBuf keep;  // carrier 0's planes from pass 0 (theta, theta_p, refsig) when the images differ
+    for (int pass = 0; pass < passes; ++pass) {
+        const float* dref = drefs[pass];
+        band_reference(c, dref, s);
+        fft2_real(c, dref, F, 1, 0.f, s);
+        for (int q = 0; q < 2; ++q) {
+            float2* R = c->refsig.as<float2>() + q * hw;
+            fcdk::DiskTable t{c->disk_rows.as<int>() + (size_t)q * 2 * c->W};
+            fcdk::disk_mask(F, R, 1, c->H, c->W, t, s);
+            fcdk::col_fft(c->H, c->W, true, R, 1, c->tw_col.as<float2>(), s);
+            fcdk::row_fft(c->W, true, fcdk::ROW_IN_COMPLEX, fcdk::ROW_OUT_COMPLEX, R, R, c->H, c->H, 0.f,
+                          c->tw_row.as<float2>(), nullptr, s);
+            fcdk::angle(R, c->theta.as<float>() + q * hw, hw, s);
+        }
+        const size_t tb = (size_t)hw * sizeof(float), rb = (size_t)hw * sizeof(float2);
+        const bool band = c->band_B != 0;
+        if (passes == 2 && pass == 0) {
+            keep.ensure(2 * tb + rb + (band ? 2 * tb : 0));
+            char* k = static_cast<char*>(keep.p);
+            HIPCHK(hipMemcpyAsync(k, c->theta.p, tb, hipMemcpyDeviceToDevice, s));
+            HIPCHK(hipMemcpyAsync(k + tb, c->refsig.p, rb, hipMemcpyDeviceToDevice, s));
+            if (band) {
+                HIPCHK(hipMemcpyAsync(k + tb + rb, c->theta_b.p, tb, hipMemcpyDeviceToDevice, s));
+                HIPCHK(hipMemcpyAsync(k + 2 * tb + rb, c->theta_p.p, tb, hipMemcpyDeviceToDevice, s));
+            }
+        } else if (passes == 2) {
+            const char* k = static_cast<const char*>(keep.p);
+            HIPCHK(hipMemcpyAsync(c->theta.p, k, tb, hipMemcpyDeviceToDevice, s));
+            HIPCHK(hipMemcpyAsync(c->refsig.p, k + tb, rb, hipMemcpyDeviceToDevice, s));
+            if (band) {
+                HIPCHK(hipMemcpyAsync(c->theta_b.p, k + tb + rb, tb, hipMemcpyDeviceToDevice, s));
+                HIPCHK(hipMemcpyAsync(c->theta_p.p, k + 2 * tb + rb, tb, hipMemcpyDeviceToDevice, s));
+            }
+        }
+    }
+    HIPCHK(hipStreamSynchronize(s));
 }
 
 // fourier.find_peaks + compute_calibration_factor + the carrier disks for nb
@@ -952,25 +1021,48 @@ FCD_API int fcd_set_reference(fcd_ctx* c, const float* reference, int flags, dou
             dref = c->frames_in.as<float>();
         }
         find_peaks_batch(c, dref, 1, square_size, nullptr, s);
-        float2* F = c->spec.as<float2>();
-        c->disk_rows.ensure(c->disk_rows_host.size() * sizeof(int));
-        upload(c->disk_rows.p, c->disk_rows_host.data(), c->disk_rows_host.size() * sizeof(int), s);
-        build_demod_tables(c, s);
-        band_reference(c, dref, s);
-        // Carrier.ccsgn = conj(ifft2(fft2(ref) * mask))  (carriers.py:22-24); we keep its angle.
-        fft2_real(c, dref, F, 1, 0.f, s);
-        c->refsig.ensure(2 * hw * sizeof(float2));
-        c->theta.ensure(2 * hw * sizeof(float));
+        reference_state(c, dref, dref, s);
+        c->has_ref = true;
+        if (info) *info = c->info;
+    })
+}
+
+FCD_API int fcd_set_carriers(fcd_ctx* c, const float* ref0, const float* ref1, int flags, double calibration_factor,
+                             const int64_t* peaks, const double* radius, fcd_ref_info* info) {
+    FCD_TRY({
+        check_ctx(c);
+        if (!ref0 || !peaks || !radius) throw FcdError(FCD_E_INVALID, "null argument");
+        if (!ref1) ref1 = ref0;
+        if (!std::isfinite(calibration_factor) || calibration_factor == 0.0)
+            throw FcdError(FCD_E_INVALID, "calibration factor must be finite and non-zero");
+        long prow[2], pcol[2];
+        double R[2];
         for (int q = 0; q < 2; ++q) {
-            float2* R = c->refsig.as<float2>() + q * hw;
-            fcdk::DiskTable t{c->disk_rows.as<int>() + (size_t)q * 2 * c->W};
-            fcdk::disk_mask(F, R, 1, c->H, c->W, t, s);
-            fcdk::col_fft(c->H, c->W, true, R, 1, c->tw_col.as<float2>(), s);
-            fcdk::row_fft(c->W, true, fcdk::ROW_IN_COMPLEX, fcdk::ROW_OUT_COMPLEX, R, R, c->H, c->H, 0.f,
-                          c->tw_row.as<float2>(), nullptr, s);
-            fcdk::angle(R, c->theta.as<float>() + q * hw, hw, s);
+            prow[q] = (long)peaks[2 * q];
+            pcol[q] = (long)peaks[2 * q + 1];
+            R[q] = radius[q];
+            if (prow[q] < 0 || prow[q] >= c->H || pcol[q] < 0 || pcol[q] >= c->W)
+                throw FcdError(FCD_E_INVALID, "carrier peak outside the image");
+            if (!(R[q] > 0.0) || !std::isfinite(R[q])) throw FcdError(FCD_E_INVALID, "carrier radius must be > 0");
         }
-        HIPCHK(hipStreamSynchronize(s));
+        hipStream_t s = c->own;
+        const long hw = c->hw();
+        c->has_ref = false;
+        const float* d0 = ref0;
+        const float* d1 = ref1;
+        if (flags != FCD_DEVICE_PTRS) {
+            const bool two = ref1 != ref0;
+            c->frames_in.ensure((two ? 2 : 1) * hw * sizeof(float));
+            upload(c->frames_in.p, ref0, hw * sizeof(float), s);
+            d0 = d1 = c->frames_in.as<float>();
+            if (two) {
+                upload(c->frames_in.as<float>() + hw, ref1, hw * sizeof(float), s);
+                d1 = c->frames_in.as<float>() + hw;
+            }
+        }
+        std::memset(&c->info, 0, sizeof(c->info));
+        carrier_geometry(c, prow, pcol, calibration_factor, R);
+        reference_state(c, d0, d1, s);
         c->has_ref = true;
         if (info) *info = c->info;
     })

@@ -215,9 +215,13 @@ class analyze:
 
     @classmethod
     def _block_stack(cls, map_folder, t_limit=None, num_blocks=64, block_index=0, zero=0):
-        """float32 [T, size, size] block of every map (memory-mapped reads of just the
-        block), NaN where the first map is 0 (analyze.py:386-417; `- zero` as
-        analyze.py:557-567)."""
+        """[T, size, size] block of every map (memory-mapped reads of just the block), NaN
+        where the first map is 0 (analyze.py:386-417; `- zero` as analyze.py:557-567), in
+        the dtype the reference's arithmetic gives: the maps' own float dtype (float32
+        from analyze.folder, float64 kept float64), promoted by an array `zero` the way
+        numpy promotes `m - zero` (a scalar `zero` does not promote, numpy 1.x value-based
+        casting as in the reference's environment); non-float maps become float64 (the
+        NaN fill)."""
         files = cls._map_files(map_folder, t_limit)
         first = np.load(os.path.join(map_folder, files[0]), mmap_mode="r")
         H, W = first.shape
@@ -226,9 +230,13 @@ class analyze:
         i0, j0 = (block_index // per_row) * n, (block_index % per_row) * n
         valid = np.asarray(first[i0:i0 + n, j0:j0 + n]) != 0
         z = zero
+        dt = first.dtype if np.issubdtype(first.dtype, np.floating) else np.dtype(np.float64)
         if np.ndim(zero) == 2:
             z = np.asarray(zero)[i0:i0 + n, j0:j0 + n]
-        out = np.empty((len(files), n, n), np.float32)
+            dt = np.result_type(dt, z.dtype)
+            if not np.issubdtype(dt, np.floating):
+                dt = np.dtype(np.float64)
+        out = np.empty((len(files), n, n), dt)
         for t, f in enumerate(files):
             m = np.load(os.path.join(map_folder, f), mmap_mode="r")[i0:i0 + n, j0:j0 + n]
             out[t] = np.where(valid, np.asarray(m) - z, np.nan)
@@ -236,7 +244,7 @@ class analyze:
 
     @classmethod
     def block_split(cls, map_folder, t_limit=None, num_blocks=64, block_index=0):
-        """[size, size, T] float32 series of one spatial block (analyze.py:364-417)."""
+        """[size, size, T] series of one spatial block (analyze.py:364-417)."""
         return np.transpose(cls._block_stack(map_folder, t_limit, num_blocks, block_index), (1, 2, 0))
 
     @classmethod

@@ -29,10 +29,10 @@ FCD_FMT_U8 = 1
 FCD_FMT_U16 = 2
 FCD_FMT_P10 = 3
 
-# Every symbol include/fcd.h declares (checked by tests/test_abi.py).
+# Every symbol include/fcd.h declares (checked by tests/test_cpu_host.py::test_header_lists_bound_symbols).
 EXPORTED = (
     "fcd_abi_version", "fcd_last_error", "fcd_create", "fcd_destroy", "fcd_synchronize",
-    "fcd_set_reference", "fcd_get_carriers", "fcd_process", "fcd_phases_from_spectrum",
+    "fcd_set_reference", "fcd_set_carriers", "fcd_get_carriers", "fcd_process", "fcd_phases_from_spectrum",
     "fcd_unwrap", "fcd_integrate", "fcd_fft2", "fcd_profile", "fcd_stage_times",
     "fcd_process_raw", "fcd_frame_bytes", "fcd_host_alloc", "fcd_host_free", "fcd_find_peaks",
     "fcd_temporal_spectrum", "fcd_temporal_bins", "fcd_spectrogram",
@@ -81,6 +81,7 @@ def load_library(path=None):
             "fcd_destroy": ([vp], i32),
             "fcd_synchronize": ([vp], i32),
             "fcd_set_reference": ([vp, vp, i32, f64, ctypes.POINTER(FcdRefInfo)], i32),
+            "fcd_set_carriers": ([vp, vp, vp, i32, f64, vp, vp, ctypes.POINTER(FcdRefInfo)], i32),
             "fcd_get_carriers": ([vp, vp, vp], i32),
             "fcd_process": ([vp, vp, i32, i32, f64, i32, vp, vp, vp, vp], i32),
             "fcd_phases_from_spectrum": ([vp, vp, i32, i32, i32, vp, vp, vp], i32),
@@ -120,6 +121,17 @@ def _ptr(a):
     return None if a is None else a.ctypes.data
 
 
+def _peaks_of(info):
+    return tuple((int(info.peaks[q][0]), int(info.peaks[q][1])) for q in range(2))
+
+
+def _same_image(a, b):
+    if a is b:
+        return True
+    a = np.asarray(a)
+    return a.shape == b.shape and np.array_equal(_f32(a), b)
+
+
 class Engine:
     """One engine context: a device, a frame shape, and (once set) a reference."""
 
@@ -136,6 +148,10 @@ class Engine:
         self.info = None
         self.ref_copy = None
         self.ref_square_size = None
+        # what the context's carriers were built from, whichever call set them:
+        # (image of carrier 0, image of carrier 1, ((r0, c0), (r1, c1)), (radius0, radius1))
+        self.geometry = None
+        self.explicit = False  # set by set_carriers (not by a find_peaks reference)
 
     def close(self):
         if getattr(self, "_h", None):
@@ -162,12 +178,50 @@ class Engine:
         # cached one first so the next call with the old reference re-uploads it
         self.ref_copy = None
         self.ref_square_size = None
+        self.geometry = None
         _check(self._lib.fcd_set_reference(self._h, ref.ctypes.data, FCD_HOST_PTRS, float(square_size),
                                            ctypes.byref(info)))
         self.info = info
         self.ref_copy = ref.copy()
         self.ref_square_size = float(square_size)
+        self.explicit = False
+        self.geometry = (self.ref_copy, self.ref_copy, _peaks_of(info), (info.radius, info.radius))
         return info
+
+    def set_carriers(self, ref0, ref1, calibration_factor, peaks, radii):
+        """fcd_set_carriers: both carriers from caller-given geometry (Carrier.__init__,
+        carriers.py:10-24): peaks ((row, col), (row, col)) fftshifted, one radius per
+        carrier, carrier q's ccsgn from image ref_q."""
+        r0 = _f32(ref0)
+        r1 = r0 if ref1 is None or ref1 is ref0 else _f32(ref1)
+        for r in (r0, r1):
+            if r.shape != self.shape:
+                raise ValueError(f"reference shape {r.shape} != engine shape {self.shape}")
+        pk = np.ascontiguousarray(np.asarray(peaks, dtype=np.int64).reshape(2, 2))
+        rad = np.ascontiguousarray(np.asarray(radii, dtype=np.float64).reshape(2))
+        info = FcdRefInfo()
+        self.ref_copy = None
+        self.ref_square_size = None
+        self.geometry = None
+        _check(self._lib.fcd_set_carriers(self._h, r0.ctypes.data, None if r1 is r0 else r1.ctypes.data,
+                                          FCD_HOST_PTRS, float(calibration_factor), pk.ctypes.data, rad.ctypes.data,
+                                          ctypes.byref(info)))
+        self.info = info
+        self.explicit = True
+        c0 = r0.copy()
+        c1 = c0 if r1 is r0 else r1.copy()
+        self.geometry = (c0, c1, _peaks_of(info), (float(rad[0]), float(rad[1])))
+        return info
+
+    def holds_carriers(self, ref0, ref1, peaks, radii):
+        """True if the context's carriers were built from these images and this geometry."""
+        if self.geometry is None:
+            return False
+        g0, g1, gp, gr = self.geometry
+        pk = tuple(tuple(int(v) for v in p) for p in peaks)
+        if pk != gp or tuple(float(r) for r in radii) != gr:
+            return False
+        return _same_image(ref0, g0) and _same_image(ref1, g1)
 
     def find_peaks(self, images, square_size=1.0):
         """fcd_find_peaks: FcdRefInfo per image of a [n, H, W] (or [H, W]) stack, the
@@ -183,7 +237,7 @@ class Engine:
         return [infos[i] for i in range(len(imgs))]
 
     def matches(self, reference, square_size):
-        if self.ref_copy is None or self.ref_square_size != float(square_size):
+        if self.explicit or self.ref_copy is None or self.ref_square_size != float(square_size):
             return False
         ref = np.asarray(reference)
         return ref.shape == self.ref_copy.shape and np.array_equal(_f32(ref), self.ref_copy)

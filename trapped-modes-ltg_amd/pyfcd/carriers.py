@@ -1,9 +1,12 @@
 """Carrier description — drop-in for /root/reference/pyfcd/carriers.py.
 
-A `Carrier` is built by the engine from its device-side reference state: the
-peak pixel, its physical wavenumber, the band-pass disk radius, the
-ifftshifted disk mask (skimage.draw.disk raster) and ccsgn =
-conj(ifft2(fft2(reference) * mask)), all computed on the MI355X.
+A `Carrier` holds what the reference's does (carriers.py:9-24): the peak pixel,
+its physical wavenumber, the band-pass disk radius, the ifftshifted disk mask
+(skimage.draw.disk raster) and ccsgn = conj(ifft2(fft2(reference) * mask)), the
+arrays computed on the MI355X.  It is a self-contained value, as in the
+reference: it also keeps the reference image and the geometry it was built
+from, so fcd.compute_phases can rebuild the engine's carrier state from the
+carriers it is handed when the engine has since moved on to another reference.
 """
 import numpy as np
 
@@ -13,24 +16,30 @@ from . import _lib
 class Carrier:
     """One demodulation carrier (carriers.py:9-24).
 
-    Construct it like the reference (reference image, calibration factor, peak,
-    radius); the arrays come from the engine that holds this reference.
+    `Carrier(reference_image, calibration_factor, peak, peak_radius)` works as in
+    the reference (carriers.py:10-15): the engine builds the disk and ccsgn for
+    this peak and radius (fcd_set_carriers).  fcd.compute_carriers builds both
+    carriers from one device pass instead (`_state`).
     """
 
-    def __init__(self, reference_image, calibration_factor, peak, peak_radius, _index=None, _engine=None):
-        ref = np.asarray(reference_image)
-        self.pixels = np.asarray(peak)
-        self.radius = peak_radius
+    def __init__(self, reference_image, calibration_factor, peak, peak_radius, _state=None):
         from .fourier import fourier
-        self.frequencies = fourier.pixel_to_wavenumber(ref.shape, self.pixels, calibration_factor)
-        eng = _engine
-        if eng is None:
-            raise TypeError("Carrier objects are created by fcd.compute_carriers on the MI355X engine")
-        cc, masks = eng.carriers_arrays()
-        i = _index
-        if i is None:
-            raise TypeError("Carrier index missing")
-        self.mask = masks[i]
-        self.ccsgn = cc[i]
-        self._engine = eng
-        self._index = i
+        ref = np.asarray(reference_image)
+        self.pixels = peak
+        self.frequencies = fourier.pixel_to_wavenumber(ref.shape, peak, calibration_factor)
+        self.radius = peak_radius
+        if _state is None:
+            if ref.ndim != 2:
+                raise ValueError("reference_image must be a 2-D image")
+            eng = _lib.engine_for(ref.shape)
+            p = (int(peak[0]), int(peak[1]))
+            eng.set_carriers(ref, None, calibration_factor, (p, p), (peak_radius, peak_radius))
+            cc, masks = eng.carriers_arrays()
+            index, ref_f32 = 0, eng.geometry[0]
+        else:
+            cc, masks, index, ref_f32 = _state
+        self.mask = masks[index]
+        self.ccsgn = cc[index]
+        # identity of the carrier for fcd.compute_phases (float32, as the engine saw it)
+        self._reference = ref_f32
+        self._calibration_factor = float(calibration_factor)

@@ -49,12 +49,38 @@ def sum_over_ranks(value, device=None):
     return float(t.item())
 
 
+def free_port():
+    """An unused TCP port on 127.0.0.1 for the rendezvous."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(nproc, script, argv, env=None):
+    """Run `script argv` as `nproc` rank processes (one per GPU) under
+    torch.distributed.run on this node, rendezvous on 127.0.0.1, and return the
+    launcher's exit code.
+
+    Called by a parent that has not touched the GPU (no HIP call, no
+    torch.cuda.is_available()): the ranks are child processes, the parent only
+    waits for them, so nothing is exec'd over a process holding a GPU context."""
+    import subprocess
+    import sys
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", script] + list(argv)
+    e = dict(os.environ if env is None else env)
+    e.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on these hosts (RCCL)
+    return subprocess.call(cmd, env=e)
+
+
 def gather_stack(local, total_frames):
     """Gather every rank's [b_r, H, W] shard into rank 0's [total, H, W] tensor.
 
-    Uses point-to-point send/recv (RCCL on GPU tensors, gloo on CPU tensors):
-    each non-root rank sends its shard once, the root receives the shards in
-    rank order; on xGMI every sender has its own link to the root.
+    One batch of point-to-point operations (dist.batch_isend_irecv: a grouped
+    ncclSend/ncclRecv on RCCL): every non-root rank posts its
+    send and the root posts all its receives at once, so on xGMI the shards
+    arrive over the root's links in parallel instead of one sender at a time.
     Returns the stacked tensor on rank 0, None elsewhere.
     """
     import torch
@@ -62,14 +88,21 @@ def gather_stack(local, total_frames):
     if not (dist.is_available() and dist.is_initialized()):
         return local
     rank, world = dist.get_rank(), dist.get_world_size()
+    a0, b0 = shard_range(total_frames, rank, world)
+    if local.shape[0] != b0 - a0:
+        raise ValueError(f"rank {rank}: shard of {local.shape[0]} frames, expected {b0 - a0}")
     if rank != 0:
-        dist.send(local.contiguous(), dst=0)
-        return None
-    out = torch.empty((total_frames,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
-    for r in range(world):
-        a, b = shard_range(total_frames, r, world)
-        if r == 0:
-            out[a:b].copy_(local)
-        elif b > a:
-            dist.recv(out[a:b], src=r)
+        ops = [dist.P2POp(dist.isend, local.contiguous(), 0)] if b0 > a0 else []
+        out = None
+    else:
+        out = torch.empty((total_frames,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+        out[a0:b0].copy_(local)
+        ops = []
+        for r in range(1, world):
+            a, b = shard_range(total_frames, r, world)
+            if b > a:
+                ops.append(dist.P2POp(dist.irecv, out[a:b], r))
+    if ops:
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
     return out

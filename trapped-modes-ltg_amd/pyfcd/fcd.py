@@ -36,8 +36,9 @@ def _engine_with_reference(reference, square_size):
 def _carriers_from_engine(eng, reference):
     info = eng.info
     cf = info.calibration_factor
-    carriers = [Carrier(reference, cf, np.array([info.peaks[i][0], info.peaks[i][1]]), info.radius, _index=i,
-                        _engine=eng) for i in range(2)]
+    cc, masks = eng.carriers_arrays()
+    carriers = [Carrier(reference, cf, np.array([info.peaks[i][0], info.peaks[i][1]]), info.radius,
+                        _state=(cc, masks, i, eng.ref_copy)) for i in range(2)]
     return carriers, cf
 
 
@@ -143,11 +144,24 @@ class fcd:
 
     @classmethod
     def compute_phases(cls, displaced_fft, carriers, unwrap=True):
-        """Phase maps [2, H, W] float64 from an unshifted spectrum (fcd.py:103-120), on the device."""
-        eng = getattr(carriers[0], "_engine", None)
-        if eng is None:
-            raise TypeError("carriers must come from fcd.compute_carriers")
-        wrapped, k = eng.phases_from_spectrum(displaced_fft, unwrap=unwrap)
+        """Phase maps [2, H, W] float64 from an unshifted spectrum (fcd.py:103-120), on the device.
+
+        Demodulates against the carriers it is given, as the reference does: if the
+        engine's carrier state was built from other carriers (another reference set
+        since, or hand-made Carrier objects), it is rebuilt from these carriers'
+        images and geometry first (fcd_set_carriers)."""
+        if len(carriers) != 2:
+            raise ValueError("compute_phases takes the two carriers of fcd.compute_carriers")
+        c0, c1 = carriers[0], carriers[1]
+        if not all(hasattr(c, "_reference") for c in (c0, c1)):
+            raise TypeError("carriers must be pyfcd.carriers.Carrier objects")
+        spec = np.asarray(displaced_fft)
+        eng = _lib.engine_for(spec.shape[-2:])
+        peaks = [(int(c.pixels[0]), int(c.pixels[1])) for c in (c0, c1)]
+        radii = (float(c0.radius), float(c1.radius))
+        if not eng.holds_carriers(c0._reference, c1._reference, peaks, radii):
+            eng.set_carriers(c0._reference, c1._reference, c0._calibration_factor, peaks, radii)
+        wrapped, k = eng.phases_from_spectrum(spec, unwrap=unwrap)
         phases = wrapped[0].astype(np.float64)
         if unwrap:
             phases += TWOPI * k[0]
