@@ -43,3 +43,19 @@ def same_up_to_constant(a, b):
     """k-fields equal up to one global integer (the unwrap's anchor)."""
     d = np.asarray(a, np.int64) - np.asarray(b, np.int64)
     return d - d.flat[0]
+
+
+def spectrum_images(golden):
+    """(fixture, {name: float32 image}) of tests/golden/spectrum.npz (make_golden.py
+    spectrum_images): the c2 board flat and rotated, the example references, stored
+    integer-valued images of other shapes."""
+    from bench_data import checkerboard
+    g = golden("spectrum")
+    imgs = {"board_flat": checkerboard(1024), "board_rot5": checkerboard(1024, 5.0),
+            "reference_2": golden("real_pair")["ref_u8"].astype(np.float32),
+            "reference_df": golden("real_df")["ref_u16"].astype(np.float32)}
+    for name in g["names"]:
+        name = str(name)
+        if name.startswith("rand_"):
+            imgs[name] = g[name + "_u16"].astype(np.float32) * np.float32(0.37)
+    return g, imgs

@@ -22,6 +22,10 @@ Fixtures (all under tests/golden/):
   ingest.npz         analyze.load_image decodes of every example picture (sha256 of the
                      float32 image), analyze.mask / center of camera frames, and the
                      analyze.folder loop body's height maps with and without the mask
+  spectrum.npz       sha256 digests of scipy.fft.fft2, np.mean and the find_peaks spectrum
+                     |fftshift(fft2(image - mean))| (fourier.py:18) for float32 images of
+                     several shapes (the bit-exact restatement in oracle/pocketfft32.py and
+                     the engine's fcd_fft2 are checked against them)
   bench_board.npz    the benchmarked c2 board (bench_data.py: pattern.py geometry, 1024^2,
                      unrotated and rotated 5 degrees): the reference's find_peaks picks,
                      blobs, cf, radius, and compute_height_map of two warped frames
@@ -332,6 +336,46 @@ def make_ingest():
     print("ingest", len(files), "files; centers", centers, "cf", cf)
 
 
+def spectrum_images():
+    """name -> float32 image: the c2 board flat / rotated (bench_data.py), the two example
+    references, and seeded integer-valued images of other shapes (stored in the fixture)."""
+    import hashlib  # noqa: F401
+    sys.path.insert(0, os.path.dirname(os.path.dirname(OUT)))
+    from bench_data import checkerboard
+    rng = np.random.default_rng(2024)
+    imgs = {
+        "board_flat": checkerboard(1024),
+        "board_rot5": checkerboard(1024, 5.0),
+        "reference_2": load_raw("reference_2.png").astype(np.float32),
+        "reference_df": load_raw("reference_df.tif").astype(np.float32),
+    }
+    stored = {}
+    for (h, w) in ((64, 64), (128, 256), (256, 128), (2048, 64), (64, 4096)):
+        u = rng.integers(0, 1024, (h, w)).astype(np.uint16)
+        stored[f"rand_{h}x{w}"] = u
+        imgs[f"rand_{h}x{w}"] = u.astype(np.float32) * np.float32(0.37)
+    return imgs, stored
+
+
+def make_spectrum():
+    import hashlib
+    imgs, stored = spectrum_images()
+    out = {"versions": VERSIONS, "names": np.array(list(imgs))}
+    for name, img in imgs.items():
+        F = fft2(img)
+        assert F.dtype == np.complex64
+        m = np.mean(img)
+        spec = np.fft.fftshift(np.abs(fft2(img - m)))  # fourier.py:18
+        out[f"{name}_fft2_sha"] = hashlib.sha256(F.tobytes()).hexdigest()
+        out[f"{name}_mean"] = np.float32(m)
+        out[f"{name}_spec_sha"] = hashlib.sha256(spec.tobytes()).hexdigest()
+        out[f"{name}_fft2_corner"] = F[:4, :4]
+    for k, v in stored.items():
+        out[k + "_u16"] = v
+    np.savez_compressed(os.path.join(OUT, "spectrum.npz"), **out)
+    print("spectrum", list(imgs))
+
+
 def make_bench_board():
     """Carrier picks of the reference on the exact board bench.py runs (configs[1]):
     bench_data.checkerboard(1024) (pattern.py geometry, pattern.py:17-36), and the same
@@ -490,7 +534,7 @@ def make_analyze_ref():
 
 if __name__ == "__main__":
     which = sys.argv[1:] or ["real_pair", "real_df", "unwrap", "synthetic", "integrate", "val", "ingest",
-                             "bench_board", "analyze_ref"]
+                             "bench_board", "analyze_ref", "spectrum"]
     if "real_pair" in which:
         make_real_pair()
     if "real_df" in which:
@@ -509,3 +553,5 @@ if __name__ == "__main__":
         make_bench_board()
     if "analyze_ref" in which:
         make_analyze_ref()
+    if "spectrum" in which:
+        make_spectrum()

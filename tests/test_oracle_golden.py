@@ -134,3 +134,20 @@ def test_residue_counter_matches_definition():
         x = p - np.asarray(q, np.float64)
         return np.where(x > np.pi, -1, np.where(x < -np.pi, 1, 0))
     assert O.count_residues(w) == int(((fw(a, b) + fw(b, c) + fw(c, d) + fw(d, a)) != 0).sum())
+
+
+def test_pocketfft32_matches_scipy_digests(golden):
+    """oracle/pocketfft32.py restates scipy 1.7.1's float32 fft2, numpy 1.26.4's float32
+    mean and complex64 abs bit for bit: sha256 of every output equals the reference
+    interpreter's (fourier.py:18's spectrum included)."""
+    import hashlib
+    from conftest import spectrum_images
+    from oracle import pocketfft32 as P
+    g, imgs = spectrum_images(golden)
+    assert sorted(imgs) == sorted(str(n) for n in g["names"])
+    for name, img in imgs.items():
+        F = P.fft2(img)
+        assert hashlib.sha256(F.tobytes()).hexdigest() == str(g[f"{name}_fft2_sha"]), name
+        assert P.mean_f32(img) == g[f"{name}_mean"], name
+        spec = P.find_peaks_spectrum(img)
+        assert hashlib.sha256(spec.tobytes()).hexdigest() == str(g[f"{name}_spec_sha"]), name

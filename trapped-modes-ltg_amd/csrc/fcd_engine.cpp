@@ -78,6 +78,77 @@ std::vector<double> wavenumber(int n, double cf, bool shifted) {
     return k;
 }
 
+// scipy 1.7.1 pocketfft plans (kernels_pocketfft.hip; restated in oracle/pocketfft32.py):
+// rfftp factors 4, 4, ... with a single 2 moved to the front; cfftp 8s, then 4s, a single
+// 2 first; twiddles (cos, sin)(2 pi m / n) rounded to float (sincos_2pibyn<float>).
+std::pair<float, float> pf_twiddle(int n, long m) {
+    const double a = 2 * kPi * (double)m / (double)n;
+    return {(float)std::cos(a), (float)std::sin(a)};
+}
+
+std::vector<int> pf_factors(int n, bool real) {
+    std::vector<int> f;
+    int left = n;
+    if (!real)
+        while ((left & 7) == 0) {
+            f.push_back(8);
+            left >>= 3;
+        }
+    while ((left & 3) == 0) {
+        f.push_back(4);
+        left >>= 2;
+    }
+    if ((left & 1) == 0) {
+        left >>= 1;
+        f.push_back(2);
+        std::swap(f.front(), f.back());
+    }
+    if (left != 1 || f.size() > 8) throw std::runtime_error("pocketfft plan: unsupported length");
+    return f;
+}
+
+void pf_row_plan(int n, fcdk::PfPlan& p, std::vector<float>& tw) {  // rfftp::comp_twiddle
+    const std::vector<int> f = pf_factors(n, true);
+    p.nf = (int)f.size();
+    long l1 = 1;
+    for (int k = 0; k < p.nf; ++k) {
+        const int ip = f[k];
+        const long ido = n / (l1 * ip);
+        p.fct[k] = ip;
+        p.tw[k] = (int)tw.size();
+        const size_t len = (size_t)std::max<long>((ip - 1) * (ido - 1), 1);
+        tw.resize(tw.size() + len, 0.f);
+        if (k < p.nf - 1)
+            for (int j = 1; j < ip; ++j)
+                for (long i = 1; i <= (ido - 1) / 2; ++i) {
+                    const auto w = pf_twiddle(n, j * l1 * i);
+                    tw[p.tw[k] + (j - 1) * (ido - 1) + 2 * i - 2] = w.first;
+                    tw[p.tw[k] + (j - 1) * (ido - 1) + 2 * i - 1] = w.second;
+                }
+        l1 *= ip;
+    }
+}
+
+void pf_col_plan(int n, fcdk::PfPlan& p, std::vector<float2>& tw) {  // cfftp::comp_twiddle
+    const std::vector<int> f = pf_factors(n, false);
+    p.nf = (int)f.size();
+    long l1 = 1;
+    for (int k = 0; k < p.nf; ++k) {
+        const int ip = f[k];
+        const long ido = n / (l1 * ip);
+        p.fct[k] = ip;
+        p.tw[k] = (int)tw.size();
+        const size_t len = (size_t)std::max<long>((ip - 1) * (ido - 1), 1);
+        tw.resize(tw.size() + len, make_float2(0.f, 0.f));
+        for (int j = 1; j < ip; ++j)
+            for (long i = 1; i < ido; ++i) {
+                const auto w = pf_twiddle(n, j * l1 * i);
+                tw[p.tw[k] + (j - 1) * (ido - 1) + i - 1] = make_float2(w.first, w.second);
+            }
+        l1 *= ip;
+    }
+}
+
 void upload(void* dst, const void* src, size_t bytes, hipStream_t s) {
     HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
 }
@@ -222,6 +293,8 @@ struct fcd_ctx {
     int chunk = 1;
     DevBuf spec, work, wrapped, kbuf, colk, rescnt, frames_in, out_h, scalar;
     DevBuf cand_idx, cand_val, pk_small, pk_F, pk_work;  // reference setup: candidates, scalars, spectra
+    fcdk::PfPlan pf_row{}, pf_col{};  // scipy pocketfft's plans for the exact reference spectrum
+    DevBuf pf_rtw, pf_ctw, pf_sums;   // their twiddles; numpy's float32 chunk sums
     DevBuf fix_raw;  // raw samples of the frames redone by the exact pass
     // temporal analysis: staged block, exp table, bins, partial sums, output, window
     DevBuf t_stage, t_tab, t_bins, t_part, t_out, t_win, t_wsum, t_slices;
@@ -884,8 +957,12 @@ void find_peaks_batch(fcd_ctx* c, const float* dimgs, int nb, double square_size
     c->cand_idx.ensure((size_t)nb * cap * sizeof(int));
     c->cand_val.ensure((size_t)nb * cap * sizeof(float));
     const double kmin = 4 * kPi / (double)std::min(H, W);  // fourier.py:22
-    fcdk::center_images(dimgs, nb, hw, sums, centered, s);
-    fft2_real(c, centered, F, nb, 0.f, s);
+    (void)sums;
+    // image - np.mean(image) and scipy's fft2 with the reference's own float32 rounding
+    // (kernels_pocketfft.hip): exact ties between carrier blobs break as they do there
+    c->pf_sums.ensure((size_t)nb * fcdk::pf_chunk_count(hw) * sizeof(float));
+    fcdk::pf_center(dimgs, nb, hw, c->pf_sums.as<float>(), centered, s);
+    fcdk::pf_fft2(centered, nb, H, W, c->pf_row, c->pf_rtw.as<float>(), c->pf_col, c->pf_ctw.as<float2>(), F, s);
     fcdk::spectrum_candidates_b(F, nb, H, W, ktab, ktab + H, kmin * kmin, mag, maxbits, counts, c->cand_idx.as<int>(),
                                 c->cand_val.as<float>(), cap, s);
     fcdk::label_peaks(counts, c->cand_idx.as<int>(), c->cand_val.as<float>(), cap, nb, H, W, res, s);
@@ -974,6 +1051,16 @@ FCD_API int fcd_create(int device, int rows, int cols, fcd_ctx** out) {
         c->twp_col.ensure(pc.size() * sizeof(float2));
         HIPCHK(hipMemcpy(c->twp_row.p, pr.data(), pr.size() * sizeof(float2), hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(c->twp_col.p, pc.data(), pc.size() * sizeof(float2), hipMemcpyHostToDevice));
+        {
+            std::vector<float> rtw;
+            std::vector<float2> ctw;
+            pf_row_plan(cols, c->pf_row, rtw);
+            pf_col_plan(rows, c->pf_col, ctw);
+            c->pf_rtw.ensure(rtw.size() * sizeof(float));
+            c->pf_ctw.ensure(ctw.size() * sizeof(float2));
+            HIPCHK(hipMemcpy(c->pf_rtw.p, rtw.data(), rtw.size() * sizeof(float), hipMemcpyHostToDevice));
+            HIPCHK(hipMemcpy(c->pf_ctw.p, ctw.data(), ctw.size() * sizeof(float2), hipMemcpyHostToDevice));
+        }
         // chunk: ~48 B of workspace per pixel per frame; keep the working set near the 256 MiB MALL
         const long per_frame = 48L * rows * cols;
         c->chunk = (int)std::max(1L, std::min(64L, (256L << 20) / per_frame));
@@ -1653,7 +1740,8 @@ FCD_API int fcd_fft2(fcd_ctx* c, const float* in, int n, int flags, float* out, 
                 x = c->frames_in.as<float>();
             }
             float2* dst = dev ? reinterpret_cast<float2*>(out) + (size_t)f0 * hw : c->spec.as<float2>();
-            fft2_real(c, x, dst, nb, 0.f, s);
+            fcdk::pf_fft2(x, nb, c->H, c->W, c->pf_row, c->pf_rtw.as<float>(), c->pf_col, c->pf_ctw.as<float2>(), dst,
+                          s);
             if (!dev) {
                 HIPCHK(hipMemcpyAsync(out + (size_t)f0 * hw * 2, dst, (size_t)nb * hw * 8, hipMemcpyDeviceToHost, s));
                 HIPCHK(hipStreamSynchronize(s));

@@ -105,7 +105,8 @@ void disk_mask(const float2* in, float2* out, int nbatch, int H, int W, DiskTabl
 // theta = atan2(R)  (reference carrier angle)
 void angle(const float2* in, float* out, long n, hipStream_t s);
 // Batched reference setup (fourier.find_peaks for nb images): out[b] = img[b] - mean(img[b])
-// (f64 mean, f32 difference); |F| * highpass per image with its maximum and the
+// (f64 mean, f32 difference; the exact numpy mean is pf_center); |F| (np.abs's float32
+// formula) * highpass per image with its maximum and the
 // above-threshold candidates (cap per image, border excluded); 8-connected labelling and
 // the 4 dimmest blobs' peaks per image (res: 8 ints per image, see kernels_fft.hip).
 void center_images(const float* img, int nb, long hw, double* sums, float* out, hipStream_t s);
@@ -114,6 +115,19 @@ void spectrum_candidates_b(const float2* F, int nb, int H, int W, const double* 
                            hipStream_t s);
 void label_peaks(const int* counts, const int* idx, const float* val, int cap, int nb, int H, int W, int* res,
                  hipStream_t s);
+// The reference's float32 spectrum bit for bit (kernels_pocketfft.hip): numpy's float32
+// mean and centring, scipy 1.7.1 pocketfft's fft2 of real float32 images.  Plans: the
+// factor sequence of rfftp (rows) / cfftp (columns) and each pass's offset into its
+// twiddle table (float cos / sin pairs for rows, float2 for columns), built on the host.
+struct PfPlan {
+    int nf;
+    int fct[8];
+    int tw[8];
+};
+int pf_chunk_count(long hw);  // sums: nb * pf_chunk_count(hw) floats
+void pf_center(const float* img, int nb, long hw, float* sums, float* out, hipStream_t s);
+void pf_fft2(const float* in, int nb, int H, int W, const PfPlan& rows, const float* rtw, const PfPlan& cols,
+             const float2* ctw, float2* F, hipStream_t s);
 
 // ---- unwrap ----
 void residues(const float* w, int nmaps, int H, int W, int* counts, hipStream_t s);

@@ -280,6 +280,35 @@ void center_images(const float* img, int nb, long hw, double* sums, float* out, 
     FCD_CHECK_LAUNCH();
 }
 
+// Correctly rounded float32 square root of a positive normal x.  v_sqrt_f32 (what
+// sqrtf / __fsqrt_rn lower to here) is within 1 ulp but not correctly rounded; the
+// neighbour on either side is taken when x lies beyond the midpoint towards it.  The
+// midpoints have 25 significant bits, so their squares are exact in f64, and x (24
+// bits) can never equal one: the comparisons decide the IEEE result exactly.
+__device__ __forceinline__ float sqrt_rn(float x) {
+    float s = __builtin_sqrtf(x);
+    const double xd = (double)x;
+    const unsigned u = __float_as_uint(s);  // s > 0: the neighbours are the adjacent encodings
+    const float up = __uint_as_float(u + 1u), dn = __uint_as_float(u - 1u);
+    const double mu = 0.5 * ((double)s + (double)up), md = 0.5 * ((double)dn + (double)s);
+    if (mu * mu < xd) s = up;
+    else if (md * md > xd) s = dn;
+    return s;
+}
+
+// np.abs of a complex64 value as numpy 1.26.4 computes it (its AVX512F loop,
+// loops_unary_complex: larger * sqrt(fma(r, r, 1)) with r = smaller / larger, inf / NaN
+// cases first); this file is compiled without FMA contraction, the one FMA is explicit,
+// the division is the IEEE sequence (v_div_scale / fmas / fixup).
+__device__ __forceinline__ float np_cabsf(float2 f) {
+    const float re = fabsf(f.x), im = fabsf(f.y);
+    if (re == INFINITY || im == INFINITY) return INFINITY;
+    if (re != re || im != im) return NAN;
+    const float big = fmaxf(re, im), small = fminf(im, re);
+    const float r = big == 0.f ? 0.f : __fdiv_rn(small, big);
+    return __fmul_rn(sqrt_rn(__fmaf_rn(r, r, 1.0f)), big);
+}
+
 __global__ void k_spectrum_mag_b(const float2* __restrict__ F, float* __restrict__ mag, unsigned* maxbits, int H,
                                  int W, long n, const double* __restrict__ krow_s, const double* __restrict__ kcol_s,
                                  double kmin2) {
@@ -297,7 +326,7 @@ __global__ void k_spectrum_mag_b(const float2* __restrict__ F, float* __restrict
             j = mj;
         }
         const float2 f = F[b * hw + (long)i * W + j];
-        m = hypotf(f.x, f.y);
+        m = np_cabsf(f);
         const double kr = krow_s[si], kc = kcol_s[sj];
         const double k2 = __dadd_rn(__dmul_rn(kr, kr), __dmul_rn(kc, kc));
         if (!(k2 > kmin2)) m = 0.f;
