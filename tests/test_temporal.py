@@ -162,6 +162,34 @@ def test_temporal_fft_path_short_series(monkeypatch, T, pair):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("path", ["0", "1"])
+def test_temporal_spectrum_inf_sample_stays_in_its_pixel(monkeypatch, path):
+    """A series holding an infinity (no NaN): np.fft gives it inf / NaN bins (which ones
+    depends on the transform's butterflies: parity unpinned for non-finite input),
+    np.nanmean keeps the inf ones.  Whichever path runs (direct DFT, or the FFT, which
+    then takes one series per transform instead of pairing the pixel with a partner),
+    every other pixel's contribution is unchanged: per bin either the pixel is left out
+    (count P - 1, sum = the other pixels' sum) or it adds an infinite |X| (count P)."""
+    from pyfcd import _lib
+    monkeypatch.setenv("FCD_TDFT_FFT", path)
+    eng = _lib.temporal_engine()
+    T, n = 1200, 16
+    st = make_stack(T, n=n, seed=21, zero_corner=False)
+    P = n * n
+    base = st.copy()
+    base[:, 3, 9] = np.nan  # the pixel left out everywhere
+    tb, cb = eng.temporal_spectrum(base, 300)
+    assert (cb == P - 1).all()
+    inf = st.copy()
+    inf[T // 3, 3, 9] = np.inf
+    ti, ci = eng.temporal_spectrum(inf, 300)
+    left_out = ci == P - 1
+    assert np.all(left_out | (ci == P))
+    np.testing.assert_allclose(ti[left_out], tb[left_out], rtol=1e-12)
+    assert np.all(np.isinf(ti[~left_out]))
+
+
+@pytest.mark.gpu
 def test_temporal_fft_equals_direct_dft(monkeypatch, tdft_family):
     """The FFT path and both direct-DFT kernel families agree to f64 rounding."""
     from pyfcd import _lib

@@ -22,16 +22,19 @@
 
 #include "../../include/fcd.h"
 #include "fft_lds.hpp"
+#include "host_logic.hpp"
 #include "kernels.hpp"
 
 namespace {
 
-thread_local std::string g_last_error;
+using fcdh::Blob;
+using fcdh::FcdError;
+using fcdh::kPi;
+using fcdh::label_candidates_host;
+using fcdh::par_copy;
+using fcdh::wavenumber;
 
-struct FcdError : std::runtime_error {
-    int code;
-    FcdError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
-};
+thread_local std::string g_last_error;
 
 #define HIPCHK(x)                                                                                  \
     do {                                                                                           \
@@ -61,93 +64,6 @@ struct DevBuf {
     template <class T>
     T* as() const { return static_cast<T*>(p); }
 };
-
-constexpr double kPi = 3.141592653589793;  // numpy.pi
-
-// fourier.wavenumber (fourier.py:43-56): fftfreq(n, cf / (2 pi)), optionally fftshifted.
-std::vector<double> wavenumber(int n, double cf, bool shifted) {
-    const double d = cf / (2 * kPi);
-    const double val = 1.0 / (n * d);
-    std::vector<double> k(n);
-    const int npos = (n - 1) / 2 + 1;
-    for (int i = 0; i < n; ++i) {
-        const long m = i < npos ? i : (long)i - n;
-        k[i] = (double)m * val;
-    }
-    if (shifted) std::rotate(k.begin(), k.begin() + (n - n / 2), k.end());  // fftshift
-    return k;
-}
-
-// scipy 1.7.1 pocketfft plans (kernels_pocketfft.hip; restated in oracle/pocketfft32.py):
-// rfftp factors 4, 4, ... with a single 2 moved to the front; cfftp 8s, then 4s, a single
-// 2 first; twiddles (cos, sin)(2 pi m / n) rounded to float (sincos_2pibyn<float>).
-std::pair<float, float> pf_twiddle(int n, long m) {
-    const double a = 2 * kPi * (double)m / (double)n;
-    return {(float)std::cos(a), (float)std::sin(a)};
-}
-
-std::vector<int> pf_factors(int n, bool real) {
-    std::vector<int> f;
-    int left = n;
-    if (!real)
-        while ((left & 7) == 0) {
-            f.push_back(8);
-            left >>= 3;
-        }
-    while ((left & 3) == 0) {
-        f.push_back(4);
-        left >>= 2;
-    }
-    if ((left & 1) == 0) {
-        left >>= 1;
-        f.push_back(2);
-        std::swap(f.front(), f.back());
-    }
-    if (left != 1 || f.size() > 8) throw std::runtime_error("pocketfft plan: unsupported length");
-    return f;
-}
-
-void pf_row_plan(int n, fcdk::PfPlan& p, std::vector<float>& tw) {  // rfftp::comp_twiddle
-    const std::vector<int> f = pf_factors(n, true);
-    p.nf = (int)f.size();
-    long l1 = 1;
-    for (int k = 0; k < p.nf; ++k) {
-        const int ip = f[k];
-        const long ido = n / (l1 * ip);
-        p.fct[k] = ip;
-        p.tw[k] = (int)tw.size();
-        const size_t len = (size_t)std::max<long>((ip - 1) * (ido - 1), 1);
-        tw.resize(tw.size() + len, 0.f);
-        if (k < p.nf - 1)
-            for (int j = 1; j < ip; ++j)
-                for (long i = 1; i <= (ido - 1) / 2; ++i) {
-                    const auto w = pf_twiddle(n, j * l1 * i);
-                    tw[p.tw[k] + (j - 1) * (ido - 1) + 2 * i - 2] = w.first;
-                    tw[p.tw[k] + (j - 1) * (ido - 1) + 2 * i - 1] = w.second;
-                }
-        l1 *= ip;
-    }
-}
-
-void pf_col_plan(int n, fcdk::PfPlan& p, std::vector<float2>& tw) {  // cfftp::comp_twiddle
-    const std::vector<int> f = pf_factors(n, false);
-    p.nf = (int)f.size();
-    long l1 = 1;
-    for (int k = 0; k < p.nf; ++k) {
-        const int ip = f[k];
-        const long ido = n / (l1 * ip);
-        p.fct[k] = ip;
-        p.tw[k] = (int)tw.size();
-        const size_t len = (size_t)std::max<long>((ip - 1) * (ido - 1), 1);
-        tw.resize(tw.size() + len, make_float2(0.f, 0.f));
-        for (int j = 1; j < ip; ++j)
-            for (long i = 1; i < ido; ++i) {
-                const auto w = pf_twiddle(n, j * l1 * i);
-                tw[p.tw[k] + (j - 1) * (ido - 1) + i - 1] = make_float2(w.first, w.second);
-            }
-        l1 *= ip;
-    }
-}
 
 void upload(void* dst, const void* src, size_t bytes, hipStream_t s) {
     HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
@@ -225,12 +141,6 @@ int fcd_env_int(const char* name, int dflt) {
     const char* v = std::getenv(name);
     return (v && *v) ? std::atoi(v) : dflt;
 }
-
-struct Blob {
-    int first;     // raster index of its first pixel (skimage label order)
-    int peak;      // raster index of its max pixel (first in row-major on ties)
-    float value;
-};
 
 // Host-pointer pipeline state (fcd_process with host frames, heights only).
 struct HostPipe {
@@ -553,180 +463,6 @@ void check_ctx(fcd_ctx* c) {
     HIPCHK(hipSetDevice(c->device));
 }
 
-// fourier.find_peak_locations (fourier.py:139-168) on the host, from an image's
-// candidate list: the images whose above-threshold set exceeds the device labelling
-// kernel's capacity (fcdk::label_peaks).  Returns the 4 dimmest blobs in order.
-std::vector<Blob> label_candidates_host(int H, int W, const std::vector<int>& idx_in, const std::vector<float>& val_in) {
-    const size_t n = idx_in.size();
-    std::vector<size_t> order(n);
-    std::iota(order.begin(), order.end(), 0);
-    std::sort(order.begin(), order.end(), [&](size_t a, size_t b) { return idx_in[a] < idx_in[b]; });
-    std::vector<int> idx(n);
-    std::vector<float> val(n);
-    for (size_t i = 0; i < n; ++i) {
-        idx[i] = idx_in[order[i]];
-        val[i] = val_in[order[i]];
-    }
-    // 8-connected labelling of the sparse set (skimage.measure.label, connectivity 2)
-    std::vector<int> parent(n);
-    std::iota(parent.begin(), parent.end(), 0);
-    auto find = [&](int x) {
-        while (parent[x] != x) {
-            parent[x] = parent[parent[x]];
-            x = parent[x];
-        }
-        return x;
-    };
-    auto lookup = [&](int r, int col) -> int {
-        if (r < 0 || col < 0 || r >= H || col >= W) return -1;
-        const int key = r * W + col;
-        auto it = std::lower_bound(idx.begin(), idx.end(), key);
-        return (it != idx.end() && *it == key) ? (int)(it - idx.begin()) : -1;
-    };
-    for (size_t i = 0; i < n; ++i) {
-        const int r = idx[i] / W, col = idx[i] % W;
-        const int nb[4][2] = {{r - 1, col - 1}, {r - 1, col}, {r - 1, col + 1}, {r, col - 1}};
-        for (auto& q : nb) {
-            const int j = lookup(q[0], q[1]);
-            if (j >= 0) {
-                const int a = find((int)i), b = find(j);
-                if (a != b) parent[std::max(a, b)] = std::min(a, b);
-            }
-        }
-    }
-    // blobs in raster order of their first pixel; per blob the max (first on ties)
-    std::vector<Blob> blobs;
-    std::vector<int> blob_of(n, -1);
-    for (size_t i = 0; i < n; ++i) {
-        const int root = find((int)i);
-        if (blob_of[root] < 0) {
-            blob_of[root] = (int)blobs.size();
-            blobs.push_back(Blob{idx[i], idx[i], val[i]});
-        } else {
-            Blob& b = blobs[blob_of[root]];
-            if (val[i] > b.value) {
-                b.value = val[i];
-                b.peak = idx[i];
-            }
-        }
-    }
-    std::stable_sort(blobs.begin(), blobs.end(), [](const Blob& a, const Blob& b) { return a.value < b.value; });
-    if (blobs.size() > 4) blobs.resize(4);
-    return blobs;
-}
-
-// Carrier geometry of both carriers (Carrier.__init__, carriers.py:10-20): peak
-// pixels (fftshifted row, col), calibration factor, physical wavenumbers
-// (pixel_to_wavenumber, carriers.py:12) and the disk band-pass raster per carrier
-// with its own radius (skimage.draw.disk: strict < 1 in f64, clipped to the image,
-// carriers.py:17-20).  Sets c->info's geometry fields and c->disk_rows_host.
-void carrier_geometry(fcd_ctx* c, const long prow[2], const long pcol[2], double cf, const double R[2]) {
-    const int H = c->H, W = c->W;
-    fcd_ref_info& info = c->info;
-    for (int q = 0; q < 2; ++q) {
-        info.peaks[q][0] = prow[q];
-        info.peaks[q][1] = pcol[q];
-    }
-    info.calibration_factor = cf;
-    info.radius = R[0];
-    const std::vector<double> krc = wavenumber(H, cf, true), kcc = wavenumber(W, cf, true);
-    for (int q = 0; q < 2; ++q) {
-        info.frequencies[q][0] = krc[info.peaks[q][0]];
-        info.frequencies[q][1] = kcc[info.peaks[q][1]];
-    }
-    // disk raster (skimage.draw.disk -> ellipse, rotation 0), per shifted column the row range
-    c->disk_rows_host.assign((size_t)4 * W, 0);
-    for (int q = 0; q < 2; ++q) {
-        const double Rq = R[q];
-        int* rows = c->disk_rows_host.data() + (size_t)q * 2 * W;
-        for (int j = 0; j < W; ++j) {
-            rows[2 * j] = 1;
-            rows[2 * j + 1] = 0;
-        }
-        const long pr = info.peaks[q][0], pc = info.peaks[q][1];
-        const long lo_r = std::max<long>((long)std::ceil((double)pr - Rq), 0);
-        const long hi_r = std::min<long>((long)std::floor((double)pr + Rq), H - 1);
-        const long lo_c = std::max<long>((long)std::ceil((double)pc - Rq), 0);
-        const long hi_c = std::min<long>((long)std::floor((double)pc + Rq), W - 1);
-        int count = 0;
-        for (long sc = lo_c; sc <= hi_c; ++sc) {
-            const double cc = (double)(sc - lo_c) - (double)(pc - lo_c);
-            const double cq = cc / Rq;
-            const double c2 = cq * cq;
-            int first = -1, last = -2;
-            for (long sr = lo_r; sr <= hi_r; ++sr) {
-                const double rr = (double)(sr - lo_r) - (double)(pr - lo_r);
-                const double rq = rr / Rq;
-                const double d = rq * rq + c2;
-                if (d < 1.0) {
-                    if (first < 0) first = (int)sr;
-                    last = (int)sr;
-                    ++count;
-                }
-            }
-            if (first >= 0) {
-                rows[2 * sc] = first;
-                rows[2 * sc + 1] = last;
-            }
-        }
-        info.mask_count[q] = count;
-    }
-}
-
-// The rest of fourier.find_peaks + compute_calibration_factor + the carrier disks
-// from the 4 dimmest blobs (fourier.py:38-39, fcd.py:53-101): sets c->info and
-// c->disk_rows_host.
-void carriers_from_blobs(fcd_ctx* c, const std::vector<Blob>& blobs, float thr, double square_size) {
-    const int H = c->H, W = c->W;
-    if (blobs.size() < 1) throw FcdError(FCD_E_NOPEAKS, "find_peaks: no spectral peaks above threshold");
-
-    const std::vector<double> kr = wavenumber(H, 1.0, true), kc = wavenumber(W, 1.0, true);
-    auto kvec = [&](int p) { return std::pair<double, double>(kr[p / W], kc[p % W]); };
-    // rightmost = min |atan2(k_row, k_col)|; perpendicular = min |k_right . k| (fourier.py:38-39)
-    size_t ir = 0;
-    double best = INFINITY;
-    for (size_t i = 0; i < blobs.size(); ++i) {
-        auto k = kvec(blobs[i].peak);
-        const double a = std::fabs(std::atan2(k.first, k.second));
-        if (a < best) {
-            best = a;
-            ir = i;
-        }
-    }
-    const auto k0 = kvec(blobs[ir].peak);
-    size_t ip = 0;
-    best = INFINITY;
-    for (size_t i = 0; i < blobs.size(); ++i) {
-        auto k = kvec(blobs[i].peak);
-        const double d = std::fabs(k0.first * k.first + k0.second * k.second);
-        if (d < best) {
-            best = d;
-            ip = i;
-        }
-    }
-    fcd_ref_info& info = c->info;
-    std::memset(&info, 0, sizeof(info));
-    info.n_blobs = (int)blobs.size();
-    for (size_t i = 0; i < blobs.size(); ++i) {
-        info.blob_peaks[i][0] = blobs[i].peak / W;
-        info.blob_peaks[i][1] = blobs[i].peak % W;
-    }
-    info.threshold = thr;
-    const int pk[2] = {blobs[ir].peak, blobs[ip].peak};
-    const long prow[2] = {pk[0] / W, pk[1] / W}, pcol[2] = {pk[0] % W, pk[1] % W};
-    // calibration factor (fcd.py:85-101): 2*sq / (2*pi / mean(|k_pix|))
-    const double ak[4] = {std::fabs(kr[prow[0]]), std::fabs(kc[pcol[0]]), std::fabs(kr[prow[1]]),
-                          std::fabs(kc[pcol[1]])};
-    const double mean = (((ak[0] + ak[1]) + ak[2]) + ak[3]) / 4.0;
-    const double pixel_wavelength = (2 * kPi) / mean;
-    const double cf = (2 * square_size) / pixel_wavelength;
-    const double dr = (double)(prow[0] - prow[1]);
-    const double dc = (double)(pcol[0] - pcol[1]);
-    const double radius = std::sqrt(dr * dr + dc * dc) / 2;  // fcd.py:68
-    const double R[2] = {radius, radius};
-    carrier_geometry(c, prow, pcol, cf, R);
-}
-
 // Band-pruned demodulation tables: which unshifted columns each carrier disk
 // covers, the half-spectrum column each one is read from (directly, or as the
 // conjugate mirror of column W - uc of the real input's spectrum), and the
@@ -932,14 +668,19 @@ void reference_state(fcd_ctx* c, const float* dref0, const float* dref1, hipStre
 // above-threshold candidates, the 8-connected labelling and the 4-blob pick
 // (kernels_fft.hip); the host finishes each image from its <= 4 peaks.  c->info and
 // c->disk_rows_host end up describing the last image; infos[i] (nullable) gets each.
-// Workspace: pk_* (16 bytes per pixel per image).
-int find_peaks_batch_max(const fcd_ctx* c) { return (int)std::max(1L, (512L << 20) / (16L * c->hw())); }
+// Workspace: pk_* (16 bytes per pixel per image) + candidates (8 bytes per kept slot).
+// candidates kept per image (the device labels up to 4096 of them): never more than the
+// image has pixels
+long find_peaks_cap(const fcd_ctx* c) { return std::min(1L << 16, c->hw()); }
+int find_peaks_batch_max(const fcd_ctx* c) {
+    return (int)std::max(1L, (512L << 20) / (16L * c->hw() + 8L * find_peaks_cap(c)));
+}
 
 void find_peaks_batch(fcd_ctx* c, const float* dimgs, int nb, double square_size, fcd_ref_info* infos, hipStream_t s) {
     const long hw = c->hw();
     const int H = c->H, W = c->W;
     if (nb <= 0) return;
-    constexpr int cap = 1 << 16;  // candidates kept per image (the device labels up to 4096 of them)
+    const int cap = (int)find_peaks_cap(c);
     c->pk_F.ensure((size_t)nb * hw * sizeof(float2));
     c->pk_work.ensure((size_t)nb * hw * 2 * sizeof(float));
     float2* F = c->pk_F.as<float2>();
@@ -994,7 +735,7 @@ void find_peaks_batch(fcd_ctx* c, const float* dimgs, int nb, double square_size
         } else {
             for (int e = 0; e < r[2]; ++e) blobs.push_back(Blob{r[3 + e], r[3 + e], 0.f});
         }
-        carriers_from_blobs(c, blobs, 0.5f * mx, square_size);
+        fcdh::carriers_from_blobs(H, W, c->info, c->disk_rows_host, blobs, 0.5f * mx, square_size);
         if (infos) infos[b] = c->info;
     }
 }
@@ -1052,14 +793,13 @@ FCD_API int fcd_create(int device, int rows, int cols, fcd_ctx** out) {
         HIPCHK(hipMemcpy(c->twp_row.p, pr.data(), pr.size() * sizeof(float2), hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(c->twp_col.p, pc.data(), pc.size() * sizeof(float2), hipMemcpyHostToDevice));
         {
-            std::vector<float> rtw;
-            std::vector<float2> ctw;
-            pf_row_plan(cols, c->pf_row, rtw);
-            pf_col_plan(rows, c->pf_col, ctw);
+            std::vector<float> rtw, ctw;  // ctw: (cos, sin) pairs = float2 on the device
+            fcdh::pf_row_plan(cols, c->pf_row, rtw);
+            fcdh::pf_col_plan(rows, c->pf_col, ctw);
             c->pf_rtw.ensure(rtw.size() * sizeof(float));
-            c->pf_ctw.ensure(ctw.size() * sizeof(float2));
+            c->pf_ctw.ensure(ctw.size() * sizeof(float));
             HIPCHK(hipMemcpy(c->pf_rtw.p, rtw.data(), rtw.size() * sizeof(float), hipMemcpyHostToDevice));
-            HIPCHK(hipMemcpy(c->pf_ctw.p, ctw.data(), ctw.size() * sizeof(float2), hipMemcpyHostToDevice));
+            HIPCHK(hipMemcpy(c->pf_ctw.p, ctw.data(), ctw.size() * sizeof(float), hipMemcpyHostToDevice));
         }
         // chunk: ~48 B of workspace per pixel per frame; keep the working set near the 256 MiB MALL
         const long per_frame = 48L * rows * cols;
@@ -1148,7 +888,7 @@ FCD_API int fcd_set_carriers(fcd_ctx* c, const float* ref0, const float* ref1, i
             }
         }
         std::memset(&c->info, 0, sizeof(c->info));
-        carrier_geometry(c, prow, pcol, calibration_factor, R);
+        fcdh::carrier_geometry(c->H, c->W, c->info, c->disk_rows_host, prow, pcol, calibration_factor, R);
         reference_state(c, d0, d1, s);
         c->has_ref = true;
         if (info) *info = c->info;
@@ -1286,24 +1026,6 @@ bool host_pinned(const void* p) {
 
 // memcpy between pageable and pinned host memory, split over threads (one
 // host thread moves ~10 GB/s; the PCIe link ~50 GB/s per direction).
-void par_copy(void* dst, const void* src, size_t bytes) {
-    constexpr size_t kPiece = 8u << 20;
-    const int nt = (int)std::min<size_t>(8, (bytes + kPiece - 1) / kPiece);
-    if (nt <= 1) {
-        std::memcpy(dst, src, bytes);
-        return;
-    }
-    const size_t part = (bytes / nt + 4095) & ~(size_t)4095;
-    std::vector<std::thread> th;
-    for (int t = 1; t < nt; ++t) {
-        const size_t o = part * t;
-        if (o >= bytes) break;
-        th.emplace_back([=] { std::memcpy((char*)dst + o, (const char*)src + o, std::min(part, bytes - o)); });
-    }
-    std::memcpy(dst, src, std::min(part, bytes));
-    for (auto& x : th) x.join();
-}
-
 void ensure_host_pipe(fcd_ctx* c, int format) {
     HostPipe& P = c->pipe;
     const long hw = c->hw();
@@ -1522,10 +1244,18 @@ int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int f
     std::vector<int> counts((size_t)n_frames * 2);
     HIPCHK(hipMemcpyAsync(counts.data(), res, counts.size() * sizeof(int), hipMemcpyDeviceToHost, s));
     // polled rather than a blocking wait: the caller's next batch is enqueued as soon
-    // as this one's census is back (a blocking wait's wake-up sat in every bench step)
-    hipError_t qe;
-    while ((qe = hipStreamQuery(s)) == hipErrorNotReady) {
+    // as this one's census is back (a blocking wait's wake-up sat in every bench step,
+    // ~17 us per 256-frame step at 1024^2).  The poll yields the core between queries
+    // and gives up after FCD_SPIN_US (default 20 ms: a 1024^2 chunk's first pass takes
+    // ~3 ms, a 4096^2 one ~6 ms), then blocks; FCD_SPIN_US=0 always blocks.
+    static const long spin_us = fcd_env_int("FCD_SPIN_US", 20000);
+    hipError_t qe = hipErrorNotReady;
+    if (spin_us > 0) {
+        const auto t_end = std::chrono::steady_clock::now() + std::chrono::microseconds(spin_us);
+        while ((qe = hipStreamQuery(s)) == hipErrorNotReady && std::chrono::steady_clock::now() < t_end)
+            std::this_thread::yield();
     }
+    if (qe == hipErrorNotReady) qe = hipStreamSynchronize(s);
     HIPCHK(qe);
     std::vector<int> redo;
     for (int f = 0; f < n_frames; ++f)
@@ -1804,7 +1534,16 @@ FCD_API int fcd_temporal_spectrum(fcd_ctx* c, const void* stack, int T, int rows
         const int P = bh * bw;
         fcdk::TfftPlan pl;
         int tiles = 1;
-        if (fcdk::temporal_spectrum_uses_fft(T, nf) && fcdk::temporal_fft_plan(T, P, &pl)) {
+        bool fft = fcdk::temporal_spectrum_uses_fft(T, nf) && fcdk::temporal_fft_plan(T, P, &pl);
+        if (fft && pl.pair) {
+            // per-pixel NaN / infinity flags; a series with an infinity keeps the block on
+            // one series per transform (kernels_tfft.hip k_tfft_flags)
+            c->t_bad.ensure((size_t)P * sizeof(int) + 64);
+            const int ninf = fcdk::temporal_inf_pixels(v.p, v.frame_pitch, v.row_pitch, bw, P, T, c->t_bad.as<int>(),
+                                                       c->t_bad.as<int>() + P, s);
+            if (ninf > 0) fcdk::temporal_fft_plan(T, P, &pl, false);
+        }
+        if (fft) {
             // Bluestein + four-step FFT: chirp, twiddles and B = FFT(b) / M from the host in f64
             std::vector<double2> chirp, tw, bhat;
             fcdk::temporal_fft_tables(T, pl, chirp, tw, bhat);
@@ -1813,10 +1552,7 @@ FCD_API int fcd_temporal_spectrum(fcd_ctx* c, const void* stack, int T, int rows
             c->t_bhat.ensure(bhat.size() * sizeof(double2));
             c->t_work.ensure((size_t)pl.work_elems * sizeof(double2));
             c->t_gpart.ensure((size_t)pl.ngroups * nf * sizeof(double2));
-            if (pl.pair) {
-                c->t_zo.ensure((size_t)pl.zo_elems * sizeof(double2));
-                c->t_bad.ensure((size_t)P * sizeof(int));
-            }
+            if (pl.pair) c->t_zo.ensure((size_t)pl.zo_elems * sizeof(double2));
             c->t_part.ensure((size_t)nf * 2 * sizeof(double));
             upload(c->t_tab.p, tw.data(), tw.size() * sizeof(double2), s);
             upload(c->t_chirp.p, chirp.data(), chirp.size() * sizeof(double2), s);

@@ -6,6 +6,8 @@
 #include <cstdint>
 #include <vector>
 
+#include "host_logic.hpp"  // fcdk::PfPlan
+
 namespace fcdk {
 
 // Row-FFT input / output modes.
@@ -119,11 +121,6 @@ void label_peaks(const int* counts, const int* idx, const float* val, int cap, i
 // mean and centring, scipy 1.7.1 pocketfft's fft2 of real float32 images.  Plans: the
 // factor sequence of rfftp (rows) / cfftp (columns) and each pass's offset into its
 // twiddle table (float cos / sin pairs for rows, float2 for columns), built on the host.
-struct PfPlan {
-    int nf;
-    int fct[8];
-    int tw[8];
-};
 int pf_chunk_count(long hw);  // sums: nb * pf_chunk_count(hw) floats
 void pf_center(const float* img, int nb, long hw, float* sums, float* out, hipStream_t s);
 void pf_fft2(const float* in, int nb, int H, int W, const PfPlan& rows, const float* rtw, const PfPlan& cols,
@@ -195,7 +192,12 @@ struct TfftWork {
     int* bad;        // [P] (pair): pixel has a non-finite sample
 };
 bool temporal_spectrum_uses_fft(int T, int nf);
-bool temporal_fft_plan(int T, int P, TfftPlan* pl);  // false: T too long for the LDS sub-transforms
+// allow_pair = false: one series per transform (a block with an infinity in some series)
+bool temporal_fft_plan(int T, int P, TfftPlan* pl, bool allow_pair = true);  // false: T too long
+// bad[P] per-pixel flags (1 NaN, 2 infinity) of the block; returns the pixels with an
+// infinity and no NaN.  Synchronises.
+int temporal_inf_pixels(Samples stack, long frame_pitch, long row_pitch, int bw, int P, int T, int* bad, int* count,
+                        hipStream_t s);
 void temporal_fft_tables(int T, const TfftPlan& pl, std::vector<double2>& chirp, std::vector<double2>& tw,
                          std::vector<double2>& bhat);
 // partial [nf][2] (sum of |X|, count) over the block

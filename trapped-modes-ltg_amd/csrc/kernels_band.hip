@@ -37,6 +37,13 @@ namespace {
 #define FCD_BAND_WAVES 3  // min waves per SIMD (launch-bounds): 3 blocks of 4 waves per CU (168 VGPRs)
 #endif
 
+// Diagnostic ablations (FCD_BAND_NOTHETA / _ABL / _NOSTORE: wrong results by design)
+// exist only in builds with -DFCD_DIAGNOSTIC (tools/ablate.sh, kbench variants); the
+// product build (Makefile) cannot turn them on.
+#if !defined(FCD_DIAGNOSTIC) && (defined(FCD_BAND_NOTHETA) || defined(FCD_BAND_ABL) || defined(FCD_BAND_NOSTORE))
+#error "FCD_BAND_* ablations are diagnostic-only: build with -DFCD_DIAGNOSTIC"
+#endif
+
 #ifndef FCD_BAND_NOTHETA
 #define FCD_BAND_NOTHETA 0  // diagnostic ablation only (wrong results): no reference-angle loads
 #endif

@@ -54,6 +54,9 @@ constexpr int PR_ROWS = FCD_PR_ROWS;  // rows per tile (one wave each)
 #ifndef FCD_PR_PKUNWRAP
 #define FCD_PR_PKUNWRAP 1  // unwrap / census on packed pairs of both maps (0: the integer-code form)
 #endif
+#if !defined(FCD_DIAGNOSTIC) && defined(FCD_PR_ABL)
+#error "FCD_PR_ABL ablations are diagnostic-only: build with -DFCD_DIAGNOSTIC"
+#endif
 #ifndef FCD_PR_ABL
 #define FCD_PR_ABL 0  // diagnostic ablations only (wrong results): 1 no reference-angle loads, 2 no Zt stores,
                       // 4 no band transforms, 8 no atan2 / wrap, 16 no z-row FFT

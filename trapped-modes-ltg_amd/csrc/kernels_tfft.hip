@@ -187,7 +187,8 @@ __device__ __forceinline__ void load_twl(double2* twl, const double2* __restrict
 
 // Step 1: column n2 = bx of group by: pixels [pbase + 8 by, +8), or with PAIR the 8
 // pixel pairs (p, p + 8), p in [pbase + 16 by, +8), as x_p + i x_{p+8} (a pixel with a
-// non-finite sample, bad[p], enters as zeros: np.nanmean drops it anyway).
+// NaN sample, bad[p], enters as zeros: np.nanmean drops it anyway; a block with an
+// infinity never runs paired).
 template <int LOG1, typename S, bool PAIR>
 __global__ __launch_bounds__(TF_NT) void k_tfft_cols_fwd(const S* __restrict__ stack, long frame_pitch,
                                                          long row_pitch, int bw, int P, int T, int pbase,
@@ -315,7 +316,12 @@ __global__ __launch_bounds__(TF_NT) void k_tfft_cols_inv(const double2* __restri
     }
 }
 
-// Pixels of the block with a non-finite sample (any t): bad[p] = 1 (zeroed beforehand).
+// Pixels of the block with a non-finite sample (any t): bad[p] |= 1 for a NaN, |= 2 for
+// an infinity (zeroed beforehand).  A NaN makes every bin of the pixel's np.fft NaN, so
+// np.nanmean leaves the pixel out: the paired path drops it (bad != 0).  An infinity
+// (and no NaN) gives inf / NaN bins that must stay the pixel's own: such a block runs
+// unpaired (temporal_inf_pixels), so it never reaches a partner series through
+// z = x_p + i x_q.
 template <typename S>
 __global__ __launch_bounds__(TF_NT) void k_tfft_flags(const S* __restrict__ stack, long frame_pitch, long row_pitch,
                                                       int bw, int P, int T, int* __restrict__ bad) {
@@ -323,17 +329,27 @@ __global__ __launch_bounds__(TF_NT) void k_tfft_flags(const S* __restrict__ stac
     if (p >= P) return;
     const S* x = stack + tf_pix_off(p, bw, row_pitch);
     const int t0 = blockIdx.y * TF_NT, t1 = min(T, t0 + TF_NT);
-    bool ok = true;
+    int code = 0;
     int t = t0;
+    auto classify = [&](double v) {
+        if (v != v) code |= 1;
+        else if (v - v != 0.0) code |= 2;  // +-inf
+    };
     for (; t + 8 <= t1; t += 8) {  // 8 loads in flight per lane
         S v[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) v[u] = x[(long)(t + u) * frame_pitch];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) ok &= isfinite((double)v[u]);
+        for (int u = 0; u < 8; ++u) classify((double)v[u]);
     }
-    for (; t < t1; ++t) ok &= isfinite((double)x[(long)t * frame_pitch]);
-    if (!ok) atomicOr(bad + p, 1);
+    for (; t < t1; ++t) classify((double)x[(long)t * frame_pitch]);
+    if (code) atomicOr(bad + p, code);
+}
+
+// Pixels whose series holds an infinity and no NaN (bad == 2) -> *count.
+__global__ void k_tfft_inf_count(const int* __restrict__ bad, int P, int* __restrict__ count) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < P && bad[p] == 2) atomicAdd(count, 1);
 }
 
 // Step 3 of the paired path: column n2 = bx of pair group by: inverse FFT over k1, then
@@ -475,12 +491,7 @@ template <typename S>
 void spectrum_fft_t(const S* stack, long fp, long rp, int bw, int P, int T, int nf, const TfftPlan& pl,
                     const double2* chirp, const double2* tw, const double2* bhat, const TfftWork& wk, double* partial,
                     hipStream_t s) {
-    if (pl.pair) {
-        FCD_TF_HIPCHK(hipMemsetAsync(wk.bad, 0, (size_t)P * sizeof(int), s));
-        hipLaunchKernelGGL(k_tfft_flags<S>, dim3((unsigned)((P + TF_NT - 1) / TF_NT), (unsigned)((T + TF_NT - 1) / TF_NT)),
-                           dim3(TF_NT), 0, s, stack, fp, rp, bw, P, T, wk.bad);
-        tf_check("temporal fft (finite flags)");
-    }
+    // pl.pair: wk.bad holds the block's flags (temporal_inf_pixels, no infinity among them)
     for (int pbase = 0; pbase < P; pbase += pl.Pb) {
         if (pl.pair) {
             // pixels of this batch, rounded up to whole 128-pixel partial rows; 16 per pair group
@@ -530,7 +541,7 @@ bool temporal_spectrum_uses_fft(int T, int nf) {
     return fft < direct;
 }
 
-bool temporal_fft_plan(int T, int P, TfftPlan* pl) {
+bool temporal_fft_plan(int T, int P, TfftPlan* pl, bool allow_pair) {
     int logM = 2;
     while ((1L << logM) < 2L * T - 1) ++logM;
     if (logM > 2 * TF_MAXLOG || T <= 0 || P <= 0) return false;
@@ -542,7 +553,7 @@ bool temporal_fft_plan(int T, int P, TfftPlan* pl) {
     pl->M2 = 1 << pl->log2;
     // FCD_TDFT_PAIR=0: one pixel per transform (diagnostic); default two (x_p + i x_q)
     const char* e = std::getenv("FCD_TDFT_PAIR");
-    pl->pair = !(e && e[0] == '0');
+    pl->pair = allow_pair && !(e && e[0] == '0');
     // pixels per batch: a work array of <= 1 GiB, a multiple of 128 pixels, <= 2^16 (grid y)
     const long cap =
         std::min(1L << 16, std::max(1L, (1L << 30) / ((long)pl->M * (long)sizeof(double2)) / TF_PS) * TF_PS);
@@ -603,6 +614,26 @@ void temporal_fft_tables(int T, const TfftPlan& pl, std::vector<double2>& chirp,
             const std::complex<double> v = b[(size_t)k1 + (size_t)pl.M1 * k2] * inv;
             bhat[(size_t)k1 * pl.M2 + k2] = make_double2(v.real(), v.imag());
         }
+}
+
+int temporal_inf_pixels(Samples stack, long frame_pitch, long row_pitch, int bw, int P, int T, int* bad, int* count,
+                        hipStream_t s) {
+    FCD_TF_HIPCHK(hipMemsetAsync(bad, 0, (size_t)P * sizeof(int), s));
+    FCD_TF_HIPCHK(hipMemsetAsync(count, 0, sizeof(int), s));
+    const dim3 g((unsigned)((P + TF_NT - 1) / TF_NT), (unsigned)((T + TF_NT - 1) / TF_NT));
+    if (stack.f64)
+        hipLaunchKernelGGL(k_tfft_flags<double>, g, dim3(TF_NT), 0, s, static_cast<const double*>(stack.p), frame_pitch,
+                           row_pitch, bw, P, T, bad);
+    else
+        hipLaunchKernelGGL(k_tfft_flags<float>, g, dim3(TF_NT), 0, s, static_cast<const float*>(stack.p), frame_pitch,
+                           row_pitch, bw, P, T, bad);
+    tf_check("temporal fft (finite flags)");
+    hipLaunchKernelGGL(k_tfft_inf_count, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, bad, P, count);
+    tf_check("temporal fft (inf count)");
+    int n = 0;
+    FCD_TF_HIPCHK(hipMemcpyAsync(&n, count, sizeof(int), hipMemcpyDeviceToHost, s));
+    FCD_TF_HIPCHK(hipStreamSynchronize(s));
+    return n;
 }
 
 void temporal_spectrum_fft(Samples stack, long frame_pitch, long row_pitch, int bw, int P, int T, int nf,
