@@ -294,6 +294,15 @@ def main():
                                         "per-frame bytes x frames per launch") if traffic else None,
                      "measured_as": "separate profiled pass of the same frames with the wrapped phases written "
                                     "(the headline path fuses the band transform with the unwrap)"},
+        # the heights-only headline path against the same 8 TB/s: its own compulsory bytes
+        # (frame f32 in + height f32 out, 8 N^2) and the BASELINE.md unit (12 N^2) at the
+        # headline rate; traffic: PMC bytes per frame summed over the headline's kernels
+        "headline_roofline": {
+            "per_gpu": True, "bytes_per_frame": 8 * n * n,
+            "achieved_GBps": round(8.0 * n * n * value / world / 1e9, 1),
+            "frac": round(8.0 * n * n * value / world / 1e9 / HBM_PEAK_GBS, 4),
+            "demod_unit_frac_at_headline_rate": round(12.0 * n * n * value / world / 1e9 / HBM_PEAK_GBS, 4),
+            "traffic_bytes_per_frame": traffic.get("headline_bytes_per_frame") if traffic else None},
         "stage_us_per_frame": per_frame,
         "event_ms_per_step": round(ev0.elapsed_time(ev1) / args.steps, 3),
     }

@@ -183,3 +183,17 @@ def test_folder_matches_reference_run(A, golden, tmp_path, fresh_engines, tag):
         assert int((h == 0).sum()) == int(A[f"folder_{tag}_zero_count"][i]), n
     cp = maps / "centers.txt"
     assert (open(str(cp)).read() if cp.exists() else "") == str(A[f"folder_{tag}_centers_txt"])
+
+
+@pytest.mark.parametrize("dt", ["float32", "float64"])
+def test_temporal_oracle_matches_reference_run(A, dt):
+    """oracle/temporal_oracle.py (the checker of tests/test_temporal.py) against the
+    reference's own block_amplitude outputs (CPU)."""
+    from oracle import temporal_oracle as ora
+    st = A[f"{dt}_stack"]
+    for k in range(3):
+        mode, blk, zero = A[f"{dt}_amp{k}_args"].tolist()
+        harm, amps, phases, f0 = ora.block_amplitude(st, tasa=500, mode=int(mode), num_blocks=4,
+                                                     block_index=int(blk), zero=zero)
+        assert f0 == float(A[f"{dt}_amp{k}_f0"])
+        _close(amps, A[f"{dt}_amp{k}_amps"], 1e-12, (dt, k))

@@ -1,9 +1,11 @@
 """Temporal post-analysis of the map stack (analyze.py:364-587):
 `analyze.block_split`, `analyze.block_amplitude`, `analyze.spectrogram`.
 
-Parity unpinned: the reference module imports cv2, absent here, so no reference-run
-vectors exist; the checker is oracle/temporal_oracle.py, the reference's own numpy /
-scipy calls restated on in-memory stacks.  The device DFTs accumulate in f64, so the
+These tests check the device against oracle/temporal_oracle.py (the reference's numpy /
+scipy calls restated on in-memory stacks) over many shapes and edge cases; the oracle
+and the device path are pinned to the reference's OWN outputs in
+tests/test_analyze_ref.py (analyze_ref.npz: block_split / block_amplitude / spectrogram
+run by /root/reference/pydata/analyze.py itself).  The device DFTs accumulate in f64, so the
 comparisons are at 1e-9 relative (the reference's np.fft is f64 as well; its
 spectrogram of a float32 series runs in float32 inside scipy, which the f64 device
 result beats — compared here against scipy on the f64 series).

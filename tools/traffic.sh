@@ -13,7 +13,9 @@ export TMPDIR=/tmp
 hb=$!
 trap 'kill $hb 2>/dev/null' EXIT
 for c in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 420 rocprofv3 --kernel-trace --pmc $c -f csv -d $out/$c -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > $out/$c.log 2>&1 || { echo "pmc $c failed"; tail -5 $out/$c.log; exit 1; }
+  # counters on the engine's kernels only: the on-device frame generator's thousands of
+  # small torch kernels are left out of the (dispatch-serialising) counter collection
+  timeout -k 10 420 rocprofv3 --kernel-trace --pmc $c --kernel-include-regex 'fcdk' -f csv -d $out/$c -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > $out/$c.log 2>&1 || { echo "pmc $c failed"; tail -5 $out/$c.log; exit 1; }
   echo "pmc $c done"
   timeout -k 10 120 rocprofv3 --kernel-trace --pmc $c -f csv -d $out/cal_$c -o run -- trapped-modes-ltg_amd/tools/membench cal > $out/cal_$c.log 2>&1 || { echo "calibration $c failed"; tail -5 $out/cal_$c.log; exit 1; }
 done

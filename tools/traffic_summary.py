@@ -20,7 +20,9 @@ from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 DEMOD = ("k_demod_rows", "k_demod_cols", "k_band_phase")
-CHAIN = DEMOD + ("k_colk", "k_int_rows2", "k_int_cols", "k_int_c2r")
+# the heights-only headline path (fused band transform + unwrap + row FFT)
+HEADLINE = ("k_demod_rows", "k_demod_cols", "k_phase_rows", "k_colk", "k_seam_check", "k_int_cols", "k_int_c2r")
+CHAIN = DEMOD + ("k_phase_rows", "k_seam_check", "k_colk", "k_int_rows2", "k_int_cols", "k_int_c2r")
 
 
 def per_dispatch(path):
@@ -83,12 +85,26 @@ def main():
     group = sum(table[k]["read_bytes_per_launch"] + table[k]["write_bytes_per_launch"] for k in DEMOD if k in table)
     # chunk size: frames per launch from the bench log line
     chunk = a.chunk
+    streams = 1
     for line in open(os.path.join(a.dir, "FETCH_SIZE.log")):
-        if chunk is None and line.startswith("{"):
-            chunk = int(round(json.loads(line)["roofline"]["frames_per_launch"]))
+        if line.startswith("{"):
+            b = json.loads(line)
+            if chunk is None:
+                chunk = int(round(b["roofline"]["frames_per_launch"]))
+            streams = int(b["config"].get("streams_per_chunk", 1))
+    # frames per kept launch: the demod kernels' largest launches are the roofline pass's
+    # whole chunks; the headline-only kernels run on each stream's share of the chunk
+    for k, t in table.items():
+        fpl = chunk if (k in DEMOD or a.chunk) else max(1, chunk // streams)
+        t["frames_per_launch"] = fpl
+        t["bytes_per_frame"] = (t["read_bytes_per_launch"] + t["write_bytes_per_launch"]) / fpl if fpl else None
+    headline = {k: table[k]["bytes_per_frame"] for k in HEADLINE if k in table}
     res = {"frame": a.frame, "chunk": chunk, "demod_group_bytes_per_launch": int(group),
            "demod_group_bytes_per_frame": int(group / chunk) if chunk else None,
            "algorithmic_bytes_per_frame": 12 * a.frame * a.frame,
+           "headline_bytes_per_frame": int(sum(headline.values())) if len(headline) == len(HEADLINE) else None,
+           "headline_kernels": headline,
+           "headline_algorithmic_bytes_per_frame": 8 * a.frame * a.frame,
            "per_kernel": table, "calibration": cal,
            "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes ({os.path.basename(a.dir)}: "
                      f"{'tools/kbench' if a.chunk else 'bench.py'}, largest launches per kernel); "
