@@ -92,10 +92,13 @@ def main():
             if chunk is None:
                 chunk = int(round(b["roofline"]["frames_per_launch"]))
             streams = int(b["config"].get("streams_per_chunk", 1))
-    # frames per kept launch: the demod kernels' largest launches are the roofline pass's
-    # whole chunks; the headline-only kernels run on each stream's share of the chunk
+    # frames per kept launch: the largest launches of every kernel are whole chunks (the
+    # roofline pass for the demod kernels; bench.py's stage-timed headline pass runs each
+    # chunk on one stream, so its headline kernels too: k_int_c2r writes exactly
+    # chunk x 4 N^2 bytes there)
+    del streams
     for k, t in table.items():
-        fpl = chunk if (k in DEMOD or a.chunk) else max(1, chunk // streams)
+        fpl = chunk
         t["frames_per_launch"] = fpl
         t["bytes_per_frame"] = (t["read_bytes_per_launch"] + t["write_bytes_per_launch"]) / fpl if fpl else None
     headline = {k: table[k]["bytes_per_frame"] for k in HEADLINE if k in table}
