@@ -385,155 +385,8 @@ __device__ __forceinline__ int2 team_scan_excl(int v, int t, int* scratch) {
 }
 
 // ------------------------------------------------------------------ I1
-// KMODE 0: phases = wrapped (unwrap=False); 1: residue-free scan unwrap + residue
-// census; 2: k-field from kin (Boruvka path for maps with residues).
-template <int W, int KMODE>
-__global__ __launch_bounds__(KCfg<W>::THREADS, FCD_MIN_WAVES) void k_int_rows(const float* __restrict__ wrapped, const int* __restrict__ colk,
-                                                    const int32_t* __restrict__ kin, int32_t* __restrict__ kout,
-                                                    int* __restrict__ rescount, int H, int nb,
-                                                    float2* __restrict__ Zt, const float2* __restrict__ tw) {
-    using C = KCfg<W>;
-    constexpr int TT = C::TT, E = C::E, TEAMS = C::TEAMS;
-    extern __shared__ __attribute__((aligned(16))) float2 lds_raw[];
-    float2* const lds = lds_raw + C::NLEN;  // lds_raw[0, NLEN): the twiddle table
-    const int team = threadIdx.x / TT, t = threadIdx.x % TT;
-    float2* s = lds + team * C::ROW;
-    int* scratch = reinterpret_cast<int*>(lds + TEAMS * C::ROW) + team * 8;
-    RegFFT<W> fft;
-    fft.init(tw, lds_raw, threadIdx.x, C::THREADS);
-    __syncthreads();
-    const int rbs = H / TILE;
-    const int j0 = t * E;  // this thread's blocked segment [j0, j0 + E)
-    for (int blk = blockIdx.x; blk < nb * rbs; blk += gridDim.x) {
-        const int f = blk / rbs, rb = blk % rbs;
-        int res[2] = {0, 0};
-        for (int rl = team; rl < TILE; rl += TEAMS) {
-            const int r = rb * TILE + rl;
-            float ph[2][E];
-#pragma unroll
-            for (int m = 0; m < 2; ++m) {
-                const float* wr = wrapped + (((long)f * 2 + m) * H + r) * W + j0;
-#pragma unroll
-                for (int j = 0; j < E; j += 4) {
-                    const float4 v = *reinterpret_cast<const float4*>(wr + j);
-                    ph[m][j] = v.x; ph[m][j + 1] = v.y; ph[m][j + 2] = v.z; ph[m][j + 3] = v.w;
-                }
-            }
-            if constexpr (KMODE == 1) {
-                float nxt[2];
-                int packed[E];
-#pragma unroll
-                for (int m = 0; m < 2; ++m) {
-                    const float* wr = wrapped + (((long)f * 2 + m) * H + r) * W;
-                    nxt[m] = (j0 + E < W) ? wr[j0 + E] : 0.f;
-                }
-                // residue census on the plaquettes (r, j)..(r+1, j+1)  (before the scan:
-                // keeps the k-field registers dead while the next row is in flight)
-#ifdef FCD_EXP_NO_RESIDUE
-                if (false) {
-#else
-                if (r + 1 < H) {
-#endif
-#pragma unroll
-                    for (int m = 0; m < 2; ++m) {
-                        const float* w1 = wrapped + (((long)f * 2 + m) * H + r + 1) * W;
-                        float lo[E + 1];
-#pragma unroll
-                        for (int j = 0; j < E; j += 4) {
-                            const float4 v = *reinterpret_cast<const float4*>(w1 + j0 + j);
-                            lo[j] = v.x; lo[j + 1] = v.y; lo[j + 2] = v.z; lo[j + 3] = v.w;
-                        }
-                        lo[E] = (j0 + E < W) ? w1[j0 + E] : 0.f;
-                        int cnt = 0;
-#pragma unroll
-                        for (int j = 0; j < E; ++j) {
-                            if (j0 + j + 1 < W) {
-                                const float a = ph[m][j], b = j + 1 < E ? ph[m][j + 1] : nxt[m];
-                                const float cc = lo[j + 1], d = lo[j];
-                                cnt += (fw_fast(a, b) + fw_fast(b, cc) + fw_fast(cc, d) + fw_fast(d, a)) != 0;
-                            }
-                        }
-                        res[m] += cnt;
-                    }
-                }
-                // d(j) = -find_wrap(w(j), w(j+1)), biased +1 and packed (map0 low, map1 high)
-                int run = 0;
-#pragma unroll
-                for (int j = 0; j < E; ++j) {
-                    int dd[2];
-#pragma unroll
-                    for (int m = 0; m < 2; ++m) {
-                        const float b = j + 1 < E ? ph[m][j + 1] : nxt[m];
-                        dd[m] = (j0 + j + 1 < W) ? -fw_fast(ph[m][j], b) : 0;
-                    }
-                    packed[j] = run;  // exclusive within the segment
-                    run += (dd[0] + 1) | ((dd[1] + 1) << 16);
-                }
-                const int2 sc = team_scan_excl<TT>(run, t, scratch);
-                int kk[2][E];
-#pragma unroll
-                for (int j = 0; j < E; ++j) {
-                    const int p = sc.x + packed[j];
-                    const int cnt = j0 + j;  // biased items before element j0 + j
-                    kk[0][j] = (p & 0xffff) - cnt;
-                    kk[1][j] = (p >> 16) - cnt;
-                }
-#pragma unroll
-                for (int m = 0; m < 2; ++m) {
-                    const int base = colk[((long)f * 2 + m) * H + r];
-#pragma unroll
-                    for (int j = 0; j < E; ++j) kk[m][j] += base;
-                }
-                if (kout) {
-#pragma unroll
-                    for (int m = 0; m < 2; ++m) {
-                        int32_t* ko = kout + (((long)f * 2 + m) * H + r) * W + j0;
-#pragma unroll
-                        for (int j = 0; j < E; j += 4)
-                            *reinterpret_cast<int4*>(ko + j) = make_int4(kk[m][j], kk[m][j + 1], kk[m][j + 2], kk[m][j + 3]);
-                    }
-                }
-#pragma unroll
-                for (int m = 0; m < 2; ++m)
-#pragma unroll
-                    for (int j = 0; j < E; ++j) ph[m][j] = fmaf((float)kk[m][j], kTwoPiF, ph[m][j]);
-            } else if constexpr (KMODE == 2) {
-#pragma unroll
-                for (int m = 0; m < 2; ++m) {
-                    const int32_t* ki = kin + (((long)f * 2 + m) * H + r) * W + j0;
-#pragma unroll
-                    for (int j = 0; j < E; ++j) ph[m][j] = (float)((double)ph[m][j] + 6.283185307179586 * (double)ki[j]);
-                }
-            }
-            // blocked (phi0, phi1) -> LDS -> natural layout -> forward row FFT
-            if constexpr (!Sched<W>::WAVE_LOCAL) __syncthreads();
-#pragma unroll
-            for (int j = 0; j < E; ++j) s[pad(j0 + j)] = make_float2(ph[0][j], ph[1][j]);
-            team_sync<W>();
-            float2 x[E];
-#pragma unroll
-            for (int q = 0; q < E; ++q) x[q] = s[pad(t + TT * q)];
-            fft.template run<false>(x, s, t);
-            float2* dst = Zt + (long)f * H * W;
-#pragma unroll
-            for (int q = 0; q < E; ++q) {
-#ifdef FCD_EXP_ZT_ROWMAJOR
-                dst[(long)r * W + t + TT * q] = x[q];  // timing experiment only (wrong layout)
-#else
-                st_stream(dst + tix(r, t + TT * q, W), x[q]);
-#endif
-            }
-        }
-        if constexpr (KMODE == 1) {
-#pragma unroll
-            for (int m = 0; m < 2; ++m) {
-                int v = res[m];
-                for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-                if ((threadIdx.x & 63) == 0 && v) atomicAdd(rescount + f * 2 + m, v);
-            }
-        }
-    }
-}
+// The row stage of the unfused chain (phases -> unwrap -> phi0 + i phi1 -> row FFT -> Zt)
+// is k_int_rows2 in int_rows.inc.
 
 // ------------------------------------------------------------------ I2
 template <int H>
@@ -574,7 +427,7 @@ __global__ __launch_bounds__(IntColsCfg<H>::THREADS, IntColsCfg<H>::V) void k_in
     float2 py[E], px[E];
     auto fetch_fc = [&](int f, int col, bool mirror, float2 (&v)[E]) {
         const int cc = mirror ? (W - col) & (W - 1) : col;
-        const float2* src = Zt + (long)f * H * W + ((long)cc << zts) + zt_lane;
+        const float2* src = Zt + (long)f * H * W + ((long)zt_col(cc, W) << zts) + zt_lane;
 #pragma unroll
         for (int q = 0; q < E; ++q) v[q] = src[q * zt_step];
     };

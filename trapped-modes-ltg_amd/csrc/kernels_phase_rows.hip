@@ -458,15 +458,15 @@ __global__ __launch_bounds__(PR_THREADS, FCD_PR_MINB) void k_phase_rows(
         PR_STAMP(9);
         __syncthreads();
         PR_STAMP(10);
-        // ---- whole 64-byte tile lines: Zt[f][rb][col][0..8)
-        {  // thread i writes column i / ROWS + 64 k, row i % ROWS
+        // ---- whole 64-byte tile lines: Zt[f][rb][j][0..8), j the mirror-paired column order
+        {  // thread i writes physical column i / ROWS + 64 k, row i % ROWS
             const int r0 = rb * PR_ROWS;
             float2* dst = Zt + (long)f * H * PR_W + (long)(r0 / PR_ZT) * PR_W * PR_ZT + (r0 % PR_ZT);
             const int c0 = threadIdx.x / PR_ROWS, rl = threadIdx.x % PR_ROWS;
             const float2* src = row_slot(rl, par ^ 1);
 #pragma unroll 4
             for (int k = 0; k < PR_W / 64; ++k) {
-                const float2 v = src[pad(c0 + 64 * k)];
+                const float2 v = src[pad(zt_col_inv(c0 + 64 * k, PR_W))];
                 if (!(FCD_PR_ABL & 2) || v.x == 1234.5f) st_stream(dst + (c0 + 64 * k) * PR_ZT + rl, v);  // 2: no Zt stores
             }
         }

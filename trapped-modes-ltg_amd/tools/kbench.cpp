@@ -100,7 +100,6 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(wrapped + nb * hw, fr.data(), fr.size() * 4, hipMemcpyHostToDevice));
     int* colk = dalloc<int>((size_t)nb * 2 * H);
     int* res = dalloc<int>((size_t)nb * 2);
-    int32_t* kbuf = dalloc<int32_t>((size_t)nb * 2 * hw);
     float2* Zt = dalloc<float2>((size_t)nb * hw);
     float2* Ht = dalloc<float2>((size_t)nb * H * (W / 2 + 1));
     const size_t irseam_bytes = fcdk::int_rows_seam_bytes(W, H, nb);  // one region per chain stream (<= 4)
