@@ -9,7 +9,7 @@ tag=${1:-traffic_kb}; N=${2:-1024}; nb=${3:-256}
 out=gpurun_out/$tag
 mkdir -p $out
 export TMPDIR=/tmp
-kb=trapped-modes-ltg_amd/tools/kbench
+kb=${KB:-trapped-modes-ltg_amd/tools/kbench}
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc $c -f csv -d $out/$c -o run -- $kb $N $nb 1 > $out/$c.log 2>&1 || { echo "pmc $c failed"; tail -5 $out/$c.log; exit 1; }
   echo "pmc $c done"

@@ -96,6 +96,9 @@ struct KCfg {
 #ifndef FCD_INTCOLS_PREF_X
 #define FCD_INTCOLS_PREF_X 1
 #endif
+#ifndef FCD_INTCOLS_QUADS
+#define FCD_INTCOLS_QUADS 1  // 4-row Zt tiles: sibling blocks on one XCD share each line's 4 columns
+#endif
 // Workgroup size of k_demod_cols up to 1024 points: 4 teams share one twiddle
 // table, 78 KB of LDS -> 2 workgroups = 16 waves per CU at 1024, which needs
 // <= 128 VGPRs, i.e. launch bounds of 4 waves per SIMD (compiles to 122):
@@ -431,34 +434,58 @@ __global__ __launch_bounds__(IntColsCfg<H>::THREADS, IntColsCfg<H>::V) void k_in
 #pragma unroll
         for (int q = 0; q < E; ++q) v[q] = src[q * zt_step];
     };
-    auto fetch_col = [&](int item, bool mirror, float2 (&v)[E]) {
-        const bool valid = item < items;
-        fetch_fc(valid ? item / NCH : 0, valid ? item % NCH : 0, mirror, v);
-    };
-    auto fetch = [&](int item) {
-        if constexpr (C::PREF_Y) fetch_col(item, true, py);
-        if constexpr (FCD_INTCOLS_PREF_X) fetch_col(item, false, px);
-    };
+    // Items are codes: frame code / CW, column code % CW (valid below NCH).
+    //
     // Each block walks a CONTIGUOUS range of columns: Zt's 8-row tiles hold a
     // column's rows in 64 bytes, half a 128-byte line whose other half is the
     // neighbouring column; the mirror columns W - c of consecutive items pair up
     // off by one, so grid-striding fetched every mirror line twice (1.5x the
     // compulsory Zt bytes).  In a contiguous range the neighbour is the next
     // iteration's item and its half line is still in L2.
-    const int per = (items + gridDim.x - 1) / gridDim.x;
-    const int i0 = blockIdx.x * per, i1 = min(i0 + per, items);
-    fetch(i0 + team < i1 ? i0 + team : items);
-    for (int base = i0; base < i1; base += TEAMS) {
-        const int item = base + team;
-        const bool valid = item < i1;
-        const int f = valid ? item / NCH : 0, col = valid ? item % NCH : 0;
+    //
+    // With 4-row Zt tiles (4096-point rows) a 128-byte line holds 4 columns x 4 rows,
+    // and a block's next column came too late: its lines had left the XCD's L2
+    // (3.9x the compulsory Zt reads, PMC r03t4096).  There the blocks work in QUADS:
+    // the 4 blocks of a group sit on one XCD (dispatch deals block b to XCD b % 8)
+    // and take columns 4k, 4k + 1, 4k + 2, 4k + 3 of the same quad at the same time.
+    const bool quad = zts == 2 && TEAMS == 1 && gridDim.x % 32 == 0 && FCD_INTCOLS_QUADS;
+    const int NQ = (NCH + 3) / 4;
+    const int CW = quad ? 4 * NQ : NCH;
+    int c0, cstep, cend;
+    if (quad) {
+        const int q = blockIdx.x / 8, j = q % 4;
+        const int grp = blockIdx.x % 8 + 8 * (q / 4), ngrp = gridDim.x / 4;
+        const int nquads = nb * NQ, perq = (nquads + ngrp - 1) / ngrp;
+        const int Q0 = min(grp * perq, nquads), Q1 = min(Q0 + perq, nquads);
+        c0 = 4 * Q0 + j;
+        cstep = 4;
+        cend = 4 * Q1;
+    } else {
+        const int per = (items + gridDim.x - 1) / gridDim.x;
+        c0 = min(blockIdx.x * per, items);
+        cstep = 1;
+        cend = min(c0 + per, items);
+    }
+    auto fetch_col = [&](int code, bool mirror, float2 (&v)[E]) {
+        const bool valid = code < cend && code % CW < NCH;
+        fetch_fc(valid ? code / CW : 0, valid ? code % CW : 0, mirror, v);
+    };
+    auto fetch = [&](int code) {
+        if constexpr (C::PREF_Y) fetch_col(code, true, py);
+        if constexpr (FCD_INTCOLS_PREF_X) fetch_col(code, false, px);
+    };
+    fetch(c0 + team * cstep);
+    for (int base = c0; base < cend; base += TEAMS * cstep) {
+        const int item = base + team * cstep;
+        const bool valid = item < cend && item % CW < NCH;
+        const int f = valid ? item / CW : 0, col = valid ? item % CW : 0;
         const int colm = (W - col) & (W - 1);
         // Z(-ky, -c) straight from the INVERSE-direction (unnormalised) transform of
         // column -c: sum_y z(y, -c) e^{+2 pi i ky y / H} at index ky, so both operands
         // of the Hermitian split sit in the same lane and slot (no mirror exchange).
         float2 x[E], y[E];
-        if constexpr (!C::PREF_Y) fetch_col(item < i1 ? item : items, true, py);
-        if constexpr (!FCD_INTCOLS_PREF_X) fetch_col(item < i1 ? item : items, false, px);
+        if constexpr (!C::PREF_Y) fetch_col(item, true, py);
+        if constexpr (!FCD_INTCOLS_PREF_X) fetch_col(item, false, px);
 #pragma unroll
         for (int q = 0; q < E; ++q) {
             y[q] = py[q];
@@ -479,7 +506,7 @@ __global__ __launch_bounds__(IntColsCfg<H>::THREADS, IntColsCfg<H>::V) void k_in
         // 3.94 vs 3.32 us/frame, kbench r02l; the next item's loads issued between them
         // hide better.  Pairing k_demod_cols' two inverse transforms: no change, r02m)
         fft.template run<true>(y, s, t);
-        if (base + TEAMS < i1) fetch(base + TEAMS + team < i1 ? base + TEAMS + team : items);
+        if (base + TEAMS * cstep < cend) fetch(base + (TEAMS + team) * cstep);
         fft.template run<false>(x, s, t);
         const float kx = c.kxe[col], kx2 = c.kx2[col];
         const float hnorm = 0.5f * c.norm;
