@@ -47,6 +47,8 @@ def main():
     ap.add_argument("dir")
     ap.add_argument("--frame", type=int, default=1024)
     ap.add_argument("--chunk", type=int, default=None, help="frames per launch (kbench runs: tools/traffic_kb.sh)")
+    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
+                    help="where to write the summary (bench.py reads profiles/traffic_latest.json: 1024^2 only)")
     a = ap.parse_args()
     known = 512 << 20
     cal = {}
@@ -113,7 +115,7 @@ def main():
                      f"{'tools/kbench' if a.chunk else 'bench.py'}, largest launches per kernel); "
                      "FETCH scaled by the membench 4/8-B-lane calibration, WRITE by the 4-B-lane one"}
     print(json.dumps(res, indent=1))
-    with open(os.path.join(ROOT, "profiles", "traffic_latest.json"), "w") as f:
+    with open(a.out, "w") as f:
         json.dump(res, f, indent=1)
 
 
