@@ -198,9 +198,9 @@ def test_unwrap_matches_oracle_random_residues(lib):
 @pytest.mark.parametrize("shape", [(256, 256), (128, 512)])
 def test_unwrap_two_level_equals_pixel_rounds(lib, monkeypatch, shape):
     """The two-level Boruvka (level-0 components from 64 x 64 tiles, 32 x 32 with
-    FCD_MST_TILE=32, or one pixel round with FCD_MST_LEVEL=1, then block-segmented
-    boundary / root lists) and the all-pixel
-    rounds (FCD_MST_LEVEL=0) build the same unique MST:
+    FCD_MST_TILE=32, then rounds on the contracted component graph; FCD_MST_LEVEL=2: the
+    tiles, then block-segmented boundary / root lists; =1: one pixel round, then the
+    lists) and the all-pixel rounds (FCD_MST_LEVEL=0) build the same unique MST:
     identical k-fields, bit for bit, over a batch of maps with thousands of residues
     (several maps per list segment, segments spanning maps), and equal to the oracle."""
     from oracle import fcd_oracle as O
@@ -218,7 +218,7 @@ def test_unwrap_two_level_equals_pixel_rounds(lib, monkeypatch, shape):
     k1, _ = eng.unwrap(w)
     assert np.array_equal(k1, k2), "32 x 32 tiles"
     monkeypatch.delenv("FCD_MST_TILE")
-    for level in ("0", "1"):  # all-pixel rounds; one pixel round before the list rounds
+    for level in ("0", "1", "2"):  # all-pixel rounds; pixel round / tiles before the list rounds
         monkeypatch.setenv("FCD_MST_LEVEL", level)
         k1, _ = eng.unwrap(w)
         assert np.array_equal(k1, k2), level

@@ -213,6 +213,7 @@ struct fcd_ctx {
     // MST workspace
     DevBuf mst_comp, mst_off, mst_rel, mst_cw, mst_ce, mst_bw, mst_be, mst_link, mst_hooks, mst_ids;
     DevBuf mst_rootof, mst_offk, mst_lb0, mst_lb1, mst_lr0, mst_lr1, mst_ll0, mst_cnt, mst_mb0, mst_mb1;  // two-level rounds
+    DevBuf cg_ncomp, cg_ecnt, cg_ea, cg_eb, cg_ew, cg_ec, cg_ed;  // component-graph rounds
     size_t mst_cap = 0;
 
     // stage timing: 4 events per chunk (start, after demod, after unwrap, after integrate)
@@ -259,7 +260,14 @@ void ensure_mst(fcd_ctx* c, int nact) {
     c->mst_bw.ensure(nv * 8);
     c->mst_be.ensure(nv * 4);
     c->mst_link.ensure(nv * 8);
-    c->mst_hooks.ensure(sizeof(int));
+    c->mst_hooks.ensure(2 * sizeof(int));  // hooks this round; component-graph overflow flag
+    // edge records for any tile side (FCD_MST_TILE may change between calls on the same buffers)
+    const size_t ne = (size_t)fcdk::mst_cg_edge_capacity((long)nv);
+    const size_t nt = (size_t)nact * c->hw() / 1024 + 1;  // tiles (32 x 32 at the smallest)
+    c->cg_ncomp.ensure(nt * 4);
+    c->cg_ecnt.ensure(nt * 4);
+    for (DevBuf* b : {&c->cg_ea, &c->cg_eb, &c->cg_ec, &c->cg_ed}) b->ensure(ne * 4);
+    c->cg_ew.ensure(ne * 8);
     for (DevBuf* b : {&c->mst_rootof, &c->mst_offk, &c->mst_lb0, &c->mst_lb1, &c->mst_lr0, &c->mst_lr1, &c->mst_ll0})
         b->ensure(nv * 4);
     c->mst_cnt.ensure((size_t)fcdk::mst_level_counts() * sizeof(int));
@@ -290,6 +298,13 @@ fcdk::MstWork mst_work(fcd_ctx* c) {
     m.cnt = c->mst_cnt.as<int>();
     m.maskB[0] = c->mst_mb0.as<unsigned char>();
     m.maskB[1] = c->mst_mb1.as<unsigned char>();
+    m.cg_ncomp = c->cg_ncomp.as<int>();
+    m.cg_ecnt = c->cg_ecnt.as<int>();
+    m.cg_ea = c->cg_ea.as<int>();
+    m.cg_eb = c->cg_eb.as<int>();
+    m.cg_ew = c->cg_ew.as<unsigned long long>();
+    m.cg_ec = c->cg_ec.as<int>();
+    m.cg_ed = c->cg_ed.as<int>();
     return m;
 }
 
@@ -313,12 +328,13 @@ void demod_phases(fcd_ctx* c, const float2* spec, int nb, float* wrapped, hipStr
     }
 }
 
-// The exact pass builds level-0 components inside 32 x 32 tiles and then runs the
-// two-level rounds (kernels_unwrap.hip).  FCD_MST_LEVEL=1: one pixel round instead of
-// the tiles; 0: every round at pixel level (both for A/B checks).
+// The exact pass builds level-0 components inside 64 x 64 tiles and then runs Boruvka
+// rounds on their contracted graph (kernels_unwrap.hip).  FCD_MST_LEVEL (A/B checks):
+// 2: the tiles, then rounds over the boundary-pixel lists; 1: one pixel round instead
+// of the tiles, then the list rounds; 0: every round at pixel level.
 int mst_level() {
     const char* e = std::getenv("FCD_MST_LEVEL");
-    return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : 2;
+    return e && e[0] >= '0' && e[0] <= '2' && !e[1] ? e[0] - '0' : 3;
 }
 
 // k-fields of nmaps wrapped maps (skimage unwrap_phase, fcd.py:119).  Synchronises.
@@ -352,7 +368,52 @@ void unwrap_maps(fcd_ctx* c, const float* w, int nmaps, int32_t* k, int* res_hos
     int rounds = 0;
     // Boruvka halves the component count every round; check convergence every
     // third round (a round after convergence hooks nothing and changes nothing).
-    const int level = mst_level();
+    int level = mst_level();
+    if (level == 3 && fcdk::mst_tile_side(c->H, c->W) > 0) {
+        HIPCHK(hipMemsetAsync(m.nhooks + 1, 0, sizeof(int), s));
+        fcdk::mst_tile_level0(w, c->mst_ids.as<int>(), nact, c->H, c->W, m, s, true);
+        bool fits = true;
+        static const bool cg_dbg = std::getenv("FCD_MST_DEBUG") != nullptr;
+        auto cg_dump = [&](int r) {  // diagnostic: components and contracted edges entering round r
+            const int t0 = fcdk::mst_tile_side(c->H, c->W);
+            const size_t nt = (size_t)nact * (c->H / t0) * (c->W / t0);
+            std::vector<int> nc(nt), ne(nt);
+            HIPCHK(hipMemcpyAsync(nc.data(), m.cg_ncomp, nt * 4, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(ne.data(), m.cg_ecnt, nt * 4, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+            long sc = 0, se = 0;
+            int mc = 0, me = 0;
+            for (size_t t = 0; t < nt; ++t) {
+                sc += nc[t];
+                se += ne[t];
+                mc = std::max(mc, nc[t]);
+                me = std::max(me, ne[t]);
+            }
+            std::fprintf(stderr, "[mst-cg] tiles %zu round %d: level-0 components %ld (max/tile %d), edges %ld (max/tile %d)\n",
+                         nt, r, sc, mc, se, me);
+        };
+        for (; rounds < max_rounds; rounds += 3) {
+            for (int g = 0; g < 3; ++g) {
+                if (cg_dbg) cg_dump(rounds + g);
+                fcdk::mst_cg_round(nact, c->H, c->W, m, rounds + g, s);
+            }
+            int flags[2] = {0, 0};  // hooks in the last round, a tile graph over its capacity
+            HIPCHK(hipMemcpyAsync(flags, m.nhooks, sizeof(flags), hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+            if (flags[1]) {
+                fits = false;
+                break;
+            }
+            if (flags[0] == 0) break;
+        }
+        if (fits) {
+            if (rounds >= max_rounds) throw FcdError(FCD_E_INTERNAL, "unwrap: Boruvka did not converge");
+            fcdk::mst_level_finalize(c->mst_ids.as<int>(), nact, c->H, c->W, m, k, s);
+            return;
+        }
+        level = 2;  // the boundary-list rounds need no capacity bound
+        rounds = 0;
+    }
     if (level >= 1) {
         if (level >= 2 && fcdk::mst_tile_side(c->H, c->W) > 0) {
             // level-0 components from Boruvka inside 32 x 32 tiles (LDS)

@@ -159,6 +159,10 @@ struct MstWork {
     // the level-0 root list, all segmented by block; cnt: mst_level_counts() ints
     int* rootof; int* offk; int* listB[2]; int* listR[2]; int* listL0; int* cnt;
     unsigned char* maskB[2];  // per boundary entry: its neighbours still outside its component
+    // component-graph rounds (mst_cg_round): per tile its level-0 component count and
+    // contracted-edge count, the edge records (SoA) in per-tile segments; nhooks[1]:
+    // set if a tile's graph did not fit (never, by the planar bound; the host falls back)
+    int* cg_ncomp; int* cg_ecnt; int* cg_ea; int* cg_eb; unsigned long long* cg_ew; int* cg_ec; int* cg_ed;
 };
 // Maps listed in map_ids (device int[nact]) of the wrapped stack w.
 void mst_init(const float* w, const int* map_ids, int nact, int H, int W, MstWork m, hipStream_t s);
@@ -173,7 +177,13 @@ int mst_level_counts();
 // Level-0 components from Boruvka inside each 32 x 32 tile (LDS), with the
 // reliabilities; replaces mst_init + the first pixel round before mst_level_setup.
 int mst_tile_side(int H, int W);  // 64, 32, or 0: no tile pass
-void mst_tile_level0(const float* w, const int* map_ids, int nact, int H, int W, MstWork m, hipStream_t s);
+// graph: write the tile's contracted component graph for mst_cg_round instead of the
+// per-pixel state of the boundary-list rounds (mst_level_setup / mst_level_round).
+void mst_tile_level0(const float* w, const int* map_ids, int nact, int H, int W, MstWork m, hipStream_t s,
+                     bool graph = false);
+long mst_cg_edge_capacity(long nv);  // edge records for nv vertices (any tile side)
+// Round r of the component-graph Boruvka (r = 0 first: resolves the cross-tile edges).
+void mst_cg_round(int nact, int H, int W, MstWork m, int r, hipStream_t s);
 void mst_level_setup(int nact, int H, int W, MstWork m, hipStream_t s);
 void mst_level_round(const float* w, const int* map_ids, int nact, int H, int W, MstWork m, int r, hipStream_t s);
 void mst_level_finalize(const int* map_ids, int nact, int H, int W, MstWork m, int32_t* k, hipStream_t s);

@@ -804,7 +804,185 @@ __device__ __forceinline__ unsigned t0_link(int parent, int off) { return ((unsi
 __device__ __forceinline__ int t0_parent(unsigned l) { return (int)(l >> 16); }
 __device__ __forceinline__ int t0_off(unsigned l) { return (int)(short)(l & 0xffffu); }
 
+// ------------------------------------------------------------------ component graph
+// The level rounds after the tile pass on the CONTRACTED graph: nodes are the level-0
+// components, edges the lightest edge between each pair of adjacent components
+// (contracting subtrees of the MST keeps the MST: of parallel edges between two
+// components only the lightest (weight, edge index) can be in it, by the cycle property
+// of the contracted graph).  When a tile's Boruvka stops, every component's lightest
+// edge leaves the tile, so every component holds a tile-border pixel: V <= 4 T0 - 4
+// components, and the contracted tile graph is planar, so at most 3 V - 6 distinct
+// adjacent pairs inside the tile, plus the 2 T0 edges leaving it to the right and
+// downwards (the other two sides are the neighbours' right / down edges).  Hence the
+// fixed per-tile capacities below and an LDS hash table that never fills.
+//
+// Per tile tg (= blockIdx.x of the tile pass): components tg * CG_CCAP + rank, edges in
+// [tg * cg_ecap, + cg_ecnt[tg]) as records (ea, eb, weight bits, global edge index,
+// ed = K_ea - K_eb from the pixel offsets and the edge's wrap count).  An edge to a
+// neighbour tile is written with eb = -1 - (neighbour pixel's vertex id) and the
+// neighbour's offset missing; the first round resolves it (comp[], off[] of the pixel).
+__host__ __device__ constexpr int cg_ccap(int T0) { return 4 * T0; }
+__host__ __device__ constexpr int cg_ecap(int T0) { return T0 == 64 ? 1024 : 512; }
+static_assert(3 * (4 * 64 - 4) - 6 + 2 * 64 <= cg_ecap(64) && 3 * (4 * 32 - 4) - 6 + 2 * 32 <= cg_ecap(32),
+              "planar bound on a tile's contracted edges");
+
+__device__ __forceinline__ void cg_write_edge(MstWork& m, long e, int ea, int eb, unsigned long long ew, int ec, int ed) {
+    m.cg_ea[e] = ea;
+    m.cg_eb[e] = eb;
+    m.cg_ew[e] = ew;
+    m.cg_ec[e] = ec;
+    m.cg_ed[e] = ed;
+}
+
+// Positions in a block-wide list for N predicates per lane: one LDS atomic per wave
+// (a block_append per predicate serialised ~200 atomics per tile on one word).
+template <int N>
+__device__ __forceinline__ void wave_append(const bool (&pred)[N], int* lds_counter, int (&pos)[N]) {
+    unsigned long long b[N];
+    int tot = 0;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        b[j] = __ballot(pred[j]);
+        tot += __popcll(b[j]);
+    }
+    const int lane = threadIdx.x & 63;
+    int base = 0;
+    if (tot) {  // wave-uniform
+        if (lane == 0) base = atomicAdd(lds_counter, tot);
+        base = __shfl(base, 0, 64);
+    }
+    const unsigned long long lt = (1ull << lane) - 1;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        pos[j] = pred[j] ? base + __popcll(b[j] & lt) : -1;
+        base += __popcll(b[j]);
+    }
+}
+
+// After the tile's rounds: lc / lo (labels, offsets) valid, the rest of the pool free.
 template <int T0>
+__device__ __forceinline__ void tile0_graph(unsigned char* pool, const unsigned long long (&ekey)[4][4], unsigned incs,
+                                            int H, int W, int gi0, int gj0, long vbase, MstWork& m) {
+    constexpr int T0N = T0 * T0, NT = T0N / 4;
+    constexpr int HS = T0 == 64 ? 2048 : 512;  // hash slots: >= 2.7x the pairs a tile can have
+    constexpr int HB = T0 == 64 ? 11 : 9;
+    constexpr int ECAP = cg_ecap(T0);
+    static_assert(16 * HS <= 8 * T0N, "hash table in the minimum-weight region");
+    unsigned* const hkey = reinterpret_cast<unsigned*>(pool);  // pair (a, b), a < b, + 1; 0: empty
+    unsigned* const hcode = hkey + HS;
+    unsigned long long* const hwt = reinterpret_cast<unsigned long long*>(pool + 8 * HS);
+    int* const rk = reinterpret_cast<int*>(pool + 8 * T0N);  // rank of each root (the links' region)
+    const short* const lc = reinterpret_cast<const short*>(pool + 12 * T0N);
+    const short* const lo = reinterpret_cast<const short*>(pool + 14 * T0N);
+    __shared__ int ncnt[2];  // roots, edges
+    if (threadIdx.x == 0) ncnt[0] = ncnt[1] = 0;
+    for (int i = threadIdx.x; i < HS; i += NT) {
+        hkey[i] = 0u;
+        hcode[i] = 0x7fffffffu;
+        hwt[i] = ~0ull;
+    }
+    __syncthreads();
+    {
+        bool root[4];
+        int r[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) root[k] = lc[threadIdx.x + NT * k] == threadIdx.x + NT * k;
+        wave_append(root, &ncnt[0], r);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (r[k] >= 0) rk[threadIdx.x + NT * k] = r[k];
+    }
+    __syncthreads();
+    const long tg = blockIdx.x;
+    const int cb = (int)(tg * cg_ccap(T0));
+    const long eb0 = tg * ECAP;
+    const int nh = H * (W - 1);
+    int slot[8], code[8];
+    bool cross[8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int i = threadIdx.x + NT * k;
+        const int li = i / T0, lj = i % T0, gi = gi0 + li, gj = gj0 + lj;
+        const long v = vbase + (long)gi * W + gj;
+        const int c = lc[i];
+        const int id = cb + rk[c];
+        m.comp[v] = id;
+        m.off[v] = lo[i];
+        if (c == i) {
+            m.rootof[id] = id;
+            m.offk[id] = 0;
+            m.link[id] = pack_link(id, 0);
+            m.best_w[id] = 0x7ff0000000000000ull;
+            m.best_e[id] = 0x7fffffff;
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {  // h = 0: right edge (d = 0), 1: down edge (d = 2)
+            const int j = 2 * k + h;
+            const bool exists = ekey[k][2 * h] != ~0ull;
+            const int ni = li + h, nj = lj + 1 - h;
+            const bool inside = ni < T0 && nj < T0;
+            code[j] = h ? nh + gi * W + gj : gi * (W - 1) + gj;
+            cross[j] = exists && !inside;  // into the neighbour tile: resolved by the first round
+            slot[j] = -1;
+            if (!exists || !inside) continue;
+            const int cy = lc[ni * T0 + nj];
+            if (cy == c) continue;
+            const unsigned key = ((unsigned)min(c, cy) << 12 | (unsigned)max(c, cy)) + 1u;
+            unsigned hs = (key * 2654435761u) >> (32 - HB);
+            for (int probe = 0; probe < HS; ++probe, hs = (hs + 1) & (HS - 1)) {
+                const unsigned cur = hkey[hs];
+                if (cur == key || (cur == 0u && (atomicCAS(hkey + hs, 0u, key) == 0u || hkey[hs] == key))) {
+                    slot[j] = (int)hs;
+                    break;
+                }
+            }
+            if (slot[j] < 0) atomicOr(m.nhooks + 1, 1);  // cannot happen (planar bound); the host falls back
+            else if (ekey[k][2 * h] < hwt[slot[j]]) atomicMin(hwt + slot[j], ekey[k][2 * h]);
+        }
+    }
+    {
+        int pos[8];
+        wave_append(cross, &ncnt[1], pos);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if (pos[j] < 0 || pos[j] >= ECAP) continue;
+            const int k = j >> 1, h = j & 1, i = threadIdx.x + NT * k;
+            const long v = vbase + (long)(gi0 + i / T0) * W + gj0 + i % T0;
+            const int delta = -((int)((incs >> (8 * k + 4 * h)) & 3u) - 1);  // k(y) - k(x)
+            cg_write_edge(m, eb0 + pos[j], cb + rk[lc[i]], (int)(-1 - (v + (h ? W : 1))), ekey[k][2 * h], code[j],
+                          -lo[i] - delta);
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        if (slot[j] >= 0 && hwt[slot[j]] == ekey[j >> 1][2 * (j & 1)]) atomicMin(hcode + slot[j], (unsigned)code[j]);
+    __syncthreads();
+    {
+        bool win[8];
+        int pos[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            win[j] = slot[j] >= 0 && hwt[slot[j]] == ekey[j >> 1][2 * (j & 1)] && hcode[slot[j]] == (unsigned)code[j];
+        wave_append(win, &ncnt[1], pos);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if (pos[j] < 0 || pos[j] >= ECAP) continue;
+            const int k = j >> 1, h = j & 1, i = threadIdx.x + NT * k, li = i / T0, lj = i % T0;
+            const int y = (li + h) * T0 + lj + 1 - h;
+            const int delta = -((int)((incs >> (8 * k + 4 * h)) & 3u) - 1);
+            cg_write_edge(m, eb0 + pos[j], cb + rk[lc[i]], cb + rk[lc[y]], ekey[k][2 * h], code[j], lo[y] - lo[i] - delta);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        m.cg_ncomp[tg] = ncnt[0];
+        m.cg_ecnt[tg] = min(ncnt[1], ECAP);
+        if (ncnt[1] > ECAP || ncnt[0] > cg_ccap(T0)) atomicOr(m.nhooks + 1, 1);
+    }
+}
+
+template <int T0, bool CG>
 __global__ __launch_bounds__(T0 * T0 / 4) void k_mst_tile0(const float* __restrict__ w, const int* __restrict__ map_ids,
                                                           int nact, int H, int W, MstWork m) {
     constexpr int T0N = T0 * T0;  // pixels per tile
@@ -869,7 +1047,7 @@ __global__ __launch_bounds__(T0 * T0 / 4) void k_mst_tile0(const float* __restri
             r = s;
         }
         rs[i] = r;
-        if (li >= 1 && li <= T0 && lj >= 1 && lj <= T0) m.rel[vbase + (long)gi * W + gj] = r;
+        if (!CG && li >= 1 && li <= T0 && lj >= 1 && lj <= T0) m.rel[vbase + (long)gi * W + gj] = r;
     }
     __syncthreads();
     T0_STAMP(0);
@@ -1025,6 +1203,9 @@ __global__ __launch_bounds__(T0 * T0 / 4) void k_mst_tile0(const float* __restri
         __syncthreads();
         T0_STAMP(6);
     }
+    if constexpr (CG) {
+        tile0_graph<T0>(pool, ekey, incs, H, W, gi0, gj0, vbase, m);
+    } else {
     // level-0 components: global ids of the tile roots, offsets to them; candidate
     // slots of every pixel reset for the level rounds
 #pragma unroll
@@ -1038,6 +1219,7 @@ __global__ __launch_bounds__(T0 * T0 / 4) void k_mst_tile0(const float* __restri
         m.best_w[v] = 0x7ff0000000000000ull;
         m.best_e[v] = 0x7fffffff;
     }
+    }
 #ifdef FCD_T0_STAMPS
     T0_STAMP(7);
     if (blockIdx.x < 256 && threadIdx.x == 0) {
@@ -1045,6 +1227,160 @@ __global__ __launch_bounds__(T0 * T0 / 4) void k_mst_tile0(const float* __restri
         g_t0_stamps[blockIdx.x * 9 + 8] = nrounds;
     }
 #endif
+}
+
+// ---- component-graph rounds: over each tile's edge segment (edges), then over each
+// tile's level-0 components (relabel).  Same weights, tie-break and hook rule as the
+// pixel rounds, so the same unique MST and k-field.
+constexpr int CG_U = 4;  // edges per thread: cg_ecap <= 1024 = 256 threads x CG_U
+static_assert(cg_ecap(64) <= 256 * CG_U, "one pass over a segment");
+
+// Candidates: per edge between different current roots, atomicMin of its weight into
+// both roots; the segment is compacted in place (edges inside a root are gone for good).
+template <bool FIRST>
+__global__ __launch_bounds__(256) void k_cg_cand(MstWork m, int ntiles, int ecap) {
+    __shared__ int nout;
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        if (threadIdx.x == 0) nout = 0;
+        __syncthreads();
+        const int n = m.cg_ecnt[t];
+        const long b0 = (long)t * ecap;
+        int ea[CG_U], eb[CG_U], ec[CG_U], ed[CG_U], ra[CG_U], rb[CG_U];
+        unsigned long long ew[CG_U];
+        bool keep[CG_U];
+#pragma unroll
+        for (int u = 0; u < CG_U; ++u) {
+            const int i = u * 256 + threadIdx.x;
+            keep[u] = i < n;
+            ea[u] = eb[u] = ec[u] = ed[u] = 0;
+            ew[u] = 0;
+            if (keep[u]) {
+                ea[u] = m.cg_ea[b0 + i];
+                eb[u] = m.cg_eb[b0 + i];
+                ew[u] = m.cg_ew[b0 + i];
+                ec[u] = m.cg_ec[b0 + i];
+                ed[u] = m.cg_ed[b0 + i];
+                if (FIRST && eb[u] < 0) {  // an edge into the neighbour tile: its component now
+                    const long y = -1 - (long)eb[u];
+                    eb[u] = m.comp[y];
+                    ed[u] += m.off[y];
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < CG_U; ++u) {
+            ra[u] = keep[u] ? m.rootof[ea[u]] : 0;
+            rb[u] = keep[u] ? m.rootof[eb[u]] : 0;
+            keep[u] = keep[u] && ra[u] != rb[u];
+        }
+        __syncthreads();  // every entry read before the survivors are written back
+#pragma unroll
+        for (int u = 0; u < CG_U; ++u) {
+            const int pos = block_append(keep[u], &nout);
+            if (pos < 0) continue;
+            if (FIRST || pos != u * 256 + (int)threadIdx.x) cg_write_edge(m, b0 + pos, ea[u], eb[u], ew[u], ec[u], ed[u]);
+            atomicMin(m.best_w + ra[u], ew[u]);
+            atomicMin(m.best_w + rb[u], ew[u]);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) m.cg_ecnt[t] = nout;
+    }
+}
+
+// Edge-index tie-break among each root's edges of minimum weight.
+__global__ __launch_bounds__(256) void k_cg_cand2(MstWork m, int ntiles, int ecap) {
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const int n = m.cg_ecnt[t];
+        const long b0 = (long)t * ecap;
+        for (int i = threadIdx.x; i < n; i += 256) {
+            const unsigned long long w = m.cg_ew[b0 + i];
+            const int ra = m.rootof[m.cg_ea[b0 + i]], rb = m.rootof[m.cg_eb[b0 + i]], c = m.cg_ec[b0 + i];
+            if (m.best_w[ra] == w) atomicMin(m.best_e + ra, c);
+            if (m.best_w[rb] == w) atomicMin(m.best_e + rb, c);
+        }
+    }
+}
+
+// Hooks: the (unique) edge that is a root's lightest links it to the other root;
+// of a mutual pair the larger root hooks onto the smaller.
+__global__ __launch_bounds__(256) void k_cg_hook(MstWork m, int ntiles, int ecap) {
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const int n = m.cg_ecnt[t];
+        const long b0 = (long)t * ecap;
+        for (int base = 0; base < n; base += 256) {
+            const int i = base + threadIdx.x;
+            bool hooked = false;
+            if (i < n) {
+                const unsigned long long w = m.cg_ew[b0 + i];
+                const int a = m.cg_ea[b0 + i], b = m.cg_eb[b0 + i], c = m.cg_ec[b0 + i];
+                const int ra = m.rootof[a], rb = m.rootof[b];
+                const bool wa = m.best_w[ra] == w && m.best_e[ra] == c;
+                const bool wb = m.best_w[rb] == w && m.best_e[rb] == c;
+                if (wa || wb) {
+                    const int kab = m.cg_ed[b0 + i] - m.offk[a] + m.offk[b];  // K_ra - K_rb
+                    if (wa && (!wb || ra > rb)) m.link[ra] = pack_link(rb, kab);
+                    else m.link[rb] = pack_link(ra, -kab);
+                    hooked = true;
+                }
+            }
+            count_hook(hooked, m.nhooks);
+        }
+    }
+}
+
+// Every level-0 component to its new root (pointer jumping with path compression,
+// as k_mst_jump: a root's link is only ever replaced by a link to a further ancestor
+// with the offsets summed); the roots reset their candidate slots.
+__global__ __launch_bounds__(256) void k_cg_relabel(MstWork m, int ntiles, int ccap) {
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const int n = m.cg_ncomp[t];
+        for (int i = threadIdx.x; i < n; i += 256) {
+            const int c = t * ccap + i;
+            const int r = m.rootof[c];
+            const unsigned long long l = __hip_atomic_load(m.link + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            int p = link_parent(l);
+            if (p != r) {
+                int o = link_off(l);
+                for (;;) {
+                    const unsigned long long l2 = __hip_atomic_load(m.link + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const int pp = link_parent(l2);
+                    if (pp == p) break;
+                    o += link_off(l2);
+                    p = pp;
+                    __hip_atomic_store(m.link + r, pack_link(p, o), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                m.rootof[c] = p;
+                m.offk[c] += o;
+            }
+            if (p == c) {
+                m.best_w[c] = 0x7ff0000000000000ull;
+                m.best_e[c] = 0x7fffffff;
+            }
+        }
+    }
+}
+
+long mst_cg_edge_capacity(long nv) { return nv / 2 + 1024; }
+static_assert(cg_ecap(32) * 2 <= 32 * 32 && cg_ecap(64) * 2 <= 64 * 64, "edge records: nv / 2 covers every tile side");
+
+void mst_cg_round(int nact, int H, int W, MstWork m, int r, hipStream_t s) {
+    const int t0 = mst_tile_side(H, W);
+    if (!t0) throw std::runtime_error("mst_cg_round: frame not a multiple of the tile");
+    const int ntiles = nact * (H / t0) * (W / t0);
+    const int ecap = cg_ecap(t0), ccap = cg_ccap(t0);
+    FCD_HIPCHK(hipMemsetAsync(m.nhooks, 0, sizeof(int), s));
+    const dim3 g((unsigned)std::min(ntiles, 4096)), b(256);
+    if (r == 0)
+        hipLaunchKernelGGL(k_cg_cand<true>, g, b, 0, s, m, ntiles, ecap);
+    else
+        hipLaunchKernelGGL(k_cg_cand<false>, g, b, 0, s, m, ntiles, ecap);
+    FCD_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_cg_cand2, g, b, 0, s, m, ntiles, ecap);
+    FCD_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_cg_hook, g, b, 0, s, m, ntiles, ecap);
+    FCD_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_cg_relabel, g, b, 0, s, m, ntiles, ccap);
+    FCD_CHECK_LAUNCH();
 }
 
 int mst_tile_side(int H, int W) {
@@ -1055,14 +1391,19 @@ int mst_tile_side(int H, int W) {
     return 0;
 }
 
-void mst_tile_level0(const float* w, const int* map_ids, int nact, int H, int W, MstWork m, hipStream_t s) {
+void mst_tile_level0(const float* w, const int* map_ids, int nact, int H, int W, MstWork m, hipStream_t s, bool graph) {
     const int t = mst_tile_side(H, W);
     if (!t) throw std::runtime_error("mst_tile_level0: frame not a multiple of the tile");
     const long nblocks = (long)nact * (H / t) * (W / t);
-    if (t == 64)
-        hipLaunchKernelGGL(k_mst_tile0<64>, dim3((unsigned)nblocks), dim3(1024), 0, s, w, map_ids, nact, H, W, m);
+    const dim3 g((unsigned)nblocks);
+    if (t == 64 && graph)
+        hipLaunchKernelGGL((k_mst_tile0<64, true>), g, dim3(1024), 0, s, w, map_ids, nact, H, W, m);
+    else if (t == 64)
+        hipLaunchKernelGGL((k_mst_tile0<64, false>), g, dim3(1024), 0, s, w, map_ids, nact, H, W, m);
+    else if (graph)
+        hipLaunchKernelGGL((k_mst_tile0<32, true>), g, dim3(256), 0, s, w, map_ids, nact, H, W, m);
     else
-        hipLaunchKernelGGL(k_mst_tile0<32>, dim3((unsigned)nblocks), dim3(256), 0, s, w, map_ids, nact, H, W, m);
+        hipLaunchKernelGGL((k_mst_tile0<32, false>), g, dim3(256), 0, s, w, map_ids, nact, H, W, m);
     FCD_CHECK_LAUNCH();
 }
 
