@@ -197,8 +197,8 @@ def test_unwrap_matches_oracle_random_residues(lib):
 
 @pytest.mark.parametrize("shape", [(256, 256), (128, 512)])
 def test_unwrap_two_level_equals_pixel_rounds(lib, monkeypatch, shape):
-    """The two-level Boruvka (level-0 components from 64 x 64 tiles, 32 x 32 with
-    FCD_MST_TILE=32, then rounds on the contracted component graph; FCD_MST_LEVEL=2: the
+    """The two-level Boruvka (level-0 components from 64 x 64 tiles, 32 x 32 or 64 x 32
+    with FCD_MST_TILE=32 / 6432, then rounds on the contracted component graph; FCD_MST_LEVEL=2: the
     tiles, then block-segmented boundary / root lists; =1: one pixel round, then the
     lists) and the all-pixel rounds (FCD_MST_LEVEL=0) build the same unique MST:
     identical k-fields, bit for bit, over a batch of maps with thousands of residues
@@ -214,9 +214,14 @@ def test_unwrap_two_level_equals_pixel_rounds(lib, monkeypatch, shape):
     eng = lib.Engine(shape)
     k2, res = eng.unwrap(w)
     assert (res > 0).all() and res.sum() > 5000
-    monkeypatch.setenv("FCD_MST_TILE", "32")
-    k1, _ = eng.unwrap(w)
-    assert np.array_equal(k1, k2), "32 x 32 tiles"
+    for tile in ("32", "6432"):  # 32 x 32, 64 wide x 32 tall
+        monkeypatch.setenv("FCD_MST_TILE", tile)
+        k1, _ = eng.unwrap(w)
+        assert np.array_equal(k1, k2), tile
+        monkeypatch.setenv("FCD_MST_LEVEL", "2")
+        k1, _ = eng.unwrap(w)
+        assert np.array_equal(k1, k2), (tile, "boundary lists")
+        monkeypatch.delenv("FCD_MST_LEVEL")
     monkeypatch.delenv("FCD_MST_TILE")
     for level in ("0", "1", "2"):  # all-pixel rounds; pixel round / tiles before the list rounds
         monkeypatch.setenv("FCD_MST_LEVEL", level)

@@ -369,14 +369,15 @@ void unwrap_maps(fcd_ctx* c, const float* w, int nmaps, int32_t* k, int* res_hos
     // Boruvka halves the component count every round; check convergence every
     // third round (a round after convergence hooks nothing and changes nothing).
     int level = mst_level();
-    if (level == 3 && fcdk::mst_tile_side(c->H, c->W) > 0) {
+    int tile_h = 0;
+    const int tile_w = fcdk::mst_tile_shape(c->H, c->W, &tile_h);
+    if (level == 3 && tile_w > 0) {
         HIPCHK(hipMemsetAsync(m.nhooks + 1, 0, sizeof(int), s));
         fcdk::mst_tile_level0(w, c->mst_ids.as<int>(), nact, c->H, c->W, m, s, true);
         bool fits = true;
         static const bool cg_dbg = std::getenv("FCD_MST_DEBUG") != nullptr;
         auto cg_dump = [&](int r) {  // diagnostic: components and contracted edges entering round r
-            const int t0 = fcdk::mst_tile_side(c->H, c->W);
-            const size_t nt = (size_t)nact * (c->H / t0) * (c->W / t0);
+            const size_t nt = (size_t)nact * (c->H / tile_h) * (c->W / tile_w);
             std::vector<int> nc(nt), ne(nt);
             HIPCHK(hipMemcpyAsync(nc.data(), m.cg_ncomp, nt * 4, hipMemcpyDeviceToHost, s));
             HIPCHK(hipMemcpyAsync(ne.data(), m.cg_ecnt, nt * 4, hipMemcpyDeviceToHost, s));
@@ -415,7 +416,7 @@ void unwrap_maps(fcd_ctx* c, const float* w, int nmaps, int32_t* k, int* res_hos
         rounds = 0;
     }
     if (level >= 1) {
-        if (level >= 2 && fcdk::mst_tile_side(c->H, c->W) > 0) {
+        if (level >= 2 && tile_w > 0) {
             // level-0 components from Boruvka inside 32 x 32 tiles (LDS)
             fcdk::mst_tile_level0(w, c->mst_ids.as<int>(), nact, c->H, c->W, m, s);
         } else {

@@ -176,7 +176,7 @@ void mst_finalize(const int* map_ids, int nact, int H, int W, MstWork m, int32_t
 int mst_level_counts();
 // Level-0 components from Boruvka inside each 32 x 32 tile (LDS), with the
 // reliabilities; replaces mst_init + the first pixel round before mst_level_setup.
-int mst_tile_side(int H, int W);  // 64, 32, or 0: no tile pass
+int mst_tile_shape(int H, int W, int* th);  // tile width (64 / 32) and height, 0: no tile pass
 // graph: write the tile's contracted component graph for mst_cg_round instead of the
 // per-pixel state of the boundary-list rounds (mst_level_setup / mst_level_round).
 void mst_tile_level0(const float* w, const int* map_ids, int nact, int H, int W, MstWork m, hipStream_t s,

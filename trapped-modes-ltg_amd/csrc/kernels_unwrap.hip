@@ -44,6 +44,12 @@ namespace fcdk {
 constexpr double kPi = 3.141592653589793;      // skimage unwrap's PI (probed: double M_PI)
 constexpr double kTwoPi = 6.283185307179586;
 constexpr double kBorderRel = 9999999.0;
+#ifndef FCD_T0_PRECHECK
+#define FCD_T0_PRECHECK 0  // 1: skip the LDS atomicMin when the minimum is already lower (r03cg6: 13.67 -> 13.9 ms, slower)
+#endif
+#ifndef FCD_MST_TILE_DEFAULT
+#define FCD_MST_TILE_DEFAULT 64  // tile pass shape code (mst_tile_shape)
+#endif
 
 // find_wrap of the reference unwrapper: -1 if w1 - w2 > pi, +1 if < -pi.
 __device__ __forceinline__ int find_wrap(float a, float b) {
@@ -784,8 +790,9 @@ void mst_level_finalize(const int* map_ids, int nact, int H, int W, MstWork m, i
 // is an MST edge, so the components are subtrees of the MST and the two-level rounds
 // finish the same tree (same k-field as the all-pixel rounds).  The tile also
 // writes the f64 reliabilities (k_mst_rel's arithmetic) the later rounds read.
-// Tile side T0 = 32 (1024 pixels, 256 threads, 35 KB of LDS: 4 workgroups per CU) or
-// 64 (4096 pixels, 1024 threads, 133 KB: one per CU); 4 pixels per thread either way.
+// Tiles of TW x TH = 64 x 64 (4096 pixels, 1024 threads, 65 KB of LDS: one workgroup
+// per CU at 128 VGPRs), 64 x 32 (512 threads, 33 KB: two) or 32 x 32 (256 threads, 17 KB:
+// four); 4 pixels per thread.
 #ifdef FCD_T0_STAMPS
 // diagnostic: per-phase cycles of the first 256 tiles (thread 0) and their round counts
 __device__ unsigned long long g_t0_stamps[256 * 9];
@@ -794,7 +801,7 @@ extern "C" __attribute__((visibility("default"))) int fcd_debug_t0_stamps(unsign
 }
 #endif
 // Edges of a tile by a local code that keeps the global edge order (horizontal edges
-// first, each kind row-major; li, lj in [-1, T0] relative to the tile origin):
+// first, each kind row-major; li in [-1, TH], lj in [-1, TW] relative to the tile origin):
 // horizontal (li, lj)-(li, lj + 1) -> (li + 1) << 7 | (lj + 1), vertical (li, lj)-(li + 1, lj)
 // -> 1 << 14 | (li + 1) << 7 | (lj + 1).  Decoding is shifts and masks.
 __device__ __forceinline__ int t0_hcode(int li, int lj) { return ((li + 1) << 7) | (lj + 1); }
@@ -810,21 +817,22 @@ __device__ __forceinline__ int t0_off(unsigned l) { return (int)(short)(l & 0xff
 // (contracting subtrees of the MST keeps the MST: of parallel edges between two
 // components only the lightest (weight, edge index) can be in it, by the cycle property
 // of the contracted graph).  When a tile's Boruvka stops, every component's lightest
-// edge leaves the tile, so every component holds a tile-border pixel: V <= 4 T0 - 4
+// edge leaves the tile, so every component holds a tile-border pixel: V <= 2 (TW + TH) - 4
 // components, and the contracted tile graph is planar, so at most 3 V - 6 distinct
-// adjacent pairs inside the tile, plus the 2 T0 edges leaving it to the right and
+// adjacent pairs inside the tile, plus the TH + TW edges leaving it to the right and
 // downwards (the other two sides are the neighbours' right / down edges).  Hence the
 // fixed per-tile capacities below and an LDS hash table that never fills.
 //
-// Per tile tg (= blockIdx.x of the tile pass): components tg * CG_CCAP + rank, edges in
+// Per tile tg (= blockIdx.x of the tile pass): components tg * cg_ccap + rank, edges in
 // [tg * cg_ecap, + cg_ecnt[tg]) as records (ea, eb, weight bits, global edge index,
 // ed = K_ea - K_eb from the pixel offsets and the edge's wrap count).  An edge to a
 // neighbour tile is written with eb = -1 - (neighbour pixel's vertex id) and the
 // neighbour's offset missing; the first round resolves it (comp[], off[] of the pixel).
-__host__ __device__ constexpr int cg_ccap(int T0) { return 4 * T0; }
-__host__ __device__ constexpr int cg_ecap(int T0) { return T0 == 64 ? 1024 : 512; }
-static_assert(3 * (4 * 64 - 4) - 6 + 2 * 64 <= cg_ecap(64) && 3 * (4 * 32 - 4) - 6 + 2 * 32 <= cg_ecap(32),
-              "planar bound on a tile's contracted edges");
+// For a TW x TH tile: V <= 2 (TW + TH) - 4, edges <= 3 V - 6 + TW + TH.
+__host__ __device__ constexpr int cg_ccap(int tw, int th) { return 2 * (tw + th); }
+__host__ __device__ constexpr int cg_pow2(int n) { return n <= 1 ? 1 : 2 * cg_pow2((n + 1) / 2); }
+__host__ __device__ constexpr int cg_ecap(int tw, int th) { return cg_pow2(3 * (2 * (tw + th) - 4) - 6 + tw + th); }
+static_assert(cg_ecap(64, 64) == 1024 && cg_ecap(64, 32) == 1024 && cg_ecap(32, 32) == 512, "capacities");
 
 __device__ __forceinline__ void cg_write_edge(MstWork& m, long e, int ea, int eb, unsigned long long ew, int ec, int ed) {
     m.cg_ea[e] = ea;
@@ -860,13 +868,14 @@ __device__ __forceinline__ void wave_append(const bool (&pred)[N], int* lds_coun
 }
 
 // After the tile's rounds: lc / lo (labels, offsets) valid, the rest of the pool free.
-template <int T0>
+template <int TW, int TH>
 __device__ __forceinline__ void tile0_graph(unsigned char* pool, const unsigned long long (&ekey)[4][4], unsigned incs,
                                             int H, int W, int gi0, int gj0, long vbase, MstWork& m) {
-    constexpr int T0N = T0 * T0, NT = T0N / 4;
-    constexpr int HS = T0 == 64 ? 2048 : 512;  // hash slots: >= 2.7x the pairs a tile can have
-    constexpr int HB = T0 == 64 ? 11 : 9;
-    constexpr int ECAP = cg_ecap(T0);
+    constexpr int T0N = TW * TH, NT = T0N / 4;
+    constexpr int HS = T0N / 2;  // hash slots: >= 2.7x the pairs a tile can have
+    constexpr int HB = HS == 2048 ? 11 : (HS == 1024 ? 10 : 9);
+    static_assert((1 << HB) == HS && 3 * (2 * (TW + TH) - 4) - 6 < HS, "hash size: more slots than pairs");
+    constexpr int ECAP = cg_ecap(TW, TH);
     static_assert(16 * HS <= 8 * T0N, "hash table in the minimum-weight region");
     unsigned* const hkey = reinterpret_cast<unsigned*>(pool);  // pair (a, b), a < b, + 1; 0: empty
     unsigned* const hcode = hkey + HS;
@@ -894,16 +903,87 @@ __device__ __forceinline__ void tile0_graph(unsigned char* pool, const unsigned 
     }
     __syncthreads();
     const long tg = blockIdx.x;
-    const int cb = (int)(tg * cg_ccap(T0));
+    const int cb = (int)(tg * cg_ccap(TW, TH));
     const long eb0 = tg * ECAP;
     const int nh = H * (W - 1);
-    int slot[8], code[8];
+    // Every global store of the write-out comes after the last barrier: a barrier is a
+    // workgroup release and would wait for the stores in flight (about a quarter of the
+    // tile's time when the comp / off stores preceded the hash phases).
+    int slot[8], pos[8];
     bool cross[8];
+    unsigned key[8];  // the pair of an edge between two components of the tile, 0: none
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int i = threadIdx.x + NT * k;
-        const int li = i / T0, lj = i % T0, gi = gi0 + li, gj = gj0 + lj;
-        const long v = vbase + (long)gi * W + gj;
+        const int li = i / TW, lj = i % TW;
+        const int c = lc[i];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {  // h = 0: right edge (d = 0), 1: down edge (d = 2)
+            const int j = 2 * k + h;
+            const bool exists = ekey[k][2 * h] != ~0ull;
+            const int ni = li + h, nj = lj + 1 - h;
+            const bool inside = ni < TH && nj < TW;
+            cross[j] = exists && !inside;  // into the neighbour tile: resolved by the first round
+            const int cy = lc[inside ? ni * TW + nj : i];
+            key[j] = exists && inside && cy != c ? ((unsigned)min(c, cy) << 12 | (unsigned)max(c, cy)) + 1u : 0u;
+        }
+    }
+    // the eight lookups' first probes issued together, then the rare collisions in turn
+    unsigned cur[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        slot[j] = (int)((key[j] * 2654435761u) >> (32 - HB));
+        cur[j] = key[j] ? hkey[slot[j]] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        if (!key[j]) {
+            slot[j] = -1;
+            continue;
+        }
+        unsigned hs = (unsigned)slot[j], c0 = cur[j];
+        slot[j] = -1;
+        for (int probe = 0; probe < HS; ++probe) {
+            if (c0 == 0u) c0 = atomicCAS(hkey + hs, 0u, key[j]);
+            if (c0 == 0u || c0 == key[j]) {
+                slot[j] = (int)hs;
+                break;
+            }
+            hs = (hs + 1) & (HS - 1);
+            c0 = hkey[hs];
+        }
+        if (slot[j] < 0) atomicOr(m.nhooks + 1, 1);  // cannot happen (planar bound); the host falls back
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        if (slot[j] >= 0) atomicMin(hwt + slot[j], ekey[j >> 1][2 * (j & 1)]);
+    auto code_of = [&](int j) {
+        const int i = threadIdx.x + NT * (j >> 1), gi = gi0 + i / TW, gj = gj0 + i % TW;
+        return (j & 1) ? nh + gi * W + gj : gi * (W - 1) + gj;
+    };
+    wave_append(cross, &ncnt[1], pos);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        if (slot[j] >= 0 && hwt[slot[j]] == ekey[j >> 1][2 * (j & 1)]) atomicMin(hcode + slot[j], (unsigned)code_of(j));
+    __syncthreads();
+    {
+        bool win[8];
+        int wpos[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            win[j] = slot[j] >= 0 && hwt[slot[j]] == ekey[j >> 1][2 * (j & 1)] && hcode[slot[j]] == (unsigned)code_of(j);
+        wave_append(win, &ncnt[1], wpos);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (win[j]) pos[j] = wpos[j];  // an edge is either inside the tile or leaves it
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int i = threadIdx.x + NT * k;
+        const int li = i / TW, lj = i % TW;
+        const long v = vbase + (long)(gi0 + li) * W + gj0 + lj;
         const int c = lc[i];
         const int id = cb + rk[c];
         m.comp[v] = id;
@@ -916,80 +996,33 @@ __device__ __forceinline__ void tile0_graph(unsigned char* pool, const unsigned 
             m.best_e[id] = 0x7fffffff;
         }
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {  // h = 0: right edge (d = 0), 1: down edge (d = 2)
+        for (int h = 0; h < 2; ++h) {
             const int j = 2 * k + h;
-            const bool exists = ekey[k][2 * h] != ~0ull;
-            const int ni = li + h, nj = lj + 1 - h;
-            const bool inside = ni < T0 && nj < T0;
-            code[j] = h ? nh + gi * W + gj : gi * (W - 1) + gj;
-            cross[j] = exists && !inside;  // into the neighbour tile: resolved by the first round
-            slot[j] = -1;
-            if (!exists || !inside) continue;
-            const int cy = lc[ni * T0 + nj];
-            if (cy == c) continue;
-            const unsigned key = ((unsigned)min(c, cy) << 12 | (unsigned)max(c, cy)) + 1u;
-            unsigned hs = (key * 2654435761u) >> (32 - HB);
-            for (int probe = 0; probe < HS; ++probe, hs = (hs + 1) & (HS - 1)) {
-                const unsigned cur = hkey[hs];
-                if (cur == key || (cur == 0u && (atomicCAS(hkey + hs, 0u, key) == 0u || hkey[hs] == key))) {
-                    slot[j] = (int)hs;
-                    break;
-                }
-            }
-            if (slot[j] < 0) atomicOr(m.nhooks + 1, 1);  // cannot happen (planar bound); the host falls back
-            else if (ekey[k][2 * h] < hwt[slot[j]]) atomicMin(hwt + slot[j], ekey[k][2 * h]);
-        }
-    }
-    {
-        int pos[8];
-        wave_append(cross, &ncnt[1], pos);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
             if (pos[j] < 0 || pos[j] >= ECAP) continue;
-            const int k = j >> 1, h = j & 1, i = threadIdx.x + NT * k;
-            const long v = vbase + (long)(gi0 + i / T0) * W + gj0 + i % T0;
             const int delta = -((int)((incs >> (8 * k + 4 * h)) & 3u) - 1);  // k(y) - k(x)
-            cg_write_edge(m, eb0 + pos[j], cb + rk[lc[i]], (int)(-1 - (v + (h ? W : 1))), ekey[k][2 * h], code[j],
-                          -lo[i] - delta);
+            if (cross[j]) {
+                cg_write_edge(m, eb0 + pos[j], id, (int)(-1 - (v + (h ? W : 1))), ekey[k][2 * h], code_of(j), -lo[i] - delta);
+            } else {
+                const int y = (li + h) * TW + lj + 1 - h;
+                cg_write_edge(m, eb0 + pos[j], id, cb + rk[lc[y]], ekey[k][2 * h], code_of(j), lo[y] - lo[i] - delta);
+            }
         }
     }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-        if (slot[j] >= 0 && hwt[slot[j]] == ekey[j >> 1][2 * (j & 1)]) atomicMin(hcode + slot[j], (unsigned)code[j]);
-    __syncthreads();
-    {
-        bool win[8];
-        int pos[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-            win[j] = slot[j] >= 0 && hwt[slot[j]] == ekey[j >> 1][2 * (j & 1)] && hcode[slot[j]] == (unsigned)code[j];
-        wave_append(win, &ncnt[1], pos);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            if (pos[j] < 0 || pos[j] >= ECAP) continue;
-            const int k = j >> 1, h = j & 1, i = threadIdx.x + NT * k, li = i / T0, lj = i % T0;
-            const int y = (li + h) * T0 + lj + 1 - h;
-            const int delta = -((int)((incs >> (8 * k + 4 * h)) & 3u) - 1);
-            cg_write_edge(m, eb0 + pos[j], cb + rk[lc[i]], cb + rk[lc[y]], ekey[k][2 * h], code[j], lo[y] - lo[i] - delta);
-        }
-    }
-    __syncthreads();
     if (threadIdx.x == 0) {
         m.cg_ncomp[tg] = ncnt[0];
         m.cg_ecnt[tg] = min(ncnt[1], ECAP);
-        if (ncnt[1] > ECAP || ncnt[0] > cg_ccap(T0)) atomicOr(m.nhooks + 1, 1);
+        if (ncnt[1] > ECAP || ncnt[0] > cg_ccap(TW, TH)) atomicOr(m.nhooks + 1, 1);
     }
 }
 
-template <int T0, bool CG>
-__global__ __launch_bounds__(T0 * T0 / 4) void k_mst_tile0(const float* __restrict__ w, const int* __restrict__ map_ids,
+template <int TW, int TH, bool CG>
+__global__ __launch_bounds__(TW * TH / 4, 4) void k_mst_tile0(const float* __restrict__ w, const int* __restrict__ map_ids,
                                                           int nact, int H, int W, MstWork m) {
-    constexpr int T0N = T0 * T0;  // pixels per tile
-    constexpr int T0W = T0 + 4;   // wrapped-phase image with a 2-pixel halo
-    constexpr int T0R = T0 + 2;   // reliabilities with a 1-pixel halo
+    constexpr int T0N = TW * TH;  // pixels per tile
+    constexpr int T0W = TW + 4;   // wrapped-phase image with a 2-pixel halo
+    constexpr int T0R = TW + 2;   // reliabilities with a 1-pixel halo
     constexpr int NT = T0N / 4;   // threads, 4 pixels each
-    static_assert(T0 <= 64, "16-bit local indices and 7-bit edge-code fields");
+    static_assert((TW == 64 || TW == 32) && TH <= 64 && T0N % 256 == 0, "16-bit local indices and 7-bit edge-code fields");
     // 16 bytes per pixel (64 KB at 64 x 64: two workgroups per CU): the rounds' arrays;
     // before them the same bytes hold the wrapped phases and reliabilities.  A root's
     // link replaces its edge code once every hook decision is made (step (c)).
@@ -1000,8 +1033,8 @@ __global__ __launch_bounds__(T0 * T0 / 4) void k_mst_tile0(const float* __restri
     short* const lc = reinterpret_cast<short*>(pool + 12 * T0N);                 // component of each pixel
     short* const lo = reinterpret_cast<short*>(pool + 14 * T0N);                 // K(pixel) - K(component)
     float* const ws = reinterpret_cast<float*>(pool);
-    double* const rs = reinterpret_cast<double*>(pool + ((T0W * T0W * 4 + 15) & ~15));
-    static_assert(((T0W * T0W * 4 + 15) & ~15) + T0R * T0R * 8 <= 16 * T0N, "phases + reliabilities fit the pool");
+    double* const rs = reinterpret_cast<double*>(pool + ((T0W * (TH + 4) * 4 + 15) & ~15));
+    static_assert(((T0W * (TH + 4) * 4 + 15) & ~15) + T0R * (TH + 2) * 8 <= 16 * T0N, "phases + reliabilities fit the pool");
 #ifdef FCD_T0_STAMPS
     unsigned long long tprev = __builtin_readcyclecounter(), ph[8] = {};
 #define T0_STAMP(i)                                                \
@@ -1016,19 +1049,19 @@ __global__ __launch_bounds__(T0 * T0 / 4) void k_mst_tile0(const float* __restri
     } while (0)
 #endif
     const long hw = (long)H * W;
-    const int tiles_x = W / T0, tiles = (H / T0) * tiles_x;
+    const int tiles_x = W / TW, tiles = (H / TH) * tiles_x;
     const int slot = blockIdx.x / tiles, tile = blockIdx.x % tiles;
-    const int gi0 = (tile / tiles_x) * T0, gj0 = (tile % tiles_x) * T0;
+    const int gi0 = (tile / tiles_x) * TH, gj0 = (tile % tiles_x) * TW;
     const float* mw = w + (long)map_ids[slot] * hw;
     const long vbase = (long)slot * hw;
     // wrapped phases, 2-pixel halo (outside the map: never read for an existing edge)
-    for (int i = threadIdx.x; i < T0W * T0W; i += NT) {
+    for (int i = threadIdx.x; i < T0W * (TH + 4); i += NT) {
         const int gi = gi0 - 2 + i / T0W, gj = gj0 - 2 + i % T0W;
         ws[i] = (gi >= 0 && gi < H && gj >= 0 && gj < W) ? mw[(long)gi * W + gj] : 0.f;
     }
     __syncthreads();
     // reliabilities of the tile and its 1-pixel halo (k_mst_rel's operation order)
-    for (int i = threadIdx.x; i < T0R * T0R; i += NT) {
+    for (int i = threadIdx.x; i < T0R * (TH + 2); i += NT) {
         const int li = i / T0R, lj = i % T0R;  // ws index (li + 1, lj + 1)
         const int gi = gi0 - 1 + li, gj = gj0 - 1 + lj;
         double r = kBorderRel;
@@ -1047,11 +1080,11 @@ __global__ __launch_bounds__(T0 * T0 / 4) void k_mst_tile0(const float* __restri
             r = s;
         }
         rs[i] = r;
-        if (!CG && li >= 1 && li <= T0 && lj >= 1 && lj <= T0) m.rel[vbase + (long)gi * W + gj] = r;
+        if (!CG && li >= 1 && li <= TH && lj >= 1 && lj <= TW) m.rel[vbase + (long)gi * W + gj] = r;
     }
     __syncthreads();
     T0_STAMP(0);
-    auto relat = [&](int li, int lj) { return rs[(li + 1) * T0R + (lj + 1)]; };  // li, lj in [-1, T0]
+    auto relat = [&](int li, int lj) { return rs[(li + 1) * T0R + (lj + 1)]; };  // li in [-1, TH], lj in [-1, TW]
     // the 4 incident edges of each of this thread's pixels, once: weight rel(p) + rel(q)
     // (f64, as k_mst_rel / k_mst_round) as its bit pattern (non-negative doubles order
     // as unsigned integers), ~0 for an edge past the map border; the rounds then only
@@ -1063,7 +1096,7 @@ __global__ __launch_bounds__(T0 * T0 / 4) void k_mst_tile0(const float* __restri
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int i = threadIdx.x + NT * k;
-        const int li = i / T0, lj = i % T0, gi = gi0 + li, gj = gj0 + lj;
+        const int li = i / TW, lj = i % TW, gi = gi0 + li, gj = gj0 + lj;
         const double rv = relat(li, lj);
         const float wc = wat(li, lj);
         incs |= (unsigned)(find_wrap(wc, wat(li, lj + 1)) + 1) << (8 * k);
@@ -1097,14 +1130,14 @@ __global__ __launch_bounds__(T0 * T0 / 4) void k_mst_tile0(const float* __restri
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int i = threadIdx.x + NT * k;
-            const int li = i / T0, lj = i % T0;
+            const int li = i / TW, lj = i % TW;
             int nbc[4];
             bool in[4];
 #pragma unroll
             for (int d = 0; d < 4; ++d) {
                 const int ni = li + (d == 2) - (d == 3), nj = lj + (d == 0) - (d == 1);
-                in[d] = ni >= 0 && ni < T0 && nj >= 0 && nj < T0;
-                nbc[d] = lc[in[d] ? ni * T0 + nj : i];
+                in[d] = ni >= 0 && ni < TH && nj >= 0 && nj < TW;
+                nbc[d] = lc[in[d] ? ni * TW + nj : i];
             }
             const int c = lc[i];
             cs[k] = c;
@@ -1123,7 +1156,7 @@ __global__ __launch_bounds__(T0 * T0 / 4) void k_mst_tile0(const float* __restri
             key[k] = bk;
             ke[k] = bev;
             kd[k] = bd;
-            if (bk != ~0ull) atomicMin(bw + c, bk);
+            if (bk != ~0ull && (!FCD_T0_PRECHECK || bk < bw[c])) atomicMin(bw + c, bk);
         }
         __syncthreads();
         T0_STAMP(2);
@@ -1141,10 +1174,10 @@ __global__ __launch_bounds__(T0 * T0 / 4) void k_mst_tile0(const float* __restri
         for (int k = 0; k < 4; ++k) {
             const int i = threadIdx.x + NT * k, c = cs[k];
             if (key[k] == ~0ull || key[k] != bw[c] || ke[k] != be[c]) continue;
-            const int li = i / T0, lj = i % T0, d = kd[k];
+            const int li = i / TW, lj = i % TW, d = kd[k];
             const int ni = li + (d == 2) - (d == 3), nj = lj + (d == 0) - (d == 1);
-            if (!(ni >= 0 && ni < T0 && nj >= 0 && nj < T0)) continue;  // leaves the tile: the level rounds take it
-            const int y = ni * T0 + nj;
+            if (!(ni >= 0 && ni < TH && nj >= 0 && nj < TW)) continue;  // leaves the tile: the level rounds take it
+            const int y = ni * TW + nj;
             const int inc = (int)((incs >> (8 * k + 2 * d)) & 3u) - 1;
             const int delta = (d == 0 || d == 2) ? -inc : inc;  // k(y) - k(i) across the edge
             const int dr = lc[y];
@@ -1204,17 +1237,17 @@ __global__ __launch_bounds__(T0 * T0 / 4) void k_mst_tile0(const float* __restri
         T0_STAMP(6);
     }
     if constexpr (CG) {
-        tile0_graph<T0>(pool, ekey, incs, H, W, gi0, gj0, vbase, m);
+        tile0_graph<TW, TH>(pool, ekey, incs, H, W, gi0, gj0, vbase, m);
     } else {
     // level-0 components: global ids of the tile roots, offsets to them; candidate
     // slots of every pixel reset for the level rounds
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int i = threadIdx.x + NT * k;
-        const int li = i / T0, lj = i % T0;
+        const int li = i / TW, lj = i % TW;
         const long v = vbase + (long)(gi0 + li) * W + (gj0 + lj);
         const int c = lc[i];
-        m.comp[v] = (int)(vbase + (long)(gi0 + c / T0) * W + (gj0 + c % T0));
+        m.comp[v] = (int)(vbase + (long)(gi0 + c / TW) * W + (gj0 + c % TW));
         m.off[v] = lo[i];
         m.best_w[v] = 0x7ff0000000000000ull;
         m.best_e[v] = 0x7fffffff;
@@ -1233,7 +1266,7 @@ __global__ __launch_bounds__(T0 * T0 / 4) void k_mst_tile0(const float* __restri
 // tile's level-0 components (relabel).  Same weights, tie-break and hook rule as the
 // pixel rounds, so the same unique MST and k-field.
 constexpr int CG_U = 4;  // edges per thread: cg_ecap <= 1024 = 256 threads x CG_U
-static_assert(cg_ecap(64) <= 256 * CG_U, "one pass over a segment");
+static_assert(cg_ecap(64, 64) <= 256 * CG_U, "one pass over a segment");
 
 // Candidates: per edge between different current roots, atomicMin of its weight into
 // both roots; the segment is compacted in place (edges inside a root are gone for good).
@@ -1241,9 +1274,10 @@ template <bool FIRST>
 __global__ __launch_bounds__(256) void k_cg_cand(MstWork m, int ntiles, int ecap) {
     __shared__ int nout;
     for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const int n = m.cg_ecnt[t];
+        if (n == 0) continue;  // block-uniform: a finished tile costs one load per round
         if (threadIdx.x == 0) nout = 0;
         __syncthreads();
-        const int n = m.cg_ecnt[t];
         const long b0 = (long)t * ecap;
         int ea[CG_U], eb[CG_U], ec[CG_U], ed[CG_U], ra[CG_U], rb[CG_U];
         unsigned long long ew[CG_U];
@@ -1361,13 +1395,15 @@ __global__ __launch_bounds__(256) void k_cg_relabel(MstWork m, int ntiles, int c
 }
 
 long mst_cg_edge_capacity(long nv) { return nv / 2 + 1024; }
-static_assert(cg_ecap(32) * 2 <= 32 * 32 && cg_ecap(64) * 2 <= 64 * 64, "edge records: nv / 2 covers every tile side");
+static_assert(cg_ecap(32, 32) * 2 <= 32 * 32 && cg_ecap(64, 32) * 2 <= 64 * 32 && cg_ecap(64, 64) * 2 <= 64 * 64,
+              "edge records: nv / 2 covers every tile shape");
 
 void mst_cg_round(int nact, int H, int W, MstWork m, int r, hipStream_t s) {
-    const int t0 = mst_tile_side(H, W);
-    if (!t0) throw std::runtime_error("mst_cg_round: frame not a multiple of the tile");
-    const int ntiles = nact * (H / t0) * (W / t0);
-    const int ecap = cg_ecap(t0), ccap = cg_ccap(t0);
+    int th = 0;
+    const int tw = mst_tile_shape(H, W, &th);
+    if (!tw) throw std::runtime_error("mst_cg_round: frame not a multiple of the tile");
+    const int ntiles = nact * (H / th) * (W / tw);
+    const int ecap = cg_ecap(tw, th), ccap = cg_ccap(tw, th);
     FCD_HIPCHK(hipMemsetAsync(m.nhooks, 0, sizeof(int), s));
     const dim3 g((unsigned)std::min(ntiles, 4096)), b(256);
     if (r == 0)
@@ -1383,27 +1419,35 @@ void mst_cg_round(int nact, int H, int W, MstWork m, int r, hipStream_t s) {
     FCD_CHECK_LAUNCH();
 }
 
-int mst_tile_side(int H, int W) {
-    const char* e = std::getenv("FCD_MST_TILE");  // diagnostic override (32 / 64), read per call
-    const int want = e ? std::atoi(e) : 64;
-    if (want == 64 && H % 64 == 0 && W % 64 == 0) return 64;
-    if (H % 32 == 0 && W % 32 == 0) return 32;
-    return 0;
+int mst_tile_shape(int H, int W, int* th) {
+    // FCD_MST_TILE (diagnostic override, read per call): 64 (64 x 64), 6432 (64 wide, 32
+    // tall) or 32 (32 x 32); the default, and the fallbacks when H, W are not multiples
+    const char* e = std::getenv("FCD_MST_TILE");
+    const int want = e ? std::atoi(e) : FCD_MST_TILE_DEFAULT;
+    if (want == 64 && H % 64 == 0 && W % 64 == 0) return *th = 64, 64;
+    if (want == 6432 && H % 32 == 0 && W % 64 == 0) return *th = 32, 64;
+    if (H % 32 == 0 && W % 32 == 0) return *th = 32, 32;
+    return *th = 0, 0;
 }
 
 void mst_tile_level0(const float* w, const int* map_ids, int nact, int H, int W, MstWork m, hipStream_t s, bool graph) {
-    const int t = mst_tile_side(H, W);
-    if (!t) throw std::runtime_error("mst_tile_level0: frame not a multiple of the tile");
-    const long nblocks = (long)nact * (H / t) * (W / t);
-    const dim3 g((unsigned)nblocks);
-    if (t == 64 && graph)
-        hipLaunchKernelGGL((k_mst_tile0<64, true>), g, dim3(1024), 0, s, w, map_ids, nact, H, W, m);
-    else if (t == 64)
-        hipLaunchKernelGGL((k_mst_tile0<64, false>), g, dim3(1024), 0, s, w, map_ids, nact, H, W, m);
-    else if (graph)
-        hipLaunchKernelGGL((k_mst_tile0<32, true>), g, dim3(256), 0, s, w, map_ids, nact, H, W, m);
-    else
-        hipLaunchKernelGGL((k_mst_tile0<32, false>), g, dim3(256), 0, s, w, map_ids, nact, H, W, m);
+    int th = 0;
+    const int tw = mst_tile_shape(H, W, &th);
+    if (!tw) throw std::runtime_error("mst_tile_level0: frame not a multiple of the tile");
+    const dim3 g((unsigned)((long)nact * (H / th) * (W / tw)));
+    const dim3 b((unsigned)(tw * th / 4));
+#define FCD_T0_LAUNCH(TW, TH, CG) hipLaunchKernelGGL((k_mst_tile0<TW, TH, CG>), g, b, 0, s, w, map_ids, nact, H, W, m)
+    if (tw == 64 && th == 64) {
+        if (graph) FCD_T0_LAUNCH(64, 64, true);
+        else FCD_T0_LAUNCH(64, 64, false);
+    } else if (tw == 64) {
+        if (graph) FCD_T0_LAUNCH(64, 32, true);
+        else FCD_T0_LAUNCH(64, 32, false);
+    } else {
+        if (graph) FCD_T0_LAUNCH(32, 32, true);
+        else FCD_T0_LAUNCH(32, 32, false);
+    }
+#undef FCD_T0_LAUNCH
     FCD_CHECK_LAUNCH();
 }
 
