@@ -466,15 +466,17 @@ def fused(monkeypatch):
     _lib._engines.clear()
 
 
-def test_fused_height_path_vs_oracle(lib, fused):
+@pytest.mark.parametrize("n,count", [(1024, 3), (2048, 2)])
+def test_fused_height_path_vs_oracle(lib, fused, n, count):
     """Height-only batches (analyze.folder's use of compute_height_map) take the fused
-    kernel (kernels_phase_rows.hip: band transforms + phase + unwrap + row FFT in one
-    pass, column-0 offsets applied in the spectra's DC bins): same heights as the
-    oracle and as the unfused path, with and without unwrapping."""
+    kernel (kernels_phase_rows.hip at 1024-point rows, kernels_phase_rows2048.hip at
+    2048: band transforms + phase + unwrap + row FFT in one pass, column-0 offsets
+    applied in the spectra's DC bins): same heights as the oracle and as the unfused
+    path, with and without unwrapping."""
     from oracle import fcd_oracle as O
     from bench_data import make_frames_numpy
     from pyfcd.fcd import fcd
-    ref, frames = make_frames_numpy(1024, 3, seed=5, rotate_deg=5.0)
+    ref, frames = make_frames_numpy(n, count, seed=5, rotate_deg=5.0)
     for unwrap in (True, False):
         hf, cf = fcd.compute_height_maps(ref, frames, 0.001, height=1.0, unwrap=unwrap)
         hu, _, _ = fcd.compute_height_maps(ref, frames, 0.001, height=1.0, unwrap=unwrap, return_phases=True)
@@ -578,7 +580,7 @@ def test_census_flags_residues_on_tile_seams(lib, monkeypatch, n, count):
         del eng
     monkeypatch.delenv("FCD_UNFUSED")
     _lib._engines.clear()
-    if n == 1024:  # the fused kernel is 1024-wide only
+    if n <= 2048:  # the fused kernel runs at 1024- and 2048-point rows
         assert np.array_equal(heights["1"], heights["0"])
 
 

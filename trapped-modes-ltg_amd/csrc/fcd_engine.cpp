@@ -598,7 +598,12 @@ void build_demod_tables(fcd_ctx* c, hipStream_t s) {
     c->fused_ok = c->band_B && fcdk::phase_rows_supported(W, c->band_B, H);
     std::vector<float2> ztw;
     if (c->fused_ok) {
-        ztw = group_twiddles(W);
+        ztw = group_twiddles(W == 2048 ? 1024 : W);
+        if (W == 2048)  // the radix-2 pass joining the two 1024-point halves (kernels_phase_rows2048.hip)
+            for (int k = 0; k < 1024; ++k) {
+                const double a = -2.0 * kPi * (double)k / 2048.0;
+                ztw.push_back(make_float2((float)std::cos(a), (float)std::sin(a)));
+            }
         c->ztw.ensure(ztw.size() * sizeof(float2));
         upload(c->ztw.p, ztw.data(), ztw.size() * sizeof(float2), s);
     }
@@ -621,7 +626,7 @@ void build_demod_tables(fcd_ctx* c, hipStream_t s) {
     c->colk.ensure(std::max(nb, (size_t)c->chunk) * 2 * H * sizeof(int));
     c->fk.ensure(nb * 2 * hw * sizeof(int32_t));
     c->col0.ensure(nb * 2 * (size_t)H * sizeof(float));
-    if (c->fused_ok) c->seam.ensure(nb * (size_t)(H / fcdk::phase_rows_tile()) * 2 * W * sizeof(float2));
+    if (c->fused_ok) c->seam.ensure(nb * (size_t)(H / fcdk::phase_rows_tile(W)) * 2 * W * sizeof(float2));
     c->ir_seam.ensure(2 * fcdk::int_rows_seam_bytes(W, H, (int)nb));
     c->rescnt.ensure(std::max(nb, (size_t)c->chunk) * 2 * sizeof(int));
     c->mst_cap = 0;  // re-size the MST workspace for the new chunk on next use
@@ -1036,13 +1041,13 @@ void first_pass_chunk(fcd_ctx* c, const float* fr, int nb, bool unwrap, bool fus
         float* col0 = c->col0.as<float>() + fo * 2 * H;
         int* colk = c->colk.as<int>() + fo * 2 * H;
         float2* Zt = c->Zt.as<float2>() + fo * H * W;
-        float2* seam = c->seam.as<float2>() + fo * (H / fcdk::phase_rows_tile()) * 2 * W;
+        float2* seam = c->seam.as<float2>() + fo * (H / fcdk::phase_rows_tile(c->W)) * 2 * W;
         float2* Ht = c->Ht.as<float2>() + fo * H * (W / 2 + 1);
         if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
         fcdk::demod_rows(c->W, fr, c->H, nb, T, Xb, c->twp_row.as<float2>(), s);
         fcdk::demod_cols(c->H, Xb, nb, T, Ab, c->NCA, c->twp_col.as<float2>(), s);
         if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
-        fcdk::phase_rows(unwrap, Ab, c->H, nb, c->NCA, c->NCc[0], c->NCc[1], c->theta_p.as<float>(),
+        fcdk::phase_rows(c->W, unwrap, Ab, c->H, nb, c->NCA, c->NCc[0], c->NCc[1], c->theta_p.as<float>(),
                          c->band_pre.as<float2>(), c->band_ptw.as<float2>(), c->ztw.as<float2>(), col0, res, Zt, seam,
                          s);
         if (unwrap) fcdk::unwrap_colk_compact(col0, 2 * nb, c->H, colk, s);

@@ -4,6 +4,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <cstdlib>
 #include <vector>
 
 #include "host_logic.hpp"  // fcdk::PfPlan
@@ -111,9 +112,12 @@ void unwrap_colk(const float* w, int nmaps, int H, int W, int* colk, hipStream_t
 // the same over compact column-0 values col0[map][H] (the fused path's side output)
 void unwrap_colk_compact(const float* col0, int nmaps, int H, int* colk, hipStream_t s);
 // fused band transform + phase + unwrap + z-row FFT (kernels_phase_rows.hip)
+// W = 1024 (B = 128) and W = 2048 (B = 256, kernels_phase_rows2048.hip; FCD_FUSED_2048=0
+// keeps the unfused chain there).  ztw: group_twiddles(W) at 1024; at 2048 the
+// 1024-point table followed by exp(-2 pi i k / 2048), k < 1024.
 bool phase_rows_supported(int W, int B, int H);
-int phase_rows_tile();
-void phase_rows(bool unwrap, const float2* Ab, int H, int nb, int NCA, int ncc0, int ncc1, const float* theta,
+int phase_rows_tile(int W);  // rows per fused tile (seam buffer: nb * H / tile * 2 * W float2)
+void phase_rows(int W, bool unwrap, const float2* Ab, int H, int nb, int NCA, int ncc0, int ncc1, const float* theta,
                 const float2* pre, const float2* ptw, const float2* ztw, float* col0, int* flags, float2* Zt,
                 float2* seam, hipStream_t s);
 
@@ -146,6 +150,14 @@ int pf_chunk_count(long hw);  // sums: nb * pf_chunk_count(hw) floats
 void pf_center(const float* img, int nb, long hw, float* sums, float* out, hipStream_t s);
 void pf_fft2(const float* in, int nb, int H, int W, const PfPlan& rows, const float* rtw, const PfPlan& cols,
              const float2* ctw, float2* F, hipStream_t s);
+
+void phase_rows2048(bool unwrap, const float2* Ab, int H, int nb, int NCA, int ncc0, int ncc1, const float* theta,
+                    const float2* pre, const float2* ptw, const float2* ztw, float* col0, int* flags, float2* Zt,
+                    float2* seam, hipStream_t s);
+inline bool fcd_fused_2048() {
+    const char* e = std::getenv("FCD_FUSED_2048");
+    return !(e && e[0] == '0');
+}
 
 // ---- unwrap ----
 void residues(const float* w, int nmaps, int H, int W, int* counts, hipStream_t s);

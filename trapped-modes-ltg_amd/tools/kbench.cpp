@@ -170,9 +170,9 @@ int main(int argc, char** argv) {
             float2* ztw = dalloc<float2>(N);
             CK(hipMemcpy(ztw, ones.data(), N * 8, hipMemcpyHostToDevice));
             float* col0 = dalloc<float>((size_t)nb * 2 * H);
-            float2* seam = dalloc<float2>((size_t)nb * (H / fcdk::phase_rows_tile()) * 2 * W);
+            float2* seam = dalloc<float2>((size_t)nb * (H / fcdk::phase_rows_tile(W)) * 2 * W);
             timeit("phase_rows (fused)", 16.0 * H * NCA + 2 * f, [&] {
-                fcdk::phase_rows(true, Ab, H, nb, NCA, NCc, NCc, theta, pre, ptw, ztw, col0, res, Zt, seam, s);
+                fcdk::phase_rows(W, true, Ab, H, nb, NCA, NCc, NCc, theta, pre, ptw, ztw, col0, res, Zt, seam, s);
             });
 #ifdef FCD_STAMPS
             {
