@@ -16,12 +16,12 @@
 //   * unwrap: 16 consecutive pixels per lane; each wave scans its half row (packed
 //     pairs of both maps, one DPP scan); the first wave's total, through LDS, is the
 //     second half's offset (the edge between pixels 1023 and 1024 belongs to the
-//     first wave's last lane);
+//     first wave's last lane), added where the second half is read;
 //   * census: vertical edges inside the tile here, the tile range edges in
 //     k_seam_check2048 (as the 1024 form);
 //   * z-row FFT: 2048 = 2 x 1024 -- wave h of the pair transforms the samples 2m + h
-//     (the wave-local 1024-point group FFT), then X[k] = E[k] + w^k O[k] and
-//     X[k + 1024] = E[k] - w^k O[k] in place (E at pad(k), O at pad(k + 1024));
+//     (the wave-local 1024-point group FFT), and the Zt write-out joins the halves,
+//     X[k] = E[k] + w^k O[k] and X[k + 1024] = E[k] - w^k O[k];
 //   * Zt: 8-row tiles at 2048 (zt_rows), so a tile writes 32-byte halves of its
 //     columns' 64-byte runs; the next tile of the block's contiguous range writes the
 //     other halves right after.
@@ -57,8 +57,8 @@ constexpr int OFFQ_CTW = OFFQ_ZTAB + Q_ZTAB;                 // w^k = exp(-2 pi 
 constexpr int OFFQ_BTAB = OFFQ_CTW + 1024;                   // band-FFT pass twiddles
 constexpr int OFFQ_SLOT = (OFFQ_BTAB + GSched<Q_B>::TABLE + 1) & ~1;
 constexpr int OFFQ_PREV = OFFQ_SLOT + Q_ROWS * Q_SLOT;       // the last row's second slot
-constexpr int OFFQ_CARRY = OFFQ_PREV + Q_SLOT;               // [ROWS] first-wave scan totals (int)
-constexpr size_t Q_LDS = (size_t)(OFFQ_CARRY + Q_ROWS) * 8;
+constexpr int OFFQ_CARRY = OFFQ_PREV + Q_SLOT;               // [ROWS + 1] first-wave scan totals (int)
+constexpr size_t Q_LDS = (size_t)(OFFQ_CARRY + Q_ROWS + 1) * 8;
 static_assert(Q_SLOT % 2 == 0 && Q_LDS <= 160 * 1024, "fused 2048 kernel LDS");
 static_assert(2 * Q_L * GSched<Q_B>::REGION <= 2 * Q_SLOT, "paired float-half band exchange fits the slot");
 static_assert(2 * Q_HALF <= Q_SLOT, "two 1024-point exchange regions per slot");
@@ -91,6 +91,13 @@ __global__ __launch_bounds__(Q_THREADS, 1) void k_phase_rows2048(
     // the last row alternates between two slots, so the previous tile's last
     // unwrapped row survives for the census against this tile's first row
     auto row_slot = [&](int w, int k) { return lds_q + (w == Q_ROWS - 1 && k ? OFFQ_PREV : OFFQ_SLOT + w * Q_SLOT); };
+    // the second half row is stored WITHOUT the first half's total k' (no barrier
+    // between the two waves' scans): that offset, 2 pi (carry0, carry1) of the row,
+    // is added where the second half is read (census, seam rows, z-row FFT)
+    auto row_carry = [&](int w, int k) {
+        const int c = carry[w == Q_ROWS - 1 && k ? Q_ROWS : w];
+        return fv2{kTwoPiQ * (float)((c & 0xffff) - 16 * 64), kTwoPiQ * (float)((c >> 16) - 16 * 64)};
+    };
     for (int i = threadIdx.x; i < GSched<Q_B>::TABLE; i += Q_THREADS) btab[i] = ptw[i];
     for (int i = threadIdx.x; i < 16 * Q_RL; i += Q_THREADS) ptl[(i % 16) * Q_RL + i / 16] = pre[i];
     for (int i = threadIdx.x; i < Q_ZTAB; i += Q_THREADS) ztab[i] = ztw[i];
@@ -212,13 +219,12 @@ __global__ __launch_bounds__(Q_THREADS, 1) void k_phase_rows2048(
                 const int packed = ((int)run.x + 16) | (((int)run.y + 16) << 16);
                 const int incl = team_scan_incl_dpp<64>(packed);
                 const int excl = incl - packed;
-                if (half == 0 && lane == 63) carry[row] = incl;  // the first half row's total
-                __syncthreads();  // carries written; every lane has read its values
+                if (half == 0 && lane == 63) carry[row == Q_ROWS - 1 && par ? Q_ROWS : row] = incl;  // first half's total
                 fv2 acc = {(float)((excl & 0xffff) - 16 * lane), (float)((excl >> 16) - 16 * lane)};
-                if (half) {
-                    const int c = carry[row];
-                    acc += fv2{(float)((c & 0xffff) - 16 * 64), (float)((c >> 16) - 16 * 64)};
-                }
+                // every lane has read its neighbour's first value; the first wave's last
+                // lane also reads pixel 1024, which the second wave's lane 0 may already
+                // have rewritten -- with its own value, as k'' = 0 there (fma(0, 2 pi, w) = w)
+                wave_sync();
 #pragma unroll
                 for (int j = 0; j < 16; ++j) {
                     slot[pad(j0 + j)] = vp(acc * kTwoPiQ + pv(v[j]));
@@ -227,17 +233,18 @@ __global__ __launch_bounds__(Q_THREADS, 1) void k_phase_rows2048(
                 bad |= amb;
             }
         }
+        __syncthreads();
         if constexpr (UNWRAP) {  // first and last unwrapped rows of the range -> seam buffer
             if ((row == 0 && blk == it0 && rb > 0) || (row == Q_ROWS - 1 && blk == it1 - 1 && rb < rbs - 1)) {
+                const fv2 cy = half ? row_carry(row, par) : fv2{0.f, 0.f};
                 float4* sd = reinterpret_cast<float4*>(seam + (((long)f * rbs + rb) * 2 + (row ? 1 : 0)) * Q_W + j0);
 #pragma unroll
                 for (int j = 0; j < 16; j += 2) {
-                    const float2 a = slot[pad(j0 + j)], b = slot[pad(j0 + j + 1)];
+                    const fv2 a = pv(slot[pad(j0 + j)]) + cy, b = pv(slot[pad(j0 + j + 1)]) + cy;
                     sd[j / 2] = make_float4(a.x, a.y, b.x, b.y);
                 }
             }
         }
-        __syncthreads();
         // ---- vertical census against the next row of the tile (range edges: k_seam_check2048)
         if constexpr (UNWRAP) {
             if (row < Q_ROWS - 1 || (blk > it0 && rb > 0)) {
@@ -245,12 +252,12 @@ __global__ __launch_bounds__(Q_THREADS, 1) void k_phase_rows2048(
                 const float2* a_row = up ? row_slot(Q_ROWS - 1, par ^ 1) : slot;
                 const float2* nx = up ? row_slot(0, 0) : row_slot(row + 1, par);
                 const float2 a0 = a_row[0], b0 = nx[0];  // phi'(r, 0) = w(r, 0)
-                const float d0 = kTwoPiQ * (float)(-fw_exact2(a0.x, b0.x));
-                const float d1 = kTwoPiQ * (float)(-fw_exact2(a0.y, b0.y));
+                fv2 dd = {kTwoPiQ * (float)(-fw_exact2(a0.x, b0.x)), kTwoPiQ * (float)(-fw_exact2(a0.y, b0.y))};
+                if (half) dd += (up ? row_carry(0, 0) : row_carry(row + 1, par)) - (up ? row_carry(Q_ROWS - 1, par ^ 1) : row_carry(row, par));
                 float m = 0.f;
 #pragma unroll
                 for (int j = 0; j < 16; ++j) {
-                    const fv2 e = (pv(nx[pad(j0 + j)]) - pv(a_row[pad(j0 + j)])) + fv2{d0, d1};
+                    const fv2 e = (pv(nx[pad(j0 + j)]) - pv(a_row[pad(j0 + j)])) + dd;
                     m = fmaxf(m, fmaxf(fabsf(e.x), fabsf(e.y)));
                 }
                 bad |= (int)(m > kQ_VLim);
@@ -261,8 +268,9 @@ __global__ __launch_bounds__(Q_THREADS, 1) void k_phase_rows2048(
         // ---- forward row FFT of phi0' + i phi1': two 1024-point halves, then one radix-2 pass
         {
             float2 x[16];
+            const fv2 cy = UNWRAP ? row_carry(row, par) : fv2{0.f, 0.f};
 #pragma unroll
-            for (int q = 0; q < 16; ++q) x[q] = slot[pad(2 * (lane + 64 * q) + half)];
+            for (int q = 0; q < 16; ++q) x[q] = q < 8 ? slot[pad(2 * (lane + 64 * q) + half)] : vp(pv(slot[pad(2 * (lane + 64 * q) + half)]) + cy);
             // the last row transforms in its other slot (the previous tile's row, no
             // longer needed): its unwrapped row stays for the next tile's census
             float2* const zs = row_slot(row, par ^ 1);
@@ -271,26 +279,22 @@ __global__ __launch_bounds__(Q_THREADS, 1) void k_phase_rows2048(
             wave_sync();
 #pragma unroll
             for (int q = 0; q < 16; ++q) zs[half * Q_HALF + pad(lane + 64 * q)] = x[q];
-            __syncthreads();
-#pragma unroll
-            for (int m = 0; m < 1024 / Q_RL; ++m) {
-                const int k = l + Q_RL * m;
-                const float2 e = zs[pad(k)], o = cmul(zs[Q_HALF + pad(k)], ctw[k]);
-                zs[pad(k)] = cadd(e, o);
-                zs[Q_HALF + pad(k)] = csub(e, o);
-            }
         }
         __syncthreads();
-        // ---- Zt: 32-byte halves of the 8-row tile's 64-byte column runs
+        // ---- Zt: 32-byte halves of the 8-row tile's 64-byte column runs; the radix-2
+        // join X[k] = E[k] + w^k O[k], X[k + 1024] = E[k] - w^k O[k] on the way out
+        static_assert(!FCD_ZT_PAIRED, "the join pairs columns k and k + 1024");
         {
             const int r0 = rb * Q_ROWS;
             float2* dst = Zt + (long)f * H * Q_W + (long)(r0 / Q_ZT) * Q_W * Q_ZT + (r0 % Q_ZT);
             const int c0 = threadIdx.x / Q_ROWS, rl = threadIdx.x % Q_ROWS;
             const float2* src = row_slot(rl, par ^ 1);
 #pragma unroll 4
-            for (int k = 0; k < Q_W / (Q_THREADS / Q_ROWS); ++k) {
+            for (int k = 0; k < 1024 / (Q_THREADS / Q_ROWS); ++k) {
                 const int c = c0 + (Q_THREADS / Q_ROWS) * k;
-                st_stream(dst + c * Q_ZT + rl, src[pad(zt_col_inv(c, Q_W))]);
+                const float2 e = src[pad(c)], o = cmul(src[Q_HALF + pad(c)], ctw[c]);
+                st_stream(dst + c * Q_ZT + rl, cadd(e, o));
+                st_stream(dst + (c + 1024) * Q_ZT + rl, csub(e, o));
             }
         }
         __syncthreads();
