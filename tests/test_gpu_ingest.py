@@ -239,3 +239,52 @@ def test_two_stream_split_equals_one_stream(df, monkeypatch, case):
     assert np.array_equal(out["1"], out["2"])
     want, _, _ = _engine(ref, sq).process(frames, 1.0, unwrap=True, want_phases=False)
     assert np.array_equal(out["2"], want)
+
+
+def test_exact_first_mode_for_residue_heavy_batches(df, monkeypatch):
+    """After a device call whose frames mostly carried residues, the next call skips the
+    fused first pass and runs the exact chain at once (demod, residue count, scan unwrap
+    for residue-free maps and the MST for the rest, integration): heights bit-identical
+    to the two-pass form for the residue frames (same kernels and k-fields), equal up to
+    float rounding for a residue-free frame of the same batch (the reference itself:
+    zero phase); a mostly residue-free call switches back."""
+    import torch
+    ref, sq = df["ref_u16"].astype(np.float32), float(df["square_size"])
+    real = df["frames_u16"].astype(np.float32)  # 3 frames, 7..1611 residues per map
+    frames = np.stack([real[0], ref, real[1], real[2]])
+    dev = torch.device("cuda", 0)
+    fd = torch.from_numpy(frames).to(dev)
+    out = {}
+    for ef in ("0", "1"):
+        monkeypatch.setenv("FCD_EXACT_FIRST", ef)
+        eng = _engine(ref, sq)
+        hd = torch.empty_like(fd)
+        eng.process_device(fd.data_ptr(), len(frames), 1.0, True, hd.data_ptr())
+        torch.cuda.synchronize()
+        out[ef] = hd.cpu().numpy()
+    real_idx = [0, 2, 3]
+    assert np.array_equal(out["0"][real_idx], out["1"][real_idx])
+    scale = np.abs(out["0"][real_idx]).max()
+    assert np.abs(out["1"][1] - out["0"][1]).max() < 1e-6 * scale
+    monkeypatch.delenv("FCD_EXACT_FIRST")
+    # auto: the first call (3 of 4 frames with residues) switches the mode for the next
+    eng = _engine(ref, sq)
+    eng.profile(True)
+    hd = torch.empty_like(fd)
+    eng.process_device(fd.data_ptr(), len(frames), 1.0, True, hd.data_ptr())
+    torch.cuda.synchronize()
+    st, _ = eng.stage_times()
+    assert st["launches"] >= 1 and int(st["fixup_frames"]) == 3
+    eng.process_device(fd.data_ptr(), len(frames), 1.0, True, hd.data_ptr())
+    torch.cuda.synchronize()
+    st, _ = eng.stage_times()
+    assert st["launches"] == 0 and int(st["fixup_frames"]) == 3  # no fused first pass ran
+    assert np.array_equal(hd.cpu().numpy()[real_idx], out["0"][real_idx])
+    # a residue-free call (the reference repeated) switches back after it
+    fr = torch.from_numpy(np.stack([ref] * 4)).to(dev)
+    eng.process_device(fr.data_ptr(), 4, 1.0, True, hd.data_ptr())
+    eng.process_device(fr.data_ptr(), 4, 1.0, True, hd.data_ptr())
+    torch.cuda.synchronize()
+    st, _ = eng.stage_times()
+    assert st["launches"] >= 1 and int(st["fixup_frames"]) == 0
+    eng.profile(False)

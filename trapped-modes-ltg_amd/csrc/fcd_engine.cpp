@@ -222,6 +222,7 @@ struct fcd_ctx {
     size_t ev_used = 0;
     long prof_frames = 0;
     double prof_fix_ms = 0;   // host wall time of the exact fix-up pass (it synchronises)
+    bool exact_first = false;  // most frames of the last device call had residues (process_impl)
     long prof_fix_frames = 0;
 
     hipStream_t pick(void* s) const { return s ? static_cast<hipStream_t>(s) : own; }
@@ -1247,6 +1248,45 @@ int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int f
         res = c->fres.as<int>();
         HIPCHK(hipMemsetAsync(res, 0, (size_t)n_frames * 2 * sizeof(int), s));
     }
+    // ---- residue-heavy input (camera frames: every map carries residues): when most
+    // frames of the previous call needed the exact pass, the fused first pass would only
+    // produce heights that pass 2 throws away, so this call runs the exact chain at once:
+    // demod, residue count, the scan unwrap for residue-free maps and the MST for the
+    // others, integration.  Same kernels and k-fields as pass 2 (bit-identical heights);
+    // FCD_EXACT_FIRST=0 / 1 forces either mode.
+    static const int ef_env = fcd_env_int("FCD_EXACT_FIRST", -1);
+    if (unwrap && dev && !wrapped_out && (ef_env >= 0 ? ef_env == 1 : c->exact_first)) {
+        const auto t0 = std::chrono::steady_clock::now();
+        long nres = 0;
+        std::vector<int> counts;
+        for (int f0 = 0; f0 < n_frames; f0 += nbmax) {
+            const int nb = std::min(nbmax, n_frames - f0);
+            const float* fr = reinterpret_cast<const float*>(static_cast<const char*>(frames) + (size_t)f0 * rb);
+            if (format != FCD_FMT_F32) {
+                std::vector<int> idx(nb);
+                std::iota(idx.begin(), idx.end(), f0);
+                stage_frames(c, frames, format, dev, idx.data(), nb, s);
+                fr = c->frames_in.as<float>();
+            }
+            fast_demod(c, fr, nb, s);
+            int32_t* kf = k_out ? k_out + (size_t)f0 * 2 * hw : c->fk.as<int32_t>();
+            counts.assign((size_t)2 * nb, 0);
+            unwrap_maps(c, c->wrapped.as<float>(), 2 * nb, kf, counts.data(), s);
+            fcdk::int_rows(c->W, 2, c->wrapped.as<float>(), nullptr, kf, nullptr, nullptr, c->H, nb, c->Zt.as<float2>(),
+                           c->twp_row.as<float2>(), nullptr, s);
+            fcdk::int_cols(c->H, c->Zt.as<float2>(), c->W, nb, coef, c->Ht.as<float2>(), c->twp_col.as<float2>(), s);
+            fcdk::int_c2r(c->W, c->Ht.as<float2>(), c->H, nb, height_out ? height_out + (size_t)f0 * hw : c->out_h.as<float>(),
+                          c->twp_row.as<float2>(), s);
+            for (int i = 0; i < nb; ++i) nres += counts[2 * (size_t)i] || counts[2 * (size_t)i + 1];
+        }
+        HIPCHK(hipStreamSynchronize(s));
+        if (4 * nres < n_frames) c->exact_first = false;  // mostly residue-free again
+        if (c->profiling) {
+            c->prof_fix_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            c->prof_fix_frames += nres;
+        }
+        return FCD_OK;
+    }
     // ---- pass 1: every frame through the band-pruned pipeline with the residue-free unwrap
     const bool fused = c->fused_ok && !wrapped_out && !k_out && !c->force_unfused;
     if (!dev && !wrapped_out && !k_out) {
@@ -1327,6 +1367,7 @@ int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int f
     std::vector<int> redo;
     for (int f = 0; f < n_frames; ++f)
         if (counts[2 * (size_t)f] || counts[2 * (size_t)f + 1]) redo.push_back(f);
+    if (dev && 2 * redo.size() >= (size_t)n_frames) c->exact_first = true;  // the next call skips pass 1
     const auto fix_t0 = std::chrono::steady_clock::now();
     struct FixTimer {
         fcd_ctx* c;
