@@ -288,3 +288,9 @@ def test_exact_first_mode_for_residue_heavy_batches(df, monkeypatch):
     st, _ = eng.stage_times()
     assert st["launches"] >= 1 and int(st["fixup_frames"]) == 0
     eng.profile(False)
+    # host-pointer calls switch the same way
+    eng = _engine(ref, sq)
+    ha, _, _ = eng.process(frames, 1.0, unwrap=True, want_phases=False)
+    hb, _, _ = eng.process(frames, 1.0, unwrap=True, want_phases=False)
+    assert np.array_equal(ha[real_idx], out["0"][real_idx]) and np.array_equal(hb[real_idx], ha[real_idx])
+    assert np.abs(hb[1] - ha[1]).max() < 1e-6 * scale

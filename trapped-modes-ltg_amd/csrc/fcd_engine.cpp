@@ -1255,28 +1255,33 @@ int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int f
     // others, integration.  Same kernels and k-fields as pass 2 (bit-identical heights);
     // FCD_EXACT_FIRST=0 / 1 forces either mode.
     static const int ef_env = fcd_env_int("FCD_EXACT_FIRST", -1);
-    if (unwrap && dev && !wrapped_out && (ef_env >= 0 ? ef_env == 1 : c->exact_first)) {
+    if (unwrap && !wrapped_out && (ef_env >= 0 ? ef_env == 1 : c->exact_first)) {
         const auto t0 = std::chrono::steady_clock::now();
         long nres = 0;
         std::vector<int> counts;
         for (int f0 = 0; f0 < n_frames; f0 += nbmax) {
             const int nb = std::min(nbmax, n_frames - f0);
             const float* fr = reinterpret_cast<const float*>(static_cast<const char*>(frames) + (size_t)f0 * rb);
-            if (format != FCD_FMT_F32) {
+            if (!dev || format != FCD_FMT_F32) {
                 std::vector<int> idx(nb);
                 std::iota(idx.begin(), idx.end(), f0);
                 stage_frames(c, frames, format, dev, idx.data(), nb, s);
                 fr = c->frames_in.as<float>();
             }
             fast_demod(c, fr, nb, s);
-            int32_t* kf = k_out ? k_out + (size_t)f0 * 2 * hw : c->fk.as<int32_t>();
+            int32_t* kf = dev && k_out ? k_out + (size_t)f0 * 2 * hw : c->fk.as<int32_t>();
             counts.assign((size_t)2 * nb, 0);
             unwrap_maps(c, c->wrapped.as<float>(), 2 * nb, kf, counts.data(), s);
             fcdk::int_rows(c->W, 2, c->wrapped.as<float>(), nullptr, kf, nullptr, nullptr, c->H, nb, c->Zt.as<float2>(),
                            c->twp_row.as<float2>(), nullptr, s);
             fcdk::int_cols(c->H, c->Zt.as<float2>(), c->W, nb, coef, c->Ht.as<float2>(), c->twp_col.as<float2>(), s);
-            fcdk::int_c2r(c->W, c->Ht.as<float2>(), c->H, nb, height_out ? height_out + (size_t)f0 * hw : c->out_h.as<float>(),
-                          c->twp_row.as<float2>(), s);
+            float* hdst = dev && height_out ? height_out + (size_t)f0 * hw : c->out_h.as<float>();
+            fcdk::int_c2r(c->W, c->Ht.as<float2>(), c->H, nb, hdst, c->twp_row.as<float2>(), s);
+            if (!dev && height_out)
+                HIPCHK(hipMemcpyAsync(height_out + (size_t)f0 * hw, hdst, (size_t)nb * hw * 4, out_kind, s));
+            if (!dev && k_out)
+                HIPCHK(hipMemcpyAsync(k_out + (size_t)f0 * 2 * hw, kf, (size_t)nb * 2 * hw * 4, out_kind, s));
+            if (!dev) HIPCHK(hipStreamSynchronize(s));
             for (int i = 0; i < nb; ++i) nres += counts[2 * (size_t)i] || counts[2 * (size_t)i + 1];
         }
         HIPCHK(hipStreamSynchronize(s));
@@ -1367,7 +1372,7 @@ int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int f
     std::vector<int> redo;
     for (int f = 0; f < n_frames; ++f)
         if (counts[2 * (size_t)f] || counts[2 * (size_t)f + 1]) redo.push_back(f);
-    if (dev && 2 * redo.size() >= (size_t)n_frames) c->exact_first = true;  // the next call skips pass 1
+    if (2 * redo.size() >= (size_t)n_frames) c->exact_first = true;  // the next call skips pass 1
     const auto fix_t0 = std::chrono::steady_clock::now();
     struct FixTimer {
         fcd_ctx* c;
