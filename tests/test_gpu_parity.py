@@ -469,7 +469,7 @@ def fused(monkeypatch):
 @pytest.mark.parametrize("n,count", [(1024, 3), (2048, 2)])
 def test_fused_height_path_vs_oracle(lib, fused, n, count):
     """Height-only batches (analyze.folder's use of compute_height_map) take the fused
-    kernel (kernels_phase_rows.hip at 1024-point rows, kernels_phase_rows2048.hip at
+    kernel (kernels_phase_rows.hip at 1024-point rows, kernels_phase_rows_wide.hip at
     2048: band transforms + phase + unwrap + row FFT in one pass, column-0 offsets
     applied in the spectra's DC bins): same heights as the oracle and as the unfused
     path, with and without unwrapping."""
@@ -580,8 +580,7 @@ def test_census_flags_residues_on_tile_seams(lib, monkeypatch, n, count):
         del eng
     monkeypatch.delenv("FCD_UNFUSED")
     _lib._engines.clear()
-    if n <= 2048:  # the fused kernel runs at 1024- and 2048-point rows
-        assert np.array_equal(heights["1"], heights["0"])
+    assert np.array_equal(heights["1"], heights["0"])  # the fused kernel runs at every size here
 
 
 def test_full_size_2048_vs_oracle(lib):
@@ -627,6 +626,13 @@ def test_full_size_4096_properties(lib):
         assert np.abs(np.diff(m, axis=0)).max() < np.pi and np.abs(np.diff(m, axis=1)).max() < np.pi
     h0, p0, _ = fcd.compute_height_maps(ref, ref[None], 0.001, height=1.0, return_phases=True)
     assert np.abs(p0).max() < 1e-3 and np.abs(h0).max() < 1e-6 * max(1.0, np.abs(hu).max())
+    # (4) the height-only calls take the fused kernel (kernels_phase_rows_wide.hip, 4096-point
+    # rows: its own 512-bin band transform and reference angles): against the unfused chain
+    # with unwrapping, against the oracle without
+    hf, _ = fcd.compute_height_maps(ref, frames, 0.001, height=1.0)
+    assert rel_l2(hf[0], hu[0]) < 1e-6
+    hfn, _ = fcd.compute_height_maps(ref, frames, 0.001, height=1.0, unwrap=False)
+    assert rel_l2(hfn[0], ho) < 1e-5
 
 
 def test_empty_batch_and_errors(lib):

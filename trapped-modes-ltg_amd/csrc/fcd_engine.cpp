@@ -187,6 +187,7 @@ struct fcd_ctx {
     int fchunk = 1;                  // frames per fast-path chunk
     DevBuf Xb, Ab, Zt, Ht, fk, fres; // per-chunk intermediates; fk: k-fields for the fix-up pass
     int band_B = 0;                  // band window of the pruned inverse (0: full-length k_demod_phase)
+    int fused_B = 0;                 // band window of the fused kernel (= band_B, or 512 at 4096-point rows)
     DevBuf band_pre, band_ptw, theta_b;  // its pre-twiddles, pass twiddles, reference angle of the band
     DevBuf theta_p;                      // theta_b in the phase kernels' lane-contiguous order
     bool fused_ok = false;           // k_phase_rows applies (height-only calls)
@@ -585,8 +586,11 @@ void build_demod_tables(fcd_ctx* c, hipStream_t s) {
     int B = 16;
     while (B < std::max(c->NCc[0], c->NCc[1])) B *= 2;
     c->band_B = fcdk::band_supported(W, B) ? B : 0;
+    // the fused wide kernel has its own band transform: at 4096-point rows it takes the
+    // 512-bin window the unfused band kernel does not (that path keeps k_demod_phase)
+    c->fused_B = (c->band_B || W == 4096) && fcdk::phase_rows_supported(W, B, H) ? B : 0;
     std::vector<float2> pre, ptw;
-    if (c->band_B) {
+    if (c->band_B || c->fused_B) {
         pre = band_pretwiddles(W, B);
         ptw = group_twiddles(B);
         c->band_pre.ensure(pre.size() * sizeof(float2));
@@ -596,13 +600,15 @@ void build_demod_tables(fcd_ctx* c, hipStream_t s) {
         c->theta_b.ensure(2 * (size_t)c->hw() * sizeof(float));
         c->theta_p.ensure(2 * (size_t)c->hw() * sizeof(float));
     }
-    c->fused_ok = c->band_B && fcdk::phase_rows_supported(W, c->band_B, H);
+    c->fused_ok = c->fused_B != 0;
     std::vector<float2> ztw;
     if (c->fused_ok) {
-        ztw = group_twiddles(W == 2048 ? 1024 : W);
-        if (W == 2048)  // the radix-2 pass joining the two 1024-point halves (kernels_phase_rows2048.hip)
+        ztw = group_twiddles(std::min(W, 1024));
+        // wider rows: the join of the W / 1024 wave-local 1024-point transforms
+        // (kernels_phase_rows_wide.hip), w^(h k) = exp(-2 pi i h k / W), h = 1 .. W/1024 - 1
+        for (int h = 1; h < W / 1024; ++h)
             for (int k = 0; k < 1024; ++k) {
-                const double a = -2.0 * kPi * (double)k / 2048.0;
+                const double a = -2.0 * kPi * (double)h * (double)k / (double)W;
                 ztw.push_back(make_float2((float)std::cos(a), (float)std::sin(a)));
             }
         c->ztw.ensure(ztw.size() * sizeof(float2));
@@ -666,13 +672,18 @@ void fast_demod(fcd_ctx* c, const float* frames, int nb, hipStream_t s, int fo =
 // Reference angle of the band-pruned inverse: the same band pipeline run on
 // the reference image, angle(y_ref) (kernels_band.hip REF mode).
 void band_reference(fcd_ctx* c, const float* dref, hipStream_t s) {
-    if (!c->band_B) return;
+    if (!c->band_B && !c->fused_B) return;
     const fcdk::DemodTables T = demod_tables(c);
     fcdk::demod_rows(c->W, dref, c->H, 1, T, c->Xb.as<float2>(), c->twp_row.as<float2>(), s);
     fcdk::demod_cols(c->H, c->Xb.as<float2>(), 1, T, c->Ab.as<float2>(), c->NCA, c->twp_col.as<float2>(), s);
-    fcdk::band_phase(c->W, c->band_B, true, c->Ab.as<float2>(), c->H, 1, c->NCA, c->NCc[0], c->NCc[1], nullptr,
-                     c->theta_b.as<float>(), c->band_pre.as<float2>(), c->band_ptw.as<float2>(), s);
-    fcdk::band_theta_lanes(c->W, c->band_B, c->theta_b.as<float>(), 2 * c->H, c->theta_p.as<float>(), s);
+    if (c->band_B)
+        fcdk::band_phase(c->W, c->band_B, true, c->Ab.as<float2>(), c->H, 1, c->NCA, c->NCc[0], c->NCc[1], nullptr,
+                         c->theta_b.as<float>(), c->band_pre.as<float2>(), c->band_ptw.as<float2>(), s);
+    else  // 4096-point rows: the fused kernel's own band transform in its REF mode
+        fcdk::phase_rows_wide_ref(c->W, c->Ab.as<float2>(), c->H, c->NCA, c->NCc[0], c->NCc[1],
+                                  c->band_pre.as<float2>(), c->band_ptw.as<float2>(), c->theta_b.as<float>(), s);
+    fcdk::band_theta_lanes(c->W, c->band_B ? c->band_B : c->fused_B, c->theta_b.as<float>(), 2 * c->H,
+                           c->theta_p.as<float>(), s);
 }
 
 // Everything the per-frame path needs from the reference once c->info and
@@ -707,7 +718,7 @@ void reference_state(fcd_ctx* c, const float* dref0, const float* dref1, hipStre
             fcdk::angle(R, c->theta.as<float>() + q * hw, hw, s);
         }
         const size_t tb = (size_t)hw * sizeof(float), rb = (size_t)hw * sizeof(float2);
-        const bool band = c->band_B != 0;
+        const bool band = c->band_B != 0 || c->fused_B != 0;
         if (passes == 2 && pass == 0) {
             keep.ensure(2 * tb + rb + (band ? 2 * tb : 0));
             char* k = static_cast<char*>(keep.p);

@@ -112,9 +112,10 @@ void unwrap_colk(const float* w, int nmaps, int H, int W, int* colk, hipStream_t
 // the same over compact column-0 values col0[map][H] (the fused path's side output)
 void unwrap_colk_compact(const float* col0, int nmaps, int H, int* colk, hipStream_t s);
 // fused band transform + phase + unwrap + z-row FFT (kernels_phase_rows.hip)
-// W = 1024 (B = 128) and W = 2048 (B = 256, kernels_phase_rows2048.hip; FCD_FUSED_2048=0
-// keeps the unfused chain there).  ztw: group_twiddles(W) at 1024; at 2048 the
-// 1024-point table followed by exp(-2 pi i k / 2048), k < 1024.
+// W = 1024 (B = 128), 2048 (B = 256) and 4096 (B = 512; kernels_phase_rows_wide.hip;
+// FCD_FUSED_2048 / FCD_FUSED_4096 = 0 keep the unfused chain there).  ztw:
+// group_twiddles(W) at 1024; wider: the 1024-point table followed by the join twiddles
+// exp(-2 pi i h k / W), h = 1 .. W/1024 - 1, k < 1024.
 bool phase_rows_supported(int W, int B, int H);
 int phase_rows_tile(int W);  // rows per fused tile (seam buffer: nb * H / tile * 2 * W float2)
 void phase_rows(int W, bool unwrap, const float2* Ab, int H, int nb, int NCA, int ncc0, int ncc1, const float* theta,
@@ -151,11 +152,15 @@ void pf_center(const float* img, int nb, long hw, float* sums, float* out, hipSt
 void pf_fft2(const float* in, int nb, int H, int W, const PfPlan& rows, const float* rtw, const PfPlan& cols,
              const float2* ctw, float2* F, hipStream_t s);
 
-void phase_rows2048(bool unwrap, const float2* Ab, int H, int nb, int NCA, int ncc0, int ncc1, const float* theta,
-                    const float2* pre, const float2* ptw, const float2* ztw, float* col0, int* flags, float2* Zt,
-                    float2* seam, hipStream_t s);
-inline bool fcd_fused_2048() {
-    const char* e = std::getenv("FCD_FUSED_2048");
+// kernels_phase_rows_wide.hip: the fused kernel at 2048- and 4096-point rows, and its
+// REF mode (4096: the reference's band angles into theta_b, [2][H][W])
+void phase_rows_wide(int W, bool unwrap, const float2* Ab, int H, int nb, int NCA, int ncc0, int ncc1, const float* theta,
+                     const float2* pre, const float2* ptw, const float2* ztw, float* col0, int* flags, float2* Zt,
+                     float2* seam, hipStream_t s);
+void phase_rows_wide_ref(int W, const float2* Ab, int H, int NCA, int ncc0, int ncc1, const float2* pre,
+                         const float2* ptw, float* theta_b, hipStream_t s);
+inline bool fcd_fused_env(const char* name) {  // FCD_FUSED_2048 / FCD_FUSED_4096 = 0: the unfused chain
+    const char* e = std::getenv(name);
     return !(e && e[0] == '0');
 }
 

@@ -521,17 +521,18 @@ extern "C" int fcd_debug_pr_stamps(unsigned long long* out) {
 
 bool phase_rows_supported(int W, int B, int H) {
     if (H % 16 != 0 || H < 16) return false;
-    if (W == 2048 && B == 256) return fcd_fused_2048();
+    if (W == 2048 && B == 256) return fcd_fused_env("FCD_FUSED_2048");
+    if (W == 4096 && B == 512) return fcd_fused_env("FCD_FUSED_4096");
     return W == PR_W && B == PR_B;
 }
 
-int phase_rows_tile(int W) { return W == 2048 ? 4 : PR_ROWS; }
+int phase_rows_tile(int W) { return W == 2048 ? 4 : (W == 4096 ? 2 : PR_ROWS); }
 
 void phase_rows(int W, bool unwrap, const float2* Ab, int H, int nb, int NCA, int ncc0, int ncc1, const float* theta,
                 const float2* pre, const float2* ptw, const float2* ztw, float* col0, int* flags, float2* Zt,
                 float2* seam, hipStream_t s) {
-    if (W == 2048) {
-        phase_rows2048(unwrap, Ab, H, nb, NCA, ncc0, ncc1, theta, pre, ptw, ztw, col0, flags, Zt, seam, s);
+    if (W == 2048 || W == 4096) {
+        phase_rows_wide(W, unwrap, Ab, H, nb, NCA, ncc0, ncc1, theta, pre, ptw, ztw, col0, flags, Zt, seam, s);
         return;
     }
     if (W != PR_W) throw std::runtime_error("phase_rows: unsupported row length");
