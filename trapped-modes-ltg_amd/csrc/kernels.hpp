@@ -199,7 +199,8 @@ int mst_tile_shape(int H, int W, int* th);  // tile width (64 / 32) and height, 
 void mst_tile_level0(const float* w, const int* map_ids, int nact, int H, int W, MstWork m, hipStream_t s,
                      bool graph = false);
 long mst_cg_edge_capacity(long nv);  // edge records for nv vertices (any tile side)
-// Round r of the component-graph Boruvka (r = 0 first: resolves the cross-tile edges).
+// Round r of the component-graph Boruvka (r = 0: the candidates come from the tile pass; its
+// hooks resolve the cross-tile edges).
 void mst_cg_round(int nact, int H, int W, MstWork m, int r, hipStream_t s);
 void mst_level_setup(int nact, int H, int W, MstWork m, hipStream_t s);
 void mst_level_round(const float* w, const int* map_ids, int nact, int H, int W, MstWork m, int r, hipStream_t s);

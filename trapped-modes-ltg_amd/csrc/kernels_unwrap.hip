@@ -827,7 +827,7 @@ __device__ __forceinline__ int t0_off(unsigned l) { return (int)(short)(l & 0xff
 // [tg * cg_ecap, + cg_ecnt[tg]) as records (ea, eb, weight bits, global edge index,
 // ed = K_ea - K_eb from the pixel offsets and the edge's wrap count).  An edge to a
 // neighbour tile is written with eb = -1 - (neighbour pixel's vertex id) and the
-// neighbour's offset missing; the first round resolves it (comp[], off[] of the pixel).
+// neighbour's offset missing; the first round's hooks resolve it (comp[], off[] of the pixel).
 // For a TW x TH tile: V <= 2 (TW + TH) - 4, edges <= 3 V - 6 + TW + TH.
 __host__ __device__ constexpr int cg_ccap(int tw, int th) { return 2 * (tw + th); }
 __host__ __device__ constexpr int cg_pow2(int n) { return n <= 1 ? 1 : 2 * cg_pow2((n + 1) / 2); }
@@ -883,8 +883,27 @@ __device__ __forceinline__ void tile0_graph(unsigned char* pool, const unsigned 
     int* const rk = reinterpret_cast<int*>(pool + 8 * T0N);  // rank of each root (the links' region)
     const short* const lc = reinterpret_cast<const short*>(pool + 12 * T0N);
     const short* const lo = reinterpret_cast<const short*>(pool + 14 * T0N);
+    const long tg = blockIdx.x;
+    const int cb = (int)(tg * cg_ccap(TW, TH));
+    const long eb0 = tg * ECAP;
+    const int nh = H * (W - 1);
+    // Round 0 of the component-graph rounds comes out of the tile's last round: every
+    // component's lightest outgoing edge (all of them leave the tile) is its minimum
+    // (bw, be) there, be as a local edge code (t0_hcode / t0_vcode).
+    const unsigned long long* const bw = reinterpret_cast<const unsigned long long*>(pool);
+    const int* const be = reinterpret_cast<const int*>(pool + 8 * T0N);
+    unsigned long long rbw[4];
+    int rbe[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int c = threadIdx.x + NT * k;
+        const bool root = lc[c] == c;
+        rbw[k] = root ? bw[c] : ~0ull;
+        rbe[k] = root ? be[c] : 0x7fffffff;
+    }
     __shared__ int ncnt[2];  // roots, edges
     if (threadIdx.x == 0) ncnt[0] = ncnt[1] = 0;
+    __syncthreads();  // the minima are read before the hash table overwrites them
     for (int i = threadIdx.x; i < HS; i += NT) {
         hkey[i] = 0u;
         hcode[i] = 0x7fffffffu;
@@ -898,14 +917,20 @@ __device__ __forceinline__ void tile0_graph(unsigned char* pool, const unsigned 
         for (int k = 0; k < 4; ++k) root[k] = lc[threadIdx.x + NT * k] == threadIdx.x + NT * k;
         wave_append(root, &ncnt[0], r);
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (r[k] >= 0) rk[threadIdx.x + NT * k] = r[k];
+        for (int k = 0; k < 4; ++k) {
+            if (r[k] < 0) continue;
+            rk[threadIdx.x + NT * k] = r[k];
+            const int code = rbe[k];  // local code -> global edge index (k_mst_cand's numbering)
+            int ge = 0x7fffffff;
+            if (code != 0x7fffffff) {
+                const int gi = gi0 + ((code >> 7) & 127) - 1, gj = gj0 + (code & 127) - 1;
+                ge = (code >> 14) ? nh + gi * W + gj : gi * (W - 1) + gj;
+            }
+            m.best_w[cb + r[k]] = rbw[k];
+            m.best_e[cb + r[k]] = ge;
+        }
     }
     __syncthreads();
-    const long tg = blockIdx.x;
-    const int cb = (int)(tg * cg_ccap(TW, TH));
-    const long eb0 = tg * ECAP;
-    const int nh = H * (W - 1);
     // Every global store of the write-out comes after the last barrier: a barrier is a
     // workgroup release and would wait for the stores in flight (about a quarter of the
     // tile's time when the comp / off stores preceded the hash phases).
@@ -988,12 +1013,10 @@ __device__ __forceinline__ void tile0_graph(unsigned char* pool, const unsigned 
         const int id = cb + rk[c];
         m.comp[v] = id;
         m.off[v] = lo[i];
-        if (c == i) {
+        if (c == i) {  // (its round-0 minimum is written above)
             m.rootof[id] = id;
             m.offk[id] = 0;
             m.link[id] = pack_link(id, 0);
-            m.best_w[id] = 0x7ff0000000000000ull;
-            m.best_e[id] = 0x7fffffff;
         }
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -1268,9 +1291,9 @@ __global__ __launch_bounds__(TW * TH / 4, 4) void k_mst_tile0(const float* __res
 constexpr int CG_U = 4;  // edges per thread: cg_ecap <= 1024 = 256 threads x CG_U
 static_assert(cg_ecap(64, 64) <= 256 * CG_U, "one pass over a segment");
 
-// Candidates: per edge between different current roots, atomicMin of its weight into
-// both roots; the segment is compacted in place (edges inside a root are gone for good).
-template <bool FIRST>
+// Candidates (rounds >= 1): per edge between different current roots, atomicMin of its
+// weight into both roots; the segment is compacted in place (edges inside a root are
+// gone for good).
 __global__ __launch_bounds__(256) void k_cg_cand(MstWork m, int ntiles, int ecap) {
     __shared__ int nout;
     for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
@@ -1294,11 +1317,6 @@ __global__ __launch_bounds__(256) void k_cg_cand(MstWork m, int ntiles, int ecap
                 ew[u] = m.cg_ew[b0 + i];
                 ec[u] = m.cg_ec[b0 + i];
                 ed[u] = m.cg_ed[b0 + i];
-                if (FIRST && eb[u] < 0) {  // an edge into the neighbour tile: its component now
-                    const long y = -1 - (long)eb[u];
-                    eb[u] = m.comp[y];
-                    ed[u] += m.off[y];
-                }
             }
         }
 #pragma unroll
@@ -1312,7 +1330,7 @@ __global__ __launch_bounds__(256) void k_cg_cand(MstWork m, int ntiles, int ecap
         for (int u = 0; u < CG_U; ++u) {
             const int pos = block_append(keep[u], &nout);
             if (pos < 0) continue;
-            if (FIRST || pos != u * 256 + (int)threadIdx.x) cg_write_edge(m, b0 + pos, ea[u], eb[u], ew[u], ec[u], ed[u]);
+            if (pos != u * 256 + (int)threadIdx.x) cg_write_edge(m, b0 + pos, ea[u], eb[u], ew[u], ec[u], ed[u]);
             atomicMin(m.best_w + ra[u], ew[u]);
             atomicMin(m.best_w + rb[u], ew[u]);
         }
@@ -1337,6 +1355,9 @@ __global__ __launch_bounds__(256) void k_cg_cand2(MstWork m, int ntiles, int eca
 
 // Hooks: the (unique) edge that is a root's lightest links it to the other root;
 // of a mutual pair the larger root hooks onto the smaller.
+// FIRST (round 0, whose minima the tile pass wrote): the edges into a neighbour tile
+// are resolved here (and written back) instead of in k_cg_cand.
+template <bool FIRST>
 __global__ __launch_bounds__(256) void k_cg_hook(MstWork m, int ntiles, int ecap) {
     for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const int n = m.cg_ecnt[t];
@@ -1346,12 +1367,21 @@ __global__ __launch_bounds__(256) void k_cg_hook(MstWork m, int ntiles, int ecap
             bool hooked = false;
             if (i < n) {
                 const unsigned long long w = m.cg_ew[b0 + i];
-                const int a = m.cg_ea[b0 + i], b = m.cg_eb[b0 + i], c = m.cg_ec[b0 + i];
+                const int a = m.cg_ea[b0 + i], c = m.cg_ec[b0 + i];
+                int b = m.cg_eb[b0 + i];
+                int ed = m.cg_ed[b0 + i];
+                if (FIRST && b < 0) {
+                    const long y = -1 - (long)b;
+                    b = m.comp[y];
+                    ed += m.off[y];
+                    m.cg_eb[b0 + i] = b;
+                    m.cg_ed[b0 + i] = ed;
+                }
                 const int ra = m.rootof[a], rb = m.rootof[b];
                 const bool wa = m.best_w[ra] == w && m.best_e[ra] == c;
                 const bool wb = m.best_w[rb] == w && m.best_e[rb] == c;
                 if (wa || wb) {
-                    const int kab = m.cg_ed[b0 + i] - m.offk[a] + m.offk[b];  // K_ra - K_rb
+                    const int kab = ed - m.offk[a] + m.offk[b];  // K_ra - K_rb
                     if (wa && (!wb || ra > rb)) m.link[ra] = pack_link(rb, kab);
                     else m.link[rb] = pack_link(ra, -kab);
                     hooked = true;
@@ -1406,15 +1436,17 @@ void mst_cg_round(int nact, int H, int W, MstWork m, int r, hipStream_t s) {
     const int ecap = cg_ecap(tw, th), ccap = cg_ccap(tw, th);
     FCD_HIPCHK(hipMemsetAsync(m.nhooks, 0, sizeof(int), s));
     const dim3 g((unsigned)std::min(ntiles, 4096)), b(256);
-    if (r == 0)
-        hipLaunchKernelGGL(k_cg_cand<true>, g, b, 0, s, m, ntiles, ecap);
-    else
-        hipLaunchKernelGGL(k_cg_cand<false>, g, b, 0, s, m, ntiles, ecap);
-    FCD_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_cg_cand2, g, b, 0, s, m, ntiles, ecap);
-    FCD_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_cg_hook, g, b, 0, s, m, ntiles, ecap);
-    FCD_CHECK_LAUNCH();
+    if (r == 0) {  // the candidates of round 0 came with the tile pass
+        hipLaunchKernelGGL(k_cg_hook<true>, g, b, 0, s, m, ntiles, ecap);
+        FCD_CHECK_LAUNCH();
+    } else {
+        hipLaunchKernelGGL(k_cg_cand, g, b, 0, s, m, ntiles, ecap);
+        FCD_CHECK_LAUNCH();
+        hipLaunchKernelGGL(k_cg_cand2, g, b, 0, s, m, ntiles, ecap);
+        FCD_CHECK_LAUNCH();
+        hipLaunchKernelGGL(k_cg_hook<false>, g, b, 0, s, m, ntiles, ecap);
+        FCD_CHECK_LAUNCH();
+    }
     hipLaunchKernelGGL(k_cg_relabel, g, b, 0, s, m, ntiles, ccap);
     FCD_CHECK_LAUNCH();
 }
