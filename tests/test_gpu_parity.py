@@ -233,6 +233,24 @@ def test_unwrap_two_level_equals_pixel_rounds(lib, monkeypatch, shape):
         assert np.all(d == d.flat[0])
 
 
+@pytest.mark.parametrize("shape", [(64, 64), (64, 128), (1024, 1024)])
+def test_residue_counts_match_oracle(lib, shape):
+    """k_residues (4 plaquettes per thread, f32 find_wrap with the exact test at
+    |fl(a - b)| = fl(pi)) against the oracle's count on noisy maps, several per batch,
+    including values exactly pi apart."""
+    from oracle import fcd_oracle as O
+    rng = np.random.default_rng(shape[0] + shape[1])
+    maps = []
+    for s_ in (0.3, 0.8, 1.5):
+        phi = rng.normal(0, s_, shape).cumsum(axis=1) * 0.5
+        maps.append(np.angle(np.exp(1j * phi)).astype(np.float32))
+    w = np.stack(maps)
+    w[0, :, 1::7] = np.float32(np.pi)  # differences of exactly fl(pi) and 0
+    w[0, :, 2::7] = np.float32(0.0)
+    _, res = lib.Engine(shape).unwrap(w)
+    assert [int(r) for r in res] == [O.count_residues(m) for m in w]
+
+
 def test_unwrap_residue_free_scan(lib):
     from oracle import fcd_oracle as O
     y, x = np.mgrid[0:256, 0:512]

@@ -72,31 +72,67 @@ __device__ __forceinline__ long xcd_block() {
 }
 
 // ------------------------------------------------------------------ residues
-__global__ void k_residues(const float* __restrict__ w, int nmaps, int H, int W, int* counts) {
-    const long hw = (long)H * W;
-    const long idx = xcd_block() * blockDim.x + threadIdx.x;
+// find_wrap in f32: fl(a - b) > fl(pi) only if a - b > M_PI; |fl(a - b)| = fl(pi) is
+// flagged for the exact f64 test (kernels_fast.hip fw_fast)
+__device__ __forceinline__ int find_wrap_f(float a, float b, bool& amb) {
+    const float d = a - b;
+    constexpr float P = 3.14159274f;
+    amb |= fabsf(d) == P;
+    return d > P ? -1 : (d < -P ? 1 : 0);
+}
+
+// Residue count per map: 4 plaquettes per thread (4 pixels of a row and the next row, 16-
+// byte loads), 1024 pixels per block, blockIdx.y = map.
+__global__ __launch_bounds__(256) void k_residues(const float* __restrict__ w, int H, int W, int* counts) {
+    const int map = blockIdx.y;
+    // XCD-aware: consecutive row blocks on one XCD (xcd_block), so the row a block shares
+    // with the next one comes from that XCD's L2
+    const unsigned G = gridDim.x, bx = blockIdx.x;
+    const int vb = (G % 8 == 0) ? (int)((bx % 8) * (G / 8) + bx / 8) : (int)bx;
+    const int p = vb * 1024 + 4 * threadIdx.x;  // first pixel of this thread (W % 4 == 0)
+    const int i = p / W, j = p % W;
     int r = 0;
-    int map = -1;
-    if (idx < nmaps * hw) {
-        map = (int)(idx / hw);
-        const long p = idx % hw;
-        const int i = (int)(p / W), j = (int)(p % W);
-        if (i < H - 1 && j < W - 1) {
-            const float* m = w + map * hw;
-            const float a = m[p], b = m[p + 1], c = m[p + W + 1], d = m[p + W];
-            r = (find_wrap(a, b) + find_wrap(b, c) + find_wrap(c, d) + find_wrap(d, a)) != 0;
+    if (p < H * W && i < H - 1) {
+        const float* m = w + (long)map * H * W + p;
+        const float4 a = *reinterpret_cast<const float4*>(m), c = *reinterpret_cast<const float4*>(m + W);
+        const bool last = j + 4 >= W;  // the row's last plaquette column is j + 2
+        const float an = last ? 0.f : m[4], cn = last ? 0.f : m[W + 4];
+        const float ra[5] = {a.x, a.y, a.z, a.w, an}, rc[5] = {c.x, c.y, c.z, c.w, cn};
+        const int nk = last ? 3 : 4;
+        bool amb = false;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            // plaquette (i, j + k): a -> b -> c -> d -> a, a = (i, j+k), b = (i, j+k+1), c = (i+1, j+k+1), d = (i+1, j+k)
+            const int s = find_wrap_f(ra[k], ra[k + 1], amb) + find_wrap_f(ra[k + 1], rc[k + 1], amb) +
+                          find_wrap_f(rc[k + 1], rc[k], amb) + find_wrap_f(rc[k], ra[k], amb);
+            r += k < nk && s != 0;
+        }
+        if (amb) {  // some difference is exactly fl(pi) apart: the f64 tests for this thread
+            r = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                r += k < nk && (find_wrap(ra[k], ra[k + 1]) + find_wrap(ra[k + 1], rc[k + 1]) + find_wrap(rc[k + 1], rc[k]) +
+                                find_wrap(rc[k], ra[k])) != 0;
         }
     }
-    // blocks never straddle maps when H*W % 256 == 0 (H, W >= 64 powers of two)
-    unsigned long long bal = __ballot(r);
-    const int wave_cnt = __popcll(bal);
-    if ((threadIdx.x & 63) == 0 && wave_cnt && map >= 0) atomicAdd(counts + map, wave_cnt);
+    // one atomic per block with residues: a map's count word takes one add per block
+    // (the camera frames' 1.6 k residues per map would otherwise queue ~1.6 k adds on it)
+    __shared__ int bc;
+    if (threadIdx.x == 0) bc = 0;
+    __syncthreads();
+    int wave_cnt = r;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) wave_cnt += __shfl_xor(wave_cnt, o, 64);
+    if ((threadIdx.x & 63) == 0 && wave_cnt) atomicAdd(&bc, wave_cnt);
+    __syncthreads();
+    if (threadIdx.x == 0 && bc) atomicAdd(counts + map, bc);
 }
 
 void residues(const float* w, int nmaps, int H, int W, int* counts, hipStream_t s) {
-    const long n = (long)nmaps * H * W;
     FCD_HIPCHK(hipMemsetAsync(counts, 0, sizeof(int) * nmaps, s));
-    hipLaunchKernelGGL(k_residues, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, w, nmaps, H, W, counts);
+    if (W % 4 != 0) throw std::runtime_error("residues: W must be a multiple of 4");
+    hipLaunchKernelGGL(k_residues, dim3((unsigned)(((long)H * W + 1023) / 1024), (unsigned)nmaps), dim3(256), 0, s, w, H, W,
+                       counts);
     FCD_CHECK_LAUNCH();
 }
 
