@@ -601,6 +601,43 @@ def test_census_flags_residues_on_tile_seams(lib, monkeypatch, n, count):
     assert np.array_equal(heights["1"], heights["0"])  # the fused kernel runs at every size here
 
 
+# (y0, x0) of dislocation pairs whose residues fall on plaquette rows 128k - 1 in both
+# carrier maps at 1024^2: the edges between the fused kernel's dynamic chunks of 16
+# eight-row tiles (FCD_PR_CHUNK), found with the oracle as SEAM_PAIRS were
+CHUNK_EDGE_PAIRS = [(512.0, 307.2), (512.0, 512.0), (639.5, 358.4), (639.75, 358.4)]
+
+
+@pytest.mark.parametrize("count", [6, 40])
+def test_fused_dynamic_schedule_matches_static(lib, monkeypatch, count):
+    """k_phase_rows at 1024^2 takes its tiles in chunks from a counter (FCD_PR_DYNAMIC=1,
+    the default) or as one contiguous range per block (=0): residue pairs on chunk
+    edges (checked by the deferred k_seam_check) and inside chunks are flagged by both
+    schedules, and every height is bit-identical; 6 frames = fewer chunks than CUs."""
+    from pyfcd import _lib
+    from bench_data import make_frames_numpy
+    n = 1024
+    ref, dis = dislocation_frames(n, [p[0] for p in CHUNK_EDGE_PAIRS] + [206.75],
+                                  [p[1] for p in CHUNK_EDGE_PAIRS] + [307.2])
+    _, smooth = make_frames_numpy(n, count - len(dis), seed=5)
+    frames = np.concatenate([dis, smooth.astype(np.float32)])
+    _lib._engines.clear()
+    heights = {}
+    for dyn in ("0", "1"):
+        monkeypatch.setenv("FCD_PR_DYNAMIC", dyn)
+        eng = lib.Engine(ref.shape)
+        eng.set_reference(ref, 0.001)
+        eng.profile(True)
+        h, _, _ = eng.process(frames, 1.0, unwrap=True, want_phases=False)
+        st, _ = eng.stage_times()
+        eng.profile(False)
+        assert int(st["fixup_frames"]) == len(dis), (dyn, st)
+        heights[dyn] = h
+        del eng
+    monkeypatch.delenv("FCD_PR_DYNAMIC")
+    _lib._engines.clear()
+    assert np.array_equal(heights["0"], heights["1"])
+
+
 def test_full_size_2048_vs_oracle(lib):
     """configs[2] geometry (2048^2, HBM-bound regime): one rotated-board frame against the
     oracle with unwrapping; peaks / cf bit-exact, phases up to one 2*pi*c, heights rel-L2."""

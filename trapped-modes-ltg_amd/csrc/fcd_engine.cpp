@@ -163,6 +163,23 @@ struct HostPipe {
     }
 };
 
+// Page-locked host buffer that only grows (the census readback of every call).
+struct PinBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    void ensure(size_t n) {
+        if (n <= cap) return;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        if (hipHostMalloc(&p, n, hipHostMallocDefault) != hipSuccess) throw std::runtime_error("hipHostMalloc failed");
+        cap = n;
+    }
+    ~PinBuf() {
+        if (p) (void)hipHostFree(p);
+    }
+};
+
 }  // namespace
 
 struct fcd_ctx {
@@ -193,12 +210,17 @@ struct fcd_ctx {
     bool fused_ok = false;           // k_phase_rows applies (height-only calls)
     bool force_unfused = false;      // FCD_UNFUSED=1: take the unfused chain (A/B measurement)
     int nstreams = 2;                // FCD_STREAMS: device-path chunks split over 1 or 2 streams
+    bool defer_seam = true;          // FCD_DEFER_SEAM: the fused chain's seam census after the integration
+    bool pr_dynamic = false;         // FCD_PR_DYNAMIC=1: the 1024 fused kernel takes tile chunks from a counter
+                                     // (r03t: 80.1-81.0k vs 80.0-81.6k frames/s static, no gain; kept as an option)
+    DevBuf pr_ctr;                   // its counter pairs, one per concurrent half (each launch leaves them 0)
     hipStream_t aux = nullptr;       // the second stream and its fork / join events
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     DevBuf ir_seam;                  // k_int_rows2's seam rows (tile-range edges), one region per stream
     DevBuf ztw, col0, seam;          // its 1024-point group-FFT twiddles; column-0 wrapped values [f][2][H];
                                      // first/last unwrapped rows of every tile [f][H/tile][2][W]
     size_t fres_cap = 0;
+    PinBuf census;                   // the census readback, page-locked: one DMA, no staging copy
 
     // workspace
     int chunk = 1;
@@ -858,9 +880,13 @@ FCD_API int fcd_create(int device, int rows, int cols, fcd_ctx** out) {
         c->device = device;
         c->force_unfused = fcd_env_int("FCD_UNFUSED", 0) != 0;
         c->nstreams = fcd_env_int("FCD_STREAMS", 2) >= 2 ? 2 : 1;
+        c->defer_seam = fcd_env_int("FCD_DEFER_SEAM", 1) != 0;
+        c->pr_dynamic = fcd_env_int("FCD_PR_DYNAMIC", 0) != 0;
         c->H = rows;
         c->W = cols;
         HIPCHK(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking));
+        c->pr_ctr.ensure(4 * sizeof(unsigned));
+        HIPCHK(hipMemset(c->pr_ctr.p, 0, 4 * sizeof(unsigned)));
         const std::vector<float2> tr = twiddles(cols), tc = twiddles(rows);
         c->tw_row.ensure(tr.size() * sizeof(float2));
         c->tw_col.ensure(tc.size() * sizeof(float2));
@@ -1059,13 +1085,19 @@ void first_pass_chunk(fcd_ctx* c, const float* fr, int nb, bool unwrap, bool fus
         fcdk::demod_rows(c->W, fr, c->H, nb, T, Xb, c->twp_row.as<float2>(), s);
         fcdk::demod_cols(c->H, Xb, nb, T, Ab, c->NCA, c->twp_col.as<float2>(), s);
         if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
+        // dynamic chunk schedule: each concurrent half (fo) has its own counter pair
+        unsigned* ctr = c->pr_dynamic ? c->pr_ctr.as<unsigned>() + (fo ? 2 : 0) : nullptr;
         fcdk::phase_rows(c->W, unwrap, Ab, c->H, nb, c->NCA, c->NCc[0], c->NCc[1], c->theta_p.as<float>(),
                          c->band_pre.as<float2>(), c->band_ptw.as<float2>(), c->ztw.as<float2>(), col0, res, Zt, seam,
-                         s);
+                         s, c->defer_seam, ctr);
         if (unwrap) fcdk::unwrap_colk_compact(col0, 2 * nb, c->H, colk, s);
         if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
         fcdk::int_cols(c->H, Zt, c->W, nb, coef, Ht, c->twp_col.as<float2>(), s, unwrap ? colk : nullptr);
         fcdk::int_c2r(c->W, Ht, c->H, nb, hdst, c->twp_row.as<float2>(), s);
+        // the census of the tile-range edges: its flags are read only when the call ends,
+        // so it runs last instead of holding the integration kernels behind it (a small
+        // grid waiting for CUs the other stream's fused kernel holds)
+        if (unwrap && c->defer_seam) fcdk::phase_rows_seam(c->W, c->H, nb, seam, res, s, ctr != nullptr);
     } else {
         const long H = c->H, W = c->W;
         float* wrapped = c->wrapped.as<float>() + fo * 2 * H * W;
@@ -1364,8 +1396,16 @@ int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int f
     }
     if (!unwrap) return FCD_OK;
     // ---- pass 2: frames whose maps have residues are redone with the Boruvka (MST) unwrap
+    // into page-locked memory: a pageable destination went through the runtime's staging
+    // copy (a blit kernel, then a host memcpy before the stream reports completion)
+    static const int pinned_env = fcd_env_int("FCD_CENSUS_PINNED", 1);
     std::vector<int> counts((size_t)n_frames * 2);
-    HIPCHK(hipMemcpyAsync(counts.data(), res, counts.size() * sizeof(int), hipMemcpyDeviceToHost, s));
+    int* cdst = counts.data();
+    if (pinned_env) {
+        c->census.ensure(counts.size() * sizeof(int));
+        cdst = static_cast<int*>(c->census.p);
+    }
+    HIPCHK(hipMemcpyAsync(cdst, res, counts.size() * sizeof(int), hipMemcpyDeviceToHost, s));
     // polled rather than a blocking wait: the caller's next batch is enqueued as soon
     // as this one's census is back (a blocking wait's wake-up sat in every bench step,
     // ~17 us per 256-frame step at 1024^2).  The poll yields the core between queries
@@ -1380,6 +1420,7 @@ int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int f
     }
     if (qe == hipErrorNotReady) qe = hipStreamSynchronize(s);
     HIPCHK(qe);
+    if (cdst != counts.data()) std::memcpy(counts.data(), cdst, counts.size() * sizeof(int));
     std::vector<int> redo;
     for (int f = 0; f < n_frames; ++f)
         if (counts[2 * (size_t)f] || counts[2 * (size_t)f + 1]) redo.push_back(f);

@@ -118,9 +118,17 @@ void unwrap_colk_compact(const float* col0, int nmaps, int H, int* colk, hipStre
 // exp(-2 pi i h k / W), h = 1 .. W/1024 - 1, k < 1024.
 bool phase_rows_supported(int W, int B, int H);
 int phase_rows_tile(int W);  // rows per fused tile (seam buffer: nb * H / tile * 2 * W float2)
+// defer_seam: the census of the edges between the blocks' tile ranges is left to a
+// later phase_rows_seam on the same stream (its flags are read only at the end of the
+// call, so the headline chain launches it after the integration kernels).
+// ctr (1024-point rows only): two zeroed device counters, private to the stream, the
+// blocks take chunks of tiles from (dynamic schedule, FCD_PR_CHUNK tiles each; the
+// launch leaves them zeroed).  phase_rows_seam's dyn must match the launch's schedule
+// (ctr != null).
 void phase_rows(int W, bool unwrap, const float2* Ab, int H, int nb, int NCA, int ncc0, int ncc1, const float* theta,
                 const float2* pre, const float2* ptw, const float2* ztw, float* col0, int* flags, float2* Zt,
-                float2* seam, hipStream_t s);
+                float2* seam, hipStream_t s, bool defer_seam = false, unsigned* ctr = nullptr);
+void phase_rows_seam(int W, int H, int nb, const float2* seam, int* flags, hipStream_t s, bool dyn = false);
 
 // In-place or out-of-place batched row FFT over nrows rows of length W.
 void row_fft(int W, bool inverse, RowIn in_mode, RowOut out_mode, const void* in, void* out, long nrows,
@@ -156,7 +164,8 @@ void pf_fft2(const float* in, int nb, int H, int W, const PfPlan& rows, const fl
 // REF mode (4096: the reference's band angles into theta_b, [2][H][W])
 void phase_rows_wide(int W, bool unwrap, const float2* Ab, int H, int nb, int NCA, int ncc0, int ncc1, const float* theta,
                      const float2* pre, const float2* ptw, const float2* ztw, float* col0, int* flags, float2* Zt,
-                     float2* seam, hipStream_t s);
+                     float2* seam, hipStream_t s, bool defer_seam = false);
+void phase_rows_wide_seam(int W, int H, int nb, const float2* seam, int* flags, hipStream_t s);
 void phase_rows_wide_ref(int W, const float2* Ab, int H, int NCA, int ncc0, int ncc1, const float2* pre,
                          const float2* ptw, float* theta_b, hipStream_t s);
 inline bool fcd_fused_env(const char* name) {  // FCD_FUSED_2048 / FCD_FUSED_4096 = 0: the unfused chain

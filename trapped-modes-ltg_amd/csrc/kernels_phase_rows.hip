@@ -29,6 +29,8 @@
 //     an LDS table) in the slot, then the tile leaves as whole 64-byte lines.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -126,7 +128,8 @@ template <bool UNWRAP>
 __global__ __launch_bounds__(PR_THREADS, FCD_PR_MINB) void k_phase_rows(
     const float2* __restrict__ Ab, int H, int nb, int NCA, int ncc0, int ncc1, const float* __restrict__ theta,
     const float2* __restrict__ pre, const float2* __restrict__ ptw, const float2* __restrict__ ztw,
-    float* __restrict__ col0, int* __restrict__ flags, float2* __restrict__ Zt, float2* __restrict__ seam, int per) {
+    float* __restrict__ col0, int* __restrict__ flags, float2* __restrict__ Zt, float2* __restrict__ seam, int per,
+    unsigned* __restrict__ ctr) {
     extern __shared__ __attribute__((aligned(16))) float2 lds_p[];
     float2* const stage = lds_p + OFF_STAGE;
     float2* const ptl = lds_p + OFF_PRE;
@@ -146,9 +149,20 @@ __global__ __launch_bounds__(PR_THREADS, FCD_PR_MINB) void k_phase_rows(
     const int rbs = H / PR_ROWS;
     const int items = nb * rbs;
     const int tiles16 = H / 16;
-    // this block's contiguous range of tiles: consecutive tiles of a frame are
-    // checked against each other here, only the range edges go to k_seam_check
-    const int it0 = blockIdx.x * per, it1 = min(it0 + per, items);
+    // Work comes in chunks of `per` consecutive tiles: consecutive tiles of a frame are
+    // checked against each other here, only the chunk edges go to k_seam_check.  Static
+    // (ctr null): chunk = block.  Dynamic: the blocks take chunks from the counter
+    // ctr[0], so a block that started late, behind the other stream's kernels, takes
+    // fewer of them instead of ending the launch late; the last block to leave (ctr[1]
+    // counts them) sets both back to 0 for the next launch on the stream.
+    const int nch = (items + per - 1) / per;
+    __shared__ int s_next;
+    int ch = blockIdx.x;
+    if (ctr) {
+        if (threadIdx.x == 0) s_next = (int)atomicAdd(ctr, 1u);
+        __syncthreads();
+        ch = s_next;
+    }
     // staged band values of the next item, prefetched into registers: entry
     // e = (c, j, row) with row fastest, 8 rows = one 64-byte run of Ab's 16-row tile
     constexpr int NST = 2 * PR_B * PR_ROWS;
@@ -167,10 +181,17 @@ __global__ __launch_bounds__(PR_THREADS, FCD_PR_MINB) void k_phase_rows(
             pf[i] = v;
         }
     };
-    if (it0 < it1) fetch(it0);
+    if (ch < nch) fetch(ch * per);
 #ifdef FCD_STAMPS
     unsigned long long ph[16] = {}, tprev = __builtin_readcyclecounter();
 #endif
+    while (ch < nch) {
+    const int it0 = ch * per, it1 = min(it0 + per, items);
+    // the next chunk, taken now so the chunk's last tile can prefetch its first band
+    // tile; read by every thread after the first staging barrier below, rewritten only
+    // at the next chunk's start (after this chunk's closing barriers)
+    if (ctr && threadIdx.x == 0) s_next = (int)atomicAdd(ctr, 1u);
+    int nxt = nch;
     for (int blk = it0; blk < it1; ++blk) {
         const int f = blk / rbs, rb = blk % rbs;
         const int r = rb * PR_ROWS + wave;           // this wave's row
@@ -184,7 +205,11 @@ __global__ __launch_bounds__(PR_THREADS, FCD_PR_MINB) void k_phase_rows(
         }
         __syncthreads();
         PR_STAMP(1);
-        if (blk + 1 < it1) fetch(blk + 1);
+        if (ctr && blk == it0) nxt = s_next;
+        if (blk + 1 < it1)
+            fetch(blk + 1);
+        else if (nxt < nch)
+            fetch(nxt * per);
         PR_STAMP(2);
         // ---- band transforms of both carriers -> wrapped phases (natural strided)
         float w0[16], w1[16];
@@ -474,6 +499,14 @@ __global__ __launch_bounds__(PR_THREADS, FCD_PR_MINB) void k_phase_rows(
         __syncthreads();
         PR_STAMP(12);
     }
+    ch = nxt;
+    }
+    // every grab of this block precedes its exit count (each atomic returns before the
+    // next is issued), so the last block out resets the counters with no grab pending
+    if (ctr && threadIdx.x == 0 && atomicAdd(ctr + 1, 1u) == gridDim.x - 1) {
+        atomicExch(ctr, 0u);
+        atomicExch(ctr + 1, 0u);
+    }
 #ifdef FCD_STAMPS
     if (blockIdx.x == 0 && lane == 0)
         for (int i = 0; i < 16; ++i) g_pr_stamps[wave * 16 + i] = ph[i];
@@ -528,14 +561,19 @@ bool phase_rows_supported(int W, int B, int H) {
 
 int phase_rows_tile(int W) { return W == 2048 ? 4 : (W == 4096 ? 2 : PR_ROWS); }
 
-void phase_rows(int W, bool unwrap, const float2* Ab, int H, int nb, int NCA, int ncc0, int ncc1, const float* theta,
-                const float2* pre, const float2* ptw, const float2* ztw, float* col0, int* flags, float2* Zt,
-                float2* seam, hipStream_t s) {
-    if (W == 2048 || W == 4096) {
-        phase_rows_wide(W, unwrap, Ab, H, nb, NCA, ncc0, ncc1, theta, pre, ptw, ztw, col0, flags, Zt, seam, s);
-        return;
-    }
-    if (W != PR_W) throw std::runtime_error("phase_rows: unsupported row length");
+// Blocks of k_phase_rows at 1024-point rows and their chunks of `per` consecutive
+// 8-row tiles.  Static: one chunk per block, the tiles split evenly over one block per
+// CU.  Dynamic (FCD_PR_CHUNK tiles per chunk, default 16): one block per CU, chunks
+// from a counter.
+static int pr_chunk_tiles() {
+    static const int v = [] {
+        const char* e = std::getenv("FCD_PR_CHUNK");
+        return std::max(1, (e && *e) ? std::atoi(e) : 16);
+    }();
+    return v;
+}
+
+static void pr_layout(int H, int nb, bool dyn, int& grid, int& per) {
     static int ncu = 0;
     if (!ncu) {
         int dev = 0;
@@ -546,26 +584,59 @@ void phase_rows(int W, bool unwrap, const float2* Ab, int H, int nb, int NCA, in
     const long items = (long)nb * (H / PR_ROWS);
     const int per_cu = std::max<int>(1, std::min<int>(160 * 1024 / (int)PR_LDS, 16 / PR_WAVES));
     const int slots = (int)std::min<long>(items, (long)ncu * per_cu);
+    grid = per = 0;
     if (slots <= 0) return;
-    const int per = (int)((items + slots - 1) / slots);  // tiles per block, a contiguous range
-    const int grid = (int)((items + per - 1) / per);
+    if (dyn) {
+        per = pr_chunk_tiles();
+        grid = (int)std::min<long>((items + per - 1) / per, slots);
+        return;
+    }
+    per = (int)((items + slots - 1) / slots);  // tiles per block, a contiguous range
+    grid = (int)((items + per - 1) / per);
+}
+
+void phase_rows(int W, bool unwrap, const float2* Ab, int H, int nb, int NCA, int ncc0, int ncc1, const float* theta,
+                const float2* pre, const float2* ptw, const float2* ztw, float* col0, int* flags, float2* Zt,
+                float2* seam, hipStream_t s, bool defer_seam, unsigned* ctr) {
+    if (W == 2048 || W == 4096) {
+        phase_rows_wide(W, unwrap, Ab, H, nb, NCA, ncc0, ncc1, theta, pre, ptw, ztw, col0, flags, Zt, seam, s,
+                        defer_seam);
+        return;
+    }
+    if (W != PR_W) throw std::runtime_error("phase_rows: unsupported row length");
+    int grid, per;
+    pr_layout(H, nb, ctr != nullptr, grid, per);
+    if (grid <= 0) return;
     if (unwrap) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_phase_rows<true>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)PR_LDS);
         hipLaunchKernelGGL(k_phase_rows<true>, dim3(grid), dim3(PR_THREADS), PR_LDS, s, Ab, H, nb, NCA, ncc0, ncc1,
-                           theta, pre, ptw, ztw, col0, flags, Zt, seam, per);
-        const int edges = grid - 1;  // range edges (those at frame starts return at once)
-        if (edges > 0)
-            hipLaunchKernelGGL(k_seam_check, dim3((unsigned)((edges + 3) / 4)), dim3(256), 0, s, seam, H, nb, per,
-                               flags);
+                           theta, pre, ptw, ztw, col0, flags, Zt, seam, per, ctr);
+        if (!defer_seam) phase_rows_seam(W, H, nb, seam, flags, s, ctr != nullptr);
     } else {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_phase_rows<false>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)PR_LDS);
         hipLaunchKernelGGL(k_phase_rows<false>, dim3(grid), dim3(PR_THREADS), PR_LDS, s, Ab, H, nb, NCA, ncc0, ncc1,
-                           theta, pre, ptw, ztw, col0, flags, Zt, seam, per);
+                           theta, pre, ptw, ztw, col0, flags, Zt, seam, per, ctr);
     }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) throw std::runtime_error(std::string("phase_rows launch: ") + hipGetErrorString(e));
+}
+
+void phase_rows_seam(int W, int H, int nb, const float2* seam, int* flags, hipStream_t s, bool dyn) {
+    if (W == 2048 || W == 4096) {
+        phase_rows_wide_seam(W, H, nb, seam, flags, s);
+        return;
+    }
+    int grid, per;
+    pr_layout(H, nb, dyn, grid, per);
+    if (grid <= 0) return;
+    const long items = (long)nb * (H / PR_ROWS);
+    const long edges = (items + per - 1) / per - 1;  // chunk edges (those at frame starts return at once)
+    if (edges > 0)
+        hipLaunchKernelGGL(k_seam_check, dim3((unsigned)((edges + 3) / 4)), dim3(256), 0, s, seam, H, nb, per, flags);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) throw std::runtime_error(std::string("phase_rows seam check launch: ") + hipGetErrorString(e));
 }
 
 }  // namespace fcdk

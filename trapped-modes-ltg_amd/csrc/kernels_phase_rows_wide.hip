@@ -471,28 +471,44 @@ void launch_wide(int grid, const float2* Ab, int H, int nb, int NCA, int ncc0, i
                        ncc0, ncc1, theta, pre, ptw, ztw, col0, flags, Zt, seam, per, theta_out);
 }
 
+// blocks of k_phase_rows_wide: one per CU, each `per` consecutive tiles
+template <int W>
+void wide_layout(int H, int nb, int& grid, int& per) {
+    const long items = (long)nb * (H / WideCfg<W>::ROWS);
+    const int slots = (int)std::min<long>(items, (long)num_cus());  // one workgroup per CU
+    grid = per = 0;
+    if (slots <= 0) return;
+    per = (int)((items + slots - 1) / slots);  // tiles per block, a contiguous range
+    grid = (int)((items + per - 1) / per);
+}
+
+template <int W>
+void seam_wide_t(int H, int nb, const float2* seam, int* flags, hipStream_t s) {
+    int grid, per;
+    wide_layout<W>(H, nb, grid, per);
+    const int edges = grid - 1;  // range edges (those at frame starts return at once)
+    if (edges > 0)
+        hipLaunchKernelGGL(k_seam_check_wide<W>, dim3((unsigned)((edges + 3) / 4)), dim3(256), 0, s, seam, H, nb, per,
+                           flags);
+}
+
 template <int W>
 void phase_rows_wide_t(int mode, const float2* Ab, int H, int nb, int NCA, int ncc0, int ncc1, const float* theta,
                        const float2* pre, const float2* ptw, const float2* ztw, float* col0, int* flags, float2* Zt,
-                       float2* seam, float* theta_out, hipStream_t s) {
+                       float2* seam, float* theta_out, hipStream_t s, bool defer_seam = false) {
     using C = WideCfg<W>;
     if (H % 16 != 0 || NCA < ncc0 || NCA < ncc1 || ncc0 > C::B || ncc1 > C::B)
         throw std::runtime_error("phase_rows_wide: unsupported geometry");
-    const long items = (long)nb * (H / C::ROWS);
-    const int slots = (int)std::min<long>(items, (long)num_cus());  // one workgroup per CU
-    if (slots <= 0) return;
-    const int per = (int)((items + slots - 1) / slots);  // tiles per block, a contiguous range
-    const int grid = (int)((items + per - 1) / per);
+    int grid, per;
+    wide_layout<W>(H, nb, grid, per);
+    if (grid <= 0) return;
     if (mode == 2) {
         launch_wide<W, false, true>(grid, Ab, H, nb, NCA, ncc0, ncc1, theta, pre, ptw, ztw, col0, flags, Zt, seam, per,
                                     theta_out, s);
     } else if (mode == 1) {
         launch_wide<W, true, false>(grid, Ab, H, nb, NCA, ncc0, ncc1, theta, pre, ptw, ztw, col0, flags, Zt, seam, per,
                                     theta_out, s);
-        const int edges = grid - 1;  // range edges (those at frame starts return at once)
-        if (edges > 0)
-            hipLaunchKernelGGL(k_seam_check_wide<W>, dim3((unsigned)((edges + 3) / 4)), dim3(256), 0, s, seam, H, nb, per,
-                               flags);
+        if (!defer_seam) seam_wide_t<W>(H, nb, seam, flags, s);
     } else {
         launch_wide<W, false, false>(grid, Ab, H, nb, NCA, ncc0, ncc1, theta, pre, ptw, ztw, col0, flags, Zt, seam, per,
                                      theta_out, s);
@@ -505,15 +521,26 @@ void phase_rows_wide_t(int mode, const float2* Ab, int H, int nb, int NCA, int n
 
 void phase_rows_wide(int W, bool unwrap, const float2* Ab, int H, int nb, int NCA, int ncc0, int ncc1, const float* theta,
                      const float2* pre, const float2* ptw, const float2* ztw, float* col0, int* flags, float2* Zt,
-                     float2* seam, hipStream_t s) {
+                     float2* seam, hipStream_t s, bool defer_seam) {
     if (W == 2048)
         phase_rows_wide_t<2048>(unwrap ? 1 : 0, Ab, H, nb, NCA, ncc0, ncc1, theta, pre, ptw, ztw, col0, flags, Zt, seam,
-                                nullptr, s);
+                                nullptr, s, defer_seam);
     else if (W == 4096)
         phase_rows_wide_t<4096>(unwrap ? 1 : 0, Ab, H, nb, NCA, ncc0, ncc1, theta, pre, ptw, ztw, col0, flags, Zt, seam,
-                                nullptr, s);
+                                nullptr, s, defer_seam);
     else
         throw std::runtime_error("phase_rows_wide: 2048- or 4096-point rows");
+}
+
+void phase_rows_wide_seam(int W, int H, int nb, const float2* seam, int* flags, hipStream_t s) {
+    if (W == 2048)
+        seam_wide_t<2048>(H, nb, seam, flags, s);
+    else if (W == 4096)
+        seam_wide_t<4096>(H, nb, seam, flags, s);
+    else
+        throw std::runtime_error("phase_rows_wide_seam: 2048- or 4096-point rows");
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) throw std::runtime_error(std::string("phase_rows_wide seam check launch: ") + hipGetErrorString(e));
 }
 
 void phase_rows_wide_ref(int W, const float2* Ab, int H, int NCA, int ncc0, int ncc1, const float2* pre,
