@@ -112,15 +112,32 @@ struct KCfg {
 #ifndef FCD_DEMODCOLS_PREF
 #define FCD_DEMODCOLS_PREF 1
 #endif
+// From FCD_DC_TW_GLOBAL_MIN points its twiddle table stays in global memory: the
+// two exchange rows alone are 70 KB at 4096, so without the 32 KB copy two workgroups
+// fit per CU (16.9 -> 15.1 us/frame at 4096^2, kbench r03u).
+#ifndef FCD_DC_TW_GLOBAL_MIN
+#define FCD_DC_TW_GLOBAL_MIN 4096
+#endif
 template <int N>
 struct DemodColsCfg : KCfg<N, (N <= 1024 ? FCD_DEMODCOLS_BLOCK : BLOCK)> {
     static constexpr int V = N <= 1024 ? 4 : ColWaves<N>::V;
+    static constexpr bool GTW = N >= FCD_DC_TW_GLOBAL_MIN;
+    static constexpr int NLEN = GTW ? 0 : N;
 };
 
+// k_int_cols at 2048 points in the lean form (FCD_INTCOLS_LEAN_2048): 128 VGPRs (no
+// prefetch of the next item's columns) and the row wavenumbers read from global memory,
+// so 4 four-wave workgroups fit per CU instead of 3 at 166 VGPRs.
+#ifndef FCD_INTCOLS_LEAN_2048
+#define FCD_INTCOLS_LEAN_2048 0
+#endif
 template <int N>
 struct IntColsCfg : KCfg<N, FCD_INTCOLS_BLOCK> {
-    static constexpr int V = N <= 1024 ? FCD_INTCOLS_WAVES : ColWaves<N>::V;
-    static constexpr bool PREF_Y = N >= 4096 ? true : FCD_INTCOLS_PREF_Y;  // 4096: 2 waves/SIMD either way
+    static constexpr bool LEAN = N == 2048 && FCD_INTCOLS_LEAN_2048;
+    static constexpr int V = N <= 1024 ? FCD_INTCOLS_WAVES : (LEAN ? 4 : ColWaves<N>::V);
+    static constexpr bool PREF_Y = LEAN ? false : (N >= 4096 ? true : FCD_INTCOLS_PREF_Y);  // 4096: 2 waves/SIMD either way
+    static constexpr bool PREF_X = LEAN ? false : FCD_INTCOLS_PREF_X;
+    static constexpr bool KY_LDS = FCD_INTCOLS_KY_LDS && !LEAN;
 };
 
 // find_wrap(a, b) of the reference unwrapper with an f32 fast path:
@@ -144,6 +161,15 @@ __device__ __forceinline__ int fw_fast(float a, float b) {
 #define FCD_DR_HCREG 2
 #endif
 constexpr int DR_HCR = FCD_DR_HCREG;
+// Rows of FCD_DR_DIRECT_MIN points and more: each row pair's band values go straight
+// to Xb (16 bytes per column: the pair's two rows of the 16-row tile, so the tile's 8
+// pairs fill each 128-byte line in L2 one after another) instead of through a staged
+// [NC][16] block, whose 56 KB at 4096 points held the kernel to one workgroup per CU.
+#ifndef FCD_DR_DIRECT_MIN
+#define FCD_DR_DIRECT_MIN (1 << 30)  // off: at 4096 25.9 vs 26.0, at 2048 5.94 vs 5.66 us/frame but k_demod_cols +0.24 (kbench r03v)
+#endif
+template <int W>
+constexpr bool dr_direct() { return W >= FCD_DR_DIRECT_MIN; }
 
 template <int W>
 __global__ __launch_bounds__(KCfg<W>::THREADS, FCD_MIN_WAVES) void k_demod_rows(const float* __restrict__ frames, int H, int nb,
@@ -190,23 +216,32 @@ __global__ __launch_bounds__(KCfg<W>::THREADS, FCD_MIN_WAVES) void k_demod_rows(
 #pragma unroll
             for (int q = 0; q < E; ++q) s[pad(t + TT * q)] = x[q];
             team_sync<W>();
+            float4* const xrow = reinterpret_cast<float4*>(Xb + (long)(blk / rbs) * H * NC + (long)(blk % rbs) * NC * TILE + 2 * pr);
             auto band = [&](int i, int hc) {
                 const float2 zk = s[pad(hc)], zm = s[pad((W - hc) & (W - 1))];
                 // X_a = (Z(k) + conj Z(-k)) / 2 ; X_b = (Z(k) - conj Z(-k)) / 2i
-                stage[i * (TILE + 1) + 2 * pr] = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y));
-                stage[i * (TILE + 1) + 2 * pr + 1] = make_float2(0.5f * (zk.y + zm.y), -0.5f * (zk.x - zm.x));
+                const float2 xa = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y));
+                const float2 xb = make_float2(0.5f * (zk.y + zm.y), -0.5f * (zk.x - zm.x));
+                if constexpr (dr_direct<W>()) {
+                    xrow[i * (TILE / 2)] = make_float4(xa.x, xa.y, xb.x, xb.y);  // tix(2 pr, i, NC)
+                } else {
+                    stage[i * (TILE + 1) + 2 * pr] = xa;
+                    stage[i * (TILE + 1) + 2 * pr + 1] = xb;
+                }
             };
 #pragma unroll
             for (int k = 0; k < DR_HCR; ++k)
                 if (t + k * TT < NC) band(t + k * TT, hcr[k]);
             for (int i = t + DR_HCR * TT; i < NC; i += TT) band(i, T.hc[i]);
         }
-        const int f = blk / rbs, rb = blk % rbs;
-        __syncthreads();
-        float2* dst = Xb + (long)f * H * NC + (long)rb * NC * TILE;
-        for (int idx = threadIdx.x; idx < NC * TILE; idx += C::THREADS)
-            dst[idx] = stage[(idx / TILE) * (TILE + 1) + (idx % TILE)];
-        __syncthreads();
+        if constexpr (!dr_direct<W>()) {
+            const int f = blk / rbs, rb = blk % rbs;
+            __syncthreads();
+            float2* dst = Xb + (long)f * H * NC + (long)rb * NC * TILE;
+            for (int idx = threadIdx.x; idx < NC * TILE; idx += C::THREADS)
+                dst[idx] = stage[(idx / TILE) * (TILE + 1) + (idx % TILE)];
+            __syncthreads();
+        }
     }
 }
 
@@ -222,7 +257,7 @@ __global__ __launch_bounds__(DemodColsCfg<H>::THREADS, DemodColsCfg<H>::V) void 
     const int team = threadIdx.x / TT, t = threadIdx.x % TT;
     float2* s = lds + team * C::ROW;            // holds the forward column spectrum
     float2* s2 = lds + (TEAMS + team) * C::ROW;  // exchanges of the inverse FFTs
-    RegFFT<H> fft;
+    RegFFT<H, C::GTW> fft;
     fft.init(tw, lds_raw, threadIdx.x, C::THREADS);
     __syncthreads();
     const int NC = T.NC;
@@ -407,7 +442,7 @@ __global__ __launch_bounds__(IntColsCfg<H>::THREADS, IntColsCfg<H>::V) void k_in
     // the row wavenumber tables (ky_eff, ky^2) of every element, read per item: LDS copies
     float* const lky = reinterpret_cast<float*>(lds + TEAMS * C::ROW);
     float* const lky2 = lky + H;
-    if constexpr (FCD_INTCOLS_KY_LDS) {
+    if constexpr (C::KY_LDS) {
         for (int i = threadIdx.x; i < H; i += C::THREADS) {
             lky[i] = c.kye[i];
             lky2[i] = c.ky2[i];
@@ -472,7 +507,7 @@ __global__ __launch_bounds__(IntColsCfg<H>::THREADS, IntColsCfg<H>::V) void k_in
     };
     auto fetch = [&](int code) {
         if constexpr (C::PREF_Y) fetch_col(code, true, py);
-        if constexpr (FCD_INTCOLS_PREF_X) fetch_col(code, false, px);
+        if constexpr (C::PREF_X) fetch_col(code, false, px);
     };
     fetch(c0 + team * cstep);
     for (int base = c0; base < cend; base += TEAMS * cstep) {
@@ -485,7 +520,7 @@ __global__ __launch_bounds__(IntColsCfg<H>::THREADS, IntColsCfg<H>::V) void k_in
         // of the Hermitian split sit in the same lane and slot (no mirror exchange).
         float2 x[E], y[E];
         if constexpr (!C::PREF_Y) fetch_col(item, true, py);
-        if constexpr (!FCD_INTCOLS_PREF_X) fetch_col(item, false, px);
+        if constexpr (!C::PREF_X) fetch_col(item, false, px);
 #pragma unroll
         for (int q = 0; q < E; ++q) {
             y[q] = py[q];
@@ -518,8 +553,8 @@ __global__ __launch_bounds__(IntColsCfg<H>::THREADS, IntColsCfg<H>::V) void k_in
             // 2 Phi0 and 2 Phi1 (the halves go into the multiplier's scale)
             const float2 f0 = make_float2(z.x + zm.x, z.y - zm.y);
             const float2 f1 = make_float2(z.y + zm.y, zm.x - z.x);
-            const float ky = FCD_INTCOLS_KY_LDS ? lky[i] : c.kye[i];
-            float k2 = kx2 + (FCD_INTCOLS_KY_LDS ? lky2[i] : c.ky2[i]);
+            const float ky = C::KY_LDS ? lky[i] : c.kye[i];
+            float k2 = kx2 + (C::KY_LDS ? lky2[i] : c.ky2[i]);
             if (i == 0 && col == 0) k2 = 1.f;
             // 1 / k^2 by the hardware reciprocal (1 ulp) instead of an IEEE division
             // (a 10-instruction sequence per element)
@@ -550,6 +585,13 @@ struct C2RCfg {
     static constexpr int TT = Sched<W>::TT;
     static constexpr int E = Sched<W>::E;
     static constexpr int RPW = c2r_rpw(W);
+    // staged block pitch: RPW + 1 (odd, conflict-free); FCD_C2R_PAD=0 leaves the 2- and
+    // 4-row blocks of the wide rows unpadded (a third / fifth less LDS, but still one
+    // workgroup per CU at 4096 and slower: 42.0 -> 43.4 us/frame, kbench r03u)
+#ifndef FCD_C2R_PAD
+#define FCD_C2R_PAD 1
+#endif
+    static constexpr int SP = (RPW == TILE || FCD_C2R_PAD) ? RPW + 1 : RPW;
     static constexpr int THREADS = (RPW / 2) * TT < 1024 ? ((RPW / 2) * TT > TT ? (RPW / 2) * TT : TT) : 1024;
     static constexpr int TEAMS = THREADS / TT;
     static constexpr int ROW = padded_len(W);
@@ -606,7 +648,7 @@ __global__ __launch_bounds__(C2RCfg<W>::THREADS) void k_int_c2r(const float2* __
 #pragma unroll
         for (int i = 0; i < SPT; ++i) {
             const int idx = threadIdx.x + i * C::THREADS;
-            if (idx < NCH * RPW) stage[(idx / RPW) * (RPW + 1) + idx % RPW] = pf[i];
+            if (idx < NCH * RPW) stage[(idx / RPW) * C::SP + idx % RPW] = pf[i];
         }
         __syncthreads();
         if (blk + G < nb * nblk) fetch(blk + G);
@@ -617,11 +659,11 @@ __global__ __launch_bounds__(C2RCfg<W>::THREADS) void k_int_c2r(const float2* __
                 const int col = t + TT * q;
                 float2 g1, g2;
                 if (col <= W / 2) {
-                    g1 = stage[col * (RPW + 1) + 2 * pr];
-                    g2 = stage[col * (RPW + 1) + 2 * pr + 1];
+                    g1 = stage[col * C::SP + 2 * pr];
+                    g2 = stage[col * C::SP + 2 * pr + 1];
                 } else {  // row-wise Hermitian: G(y, W - c) = conj G(y, c)
-                    g1 = stage[(W - col) * (RPW + 1) + 2 * pr];
-                    g2 = stage[(W - col) * (RPW + 1) + 2 * pr + 1];
+                    g1 = stage[(W - col) * C::SP + 2 * pr];
+                    g2 = stage[(W - col) * C::SP + 2 * pr + 1];
                     g1.y = -g1.y;
                     g2.y = -g2.y;
                 }
@@ -680,7 +722,7 @@ template <int W>
 static void launch_demod_rows(const float* frames, int H, int nb, const DemodTables& T, float2* Xb, const float2* tw,
                               hipStream_t s) {
     using C = KCfg<W>;
-    const size_t lds = (size_t)C::NLEN * 8 + (size_t)C::TEAMS * C::ROW * 8 + (size_t)T.NC * (TILE + 1) * 8;
+    const size_t lds = (size_t)C::NLEN * 8 + (size_t)C::TEAMS * C::ROW * 8 + (dr_direct<W>() ? 0 : (size_t)T.NC * (TILE + 1) * 8);
     set_lds(k_demod_rows<W>, lds);
     const int grid = grid_for((long)nb * (H / TILE), 4);
     hipLaunchKernelGGL(k_demod_rows<W>, dim3(grid), dim3(C::THREADS), lds, s, frames, H, nb, T, Xb, tw);
@@ -758,7 +800,7 @@ template <int H>
 static void launch_int_cols(const float2* Zt, int W, int nb, const IntegCoef& c, float2* Ht, const float2* tw,
                             hipStream_t s, const int* colk) {
     using C = IntColsCfg<H>;
-    const size_t lds = (size_t)C::NLEN * 8 + (size_t)C::TEAMS * C::ROW * 8 + (FCD_INTCOLS_KY_LDS ? (size_t)H * 8 : 0);
+    const size_t lds = (size_t)C::NLEN * 8 + (size_t)C::TEAMS * C::ROW * 8 + (C::KY_LDS ? (size_t)H * 8 : 0);
     set_lds(k_int_cols<H>, lds);
     const int grid = grid_for(((long)nb * (W / 2 + 1) + C::TEAMS - 1) / C::TEAMS, 4);
     const int zt = zt_rows(W);
@@ -773,7 +815,7 @@ template <int W>
 static void launch_int_c2r(const float2* Ht, int H, int nb, float* h, const float2* tw, hipStream_t s) {
     using C = C2RCfg<W>;
     const int rpw = C::RPW;
-    const size_t lds = (size_t)C::NLEN * 8 + (size_t)C::TEAMS * C::ROW * 8 + (size_t)(W / 2 + 1) * (rpw + 1) * 8;
+    const size_t lds = (size_t)C::NLEN * 8 + (size_t)C::TEAMS * C::ROW * 8 + (size_t)(W / 2 + 1) * C::SP * 8;
     set_lds(k_int_c2r<W>, lds);
     const int grid = grid_for((long)nb * (H / rpw), 2);
     hipLaunchKernelGGL(k_int_c2r<W>, dim3(grid), dim3(C::THREADS), lds, s, Ht, H, nb, rpw, h, tw);

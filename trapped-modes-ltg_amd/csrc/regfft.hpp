@@ -72,11 +72,18 @@ __device__ __forceinline__ void team_sync() {
 // (pass_twiddle_table in fcd_engine.cpp): for passes P = 1..NP-1, for
 // k < L_P, for r = 1..R_P-1: exp(-2 pi i r k / (L_P R_P)).  A butterfly reads
 // its R-1 twiddles contiguously: one address + immediate offsets.
-template <int N>
+// GLOBAL_TW: the pass-major table stays in global memory (L1 / L2 hits) instead of an
+// LDS copy of 8 N bytes per workgroup (32 KB at 4096 points).  Only where the LDS it
+// frees buys a second workgroup per CU (k_demod_cols at 4096 points: 16.9 -> 15.1
+// us/frame, kbench r03u); elsewhere the table reads from L1 / L2 cost more than the
+// occupancy (k_int_cols 4096: 85 -> 114 us/frame, VGPR-bound at one workgroup anyway).
+template <int N, bool GTW = false>
 struct RegFFT {
     using S = Sched<N>;
     static constexpr int E = S::E, TT = S::TT, NP = S::NP;
-    const float2* tw;  // the workgroup's LDS copy of the pass-major table (< N entries)
+    static constexpr bool GLOBAL_TW = GTW;
+    static constexpr int LDS_TW = GLOBAL_TW ? 0 : N;  // float2 of LDS the table takes
+    const float2* tw;  // the pass-major table: the workgroup's LDS copy, or global memory
 
     static constexpr int passoff(int p) {
         int o = 0;
@@ -86,8 +93,12 @@ struct RegFFT {
 
     // Cooperative copy of the host's twiddle table into LDS (caller syncs after).
     __device__ __forceinline__ void init(const float2* __restrict__ table, float2* lds_tw, int tid, int nthreads) {
-        for (int i = tid; i < N; i += nthreads) lds_tw[i] = table[i];
-        tw = lds_tw;
+        if constexpr (GLOBAL_TW) {
+            tw = table;
+        } else {
+            for (int i = tid; i < N; i += nthreads) lds_tw[i] = table[i];
+            tw = lds_tw;
+        }
     }
 
     // x: natural strided layout in and out.  s: the team's LDS row (padded_len(N)).
