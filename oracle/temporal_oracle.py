@@ -11,10 +11,13 @@ Follows /root/reference/pydata/analyze.py:
   * spectrogram      analyze.py:419-531  (scipy.signal.spectrogram per pixel, NaN gaps
                                           filled by np.interp, all-NaN pixels -> NaN)
 
-Parity unpinned: analyze.py imports cv2 (absent here), so the reference module
-cannot run in this container and no golden vectors exist for these functions;
-the restatement uses the same numpy / scipy calls the reference makes, on
-in-memory stacks instead of map folders.
+Pinned (round 3) to the reference module's own outputs: tests/golden/make_golden.py
+imports analyze.py as shipped, with a placeholder for its module-level `import cv2`
+(analyze.py:21; cv2 is used only on the polar paths, which no fixture runs), and
+records block_split / block_amplitude / spectrogram on synthetic map folders
+(tests/golden/analyze_ref.npz); tests/test_analyze_ref.py checks this restatement
+against them at 1e-12.  The restatement uses the same numpy / scipy calls the
+reference makes, on in-memory stacks instead of map folders.
 """
 import numpy as np
 from scipy import signal
