@@ -81,6 +81,9 @@ const char* fcd_last_error(void);
 /* Allocate a context for `rows` x `cols` frames on HIP device `device`. */
 int fcd_create(int device, int rows, int cols, fcd_ctx** out);
 int fcd_destroy(fcd_ctx* ctx);
+/* Waits for the context's own stream and for the last device-pointer call's work on
+ * the stream it was given (fcd_process may return before its integration kernels
+ * finish, see there). */
 int fcd_synchronize(fcd_ctx* ctx);
 
 /* Replaces fcd.compute_carriers(reference, square_size) (fcd.py:53-70) and,
@@ -126,7 +129,11 @@ int fcd_get_carriers(fcd_ctx* ctx, float* ccsgn, uint8_t* mask);
  *   wrapped_out float32 [n][2][rows][cols]  -angle(ifft2(D*mask)*ccsgn) (fcd.py:118)
  *   k_out       int32   [n][2][rows][cols]  2*pi multiples: phases = wrapped + 2*pi*k (fcd.py:119)
  * With unwrap == 0 the phases are the wrapped angles (k_out is zero-filled).
- * Synchronises once per internal chunk when unwrap != 0 (residue census). */
+ * Synchronises on the residue census when unwrap != 0.  Device pointers and only
+ * height_out (the fused chain): the census is read back as soon as its flags are final,
+ * so the call returns with the integration kernels still queued on `stream` (order later
+ * work on that stream, or call fcd_synchronize); frames with residues are then redone by
+ * the exact pass before the call returns. */
 int fcd_process(fcd_ctx* ctx, const float* frames, int n_frames, int flags, double height, int unwrap,
                 float* height_out, float* wrapped_out, int32_t* k_out, void* stream);
 

@@ -211,6 +211,10 @@ struct fcd_ctx {
     bool force_unfused = false;      // FCD_UNFUSED=1: take the unfused chain (A/B measurement)
     int nstreams = 2;                // FCD_STREAMS: device-path chunks split over 1 or 2 streams
     bool defer_seam = true;          // FCD_DEFER_SEAM: the fused chain's seam census after the integration
+    bool early_census = true;        // FCD_EARLY_CENSUS: device calls read the census back before the integration
+    hipStream_t cstream = nullptr;   // its copy stream and the two halves' "census complete" events
+    hipEvent_t ev_cen[2] = {nullptr, nullptr};
+    hipEvent_t ev_done = nullptr;    // end of the last device call's work on its (caller's) stream
     bool pr_dynamic = false;         // FCD_PR_DYNAMIC=1: the 1024 fused kernel takes tile chunks from a counter
                                      // (r03t: 80.1-81.0k vs 80.0-81.6k frames/s static, no gain; kept as an option)
     DevBuf pr_ctr;                   // its counter pairs, one per concurrent half (each launch leaves them 0)
@@ -881,6 +885,7 @@ FCD_API int fcd_create(int device, int rows, int cols, fcd_ctx** out) {
         c->force_unfused = fcd_env_int("FCD_UNFUSED", 0) != 0;
         c->nstreams = fcd_env_int("FCD_STREAMS", 2) >= 2 ? 2 : 1;
         c->defer_seam = fcd_env_int("FCD_DEFER_SEAM", 1) != 0;
+        c->early_census = fcd_env_int("FCD_EARLY_CENSUS", 1) != 0;
         c->pr_dynamic = fcd_env_int("FCD_PR_DYNAMIC", 0) != 0;
         c->H = rows;
         c->W = cols;
@@ -919,8 +924,17 @@ FCD_API int fcd_destroy(fcd_ctx* ctx) {
     FCD_TRY({
         if (!ctx) return FCD_OK;
         (void)hipSetDevice(ctx->device);
+        // a device call may return with its integration still queued on the caller's
+        // stream (early census): wait for it before the workspace goes
+        if (ctx->ev_done) (void)hipEventSynchronize(ctx->ev_done);
         (void)hipStreamSynchronize(ctx->own);
         (void)hipStreamDestroy(ctx->own);
+        if (ctx->cstream) {
+            (void)hipStreamSynchronize(ctx->cstream);
+            (void)hipStreamDestroy(ctx->cstream);
+            for (hipEvent_t e : ctx->ev_cen) (void)hipEventDestroy(e);
+        }
+        if (ctx->ev_done) (void)hipEventDestroy(ctx->ev_done);
         if (ctx->aux) {
             (void)hipStreamSynchronize(ctx->aux);
             (void)hipStreamDestroy(ctx->aux);
@@ -934,6 +948,7 @@ FCD_API int fcd_destroy(fcd_ctx* ctx) {
 FCD_API int fcd_synchronize(fcd_ctx* ctx) {
     FCD_TRY({
         check_ctx(ctx);
+        if (ctx->ev_done) HIPCHK(hipEventSynchronize(ctx->ev_done));
         HIPCHK(hipStreamSynchronize(ctx->own));
     })
 }
@@ -1067,8 +1082,11 @@ namespace {
 // fo: first workspace frame of the chunk (the fused chain's per-frame
 // intermediates are frame-strided, so disjoint frame ranges of one workspace can
 // run concurrently on different streams).
+// census_ev (fused chain only): recorded once the chunk's census flags are final (fused
+// kernel + tile-range census, which then runs right after it), before the integration.
 void first_pass_chunk(fcd_ctx* c, const float* fr, int nb, bool unwrap, bool fused, int* res, float* hdst,
-                      int32_t* kdst, const fcdk::IntegCoef& coef, hipStream_t s, int fo = 0) {
+                      int32_t* kdst, const fcdk::IntegCoef& coef, hipStream_t s, int fo = 0,
+                      hipEvent_t census_ev = nullptr) {
     if (fused) {
         // height only: band transforms, phase, unwrap and the z-row FFT in one
         // pass (kernels_phase_rows.hip); colk lands in the spectra's DC bins
@@ -1087,9 +1105,11 @@ void first_pass_chunk(fcd_ctx* c, const float* fr, int nb, bool unwrap, bool fus
         if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
         // dynamic chunk schedule: each concurrent half (fo) has its own counter pair
         unsigned* ctr = c->pr_dynamic ? c->pr_ctr.as<unsigned>() + (fo ? 2 : 0) : nullptr;
+        const bool defer = c->defer_seam && !census_ev;
         fcdk::phase_rows(c->W, unwrap, Ab, c->H, nb, c->NCA, c->NCc[0], c->NCc[1], c->theta_p.as<float>(),
                          c->band_pre.as<float2>(), c->band_ptw.as<float2>(), c->ztw.as<float2>(), col0, res, Zt, seam,
-                         s, c->defer_seam, ctr);
+                         s, defer, ctr);
+        if (census_ev) HIPCHK(hipEventRecord(census_ev, s));
         if (unwrap) fcdk::unwrap_colk_compact(col0, 2 * nb, c->H, colk, s);
         if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
         fcdk::int_cols(c->H, Zt, c->W, nb, coef, Ht, c->twp_col.as<float2>(), s, unwrap ? colk : nullptr);
@@ -1097,7 +1117,7 @@ void first_pass_chunk(fcd_ctx* c, const float* fr, int nb, bool unwrap, bool fus
         // the census of the tile-range edges: its flags are read only when the call ends,
         // so it runs last instead of holding the integration kernels behind it (a small
         // grid waiting for CUs the other stream's fused kernel holds)
-        if (unwrap && c->defer_seam) fcdk::phase_rows_seam(c->W, c->H, nb, seam, res, s, ctr != nullptr);
+        if (unwrap && defer) fcdk::phase_rows_seam(c->W, c->H, nb, seam, res, s, ctr != nullptr);
     } else {
         const long H = c->H, W = c->W;
         float* wrapped = c->wrapped.as<float>() + fo * 2 * H * W;
@@ -1337,6 +1357,12 @@ int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int f
     }
     // ---- pass 1: every frame through the band-pruned pipeline with the residue-free unwrap
     const bool fused = c->fused_ok && !wrapped_out && !k_out && !c->force_unfused;
+    // device-pointer calls of the fused chain read the census back as soon as its flags
+    // are final: the call returns while the integration kernels still run on `stream`
+    // (asynchronous as every device-pointer call, fcd.h), so the caller's next batch is
+    // queued behind them instead of after a host round trip with the GPU idle
+    const bool early = c->early_census && dev && fused && unwrap && height_out != nullptr;
+    int cen_halves = 0;
     if (!dev && !wrapped_out && !k_out) {
         host_pipeline(c, frames, format, n_frames, unwrap != 0, fused, res, height_out, coef, s);
     } else {
@@ -1356,6 +1382,19 @@ int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int f
             // the fused (1024-wide) chain only: split, the unfused chain at 2048^2 / 4096^2
             // measured 1-2 % slower (r01br), though its workspace offsets allow it
             const int nsplit = fused && !c->profiling && nb >= 2 ? c->nstreams : 1;
+            // early census: the last chunk's halves mark when their census flags are final,
+            // and the readback below waits for those marks only, not for the integration
+            const bool last = f0 + nb >= n_frames;
+            hipEvent_t cen0 = nullptr, cen1 = nullptr;
+            if (early && last) {
+                if (!c->cstream) {
+                    HIPCHK(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
+                    for (auto& e : c->ev_cen) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+                }
+                cen0 = c->ev_cen[0];
+                cen1 = nsplit == 2 ? c->ev_cen[1] : nullptr;
+                cen_halves = nsplit;
+            }
             if (nsplit == 2) {
                 // two halves of the chunk on two streams: kernels bound by different
                 // resources (HBM-bound c2r / demod_rows, latency-bound phase_rows /
@@ -1370,13 +1409,13 @@ int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int f
                 // second half after the first half's demod kernels instead: no gain)
                 HIPCHK(hipEventRecord(c->ev_fork, s));
                 HIPCHK(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
-                first_pass_chunk(c, fr, na, unwrap != 0, fused, rs, hdst, nullptr, coef, s, 0);
+                first_pass_chunk(c, fr, na, unwrap != 0, fused, rs, hdst, nullptr, coef, s, 0, cen0);
                 first_pass_chunk(c, fr + (size_t)na * hw, nb2, unwrap != 0, fused, rs ? rs + 2 * na : nullptr,
-                                 hdst + (size_t)na * hw, nullptr, coef, c->aux, na);
+                                 hdst + (size_t)na * hw, nullptr, coef, c->aux, na, cen1);
                 HIPCHK(hipEventRecord(c->ev_join, c->aux));
                 HIPCHK(hipStreamWaitEvent(s, c->ev_join, 0));
             } else {
-                first_pass_chunk(c, fr, nb, unwrap != 0, fused, rs, hdst, kdst, coef, s);
+                first_pass_chunk(c, fr, nb, unwrap != 0, fused, rs, hdst, kdst, coef, s, 0, cen0);
             }
             if (height_out && !dev)
                 HIPCHK(hipMemcpyAsync(height_out + (size_t)f0 * hw, hdst, (size_t)nb * hw * 4, out_kind, s));
@@ -1394,6 +1433,10 @@ int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int f
             if (!dev) HIPCHK(hipStreamSynchronize(s));
         }
     }
+    if (dev) {  // the call's last work on the caller's stream so far (fcd_destroy / fcd_synchronize wait on it)
+        if (!c->ev_done) HIPCHK(hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming));
+        HIPCHK(hipEventRecord(c->ev_done, s));
+    }
     if (!unwrap) return FCD_OK;
     // ---- pass 2: frames whose maps have residues are redone with the Boruvka (MST) unwrap
     // into page-locked memory: a pageable destination went through the runtime's staging
@@ -1405,7 +1448,12 @@ int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int f
         c->census.ensure(counts.size() * sizeof(int));
         cdst = static_cast<int*>(c->census.p);
     }
-    HIPCHK(hipMemcpyAsync(cdst, res, counts.size() * sizeof(int), hipMemcpyDeviceToHost, s));
+    hipStream_t qs = s;  // the stream the readback runs on (and the poll below queries)
+    if (cen_halves > 0) {
+        qs = c->cstream;
+        for (int h = 0; h < cen_halves; ++h) HIPCHK(hipStreamWaitEvent(qs, c->ev_cen[h], 0));
+    }
+    HIPCHK(hipMemcpyAsync(cdst, res, counts.size() * sizeof(int), hipMemcpyDeviceToHost, qs));
     // polled rather than a blocking wait: the caller's next batch is enqueued as soon
     // as this one's census is back (a blocking wait's wake-up sat in every bench step,
     // ~17 us per 256-frame step at 1024^2).  The poll yields the core between queries
@@ -1415,10 +1463,10 @@ int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int f
     hipError_t qe = hipErrorNotReady;
     if (spin_us > 0) {
         const auto t_end = std::chrono::steady_clock::now() + std::chrono::microseconds(spin_us);
-        while ((qe = hipStreamQuery(s)) == hipErrorNotReady && std::chrono::steady_clock::now() < t_end)
+        while ((qe = hipStreamQuery(qs)) == hipErrorNotReady && std::chrono::steady_clock::now() < t_end)
             std::this_thread::yield();
     }
-    if (qe == hipErrorNotReady) qe = hipStreamSynchronize(s);
+    if (qe == hipErrorNotReady) qe = hipStreamSynchronize(qs);
     HIPCHK(qe);
     if (cdst != counts.data()) std::memcpy(counts.data(), cdst, counts.size() * sizeof(int));
     std::vector<int> redo;
