@@ -294,3 +294,36 @@ def test_exact_first_mode_for_residue_heavy_batches(df, monkeypatch):
     hb, _, _ = eng.process(frames, 1.0, unwrap=True, want_phases=False)
     assert np.array_equal(ha[real_idx], out["0"][real_idx]) and np.array_equal(hb[real_idx], ha[real_idx])
     assert np.abs(hb[1] - ha[1]).max() < 1e-6 * scale
+
+
+def test_early_census_device_calls(df, monkeypatch):
+    """Device-pointer calls read the residue census back before their integration kernels
+    and return with those still queued (FCD_EARLY_CENSUS=1, the default): several chunks
+    per call (FCD_CHUNK_MAX=3: the early readback waits only for the last chunk's census,
+    the earlier chunks' flags precede it on the same streams), residue frames in the first
+    and the last chunk redone by the exact pass, and two calls issued back to back into
+    different outputs before one synchronisation -- every height bit-identical to the
+    census read back after the whole chain (=0)."""
+    import torch
+    ref, sq = df["ref_u16"].astype(np.float32), float(df["square_size"])
+    real = df["frames_u16"].astype(np.float32)  # 7..1611 residues per map
+    from bench_data import displacement_numpy, warp_numpy
+    smooth = [warp_numpy(ref, *displacement_numpy(ref.shape[0], 3 + i)) for i in range(5)]
+    frames = np.stack([real[0], smooth[0], smooth[1], smooth[2], smooth[3], ref, smooth[4], real[1]])
+    other = np.stack([ref, real[2], smooth[1]])
+    dev = torch.device("cuda", 0)
+    fd, od = torch.from_numpy(frames).to(dev), torch.from_numpy(other).to(dev)
+    monkeypatch.setenv("FCD_CHUNK_MAX", "3")
+    out = {}
+    for early in ("0", "1"):
+        monkeypatch.setenv("FCD_EARLY_CENSUS", early)
+        eng = _engine(ref, sq)
+        hd, ho = torch.empty_like(fd), torch.empty_like(od)
+        eng.process_device(fd.data_ptr(), len(frames), 1.0, True, hd.data_ptr())
+        eng.process_device(od.data_ptr(), len(other), 1.0, True, ho.data_ptr())
+        torch.cuda.synchronize()
+        out[early] = (hd.cpu().numpy(), ho.cpu().numpy())
+        del eng
+    assert np.array_equal(out["0"][0], out["1"][0])
+    assert np.array_equal(out["0"][1], out["1"][1])
+    assert np.isfinite(out["1"][0]).all() and np.abs(out["1"][0][0]).max() > 0
