@@ -81,8 +81,8 @@ std::vector<float2> twiddles(int n) {
 // Pass-major twiddles of the register FFT (regfft.hpp): the schedule of
 // fcdk::Sched<n> (radix E = fft_elems(n) passes, a smaller last one), and for
 // each pass p >= 1, k < L_p, r = 1..R_p-1: exp(-2 pi i r k / (L_p R_p)).
-std::vector<float2> pass_twiddles(int n) {
-    const int E = fcdk::fft_elems(n);
+std::vector<float2> pass_twiddles(int n, int e = 0) {
+    const int E = e ? e : fcdk::fft_elems(n);
     std::vector<float2> t;
     int L = 1, p = 0;
     while (L < n) {
@@ -187,6 +187,7 @@ struct fcd_ctx {
     hipStream_t own = nullptr;
     DevBuf tw_row, tw_col;        // plain tables exp(-2 pi i m / n) (generic LDS FFT kernels)
     DevBuf twp_row, twp_col;      // pass-major tables (register FFT kernels)
+    DevBuf twp_ic;                // k_int_cols' own, where its element count differs (int_cols_elems)
 
     // reference state
     bool has_ref = false;
@@ -548,6 +549,9 @@ void integrate_z(fcd_ctx* c, int nb, const fcdk::IntegCoef& k, float* h_out, hip
                   c->tw_row.as<float2>(), nullptr, s);
 }
 
+// k_int_cols' pass-major table (its element count may differ from the other kernels')
+const float2* ic_tw(fcd_ctx* c) { return c->twp_ic.p ? c->twp_ic.as<float2>() : c->twp_col.as<float2>(); }
+
 void check_ctx(fcd_ctx* c) {
     if (!c) throw FcdError(FCD_E_INVALID, "null context");
     HIPCHK(hipSetDevice(c->device));
@@ -902,6 +906,11 @@ FCD_API int fcd_create(int device, int rows, int cols, fcd_ctx** out) {
         c->twp_col.ensure(pc.size() * sizeof(float2));
         HIPCHK(hipMemcpy(c->twp_row.p, pr.data(), pr.size() * sizeof(float2), hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(c->twp_col.p, pc.data(), pc.size() * sizeof(float2), hipMemcpyHostToDevice));
+        if (fcdk::int_cols_elems(rows) != fcdk::fft_elems(rows)) {
+            const std::vector<float2> pi = pass_twiddles(rows, fcdk::int_cols_elems(rows));
+            c->twp_ic.ensure(pi.size() * sizeof(float2));
+            HIPCHK(hipMemcpy(c->twp_ic.p, pi.data(), pi.size() * sizeof(float2), hipMemcpyHostToDevice));
+        }
         {
             std::vector<float> rtw, ctw;  // ctw: (cos, sin) pairs = float2 on the device
             fcdh::pf_row_plan(cols, c->pf_row, rtw);
@@ -1112,7 +1121,7 @@ void first_pass_chunk(fcd_ctx* c, const float* fr, int nb, bool unwrap, bool fus
         if (census_ev) HIPCHK(hipEventRecord(census_ev, s));
         if (unwrap) fcdk::unwrap_colk_compact(col0, 2 * nb, c->H, colk, s);
         if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
-        fcdk::int_cols(c->H, Zt, c->W, nb, coef, Ht, c->twp_col.as<float2>(), s, unwrap ? colk : nullptr);
+        fcdk::int_cols(c->H, Zt, c->W, nb, coef, Ht, ic_tw(c), s, unwrap ? colk : nullptr);
         fcdk::int_c2r(c->W, Ht, c->H, nb, hdst, c->twp_row.as<float2>(), s);
         // the census of the tile-range edges: its flags are read only when the call ends,
         // so it runs last instead of holding the integration kernels behind it (a small
@@ -1134,7 +1143,7 @@ void first_pass_chunk(fcd_ctx* c, const float* fr, int nb, bool unwrap, bool fus
                        (fo ? fcdk::int_rows_seam_bytes(c->W, c->H, c->fchunk) / sizeof(float2) : 0);
         fcdk::int_rows(c->W, unwrap ? 1 : 0, wrapped, colk, nullptr, kdst, res, c->H, nb, Zt, c->twp_row.as<float2>(),
                        seam, s);
-        fcdk::int_cols(c->H, Zt, c->W, nb, coef, Ht, c->twp_col.as<float2>(), s);
+        fcdk::int_cols(c->H, Zt, c->W, nb, coef, Ht, ic_tw(c), s);
         fcdk::int_c2r(c->W, Ht, c->H, nb, hdst, c->twp_row.as<float2>(), s);
     }
     if (c->profiling) {
@@ -1337,7 +1346,7 @@ int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int f
             unwrap_maps(c, c->wrapped.as<float>(), 2 * nb, kf, counts.data(), s);
             fcdk::int_rows(c->W, 2, c->wrapped.as<float>(), nullptr, kf, nullptr, nullptr, c->H, nb, c->Zt.as<float2>(),
                            c->twp_row.as<float2>(), nullptr, s);
-            fcdk::int_cols(c->H, c->Zt.as<float2>(), c->W, nb, coef, c->Ht.as<float2>(), c->twp_col.as<float2>(), s);
+            fcdk::int_cols(c->H, c->Zt.as<float2>(), c->W, nb, coef, c->Ht.as<float2>(), ic_tw(c), s);
             float* hdst = dev && height_out ? height_out + (size_t)f0 * hw : c->out_h.as<float>();
             fcdk::int_c2r(c->W, c->Ht.as<float2>(), c->H, nb, hdst, c->twp_row.as<float2>(), s);
             if (!dev && height_out)
@@ -1504,7 +1513,7 @@ int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int f
         unwrap_maps(c, c->wrapped.as<float>(), 2 * ng, kf, nullptr, s, true);
         fcdk::int_rows(c->W, 2, c->wrapped.as<float>(), nullptr, kf, nullptr, nullptr, c->H, ng, c->Zt.as<float2>(),
                        c->twp_row.as<float2>(), nullptr, s);
-        fcdk::int_cols(c->H, c->Zt.as<float2>(), c->W, ng, coef, c->Ht.as<float2>(), c->twp_col.as<float2>(), s);
+        fcdk::int_cols(c->H, c->Zt.as<float2>(), c->W, ng, coef, c->Ht.as<float2>(), ic_tw(c), s);
         const bool direct = run && dev && height_out;
         float* hdst = direct ? height_out + (size_t)gi[0] * hw : c->out_h.as<float>();
         fcdk::int_c2r(c->W, c->Ht.as<float2>(), c->H, ng, hdst, c->twp_row.as<float2>(), s);

@@ -117,6 +117,14 @@ __host__ __device__ constexpr int fft_elems(int n) {
 }
 // Threads per team.
 __host__ __device__ constexpr int fft_team(int n) { return n / fft_elems(n); }
+// k_int_cols' own count at 1024 points: 16 per lane (wave-local 64-lane teams, so the
+// transforms' exchanges need no workgroup barrier) at 2 waves / SIMD, 2.88 -> 2.75
+// us/frame (kbench r03zb); elsewhere fft_elems.  Its pass-major twiddle table follows
+// (pass_twiddles(n, int_cols_elems(n)) on the host).
+#ifndef FCD_INTCOLS_ELEMS_1024
+#define FCD_INTCOLS_ELEMS_1024 16
+#endif
+__host__ __device__ constexpr int int_cols_elems(int n) { return n == 1024 ? FCD_INTCOLS_ELEMS_1024 : fft_elems(n); }
 // Padded LDS index: one spare complex per 16.  With this padding every
 // exchange pattern of the register FFT (16t + r, t + 64q, base + 16r) is affine
 // in the compile-time index (one address register + immediate offsets) and

@@ -68,10 +68,10 @@ __device__ __forceinline__ long tix(int row, int col, int ncols) {
 #define FCD_INTCOLS_BLOCK 256
 #endif
 
-template <int N, int B = BLOCK>
+template <int N, int B = BLOCK, int EE = fft_elems(N)>
 struct KCfg {
-    static constexpr int TT = Sched<N>::TT;
-    static constexpr int E = Sched<N>::E;
+    static constexpr int TT = Sched<N, EE>::TT;
+    static constexpr int E = Sched<N, EE>::E;
     static constexpr int THREADS = TT > B ? TT : B;  // 4096-point teams span 8 waves
     static constexpr int TEAMS = THREADS / TT;
     static constexpr int ROW = padded_len(N);  // float2 per team row
@@ -132,9 +132,10 @@ struct DemodColsCfg : KCfg<N, (N <= 1024 ? FCD_DEMODCOLS_BLOCK : BLOCK)> {
 #define FCD_INTCOLS_LEAN_2048 0
 #endif
 template <int N>
-struct IntColsCfg : KCfg<N, FCD_INTCOLS_BLOCK> {
+struct IntColsCfg : KCfg<N, FCD_INTCOLS_BLOCK, int_cols_elems(N)> {
     static constexpr bool LEAN = N == 2048 && FCD_INTCOLS_LEAN_2048;
-    static constexpr int V = N <= 1024 ? FCD_INTCOLS_WAVES : (LEAN ? 4 : ColWaves<N>::V);
+    // 16 elements per lane at 1024: 186 VGPRs, 2 waves / SIMD
+    static constexpr int V = N <= 1024 ? (int_cols_elems(N) == 16 ? 2 : FCD_INTCOLS_WAVES) : (LEAN ? 4 : ColWaves<N>::V);
     static constexpr bool PREF_Y = LEAN ? false : (N >= 4096 ? true : FCD_INTCOLS_PREF_Y);  // 4096: 2 waves/SIMD either way
     static constexpr bool PREF_X = LEAN ? false : FCD_INTCOLS_PREF_X;
     static constexpr bool KY_LDS = FCD_INTCOLS_KY_LDS && !LEAN;
@@ -437,7 +438,7 @@ __global__ __launch_bounds__(IntColsCfg<H>::THREADS, IntColsCfg<H>::V) void k_in
     float2* const lds = lds_raw + C::NLEN;  // lds_raw[0, NLEN): the twiddle table
     const int team = threadIdx.x / TT, t = threadIdx.x % TT;
     float2* s = lds + team * C::ROW;
-    RegFFT<H> fft;
+    RegFFT<H, false, C::E> fft;
     fft.init(tw, lds_raw, threadIdx.x, C::THREADS);
     // the row wavenumber tables (ky_eff, ky^2) of every element, read per item: LDS copies
     float* const lky = reinterpret_cast<float*>(lds + TEAMS * C::ROW);

@@ -22,9 +22,9 @@
 
 namespace fcdk {
 
-template <int N>
+template <int N, int EE = fft_elems(N)>
 struct Sched {
-    static constexpr int E = fft_elems(N);
+    static constexpr int E = EE;
     static constexpr int TT = N / E;
     static constexpr int radix(int p) {
         int L = 1;
@@ -60,12 +60,17 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <int N>
-__device__ __forceinline__ void team_sync() {
-    if constexpr (Sched<N>::WAVE_LOCAL)
+template <class S>
+__device__ __forceinline__ void team_sync_of() {
+    if constexpr (S::WAVE_LOCAL)
         wave_sync();
     else
         __syncthreads();
+}
+
+template <int N>
+__device__ __forceinline__ void team_sync() {
+    team_sync_of<Sched<N>>();
 }
 
 // Pass-major twiddle table, built on the host in double precision
@@ -77,9 +82,9 @@ __device__ __forceinline__ void team_sync() {
 // frees buys a second workgroup per CU (k_demod_cols at 4096 points: 16.9 -> 15.1
 // us/frame, kbench r03u); elsewhere the table reads from L1 / L2 cost more than the
 // occupancy (k_int_cols 4096: 85 -> 114 us/frame, VGPR-bound at one workgroup anyway).
-template <int N, bool GTW = false>
+template <int N, bool GTW = false, int EE = fft_elems(N)>
 struct RegFFT {
-    using S = Sched<N>;
+    using S = Sched<N, EE>;
     static constexpr int E = S::E, TT = S::TT, NP = S::NP;
     static constexpr bool GLOBAL_TW = GTW;
     static constexpr int LDS_TW = GLOBAL_TW ? 0 : N;  // float2 of LDS the table takes
@@ -140,7 +145,7 @@ struct RegFFT {
 #pragma unroll
                 for (int r = 0; r < R; ++r) s[pad(base + r * L)] = a[b][r];
             }
-            team_sync<N>();
+            team_sync_of<S>();
 #pragma unroll
             for (int q = 0; q < E; ++q) x[q] = s[pad(t + TT * q)];
             run_pass<P + 1, INV>(x, s, t);
