@@ -187,7 +187,7 @@ struct fcd_ctx {
     hipStream_t own = nullptr;
     DevBuf tw_row, tw_col;        // plain tables exp(-2 pi i m / n) (generic LDS FFT kernels)
     DevBuf twp_row, twp_col;      // pass-major tables (register FFT kernels)
-    DevBuf twp_ic;                // k_int_cols' own, where its element count differs (int_cols_elems)
+    DevBuf twp_col16;             // the column table for 16 elements per lane (k_int_cols / k_demod_cols at 1024)
 
     // reference state
     bool has_ref = false;
@@ -549,8 +549,14 @@ void integrate_z(fcd_ctx* c, int nb, const fcdk::IntegCoef& k, float* h_out, hip
                   c->tw_row.as<float2>(), nullptr, s);
 }
 
-// k_int_cols' pass-major table (its element count may differ from the other kernels')
-const float2* ic_tw(fcd_ctx* c) { return c->twp_ic.p ? c->twp_ic.as<float2>() : c->twp_col.as<float2>(); }
+// The column kernels' pass-major tables (their element counts may differ from fft_elems)
+const float2* col_tw(fcd_ctx* c, int elems) {
+    if (elems == fcdk::fft_elems(c->H)) return c->twp_col.as<float2>();
+    if (elems != 16 || !c->twp_col16.p) throw FcdError(FCD_E_INTERNAL, "no pass table for this element count");
+    return c->twp_col16.as<float2>();
+}
+const float2* ic_tw(fcd_ctx* c) { return col_tw(c, fcdk::int_cols_elems(c->H)); }
+const float2* dc_tw(fcd_ctx* c) { return col_tw(c, fcdk::demod_cols_elems(c->H)); }
 
 void check_ctx(fcd_ctx* c) {
     if (!c) throw FcdError(FCD_E_INVALID, "null context");
@@ -691,7 +697,7 @@ void fast_demod(fcd_ctx* c, const float* frames, int nb, hipStream_t s, int fo =
     float2* Ab = c->Ab.as<float2>() + fo * 2 * H * c->NCA;
     float* wrapped = c->wrapped.as<float>() + fo * 2 * c->hw();
     fcdk::demod_rows(c->W, frames, c->H, nb, T, Xb, c->twp_row.as<float2>(), s);
-    fcdk::demod_cols(c->H, Xb, nb, T, Ab, c->NCA, c->twp_col.as<float2>(), s);
+    fcdk::demod_cols(c->H, Xb, nb, T, Ab, c->NCA, dc_tw(c), s);
     if (c->band_B)
         fcdk::band_phase(c->W, c->band_B, false, Ab, c->H, nb, c->NCA, c->NCc[0], c->NCc[1], c->theta_p.as<float>(),
                          wrapped, c->band_pre.as<float2>(), c->band_ptw.as<float2>(), s);
@@ -705,7 +711,7 @@ void band_reference(fcd_ctx* c, const float* dref, hipStream_t s) {
     if (!c->band_B && !c->fused_B) return;
     const fcdk::DemodTables T = demod_tables(c);
     fcdk::demod_rows(c->W, dref, c->H, 1, T, c->Xb.as<float2>(), c->twp_row.as<float2>(), s);
-    fcdk::demod_cols(c->H, c->Xb.as<float2>(), 1, T, c->Ab.as<float2>(), c->NCA, c->twp_col.as<float2>(), s);
+    fcdk::demod_cols(c->H, c->Xb.as<float2>(), 1, T, c->Ab.as<float2>(), c->NCA, dc_tw(c), s);
     if (c->band_B)
         fcdk::band_phase(c->W, c->band_B, true, c->Ab.as<float2>(), c->H, 1, c->NCA, c->NCc[0], c->NCc[1], nullptr,
                          c->theta_b.as<float>(), c->band_pre.as<float2>(), c->band_ptw.as<float2>(), s);
@@ -906,10 +912,10 @@ FCD_API int fcd_create(int device, int rows, int cols, fcd_ctx** out) {
         c->twp_col.ensure(pc.size() * sizeof(float2));
         HIPCHK(hipMemcpy(c->twp_row.p, pr.data(), pr.size() * sizeof(float2), hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(c->twp_col.p, pc.data(), pc.size() * sizeof(float2), hipMemcpyHostToDevice));
-        if (fcdk::int_cols_elems(rows) != fcdk::fft_elems(rows)) {
-            const std::vector<float2> pi = pass_twiddles(rows, fcdk::int_cols_elems(rows));
-            c->twp_ic.ensure(pi.size() * sizeof(float2));
-            HIPCHK(hipMemcpy(c->twp_ic.p, pi.data(), pi.size() * sizeof(float2), hipMemcpyHostToDevice));
+        if (fcdk::int_cols_elems(rows) == 16 || fcdk::demod_cols_elems(rows) == 16) {
+            const std::vector<float2> pi = pass_twiddles(rows, 16);
+            c->twp_col16.ensure(pi.size() * sizeof(float2));
+            HIPCHK(hipMemcpy(c->twp_col16.p, pi.data(), pi.size() * sizeof(float2), hipMemcpyHostToDevice));
         }
         {
             std::vector<float> rtw, ctw;  // ctw: (cos, sin) pairs = float2 on the device
@@ -1110,7 +1116,7 @@ void first_pass_chunk(fcd_ctx* c, const float* fr, int nb, bool unwrap, bool fus
         float2* Ht = c->Ht.as<float2>() + fo * H * (W / 2 + 1);
         if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
         fcdk::demod_rows(c->W, fr, c->H, nb, T, Xb, c->twp_row.as<float2>(), s);
-        fcdk::demod_cols(c->H, Xb, nb, T, Ab, c->NCA, c->twp_col.as<float2>(), s);
+        fcdk::demod_cols(c->H, Xb, nb, T, Ab, c->NCA, dc_tw(c), s);
         if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
         // dynamic chunk schedule: each concurrent half (fo) has its own counter pair
         unsigned* ctr = c->pr_dynamic ? c->pr_ctr.as<unsigned>() + (fo ? 2 : 0) : nullptr;

@@ -125,6 +125,11 @@ __host__ __device__ constexpr int fft_team(int n) { return n / fft_elems(n); }
 #define FCD_INTCOLS_ELEMS_1024 16
 #endif
 __host__ __device__ constexpr int int_cols_elems(int n) { return n == 1024 ? FCD_INTCOLS_ELEMS_1024 : fft_elems(n); }
+// k_demod_cols' count at 1024 points (FCD_DEMODCOLS_ELEMS_1024; its table likewise)
+#ifndef FCD_DEMODCOLS_ELEMS_1024
+#define FCD_DEMODCOLS_ELEMS_1024 8
+#endif
+__host__ __device__ constexpr int demod_cols_elems(int n) { return n == 1024 ? FCD_DEMODCOLS_ELEMS_1024 : fft_elems(n); }
 // Padded LDS index: one spare complex per 16.  With this padding every
 // exchange pattern of the register FFT (16t + r, t + 64q, base + 16r) is affine
 // in the compile-time index (one address register + immediate offsets) and

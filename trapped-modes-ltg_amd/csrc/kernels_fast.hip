@@ -118,9 +118,12 @@ struct KCfg {
 #ifndef FCD_DC_TW_GLOBAL_MIN
 #define FCD_DC_TW_GLOBAL_MIN 4096
 #endif
+#ifndef FCD_DEMODCOLS_V16
+#define FCD_DEMODCOLS_V16 2
+#endif
 template <int N>
-struct DemodColsCfg : KCfg<N, (N <= 1024 ? FCD_DEMODCOLS_BLOCK : BLOCK)> {
-    static constexpr int V = N <= 1024 ? 4 : ColWaves<N>::V;
+struct DemodColsCfg : KCfg<N, (N <= 1024 ? FCD_DEMODCOLS_BLOCK : BLOCK), demod_cols_elems(N)> {
+    static constexpr int V = N <= 1024 ? (demod_cols_elems(N) == 16 ? FCD_DEMODCOLS_V16 : 4) : ColWaves<N>::V;
     static constexpr bool GTW = N >= FCD_DC_TW_GLOBAL_MIN;
     static constexpr int NLEN = GTW ? 0 : N;
 };
@@ -258,7 +261,7 @@ __global__ __launch_bounds__(DemodColsCfg<H>::THREADS, DemodColsCfg<H>::V) void 
     const int team = threadIdx.x / TT, t = threadIdx.x % TT;
     float2* s = lds + team * C::ROW;            // holds the forward column spectrum
     float2* s2 = lds + (TEAMS + team) * C::ROW;  // exchanges of the inverse FFTs
-    RegFFT<H, C::GTW> fft;
+    RegFFT<H, C::GTW, C::E> fft;
     fft.init(tw, lds_raw, threadIdx.x, C::THREADS);
     __syncthreads();
     const int NC = T.NC;
@@ -299,14 +302,14 @@ __global__ __launch_bounds__(DemodColsCfg<H>::THREADS, DemodColsCfg<H>::V) void 
         int4 on = T.outs[i * 4];     // carrier, cslot, mirror, uc
         int2 rn = T.outrows[i * 4];  // shifted rows [lo, hi]
         fft.template run<false>(x, s, t);
-        if constexpr (!Sched<H>::WAVE_LOCAL) __syncthreads();
+        if constexpr (!Sched<H, C::E>::WAVE_LOCAL) __syncthreads();
 #pragma unroll
         for (int q = 0; q < E; ++q) s[pad(t + TT * q)] = x[q];
-        team_sync<H>();
+        team_sync_of<Sched<H, C::E>>();
         // teams spanning waves share the workgroup barrier: every team loops to
         // the largest output count among the workgroup's items
         int nmax = nout;
-        if constexpr (!Sched<H>::WAVE_LOCAL && TEAMS > 1) {
+        if constexpr (!Sched<H, C::E>::WAVE_LOCAL && TEAMS > 1) {
             nmax = 0;
 #pragma unroll
             for (int tm = 0; tm < TEAMS; ++tm) {
