@@ -422,8 +422,12 @@ void unwrap_maps(fcd_ctx* c, const float* w, int nmaps, int32_t* k, int* res_hos
             std::fprintf(stderr, "[mst-cg] tiles %zu round %d: level-0 components %ld (max/tile %d), edges %ld (max/tile %d)\n",
                          nt, r, sc, mc, se, me);
         };
-        for (; rounds < max_rounds; rounds += 3) {
-            for (int g = 0; g < 3; ++g) {
+        // the first check after FCD_CG_FIRST rounds (camera frames converge in 7-9, and a
+        // round of finished tiles costs one load per tile), then every third: each check
+        // is a host round trip with the GPU idle
+        static const int first = std::max(1, fcd_env_int("FCD_CG_FIRST", 9));
+        for (int step = first; rounds < max_rounds; rounds += step, step = 3) {
+            for (int g = 0; g < step; ++g) {
                 if (cg_dbg) cg_dump(rounds + g);
                 fcdk::mst_cg_round(nact, c->H, c->W, m, rounds + g, s);
             }
