@@ -547,7 +547,7 @@ __global__ __launch_bounds__(256) void k_seam_check(const float2* __restrict__ s
 }
 
 #ifdef FCD_STAMPS
-extern "C" int fcd_debug_pr_stamps(unsigned long long* out) {
+extern "C" __attribute__((visibility("default"))) int fcd_debug_pr_stamps(unsigned long long* out) {
     return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pr_stamps), sizeof(g_pr_stamps));
 }
 #endif
