@@ -133,7 +133,8 @@ int fcd_get_carriers(fcd_ctx* ctx, float* ccsgn, uint8_t* mask);
  * height_out (the fused chain): the census is read back as soon as its flags are final,
  * so the call returns with the integration kernels still queued on `stream` (order later
  * work on that stream, or call fcd_synchronize); frames with residues are then redone by
- * the exact pass before the call returns. */
+ * the exact pass before the call returns.  A later call on another stream, and every
+ * other entry point of the context, first waits for that queued work. */
 int fcd_process(fcd_ctx* ctx, const float* frames, int n_frames, int flags, double height, int unwrap,
                 float* height_out, float* wrapped_out, int32_t* k_out, void* stream);
 

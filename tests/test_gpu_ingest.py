@@ -327,3 +327,37 @@ def test_early_census_device_calls(df, monkeypatch):
     assert np.array_equal(out["0"][0], out["1"][0])
     assert np.array_equal(out["0"][1], out["1"][1])
     assert np.isfinite(out["1"][0]).all() and np.abs(out["1"][0][0]).max() > 0
+
+
+def test_pending_device_call_orders_later_calls(df):
+    """A device call returns with its integration queued on its stream; a following call
+    on another stream, or a new reference (which rewrites the tables those kernels read),
+    must not overtake it: heights equal to the same call run on its own.  Residue-free
+    frames (warps of the reference), so no exact pass synchronises the calls."""
+    import torch
+    from bench_data import checkerboard, displacement_numpy, warp_numpy
+    ref, sq = df["ref_u16"].astype(np.float32), float(df["square_size"])
+    board = checkerboard(ref.shape[0])
+    frames = np.stack([warp_numpy(ref, *displacement_numpy(ref.shape[0], 11 + i)) for i in range(6)])
+    dev = torch.device("cuda", 0)
+    fd = torch.from_numpy(frames).to(dev)
+    fflip = fd.flip(0).contiguous()
+    eng = _engine(ref, sq)
+    want = torch.empty_like(fd)
+    eng.process_device(fd.data_ptr(), len(frames), 1.0, True, want.data_ptr())
+    torch.cuda.synchronize()
+    # (1) a new reference right after the call
+    got = torch.empty_like(fd)
+    eng.process_device(fd.data_ptr(), len(frames), 1.0, True, got.data_ptr())
+    eng.set_reference(board, 0.001)
+    torch.cuda.synchronize()
+    assert torch.equal(got, want)
+    # (2) a call on another stream, into the same workspace, right after the call
+    eng.set_reference(ref, sq)
+    side = torch.cuda.Stream(dev)
+    got2, other = torch.empty_like(fd), torch.empty_like(fd)
+    eng.process_device(fd.data_ptr(), len(frames), 1.0, True, got2.data_ptr())
+    eng.process_device(fflip.data_ptr(), len(frames), 1.0, True, other.data_ptr(), stream=side.cuda_stream)
+    torch.cuda.synchronize()
+    assert torch.equal(got2, want)
+    assert torch.equal(other.flip(0), want)

@@ -216,6 +216,8 @@ struct fcd_ctx {
     hipStream_t cstream = nullptr;   // its copy stream and the two halves' "census complete" events
     hipEvent_t ev_cen[2] = {nullptr, nullptr};
     hipEvent_t ev_done = nullptr;    // end of the last device call's work on its (caller's) stream
+    hipStream_t done_stream = nullptr;  // that stream, while the work may still be running
+    bool done_pending = false;
     bool pr_dynamic = false;         // FCD_PR_DYNAMIC=1: the 1024 fused kernel takes tile chunks from a counter
                                      // (r03t: 80.1-81.0k vs 80.0-81.6k frames/s static, no gain; kept as an option)
     DevBuf pr_ctr;                   // its counter pairs, one per concurrent half (each launch leaves them 0)
@@ -562,9 +564,22 @@ const float2* col_tw(fcd_ctx* c, int elems) {
 const float2* ic_tw(fcd_ctx* c) { return col_tw(c, fcdk::int_cols_elems(c->H)); }
 const float2* dc_tw(fcd_ctx* c) { return col_tw(c, fcdk::demod_cols_elems(c->H)); }
 
-void check_ctx(fcd_ctx* c) {
+// A device call may return with its integration kernels still queued on the caller's
+// stream (early census readback).  Work on that same stream is ordered after them; any
+// other entry point (another stream, the context's own stream, state changes such as a
+// new reference) first waits for them on the host, since it may touch the workspace and
+// tables those kernels read.
+void settle(fcd_ctx* c, hipStream_t same = nullptr) {
+    if (!c->done_pending) return;
+    if (same && same == c->done_stream) return;
+    HIPCHK(hipEventSynchronize(c->ev_done));
+    c->done_pending = false;
+}
+
+void check_ctx(fcd_ctx* c, bool settle_pending = true) {
     if (!c) throw FcdError(FCD_E_INVALID, "null context");
     HIPCHK(hipSetDevice(c->device));
+    if (settle_pending) settle(c);
 }
 
 // Band-pruned demodulation tables: which unshifted columns each carrier disk
@@ -968,6 +983,7 @@ FCD_API int fcd_synchronize(fcd_ctx* ctx) {
     FCD_TRY({
         check_ctx(ctx);
         if (ctx->ev_done) HIPCHK(hipEventSynchronize(ctx->ev_done));
+        ctx->done_pending = false;
         HIPCHK(hipStreamSynchronize(ctx->own));
     })
 }
@@ -1303,7 +1319,8 @@ void stage_frames(fcd_ctx* c, const void* frames, int format, bool dev, const in
 
 int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int flags, double height, int unwrap,
                  float* height_out, float* wrapped_out, int32_t* k_out, void* stream) {
-    check_ctx(c);
+    check_ctx(c, false);
+    settle(c, c->pick(stream));  // the previous call's queued work: ordered if on this stream
     if (!c->has_ref) throw FcdError(FCD_E_STATE, "no reference set");
     if (!frames || n_frames < 0) throw FcdError(FCD_E_INVALID, "bad frames");
     if (fcdk::raw_frame_bytes(format, c->H, c->W) == 0) throw FcdError(FCD_E_INVALID, "unknown frame format");
@@ -1455,6 +1472,8 @@ int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int f
     if (dev) {  // the call's last work on the caller's stream so far (fcd_destroy / fcd_synchronize wait on it)
         if (!c->ev_done) HIPCHK(hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming));
         HIPCHK(hipEventRecord(c->ev_done, s));
+        c->done_stream = s;
+        c->done_pending = true;
     }
     if (!unwrap) return FCD_OK;
     // ---- pass 2: frames whose maps have residues are redone with the Boruvka (MST) unwrap
