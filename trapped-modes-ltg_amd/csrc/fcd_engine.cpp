@@ -1383,7 +1383,14 @@ int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int f
             if (!dev) HIPCHK(hipStreamSynchronize(s));
             for (int i = 0; i < nb; ++i) nres += counts[2 * (size_t)i] || counts[2 * (size_t)i + 1];
         }
-        HIPCHK(hipStreamSynchronize(s));
+        if (dev && !c->profiling) {  // the integration stays queued on the caller's stream, as in pass 1 below
+            if (!c->ev_done) HIPCHK(hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming));
+            HIPCHK(hipEventRecord(c->ev_done, s));
+            c->done_stream = s;
+            c->done_pending = true;
+        } else {
+            HIPCHK(hipStreamSynchronize(s));
+        }
         if (4 * nres < n_frames) c->exact_first = false;  // mostly residue-free again
         if (c->profiling) {
             c->prof_fix_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
