@@ -124,7 +124,13 @@ __host__ __device__ constexpr int fft_team(int n) { return n / fft_elems(n); }
 #ifndef FCD_INTCOLS_ELEMS_1024
 #define FCD_INTCOLS_ELEMS_1024 16
 #endif
-__host__ __device__ constexpr int int_cols_elems(int n) { return n == 1024 ? FCD_INTCOLS_ELEMS_1024 : fft_elems(n); }
+// and at 2048 / 4096 points (FCD_INTCOLS_ELEMS_WIDE, 0: fft_elems; 16: 256 / 192 VGPRs, no spills)
+#ifndef FCD_INTCOLS_ELEMS_WIDE
+#define FCD_INTCOLS_ELEMS_WIDE 16  // r03zk: 4096 85.4 -> 80.7, 2048 13.3 -> 12.4 us/frame
+#endif
+__host__ __device__ constexpr int int_cols_elems(int n) {
+    return n == 1024 ? FCD_INTCOLS_ELEMS_1024 : (n >= 2048 && FCD_INTCOLS_ELEMS_WIDE ? FCD_INTCOLS_ELEMS_WIDE : fft_elems(n));
+}
 // k_demod_cols' count at 1024 points (FCD_DEMODCOLS_ELEMS_1024; its table likewise)
 #ifndef FCD_DEMODCOLS_ELEMS_1024
 #define FCD_DEMODCOLS_ELEMS_1024 8
