@@ -87,6 +87,9 @@ struct KCfg {
 #endif
 // Prefetch the mirror column of the next item too (1), or load it at the top of
 // the item (0: 16 fewer VGPRs live across the transforms).
+#ifndef FCD_INTCOLS_WAVES_E16
+#define FCD_INTCOLS_WAVES_E16 2  // at 16 elements per lane (3: 168 VGPRs, 22 spilled, 2.81 -> 3.71 us/frame, kbench r03w3)
+#endif
 #ifndef FCD_INTCOLS_PREF_Y
 #define FCD_INTCOLS_PREF_Y 0
 #endif
@@ -138,7 +141,7 @@ template <int N>
 struct IntColsCfg : KCfg<N, FCD_INTCOLS_BLOCK, int_cols_elems(N)> {
     static constexpr bool LEAN = N == 2048 && FCD_INTCOLS_LEAN_2048;
     // 16 elements per lane at 1024: 186 VGPRs, 2 waves / SIMD
-    static constexpr int V = N <= 1024 ? (int_cols_elems(N) == 16 ? 2 : FCD_INTCOLS_WAVES) : (LEAN ? 4 : ColWaves<N>::V);
+    static constexpr int V = N <= 1024 ? (int_cols_elems(N) == 16 ? FCD_INTCOLS_WAVES_E16 : FCD_INTCOLS_WAVES) : (LEAN ? 4 : ColWaves<N>::V);
     static constexpr bool PREF_Y = LEAN ? false : (N >= 4096 ? true : FCD_INTCOLS_PREF_Y);  // 4096: 2 waves/SIMD either way
     static constexpr bool PREF_X = LEAN ? false : FCD_INTCOLS_PREF_X;
     static constexpr bool KY_LDS = FCD_INTCOLS_KY_LDS && !LEAN;
