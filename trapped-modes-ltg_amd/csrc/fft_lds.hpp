@@ -135,7 +135,14 @@ __host__ __device__ constexpr int int_cols_elems(int n) {
 #ifndef FCD_DEMODCOLS_ELEMS_1024
 #define FCD_DEMODCOLS_ELEMS_1024 8
 #endif
-__host__ __device__ constexpr int demod_cols_elems(int n) { return n == 1024 ? FCD_DEMODCOLS_ELEMS_1024 : fft_elems(n); }
+// and at 4096 points (FCD_DEMODCOLS_ELEMS_4096, 0: fft_elems; 16: 180 VGPRs, no spills,
+// 14.65 -> 13.1 us/frame; the same at 2048 measured 3.31 -> 4.03, kbench r03dc)
+#ifndef FCD_DEMODCOLS_ELEMS_4096
+#define FCD_DEMODCOLS_ELEMS_4096 16
+#endif
+__host__ __device__ constexpr int demod_cols_elems(int n) {
+    return n == 1024 ? FCD_DEMODCOLS_ELEMS_1024 : (n == 4096 && FCD_DEMODCOLS_ELEMS_4096 ? FCD_DEMODCOLS_ELEMS_4096 : fft_elems(n));
+}
 // Padded LDS index: one spare complex per 16.  With this padding every
 // exchange pattern of the register FFT (16t + r, t + 64q, base + 16r) is affine
 // in the compile-time index (one address register + immediate offsets) and
