@@ -582,10 +582,13 @@ __global__ __launch_bounds__(IntColsCfg<H>::THREADS, IntColsCfg<H>::V) void k_in
 }
 
 // ------------------------------------------------------------------ I3
-// Rows per workgroup: the staged block of the half spectrum (W/2+1 columns x
+// Rows per workgroup (FCD_C2R_RPW_2048 at 2048): the staged block of the half spectrum (W/2+1 columns x
 // RPW rows) plus one exchange row per team stays under ~156 KiB of LDS; one
 // team per row pair, so W = 1024 runs 16 waves per CU from one workgroup.
-__host__ __device__ constexpr int c2r_rpw(int W) { return W <= 1024 ? 16 : (W == 2048 ? 4 : 2); }
+#ifndef FCD_C2R_RPW_2048
+#define FCD_C2R_RPW_2048 8  // 16 waves per CU in 156 KB of LDS: 8.97 -> 7.17 us/frame (kbench r03c8; 4 before)
+#endif
+__host__ __device__ constexpr int c2r_rpw(int W) { return W <= 1024 ? 16 : (W == 2048 ? FCD_C2R_RPW_2048 : 2); }
 
 template <int W>
 struct C2RCfg {
