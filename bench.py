@@ -202,7 +202,14 @@ def main():
     heights = torch.empty((B, n, n), dtype=torch.float32, device=dev)
     eng = _lib.Engine((n, n), device=local)
     eng.set_reference(ref_t.cpu().numpy(), SQUARE_SIZE)
-    stream = torch.cuda.current_stream(dev).cuda_stream
+    # a dedicated (non-default) stream: the engine keeps a call on a caller stream
+    # asynchronous (the integration stays queued behind the census read-back), while a
+    # null stream (torch's default stream has cuda_stream == 0) makes it wait before
+    # returning; the HIP events below record on it too (torch.cuda.stream context)
+    torch.cuda.synchronize(dev)  # the frames were generated on the default stream
+    work = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(work)
+    stream = work.cuda_stream
 
     def step():
         eng.process_device(frames.data_ptr(), B, 1.0, True, heights.data_ptr(), stream=stream)

@@ -86,6 +86,39 @@ def make_frames_numpy(n, count, seed=0, rotate_deg=0.0):
     return ref, frames
 
 
+def dislocation_displacement(n, pairs, length=200):
+    """u_x of edge-dislocation pairs, sum over (y0, x0) of
+    P / (2 pi) * (atan2(y - y0, x - x0) - atan2(y - y0, x - x0 - length)), P = 20 px (the
+    board's period, so the cut between the two cores is invisible): both carrier phases
+    wind by +-2 pi around each core, i.e. a residue pair on row ~y0."""
+    y, x = np.mgrid[0:n, 0:n].astype(np.float64)
+    ux = np.zeros((n, n))
+    for y0, x0 in pairs:
+        ux += (2 * SQUARE_PX / (2 * np.pi)) * (np.arctan2(y - y0, x - x0) - np.arctan2(y - y0, x - x0 - length))
+    return ux
+
+
+def make_residue_frame(n, pairs, seed=None, rotate_deg=0.0, length=200, quantum=None):
+    """One frame whose wrapped maps carry residues: the board warped by the bump field of
+    `seed` (none if None) plus the dislocation pairs' u_x (the exact-unwrap workload of
+    camera frames at the c3 / c5 sizes).
+
+    `quantum` (e.g. 4096) rounds the displacement to multiples of 1 / quantum px before the
+    warp.  np.exp / np.arctan2 differ in the last bit between numpy builds and SIMD paths
+    (numpy 1.26 and 2.2 disagree on 4096^2 grids); after the rounding the frame is made of
+    IEEE +, *, floor only, so the same bytes come out of the reference's interpreter, this
+    one and the GPU box's (the golden fixtures store the frame's digest)."""
+    ref = checkerboard(n, rotate_deg)
+    if seed is None:
+        gy, gx = np.zeros((n, n)), np.zeros((n, n))
+    else:
+        gy, gx = displacement_numpy(n, seed)
+    gx = gx + dislocation_displacement(n, pairs, length)
+    if quantum:
+        gy, gx = np.round(gy * quantum) / quantum, np.round(gx * quantum) / quantum
+    return ref, warp_numpy(ref, gy, gx)
+
+
 def make_frames_torch(n, count, seed=0, rotate_deg=0.0, device="cuda", chunk=64):
     """Same recipe on the GPU; returns (ref float32 [n,n], frames float32 [count,n,n]) device tensors."""
     import torch

@@ -29,6 +29,10 @@ Fixtures (all under tests/golden/):
   bench_board.npz    the benchmarked c2 board (bench_data.py: pattern.py geometry, 1024^2,
                      unrotated and rotated 5 degrees): the reference's find_peaks picks,
                      blobs, cf, radius, and compute_height_map of two warped frames
+  large.npz          the c3 / c5 frame sizes (2048^2, 4096^2): per size one residue-free
+                     rotated-board frame and one with residues (bump field + edge-dislocation
+                     pairs), the reference's carrier picks, heights, wrapped phases and FULL
+                     unwrap k-fields (bench_data.make_residue_frame, frame digests stored)
   analyze_ref.npz    pydata/analyze.py ITSELF (imported with a placeholder `cv2` module
                      whose every attribute access raises: cv2 is only used on the polar
                      paths, analyze.py:237-241, 674-676, which are not run): analyze.mask /
@@ -405,6 +409,68 @@ def make_bench_board():
     np.savez_compressed(os.path.join(OUT, "bench_board.npz"), **out)
 
 
+# The c3 / c5 frame sizes (BASELINE configs[2], [4]): one residue-free rotated-board frame
+# (bench_data.make_frames_numpy) and one frame with residues (bump field + edge-dislocation
+# pairs, bench_data.make_residue_frame) per size, each through the reference's
+# compute_height_map with its skimage unwrap (fcd.py:13-35, 119).
+LARGE_CASES = {
+    "s2048": dict(n=2048, seed=11, pairs=[]),
+    "r2048": dict(n=2048, seed=21, pairs=[(487.0, 870.4), (1300.3, 1200.7), (1700.6, 400.2)]),
+    "s4096": dict(n=4096, seed=2, pairs=[]),
+    "r4096": dict(n=4096, seed=23, pairs=[(607.0, 870.4), (2500.3, 3000.1), (3300.6, 1500.2)]),
+}
+
+
+def large_case_frames(spec):
+    """(ref, frame) of a LARGE_CASES entry: bench_data.make_residue_frame with the
+    displacement rounded to 1/4096 px, so the frame bytes do not depend on the numpy
+    build (tests regenerate it and check the digest)."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(OUT)))  # the repo root: bench_data.py (numpy only)
+    from bench_data import make_residue_frame
+    return make_residue_frame(spec["n"], spec["pairs"], seed=spec["seed"], rotate_deg=5.0, quantum=4096)
+
+
+def residue_count(w):
+    w = np.asarray(w, np.float64)
+    wr = lambda d: (d + np.pi) % (2 * np.pi) - np.pi  # noqa: E731
+    c = (wr(w[:-1, 1:] - w[:-1, :-1]) + wr(w[1:, 1:] - w[:-1, 1:]) + wr(w[1:, :-1] - w[1:, 1:])
+         + wr(w[:-1, :-1] - w[1:, :-1]))
+    return int((np.abs(c) > 1).sum())
+
+
+def make_large():
+    """large.npz: per case the frame digests, the reference's carrier picks, its height on a
+    256^2 sub-grid (+ sum / norm / max over the full map), wrapped phases on a 128^2
+    sub-grid, and the FULL unwrap k-fields of both maps (int8, exact up to one global
+    integer per map; they compress to runs), plus the residue count per map."""
+    import hashlib
+    out = {"versions": VERSIONS, "cases": np.array(list(LARGE_CASES))}
+    for tag, spec in LARGE_CASES.items():
+        n = spec["n"]
+        ref, frame = large_case_frames(spec)
+        sq = 0.001
+        r = run_pair(ref, frame, sq, height=1.0)
+        locs, thr = peak_locations(ref)
+        k = np.stack([kfield(w, p) for w, p in zip(r["wrapped"], r["phases"])])
+        assert np.abs(k).max() < 127
+        out.update({
+            f"{tag}_n": n, f"{tag}_seed": spec["seed"], f"{tag}_pairs": np.array(spec["pairs"], np.float64).reshape(-1, 2),
+            f"{tag}_ref_sha": hashlib.sha256(ref.tobytes()).hexdigest(),
+            f"{tag}_frame_sha": hashlib.sha256(frame.tobytes()).hexdigest(),
+            f"{tag}_peaks": r["peaks"], f"{tag}_cf": r["cf"], f"{tag}_radius": r["radius"],
+            f"{tag}_freqs": r["freqs"], f"{tag}_mask_count": r["mask_count"],
+            f"{tag}_blob_peaks": locs, f"{tag}_threshold": thr,
+            f"{tag}_height_sub": r["height"][::n // 256, ::n // 256].astype(np.float32),
+            f"{tag}_height_stats": stats(r["height"]),
+            f"{tag}_wrapped_sub": r["wrapped"][:, ::n // 128, ::n // 128],
+            f"{tag}_k": k.astype(np.int8),
+            f"{tag}_residues": np.array([residue_count(w) for w in r["wrapped"]]),
+        })
+        print("large", tag, r["peaks"].tolist(), r["cf"], "residues", out[f"{tag}_residues"].tolist(),
+              "k range", int(k.min()), int(k.max()), flush=True)
+    np.savez_compressed(os.path.join(OUT, "large.npz"), **out)
+
+
 def import_reference_analyze():
     """/root/reference/pydata/analyze.py, imported as the reference ships it.  Its module
     top level does `import cv2` (analyze.py:21), absent here; cv2 is used only by the
@@ -534,7 +600,7 @@ def make_analyze_ref():
 
 if __name__ == "__main__":
     which = sys.argv[1:] or ["real_pair", "real_df", "unwrap", "synthetic", "integrate", "val", "ingest",
-                             "bench_board", "analyze_ref", "spectrum"]
+                             "bench_board", "analyze_ref", "spectrum", "large"]
     if "real_pair" in which:
         make_real_pair()
     if "real_df" in which:
@@ -555,3 +621,5 @@ if __name__ == "__main__":
         make_analyze_ref()
     if "spectrum" in which:
         make_spectrum()
+    if "large" in which:
+        make_large()

@@ -138,6 +138,20 @@ def test_find_peak_locations_host_helper(golden):
     assert [p.tolist() for p in a] == [p.tolist() for p in b]
 
 
+def test_no_peaks_error_is_a_value_error():
+    """FCD_E_NOPEAKS surfaces as FcdNoPeaksError, an FcdError (RuntimeError) that is also a
+    ValueError, as the reference raises there (min() of an empty sequence, fourier.py:38);
+    other codes stay plain FcdErrors."""
+    from pyfcd import _lib
+    with pytest.raises(ValueError) as e:
+        _lib._check(_lib.FCD_E_NOPEAKS)
+    assert isinstance(e.value, _lib.FcdError) and isinstance(e.value, RuntimeError)
+    assert e.value.code == _lib.FCD_E_NOPEAKS
+    with pytest.raises(_lib.FcdError) as e2:
+        _lib._check(_lib.FCD_E_INVALID)
+    assert not isinstance(e2.value, ValueError)
+
+
 @pytest.mark.parametrize("total,world", [(256, 1), (256, 2), (8192, 8), (10, 4), (3, 8)])
 def test_shard_range_partitions(total, world):
     from pyfcd.dist import shard_range
@@ -161,6 +175,11 @@ def _gloo_worker(rank, world, port, q):
         local = torch.arange(a, b, dtype=torch.float32)[:, None, None].expand(b - a, 2, 3).contiguous()
         out = gather_stack(local, total)
         again = gather_stack(local, total)  # a second grouped batch on the same channels
+        try:  # fewer frames than ranks: refused on every rank before any communication
+            gather_stack(local[:1] if rank == 0 else local[:0], 1)
+            raise AssertionError("gather_stack accepted an empty shard")
+        except ValueError:
+            pass
         t = max_over_ranks(float(rank + 1))
         n = sum_over_ranks(float(b - a))
         if rank == 0:

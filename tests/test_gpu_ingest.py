@@ -314,13 +314,15 @@ def test_early_census_device_calls(df, monkeypatch):
     dev = torch.device("cuda", 0)
     fd, od = torch.from_numpy(frames).to(dev), torch.from_numpy(other).to(dev)
     monkeypatch.setenv("FCD_CHUNK_MAX", "3")
+    work = torch.cuda.Stream(dev)  # a caller stream: the calls stay asynchronous
     out = {}
     for early in ("0", "1"):
         monkeypatch.setenv("FCD_EARLY_CENSUS", early)
         eng = _engine(ref, sq)
         hd, ho = torch.empty_like(fd), torch.empty_like(od)
-        eng.process_device(fd.data_ptr(), len(frames), 1.0, True, hd.data_ptr())
-        eng.process_device(od.data_ptr(), len(other), 1.0, True, ho.data_ptr())
+        torch.cuda.synchronize()
+        eng.process_device(fd.data_ptr(), len(frames), 1.0, True, hd.data_ptr(), stream=work.cuda_stream)
+        eng.process_device(od.data_ptr(), len(other), 1.0, True, ho.data_ptr(), stream=work.cuda_stream)
         torch.cuda.synchronize()
         out[early] = (hd.cpu().numpy(), ho.cpu().numpy())
         del eng
@@ -346,9 +348,11 @@ def test_pending_device_call_orders_later_calls(df):
     want = torch.empty_like(fd)
     eng.process_device(fd.data_ptr(), len(frames), 1.0, True, want.data_ptr())
     torch.cuda.synchronize()
+    main = torch.cuda.Stream(dev)  # a caller stream: the calls return with work queued
     # (1) a new reference right after the call
     got = torch.empty_like(fd)
-    eng.process_device(fd.data_ptr(), len(frames), 1.0, True, got.data_ptr())
+    torch.cuda.synchronize()
+    eng.process_device(fd.data_ptr(), len(frames), 1.0, True, got.data_ptr(), stream=main.cuda_stream)
     eng.set_reference(board, 0.001)
     torch.cuda.synchronize()
     assert torch.equal(got, want)
@@ -356,8 +360,34 @@ def test_pending_device_call_orders_later_calls(df):
     eng.set_reference(ref, sq)
     side = torch.cuda.Stream(dev)
     got2, other = torch.empty_like(fd), torch.empty_like(fd)
-    eng.process_device(fd.data_ptr(), len(frames), 1.0, True, got2.data_ptr())
+    torch.cuda.synchronize()
+    eng.process_device(fd.data_ptr(), len(frames), 1.0, True, got2.data_ptr(), stream=main.cuda_stream)
     eng.process_device(fflip.data_ptr(), len(frames), 1.0, True, other.data_ptr(), stream=side.cuda_stream)
     torch.cuda.synchronize()
     assert torch.equal(got2, want)
     assert torch.equal(other.flip(0), want)
+
+
+def test_null_stream_call_returns_finished_heights(df):
+    """A device call without a caller stream (torch's default stream has cuda_stream == 0,
+    which arrives as NULL) runs on the context's own non-blocking stream, which no torch
+    stream is ordered with: the call must wait for its work, so torch ops on the default
+    stream right after it read finished heights (the early-census return used
+    to leave the integration queued there).  Back-to-back calls into fresh tensors, each
+    read on the default stream after only that stream's own synchronisation."""
+    import torch
+    from bench_data import displacement_numpy, warp_numpy
+    ref, sq = df["ref_u16"].astype(np.float32), float(df["square_size"])
+    frames = np.stack([warp_numpy(ref, *displacement_numpy(ref.shape[0], 21 + i)) for i in range(8)])
+    dev = torch.device("cuda", 0)
+    fd = torch.from_numpy(frames).to(dev)
+    eng = _engine(ref, sq)
+    want, _, _ = eng.process(frames, 1.0, unwrap=True, want_phases=False)
+    torch.cuda.synchronize()
+    for _ in range(3):
+        hd = torch.full_like(fd, float("nan"))
+        torch.cuda.current_stream(dev).synchronize()
+        eng.process_device(fd.data_ptr(), len(frames), 1.0, True, hd.data_ptr(),
+                           stream=torch.cuda.current_stream(dev).cuda_stream)
+        got = (hd * 1.0).cpu().numpy()  # a torch kernel + copy on the default stream
+        assert np.array_equal(got, want)

@@ -539,13 +539,9 @@ def dislocation_frames(n, rows, x0s, length=200):
     u_x = P / (2 pi) * (atan2(y - y0, x - x0) - atan2(y - y0, x - x0 - length))
     (P = 20 px, the board's period, so the cut between the cores is invisible): both
     carrier phases wind by +-2 pi around the two cores, a residue pair on row ~y0."""
-    from bench_data import checkerboard, warp_numpy
-    ref = checkerboard(n)
-    y, x = np.mgrid[0:n, 0:n].astype(np.float64)
-    frames = [warp_numpy(ref, np.zeros_like(x),
-                         (20.0 / TWOPI) * (np.arctan2(y - y0, x - x0) - np.arctan2(y - y0, x - x0 - length)))
-              for y0, x0 in zip(rows, x0s)]
-    return ref, np.stack(frames)
+    from bench_data import make_residue_frame
+    frames = [make_residue_frame(n, [(y0, x0)], length=length) for y0, x0 in zip(rows, x0s)]
+    return frames[0][0], np.stack([f for _, f in frames])
 
 
 def residue_rows(w):
@@ -785,17 +781,32 @@ def test_non_square_frames_vs_oracle(lib, golden, rows, cols):
     assert cf == cfo
     carriers, _ = fcd.compute_carriers(ref, sq)
     assert [c.pixels.tolist() for c in carriers] == [np.asarray(c.pixels).tolist() for c in ex["carriers"]]
-    assert rel_l2(h, ho) < 1e-4, rel_l2(h, ho)
+    # the camera crops carry residues: the engine's exact unwrap of its own wrapped phases
+    # equals the oracle's Herraez restatement of them on every pixel (up to the anchor)
+    eng = lib.engine_for(ref.shape)
+    _, w, k = eng.process(disp[None], 1.0, unwrap=True, want_phases=True)
+    for m in range(2):
+        _, ko = O.unwrap(w[0][m])
+        d = k[0][m].astype(np.int64) - ko
+        assert np.all(d == d.flat[0]), (m, int((d != d.flat[0]).sum()))
+    # and the same k-fields as the oracle's own float64 phases: heights at the synthetic bound
+    for m in range(2):
+        d, _ = const_offset(ph[m], po[m])
+        assert np.abs(d).max() < 1e-3, m
+    assert rel_l2(h, ho) < 1e-5, rel_l2(h, ho)
 
 
 def test_reference_without_carriers_raises(lib):
     """A reference with no checkerboard (flat / pure noise below the high-pass threshold
     structure) has no carrier peaks: the reference raises (min() of an empty sequence /
-    IndexError, fcd.py:68, fourier.py:38); the engine raises FcdError and keeps working."""
+    IndexError, fcd.py:68, fourier.py:38); the engine raises FcdNoPeaksError, a ValueError
+    as the reference's, and keeps working."""
+    from pyfcd import _lib
     from pyfcd.fcd import fcd
     flat = np.full((256, 256), 7.0, np.float32)
-    with pytest.raises(Exception):
+    with pytest.raises(ValueError) as e:
         fcd.compute_height_map(flat, flat, 0.001, height=1.0)
+    assert isinstance(e.value, _lib.FcdNoPeaksError)
     from bench_data import make_frames_numpy
     ref, frames = make_frames_numpy(256, 1, seed=2, rotate_deg=5.0)
     h, _, _ = fcd.compute_height_map(ref, frames[0], 0.001, height=1.0)

@@ -151,3 +151,29 @@ def test_pocketfft32_matches_scipy_digests(golden):
         assert P.mean_f32(img) == g[f"{name}_mean"], name
         spec = P.find_peaks_spectrum(img)
         assert hashlib.sha256(spec.tobytes()).hexdigest() == str(g[f"{name}_spec_sha"]), name
+
+
+@pytest.mark.parametrize("tag", ["s2048", "r2048"])
+def test_oracle_large_frames_vs_reference_run(golden, tag):
+    """The oracle at the c3 frame size against the reference's own run (large.npz): setup
+    bit-exact, the full unwrap k-fields of a residue-free and a residue frame exact up to
+    the anchor off the border ring, heights at float32-FFT tolerance (the GPU tests at
+    2048^2 / 4096^2 compare the engine with the same fixture directly)."""
+    import hashlib
+    from bench_data import make_residue_frame
+    g = golden("large")
+    n = int(g[f"{tag}_n"])
+    ref, frame = make_residue_frame(n, [tuple(p) for p in g[f"{tag}_pairs"]], seed=int(g[f"{tag}_seed"]),
+                                    rotate_deg=5.0, quantum=4096)
+    assert hashlib.sha256(frame.tobytes()).hexdigest() == str(g[f"{tag}_frame_sha"])
+    h, ph, cf, ex = O.compute_height_map(ref, frame, 0.001, height=1.0)
+    assert cf == float(g[f"{tag}_cf"])
+    assert np.array_equal([np.asarray(c.pixels) for c in ex["carriers"]], g[f"{tag}_peaks"])
+    assert [O.count_residues(w) for w in ex["wrapped"]] == list(g[f"{tag}_residues"])
+    for m in range(2):
+        d = ex["k"][m].astype(np.int64) - g[f"{tag}_k"][m]
+        inner = d[1:-1, 1:-1]
+        assert np.all(inner == inner.flat[0]), int((inner != inner.flat[0]).sum())
+    sub = n // 256
+    hs = h[::sub, ::sub]
+    assert np.linalg.norm(hs - g[f"{tag}_height_sub"]) / np.linalg.norm(g[f"{tag}_height_sub"]) < 1e-5

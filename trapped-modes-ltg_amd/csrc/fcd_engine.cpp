@@ -564,14 +564,19 @@ const float2* col_tw(fcd_ctx* c, int elems) {
 const float2* ic_tw(fcd_ctx* c) { return col_tw(c, fcdk::int_cols_elems(c->H)); }
 const float2* dc_tw(fcd_ctx* c) { return col_tw(c, fcdk::demod_cols_elems(c->H)); }
 
-// A device call may return with its integration kernels still queued on the caller's
-// stream (early census readback).  Work on that same stream is ordered after them; any
-// other entry point (another stream, the context's own stream, state changes such as a
-// new reference) first waits for them on the host, since it may touch the workspace and
-// tables those kernels read.
+// A device call on a caller stream may return with its integration kernels still queued
+// on that stream (early census readback).  A later device call on the same stream is
+// ordered after them on the device: the stream waits on the call's end event, which also
+// covers a stream the caller destroyed and whose handle the runtime handed out again.
+// Any other entry point (another stream, host pointers, the context's own stream, state
+// changes such as a new reference) first waits for them on the host, since it may touch
+// the workspace and tables those kernels read.
 void settle(fcd_ctx* c, hipStream_t same = nullptr) {
     if (!c->done_pending) return;
-    if (same && same == c->done_stream) return;
+    if (same && same == c->done_stream) {
+        HIPCHK(hipStreamWaitEvent(same, c->ev_done, 0));
+        return;
+    }
     HIPCHK(hipEventSynchronize(c->ev_done));
     c->done_pending = false;
 }
@@ -1320,7 +1325,9 @@ void stage_frames(fcd_ctx* c, const void* frames, int format, bool dev, const in
 int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int flags, double height, int unwrap,
                  float* height_out, float* wrapped_out, int32_t* k_out, void* stream) {
     check_ctx(c, false);
-    settle(c, c->pick(stream));  // the previous call's queued work: ordered if on this stream
+    // the previous call's queued work: ordered on the device for a device call on the same
+    // caller stream, waited for on the host otherwise
+    settle(c, flags == FCD_DEVICE_PTRS && stream ? static_cast<hipStream_t>(stream) : nullptr);
     if (!c->has_ref) throw FcdError(FCD_E_STATE, "no reference set");
     if (!frames || n_frames < 0) throw FcdError(FCD_E_INVALID, "bad frames");
     if (fcdk::raw_frame_bytes(format, c->H, c->W) == 0) throw FcdError(FCD_E_INVALID, "unknown frame format");
@@ -1573,16 +1580,27 @@ int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int f
 
 }  // namespace
 
+// Only a device call on a caller stream returns with work still queued: with a null
+// stream the work runs on the context's own (non-blocking) stream, which no caller stream
+// is ordered with, so the call waits for it before returning (fcd.h).
+static int process_entry(fcd_ctx* c, const void* frames, int format, int n_frames, int flags, double height, int unwrap,
+                  float* height_out, float* wrapped_out, int32_t* k_out, void* stream) {
+    const int rc = process_impl(c, frames, format, n_frames, flags, height, unwrap, height_out, wrapped_out, k_out,
+                                stream);
+    if (!stream) settle(c);
+    return rc;
+}
+
 FCD_API int fcd_process(fcd_ctx* c, const float* frames, int n_frames, int flags, double height, int unwrap,
                         float* height_out, float* wrapped_out, int32_t* k_out, void* stream) {
-    FCD_TRY(return process_impl(c, frames, FCD_FMT_F32, n_frames, flags, height, unwrap, height_out, wrapped_out,
-                                k_out, stream))
+    FCD_TRY(return process_entry(c, frames, FCD_FMT_F32, n_frames, flags, height, unwrap, height_out, wrapped_out,
+                                 k_out, stream))
 }
 
 FCD_API int fcd_process_raw(fcd_ctx* c, const void* frames, int format, int n_frames, int flags, double height,
                             int unwrap, float* height_out, float* wrapped_out, int32_t* k_out, void* stream) {
-    FCD_TRY(return process_impl(c, frames, format, n_frames, flags, height, unwrap, height_out, wrapped_out, k_out,
-                                stream))
+    FCD_TRY(return process_entry(c, frames, format, n_frames, flags, height, unwrap, height_out, wrapped_out, k_out,
+                                 stream))
 }
 
 FCD_API int fcd_frame_bytes(fcd_ctx* c, int format, int64_t* bytes) {

@@ -58,6 +58,12 @@ class FcdError(RuntimeError):
         self.code = code
 
 
+class FcdNoPeaksError(FcdError, ValueError):
+    """FCD_E_NOPEAKS: the reference has fewer than two carrier peaks.  Also a ValueError,
+    as the reference raises there (`min()` of an empty sequence, fourier.py:38), so a
+    caller catching ValueError keeps working."""
+
+
 _lib = None
 _lib_lock = threading.Lock()
 
@@ -110,7 +116,8 @@ def load_library(path=None):
 
 def _check(rc):
     if rc != FCD_OK:
-        raise FcdError(rc, load_library().fcd_last_error().decode(errors="replace"))
+        cls = FcdNoPeaksError if rc == FCD_E_NOPEAKS else FcdError
+        raise cls(rc, load_library().fcd_last_error().decode(errors="replace"))
 
 
 def _f32(a):
@@ -149,7 +156,8 @@ class Engine:
         self.ref_copy = None
         self.ref_square_size = None
         # what the context's carriers were built from, whichever call set them:
-        # (image of carrier 0, image of carrier 1, ((r0, c0), (r1, c1)), (radius0, radius1))
+        # (image of carrier 0, image of carrier 1, ((r0, c0), (r1, c1)), (radius0, radius1),
+        #  calibration factor)
         self.geometry = None
         self.explicit = False  # set by set_carriers (not by a find_peaks reference)
 
@@ -185,7 +193,8 @@ class Engine:
         self.ref_copy = ref.copy()
         self.ref_square_size = float(square_size)
         self.explicit = False
-        self.geometry = (self.ref_copy, self.ref_copy, _peaks_of(info), (info.radius, info.radius))
+        self.geometry = (self.ref_copy, self.ref_copy, _peaks_of(info), (info.radius, info.radius),
+                         info.calibration_factor)
         return info
 
     def set_carriers(self, ref0, ref1, calibration_factor, peaks, radii):
@@ -210,16 +219,18 @@ class Engine:
         self.explicit = True
         c0 = r0.copy()
         c1 = c0 if r1 is r0 else r1.copy()
-        self.geometry = (c0, c1, _peaks_of(info), (float(rad[0]), float(rad[1])))
+        self.geometry = (c0, c1, _peaks_of(info), (float(rad[0]), float(rad[1])), float(calibration_factor))
         return info
 
-    def holds_carriers(self, ref0, ref1, peaks, radii):
-        """True if the context's carriers were built from these images and this geometry."""
+    def holds_carriers(self, ref0, ref1, peaks, radii, calibration_factor):
+        """True if the context's carriers were built from these images, this geometry and
+        this calibration factor (the phases depend on mask and ccsgn only, but the
+        context's info -- calibration factor, frequencies -- must describe these carriers)."""
         if self.geometry is None:
             return False
-        g0, g1, gp, gr = self.geometry
+        g0, g1, gp, gr, gcf = self.geometry
         pk = tuple(tuple(int(v) for v in p) for p in peaks)
-        if pk != gp or tuple(float(r) for r in radii) != gr:
+        if pk != gp or tuple(float(r) for r in radii) != gr or float(calibration_factor) != gcf:
             return False
         return _same_image(ref0, g0) and _same_image(ref1, g1)
 

@@ -88,11 +88,15 @@ def gather_stack(local, total_frames):
     if not (dist.is_available() and dist.is_initialized()):
         return local
     rank, world = dist.get_rank(), dist.get_world_size()
+    if total_frames < world:
+        # an empty shard would leave its rank out of the grouped send/recv; on RCCL every
+        # rank must enter a group's first point-to-point batch
+        raise ValueError(f"gather_stack: {total_frames} frames over {world} ranks leaves a rank without frames")
     a0, b0 = shard_range(total_frames, rank, world)
     if local.shape[0] != b0 - a0:
         raise ValueError(f"rank {rank}: shard of {local.shape[0]} frames, expected {b0 - a0}")
     if rank != 0:
-        ops = [dist.P2POp(dist.isend, local.contiguous(), 0)] if b0 > a0 else []
+        ops = [dist.P2POp(dist.isend, local.contiguous(), 0)]
         out = None
     else:
         out = torch.empty((total_frames,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
@@ -100,9 +104,7 @@ def gather_stack(local, total_frames):
         ops = []
         for r in range(1, world):
             a, b = shard_range(total_frames, r, world)
-            if b > a:
-                ops.append(dist.P2POp(dist.irecv, out[a:b], r))
-    if ops:
-        for w in dist.batch_isend_irecv(ops):
-            w.wait()
+            ops.append(dist.P2POp(dist.irecv, out[a:b], r))
+    for w in dist.batch_isend_irecv(ops):
+        w.wait()
     return out

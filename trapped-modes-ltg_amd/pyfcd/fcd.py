@@ -159,7 +159,7 @@ class fcd:
         eng = _lib.engine_for(spec.shape[-2:])
         peaks = [(int(c.pixels[0]), int(c.pixels[1])) for c in (c0, c1)]
         radii = (float(c0.radius), float(c1.radius))
-        if not eng.holds_carriers(c0._reference, c1._reference, peaks, radii):
+        if not eng.holds_carriers(c0._reference, c1._reference, peaks, radii, c0._calibration_factor):
             eng.set_carriers(c0._reference, c1._reference, c0._calibration_factor, peaks, radii)
         wrapped, k = eng.phases_from_spectrum(spec, unwrap=unwrap)
         phases = wrapped[0].astype(np.float64)
@@ -182,11 +182,14 @@ class fcd:
 
     @staticmethod
     def fft_peaks(image):
-        """Plot |FFT| with the detected blob peaks and the chosen carriers (fcd.py:141-175)."""
+        """Plot |FFT| with the detected blob peaks and the chosen carriers (fcd.py:141-175).
+
+        The picks come from fcd_find_peaks, which leaves the engine's reference (and so the
+        next compute_height_map's cached carriers) untouched."""
         import matplotlib.pyplot as plt
         img = np.asarray(image)
         eng = _lib.engine_for(img.shape)
-        info = eng.set_reference(img, 1.0)
+        info = eng.find_peaks(img, 1.0)[0]
         spec = np.fft.fftshift(np.abs(eng.fft2(img - np.mean(img))))
         fig, ax = plt.subplots()
         ax.imshow(np.log1p(spec), origin="lower", cmap="magma")
