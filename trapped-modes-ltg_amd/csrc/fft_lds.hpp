@@ -16,13 +16,12 @@
 
 namespace fcdk {
 
-#ifndef FCD_PACKED
-#define FCD_PACKED 1  // complex arithmetic on packed-FP32 VALU ops (v_pk_add/mul/fma_f32: two lanes of work per op)
-#endif
+// Complex arithmetic on packed-FP32 VALU ops (v_pk_add/mul/fma_f32: two lanes of work
+// per op; on gfx950 a packed op issues at half the rate of a plain one, so this saves
+// instructions, not issue time).
 typedef float fv2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ fv2 pv(float2 a) { return fv2{a.x, a.y}; }
 __device__ __forceinline__ float2 vp(fv2 v) { return make_float2(v.x, v.y); }
-#if FCD_PACKED
 // The swaps and sign flips of complex products and of +-i multiplications are
 // VOP3P operand modifiers (op_sel / op_sel_hi / neg_lo / neg_hi); the compiler
 // does not fold a lane swap into them, so those forms are written out
@@ -67,30 +66,13 @@ __device__ __forceinline__ float2 cmulmi(float2 a) {
     asm("v_pk_add_f32 %0, 0, %1 op_sel:[0,1] op_sel_hi:[0,0] neg_hi:[0,1]" : "=v"(r) : "v"(pv(a)));
     return vp(r);
 }
-#else
-__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
-__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
-__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
-    return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
-}
-__device__ __forceinline__ float2 cmulc(float2 a, float2 b) {
-    return make_float2(a.x * b.x + a.y * b.y, a.y * b.x - a.x * b.y);
-}
-__device__ __forceinline__ float2 caddi(float2 a, float2 b) { return make_float2(a.x - b.y, a.y + b.x); }
-__device__ __forceinline__ float2 csubi(float2 a, float2 b) { return make_float2(a.x + b.y, a.y - b.x); }
-__device__ __forceinline__ float2 cmuli(float2 a) { return make_float2(-a.y, a.x); }
-__device__ __forceinline__ float2 cmulmi(float2 a) { return make_float2(a.y, -a.x); }
-#endif
-#ifndef FCD_NT_STORES
-#define FCD_NT_STORES 1  // streaming (nt) stores for outputs no kernel re-reads soon
-#endif
 // Streaming store: the line is not kept in L2 / the Infinity Cache, so a large
 // output stream does not evict the small inputs every frame re-reads.
 __device__ __forceinline__ void st_stream(float* p, float v) {
-    if constexpr (FCD_NT_STORES) __builtin_nontemporal_store(v, p); else *p = v;
+    __builtin_nontemporal_store(v, p);
 }
 __device__ __forceinline__ void st_stream(float2* p, float2 v) {
-    if constexpr (FCD_NT_STORES) __builtin_nontemporal_store(pv(v), reinterpret_cast<fv2*>(p)); else *p = v;
+    __builtin_nontemporal_store(pv(v), reinterpret_cast<fv2*>(p));
 }
 
 // a * w (forward) or a * conj(w) (inverse) for a forward twiddle w
@@ -177,12 +159,8 @@ __device__ __forceinline__ float2 twc(float2 v) {
     } else {
         const float c = kC16[m];
         const float s = INV ? kS16[m] : -kS16[m];
-#if FCD_PACKED
         const fv2 V = pv(v);
         return vp(__builtin_elementwise_fma(V.yy, fv2{-s, c}, V.xx * fv2{c, s}));
-#else
-        return make_float2(v.x * c - v.y * s, v.x * s + v.y * c);
-#endif
     }
 }
 

@@ -356,88 +356,47 @@ __host__ __device__ constexpr float atan_coef(int i) {
 }
 static_assert(kAtanN >= 7 && kAtanN <= 9, "FCD_ATAN_TERMS: 7, 8 or 9");
 
-// Reduction of atan2 (FCD_ATAN_FORM):
-//  0: octant form  -- r = min(|x|,|y|) / max(|x|,|y|) in [0, 1], atan(r) = r P(r^2), then
-//     pi/2 - a where |y| > |x| and pi - a where x < 0 (two compare / select pairs);
-//  1: quadrant form -- r = (|y| - |x|) / (|y| + |x|) in [-1, 1], the first-quadrant angle
-//     pi/4 + r P(r^2) (the same odd polynomial: atan is odd, so the fit on [0, 1] holds on
-//     [-1, 1]), then pi - a where x < 0.  One compare / select pair less, and the zero
-//     guard is the legacy multiply (0 * rcp(0) = 0) instead of a clamp of the divisor.
-//     Same f32 error (max 3.3e-7 vs 3.2e-7 rad, rms 7.8e-8 either way, over 4 M random
-//     angles at magnitudes e^-20 .. e^20); atan2(0, 0) = pi/4 instead of 0, which no
-//     phase path depends on: theta and the frame phases of a path use the same form, so
-//     a frame equal to the reference still gives exactly 0.
-#ifndef FCD_ATAN_FORM
-#define FCD_ATAN_FORM 1
-#endif
+// Reduction of atan2, the quadrant form: r = (|y| - |x|) / (|y| + |x|) in [-1, 1], the
+// first-quadrant angle pi/4 + r P(r^2) (the same odd polynomial: atan is odd, so the fit
+// on [0, 1] holds on [-1, 1]), then pi - a where x < 0.  Against the octant form (r =
+// min / max in [0, 1], then pi/2 - a where |y| > |x| and pi - a where x < 0) one compare /
+// select pair less, and the zero guard is the legacy multiply (0 * rcp(0) = 0) instead of
+// a clamp of the divisor.  Same f32 error (max 3.3e-7 vs 3.2e-7 rad, rms 7.8e-8 either
+// way, over 4 M random angles at magnitudes e^-20 .. e^20); atan2(0, 0) = pi/4 instead of
+// 0, which no phase path depends on: theta and the frame phases use the same form, so a
+// frame equal to the reference still gives exactly 0.  (Fused 1024 kernel 5.87 -> 5.82
+// us/frame, r03s.)
 // v_mul_legacy_f32: 0 * x = 0 for every x, inf and NaN included (no clang builtin)
 extern "C" __device__ float fmul_legacy(float, float) __asm("llvm.amdgcn.fmul.legacy");
 
-// atan2(y, x) in f32 (atan_coef after the octant reduction, v_rcp_f32 division);
-// atan2(0, 0) = 0, like atan2f.  About 20 VALU operations.
+// atan2(y, x) in f32 (atan_coef after the quadrant reduction, v_rcp_f32 division).
+// About 20 VALU operations.
 __device__ __forceinline__ float fast_atan2(float y, float x) {
-#if FCD_ATAN_FORM == 1
-    {
-        const float r = fmul_legacy(fabsf(y) - fabsf(x), __builtin_amdgcn_rcpf(fabsf(y) + fabsf(x)));
-        const float s = r * r;
-        float p = atan_coef(0);
-#pragma unroll
-        for (int c = 1; c < kAtanN; ++c) p = fmaf(p, s, atan_coef(c));
-        float a = fmaf(r, p, 0.785398163397448310f);
-        a = x < 0.f ? 3.14159265358979324f - a : a;
-        return copysignf(a, y);
-    }
-#else
-    const float ax = fabsf(x), ay = fabsf(y);
-    const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
-    const float r = mx > 0.f ? mn * __builtin_amdgcn_rcpf(mx) : 0.f;
+    const float r = fmul_legacy(fabsf(y) - fabsf(x), __builtin_amdgcn_rcpf(fabsf(y) + fabsf(x)));
     const float s = r * r;
     float p = atan_coef(0);
 #pragma unroll
     for (int c = 1; c < kAtanN; ++c) p = fmaf(p, s, atan_coef(c));
-    float a = r * p;
-    a = ay > ax ? 1.57079632679489662f - a : a;
+    float a = fmaf(r, p, 0.785398163397448310f);
     a = x < 0.f ? 3.14159265358979324f - a : a;
     return copysignf(a, y);
-#endif
 }
 
-// fast_atan2 of two values at once: the reduction's divide, square,
-// polynomial and final product run as packed-FP32 ops (v_pk_mul / v_pk_fma: both
-// values per instruction), the octant fix-ups per value; the zero-magnitude
-// guard is a clamp of the divisor to FLT_MIN (0 * rcp(FLT_MIN) = 0) instead of
-// a select.  Same polynomial and operation order as fast_atan2 per value:
-// 38 VALU ops per pair instead of 60 (gfx950 ISA count).
+// fast_atan2 of two values at once: the reduction's square, polynomial and final
+// product run as packed-FP32 ops (v_pk_mul / v_pk_fma: both values per instruction), the
+// quadrant fix-ups per value.  Same polynomial and operation order as fast_atan2 per
+// value.
 __device__ __forceinline__ fv2 fast_atan2_pk(fv2 y, fv2 x) {
-#if FCD_ATAN_FORM == 1
-    {
-        const fv2 r = {fmul_legacy(fabsf(y.x) - fabsf(x.x), __builtin_amdgcn_rcpf(fabsf(y.x) + fabsf(x.x))),
-                       fmul_legacy(fabsf(y.y) - fabsf(x.y), __builtin_amdgcn_rcpf(fabsf(y.y) + fabsf(x.y)))};
-        const fv2 s = r * r;
-        fv2 p = fv2{atan_coef(0), atan_coef(0)};
-#pragma unroll
-        for (int c = 1; c < kAtanN; ++c) p = p * s + atan_coef(c);
-        fv2 a = r * p + 0.785398163397448310f;
-        a.x = x.x < 0.f ? 3.14159265358979324f - a.x : a.x;
-        a.y = x.y < 0.f ? 3.14159265358979324f - a.y : a.y;
-        return fv2{copysignf(a.x, y.x), copysignf(a.y, y.y)};
-    }
-#else
-    const float mx0 = fmaxf(fmaxf(fabsf(x.x), fabsf(y.x)), 1.17549435e-38f);
-    const float mx1 = fmaxf(fmaxf(fabsf(x.y), fabsf(y.y)), 1.17549435e-38f);
-    const fv2 mn = {fminf(fabsf(x.x), fabsf(y.x)), fminf(fabsf(x.y), fabsf(y.y))};
-    const fv2 r = mn * fv2{__builtin_amdgcn_rcpf(mx0), __builtin_amdgcn_rcpf(mx1)};
+    const fv2 r = {fmul_legacy(fabsf(y.x) - fabsf(x.x), __builtin_amdgcn_rcpf(fabsf(y.x) + fabsf(x.x))),
+                   fmul_legacy(fabsf(y.y) - fabsf(x.y), __builtin_amdgcn_rcpf(fabsf(y.y) + fabsf(x.y)))};
     const fv2 s = r * r;
     fv2 p = fv2{atan_coef(0), atan_coef(0)};
 #pragma unroll
     for (int c = 1; c < kAtanN; ++c) p = p * s + atan_coef(c);
-    fv2 a = r * p;
-    a.x = fabsf(y.x) > fabsf(x.x) ? 1.57079632679489662f - a.x : a.x;
-    a.y = fabsf(y.y) > fabsf(x.y) ? 1.57079632679489662f - a.y : a.y;
+    fv2 a = r * p + 0.785398163397448310f;
     a.x = x.x < 0.f ? 3.14159265358979324f - a.x : a.x;
     a.y = x.y < 0.f ? 3.14159265358979324f - a.y : a.y;
     return fv2{copysignf(a.x, y.x), copysignf(a.y, y.y)};
-#endif
 }
 
 // wrap(theta - atan2(u.y, u.x)) for two pixels (u0, u1): d - 2 pi rint(d / 2 pi),
@@ -458,7 +417,6 @@ __device__ __forceinline__ fv2 wrapped_phase_pk(fv2 theta, float2 u0, float2 u1)
 template <int NP>
 __device__ __forceinline__ void wrapped_phase_pkn(const fv2 (&theta)[NP], const float2 (&u)[2 * NP], fv2 (&out)[NP]) {
     fv2 r[NP], s[NP], p[NP];
-#if FCD_ATAN_FORM == 1
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
         const float2 u0 = u[2 * k], u1 = u[2 * k + 1];
@@ -483,36 +441,6 @@ __device__ __forceinline__ void wrapped_phase_pkn(const fv2 (&theta)[NP], const 
         const fv2 q = d * 0.159154943091895f;
         out[k] = fv2{rintf(q.x), rintf(q.y)} * -6.28318530717959f + d;
     }
-#else
-#pragma unroll
-    for (int k = 0; k < NP; ++k) {
-        const float2 u0 = u[2 * k], u1 = u[2 * k + 1];
-        const float mx0 = fmaxf(fmaxf(fabsf(u0.x), fabsf(u0.y)), 1.17549435e-38f);
-        const float mx1 = fmaxf(fmaxf(fabsf(u1.x), fabsf(u1.y)), 1.17549435e-38f);
-        const fv2 mn = {fminf(fabsf(u0.x), fabsf(u0.y)), fminf(fabsf(u1.x), fabsf(u1.y))};
-        r[k] = mn * fv2{__builtin_amdgcn_rcpf(mx0), __builtin_amdgcn_rcpf(mx1)};
-    }
-#pragma unroll
-    for (int k = 0; k < NP; ++k) s[k] = r[k] * r[k];
-#pragma unroll
-    for (int k = 0; k < NP; ++k) p[k] = s[k] * atan_coef(0) + atan_coef(1);
-#pragma unroll
-    for (int c = 2; c < kAtanN; ++c)
-#pragma unroll
-        for (int k = 0; k < NP; ++k) p[k] = p[k] * s[k] + atan_coef(c);
-#pragma unroll
-    for (int k = 0; k < NP; ++k) {
-        const float2 u0 = u[2 * k], u1 = u[2 * k + 1];
-        fv2 a = r[k] * p[k];
-        a.x = fabsf(u0.y) > fabsf(u0.x) ? 1.57079632679489662f - a.x : a.x;
-        a.y = fabsf(u1.y) > fabsf(u1.x) ? 1.57079632679489662f - a.y : a.y;
-        a.x = u0.x < 0.f ? 3.14159265358979324f - a.x : a.x;
-        a.y = u1.x < 0.f ? 3.14159265358979324f - a.y : a.y;
-        const fv2 d = theta[k] - fv2{copysignf(a.x, u0.y), copysignf(a.y, u1.y)};
-        const fv2 q = d * 0.159154943091895f;
-        out[k] = fv2{rintf(q.x), rintf(q.y)} * -6.28318530717959f + d;
-    }
-#endif
 }
 
 }  // namespace fcdk

@@ -54,27 +54,10 @@ struct DemodTables {
 #ifndef FCD_ZT_1024
 #define FCD_ZT_1024 8
 #endif
-// FCD_ZT_PAIRED=1: Zt's column order inside a tile pairs every column with its
-// Hermitian mirror (physical column j = 2p + h holds column p (h = 0) and W - p (h = 1)
-// for 0 < p < W/2, columns 0 / W/2 at j = 0 / 1), so with 8-row tiles a 128-byte line is
-// exactly the (column, mirror) pair one k_int_cols item reads.  The natural order (0,
-// the default) shares each line with the neighbouring column and reads 1.42x the
-// compulsory Zt bytes (r03m PMC), yet is the faster one: kbench r03k1, paired vs
-// natural, int_cols 3.02 vs 2.86, int_rows k1 4.47 vs 4.33, phase_rows 5.92 vs 5.86
-// us/frame (heights bit-identical either way).
-#ifndef FCD_ZT_PAIRED
-#define FCD_ZT_PAIRED 0
-#endif
-__host__ __device__ inline int zt_col(int c, int W) {
-    if (!FCD_ZT_PAIRED) return c;
-    const int h = W >> 1;
-    return c == 0 ? 0 : (c == h ? 1 : (c < h ? 2 * c : 2 * (W - c) + 1));
-}
-__host__ __device__ inline int zt_col_inv(int j, int W) {
-    if (!FCD_ZT_PAIRED) return j;
-    const int p = j >> 1, h = j & 1;
-    return p == 0 ? (h ? W >> 1 : 0) : (h ? W - p : p);
-}
+// Zt keeps the natural column order inside a tile.  (A mirror-paired order, every
+// column next to its Hermitian mirror so that a 128-byte line is exactly the pair one
+// k_int_cols item reads, cut Zt reads by 30 % but measured slower: kbench r03k1, int_cols
+// 3.02 vs 2.86, int_rows 4.47 vs 4.33, phase_rows 5.92 vs 5.86 us/frame)
 bool fft_size_supported(int n);
 // frame ingest (kernels_ingest.hip): raw samples (FCD_FMT_*) -> float32 frames
 size_t raw_frame_bytes(int format, int H, int W);

@@ -52,10 +52,6 @@ namespace {
 #define FCD_BAND_THREADS_2048 512  // workgroup size of the 2048-point band kernel (256: 25.1, 512: 22.5, 768: 23.4 us/frame, kbench r01ar)
 #endif
 
-#ifndef FCD_BAND_FMAJOR
-#define FCD_BAND_FMAJOR 1  // item order frame-fastest: concurrent blocks share the (carrier, row tile) and its theta
-#endif
-
 #ifndef FCD_BAND_ABL
 #define FCD_BAND_ABL 0  // diagnostic ablations only (wrong results): 1 no transform, 2 no atan2, 4 no LDS stage reads
 #endif
@@ -121,9 +117,9 @@ __global__ __launch_bounds__((BPCfg<W, B>::THREADS), FCD_BAND_WAVES) void k_band
     // item -> (frame, carrier, row tile).  Frame-fastest order: the blocks running
     // at one time work on the same (carrier, row tile) of different frames, so the
     // tile's reference angles (64 KB) are read from HBM once and then hit in L2.
-    auto item_f = [&](int blk) { return FCD_BAND_FMAJOR ? blk % nb : blk / (2 * rbs); };
-    auto item_c = [&](int blk) { return FCD_BAND_FMAJOR ? (blk / nb) % 2 : (blk / rbs) % 2; };
-    auto item_rb = [&](int blk) { return FCD_BAND_FMAJOR ? blk / (2 * nb) : blk % rbs; };
+    auto item_f = [&](int blk) { return blk % nb; };
+    auto item_c = [&](int blk) { return (blk / nb) % 2; };
+    auto item_rb = [&](int blk) { return blk / (2 * nb); };
     // Tile staging is software-pipelined: the next item's tile is loaded into
     // registers (SPT values per thread, all loads in flight at once) while
     // the current item's rows are transformed.

@@ -90,15 +90,9 @@ struct KCfg {
 #ifndef FCD_INTCOLS_WAVES_E16
 #define FCD_INTCOLS_WAVES_E16 2  // at 16 elements per lane (3: 168 VGPRs, 22 spilled, 2.81 -> 3.71 us/frame, kbench r03w3)
 #endif
-#ifndef FCD_INTCOLS_PREF_Y
-#define FCD_INTCOLS_PREF_Y 0
-#endif
-#ifndef FCD_INTCOLS_KY_LDS
-#define FCD_INTCOLS_KY_LDS 1  // k_int_cols reads ky_eff / ky^2 from LDS copies (0: from the global tables)
-#endif
-#ifndef FCD_INTCOLS_PREF_X
-#define FCD_INTCOLS_PREF_X 1
-#endif
+// k_int_cols prefetches the next item's column (PREF_X) always and its mirror column
+// (PREF_Y) at 4096 points (2 waves / SIMD either way there); it reads ky_eff / ky^2 from
+// LDS copies.
 #ifndef FCD_INTCOLS_QUADS
 #define FCD_INTCOLS_QUADS 1  // 4-row Zt tiles: sibling blocks on one XCD share each line's 4 columns
 #endif
@@ -110,41 +104,27 @@ struct KCfg {
 #ifndef FCD_DEMODCOLS_BLOCK
 #define FCD_DEMODCOLS_BLOCK 512
 #endif
-// k_demod_cols loads the next item's column during the current item's transforms
-// (1) or at the top of each item (0).
-#ifndef FCD_DEMODCOLS_PREF
-#define FCD_DEMODCOLS_PREF 1
-#endif
-// From FCD_DC_TW_GLOBAL_MIN points its twiddle table stays in global memory: the
+// From kDcTwGlobalMin points k_demod_cols' twiddle table stays in global memory: the
 // two exchange rows alone are 70 KB at 4096, so without the 32 KB copy two workgroups
 // fit per CU (16.9 -> 15.1 us/frame at 4096^2, kbench r03u).
-#ifndef FCD_DC_TW_GLOBAL_MIN
-#define FCD_DC_TW_GLOBAL_MIN 4096
-#endif
+constexpr int kDcTwGlobalMin = 4096;
 #ifndef FCD_DEMODCOLS_V16
 #define FCD_DEMODCOLS_V16 2
 #endif
 template <int N>
 struct DemodColsCfg : KCfg<N, (N <= 1024 ? FCD_DEMODCOLS_BLOCK : BLOCK), demod_cols_elems(N)> {
     static constexpr int V = N <= 1024 ? (demod_cols_elems(N) == 16 ? FCD_DEMODCOLS_V16 : 4) : ColWaves<N>::V;
-    static constexpr bool GTW = N >= FCD_DC_TW_GLOBAL_MIN;
+    static constexpr bool GTW = N >= kDcTwGlobalMin;
     static constexpr int NLEN = GTW ? 0 : N;
 };
 
-// k_int_cols at 2048 points in the lean form (FCD_INTCOLS_LEAN_2048): 128 VGPRs (no
-// prefetch of the next item's columns) and the row wavenumbers read from global memory,
-// so 4 four-wave workgroups fit per CU instead of 3 at 166 VGPRs.
-#ifndef FCD_INTCOLS_LEAN_2048
-#define FCD_INTCOLS_LEAN_2048 0
-#endif
+// (A lean 2048-point form without the prefetch and with the row wavenumbers from
+// global memory, 128 VGPRs for 4 workgroups per CU, measured 13.1 -> 13.6 us/frame, r03v.)
 template <int N>
 struct IntColsCfg : KCfg<N, FCD_INTCOLS_BLOCK, int_cols_elems(N)> {
-    static constexpr bool LEAN = N == 2048 && FCD_INTCOLS_LEAN_2048;
     // 16 elements per lane at 1024: 186 VGPRs, 2 waves / SIMD
-    static constexpr int V = N <= 1024 ? (int_cols_elems(N) == 16 ? FCD_INTCOLS_WAVES_E16 : FCD_INTCOLS_WAVES) : (LEAN ? 4 : ColWaves<N>::V);
-    static constexpr bool PREF_Y = LEAN ? false : (N >= 4096 ? true : FCD_INTCOLS_PREF_Y);  // 4096: 2 waves/SIMD either way
-    static constexpr bool PREF_X = LEAN ? false : FCD_INTCOLS_PREF_X;
-    static constexpr bool KY_LDS = FCD_INTCOLS_KY_LDS && !LEAN;
+    static constexpr int V = N <= 1024 ? (int_cols_elems(N) == 16 ? FCD_INTCOLS_WAVES_E16 : FCD_INTCOLS_WAVES) : ColWaves<N>::V;
+    static constexpr bool PREF_Y = N >= 4096;
 };
 
 // find_wrap(a, b) of the reference unwrapper with an f32 fast path:
@@ -168,15 +148,9 @@ __device__ __forceinline__ int fw_fast(float a, float b) {
 #define FCD_DR_HCREG 2
 #endif
 constexpr int DR_HCR = FCD_DR_HCREG;
-// Rows of FCD_DR_DIRECT_MIN points and more: each row pair's band values go straight
-// to Xb (16 bytes per column: the pair's two rows of the 16-row tile, so the tile's 8
-// pairs fill each 128-byte line in L2 one after another) instead of through a staged
-// [NC][16] block, whose 56 KB at 4096 points held the kernel to one workgroup per CU.
-#ifndef FCD_DR_DIRECT_MIN
-#define FCD_DR_DIRECT_MIN (1 << 30)  // off: at 4096 25.9 vs 26.0, at 2048 5.94 vs 5.66 us/frame but k_demod_cols +0.24 (kbench r03v)
-#endif
-template <int W>
-constexpr bool dr_direct() { return W >= FCD_DR_DIRECT_MIN; }
+// The band values leave through a staged [NC][16] block.  (Writing each row pair's
+// values straight to Xb instead, 16 bytes per column, measured 25.9 vs 26.0 us/frame at
+// 4096 and 5.94 vs 5.66 at 2048 but k_demod_cols +0.24 behind it, kbench r03v.)
 
 template <int W>
 __global__ __launch_bounds__(KCfg<W>::THREADS, FCD_MIN_WAVES) void k_demod_rows(const float* __restrict__ frames, int H, int nb,
@@ -223,25 +197,20 @@ __global__ __launch_bounds__(KCfg<W>::THREADS, FCD_MIN_WAVES) void k_demod_rows(
 #pragma unroll
             for (int q = 0; q < E; ++q) s[pad(t + TT * q)] = x[q];
             team_sync<W>();
-            float4* const xrow = reinterpret_cast<float4*>(Xb + (long)(blk / rbs) * H * NC + (long)(blk % rbs) * NC * TILE + 2 * pr);
             auto band = [&](int i, int hc) {
                 const float2 zk = s[pad(hc)], zm = s[pad((W - hc) & (W - 1))];
                 // X_a = (Z(k) + conj Z(-k)) / 2 ; X_b = (Z(k) - conj Z(-k)) / 2i
                 const float2 xa = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y));
                 const float2 xb = make_float2(0.5f * (zk.y + zm.y), -0.5f * (zk.x - zm.x));
-                if constexpr (dr_direct<W>()) {
-                    xrow[i * (TILE / 2)] = make_float4(xa.x, xa.y, xb.x, xb.y);  // tix(2 pr, i, NC)
-                } else {
-                    stage[i * (TILE + 1) + 2 * pr] = xa;
-                    stage[i * (TILE + 1) + 2 * pr + 1] = xb;
-                }
+                stage[i * (TILE + 1) + 2 * pr] = xa;
+                stage[i * (TILE + 1) + 2 * pr + 1] = xb;
             };
 #pragma unroll
             for (int k = 0; k < DR_HCR; ++k)
                 if (t + k * TT < NC) band(t + k * TT, hcr[k]);
             for (int i = t + DR_HCR * TT; i < NC; i += TT) band(i, T.hc[i]);
         }
-        if constexpr (!dr_direct<W>()) {
+        {
             const int f = blk / rbs, rb = blk % rbs;
             __syncthreads();
             float2* dst = Xb + (long)f * H * NC + (long)rb * NC * TILE;
@@ -274,8 +243,8 @@ __global__ __launch_bounds__(DemodColsCfg<H>::THREADS, DemodColsCfg<H>::V) void 
     static_assert(TT % TILE == 0, "row stride across whole tiles");
     const long xb_lane = (long)(t >> 4) * NC * TILE + (t & 15), xb_step = (long)TT * NC;
     const long ab_lane = (long)(t >> 4) * NCA * TILE + (t & 15), ab_step = (long)TT * NCA;
-#if FCD_DEMODCOLS_PREF
-    // the next item's column is loaded while the current one is transformed
+    // the next item's column is loaded while the current one is transformed (0.865 ->
+    // 0.84 us/frame against a load at the top of each item, kbench r02c1)
     float2 xn[E];
     auto fetch = [&](int it) {
         const int fi = it < items ? it / NC : 0, ii = it < items ? it % NC : 0;
@@ -284,21 +253,14 @@ __global__ __launch_bounds__(DemodColsCfg<H>::THREADS, DemodColsCfg<H>::V) void 
         for (int q = 0; q < E; ++q) xn[q] = src[q * xb_step];  // tix(t + TT q, ii, NC)
     };
     fetch(blockIdx.x * TEAMS + team);
-#endif
     for (int base = blockIdx.x * TEAMS; base < items; base += gridDim.x * TEAMS) {
         const int item = base + team;
         const bool valid = item < items;
         const int f = valid ? item / NC : 0, i = valid ? item % NC : 0;
         float2 x[E];
-#if FCD_DEMODCOLS_PREF
 #pragma unroll
         for (int q = 0; q < E; ++q) x[q] = xn[q];
         if (base + (int)gridDim.x * TEAMS < items) fetch(item + gridDim.x * TEAMS);
-#else
-        const float2* src = Xb + (long)f * H * NC + (long)i * TILE + xb_lane;
-#pragma unroll
-        for (int q = 0; q < E; ++q) x[q] = src[q * xb_step];  // tix(t + TT q, i, NC)
-#endif
         // the item's output count and first output (every column has 4 table slots),
         // read before the forward transform so that it hides their latency
         const int nout = valid ? T.nouts[i] : 0;
@@ -449,11 +411,9 @@ __global__ __launch_bounds__(IntColsCfg<H>::THREADS, IntColsCfg<H>::V) void k_in
     // the row wavenumber tables (ky_eff, ky^2) of every element, read per item: LDS copies
     float* const lky = reinterpret_cast<float*>(lds + TEAMS * C::ROW);
     float* const lky2 = lky + H;
-    if constexpr (C::KY_LDS) {
-        for (int i = threadIdx.x; i < H; i += C::THREADS) {
-            lky[i] = c.kye[i];
-            lky2[i] = c.ky2[i];
-        }
+    for (int i = threadIdx.x; i < H; i += C::THREADS) {
+        lky[i] = c.kye[i];
+        lky2[i] = c.ky2[i];
     }
     __syncthreads();
     const int NCH = W / 2 + 1;
@@ -472,7 +432,7 @@ __global__ __launch_bounds__(IntColsCfg<H>::THREADS, IntColsCfg<H>::V) void k_in
     float2 py[E], px[E];
     auto fetch_fc = [&](int f, int col, bool mirror, float2 (&v)[E]) {
         const int cc = mirror ? (W - col) & (W - 1) : col;
-        const float2* src = Zt + (long)f * H * W + ((long)zt_col(cc, W) << zts) + zt_lane;
+        const float2* src = Zt + (long)f * H * W + ((long)cc << zts) + zt_lane;
 #pragma unroll
         for (int q = 0; q < E; ++q) v[q] = src[q * zt_step];
     };
@@ -514,7 +474,7 @@ __global__ __launch_bounds__(IntColsCfg<H>::THREADS, IntColsCfg<H>::V) void k_in
     };
     auto fetch = [&](int code) {
         if constexpr (C::PREF_Y) fetch_col(code, true, py);
-        if constexpr (C::PREF_X) fetch_col(code, false, px);
+        fetch_col(code, false, px);
     };
     fetch(c0 + team * cstep);
     for (int base = c0; base < cend; base += TEAMS * cstep) {
@@ -527,7 +487,6 @@ __global__ __launch_bounds__(IntColsCfg<H>::THREADS, IntColsCfg<H>::V) void k_in
         // of the Hermitian split sit in the same lane and slot (no mirror exchange).
         float2 x[E], y[E];
         if constexpr (!C::PREF_Y) fetch_col(item, true, py);
-        if constexpr (!C::PREF_X) fetch_col(item, false, px);
 #pragma unroll
         for (int q = 0; q < E; ++q) {
             y[q] = py[q];
@@ -560,8 +519,8 @@ __global__ __launch_bounds__(IntColsCfg<H>::THREADS, IntColsCfg<H>::V) void k_in
             // 2 Phi0 and 2 Phi1 (the halves go into the multiplier's scale)
             const float2 f0 = make_float2(z.x + zm.x, z.y - zm.y);
             const float2 f1 = make_float2(z.y + zm.y, zm.x - z.x);
-            const float ky = C::KY_LDS ? lky[i] : c.kye[i];
-            float k2 = kx2 + (C::KY_LDS ? lky2[i] : c.ky2[i]);
+            const float ky = lky[i];
+            float k2 = kx2 + lky2[i];
             if (i == 0 && col == 0) k2 = 1.f;
             // 1 / k^2 by the hardware reciprocal (1 ulp) instead of an IEEE division
             // (a 10-instruction sequence per element)
@@ -595,13 +554,10 @@ struct C2RCfg {
     static constexpr int TT = Sched<W>::TT;
     static constexpr int E = Sched<W>::E;
     static constexpr int RPW = c2r_rpw(W);
-    // staged block pitch: RPW + 1 (odd, conflict-free); FCD_C2R_PAD=0 leaves the 2- and
-    // 4-row blocks of the wide rows unpadded (a third / fifth less LDS, but still one
-    // workgroup per CU at 4096 and slower: 42.0 -> 43.4 us/frame, kbench r03u)
-#ifndef FCD_C2R_PAD
-#define FCD_C2R_PAD 1
-#endif
-    static constexpr int SP = (RPW == TILE || FCD_C2R_PAD) ? RPW + 1 : RPW;
+    // staged block pitch: RPW + 1 (odd, conflict-free; the 2- and 4-row blocks of the
+    // wide rows unpadded have a third / fifth less LDS but still one workgroup per CU at
+    // 4096 and were slower: 42.0 -> 43.4 us/frame, kbench r03u)
+    static constexpr int SP = RPW + 1;
     static constexpr int THREADS = (RPW / 2) * TT < 1024 ? ((RPW / 2) * TT > TT ? (RPW / 2) * TT : TT) : 1024;
     static constexpr int TEAMS = THREADS / TT;
     static constexpr int ROW = padded_len(W);
@@ -732,7 +688,7 @@ template <int W>
 static void launch_demod_rows(const float* frames, int H, int nb, const DemodTables& T, float2* Xb, const float2* tw,
                               hipStream_t s) {
     using C = KCfg<W>;
-    const size_t lds = (size_t)C::NLEN * 8 + (size_t)C::TEAMS * C::ROW * 8 + (dr_direct<W>() ? 0 : (size_t)T.NC * (TILE + 1) * 8);
+    const size_t lds = (size_t)C::NLEN * 8 + (size_t)C::TEAMS * C::ROW * 8 + (size_t)T.NC * (TILE + 1) * 8;
     set_lds(k_demod_rows<W>, lds);
     const int grid = grid_for((long)nb * (H / TILE), 4);
     hipLaunchKernelGGL(k_demod_rows<W>, dim3(grid), dim3(C::THREADS), lds, s, frames, H, nb, T, Xb, tw);
@@ -775,20 +731,18 @@ static void launch_int_rows(int kmode, const float* w, const int* colk, const in
     const size_t lds = C::LDS_BYTES;
     int grid = int_rows_grid<W>(H, nb);
     const long items = (long)nb * (H / C::ZT);
-    const int per = (int)((items + grid - 1) / grid);  // KMODE 1 with C::SEAM: tiles per block, a contiguous range
+    const int per = (int)((items + grid - 1) / grid);  // KMODE 1: tiles per block, a contiguous range
     if (kmode == 0) {
         set_lds(k_int_rows2<W, 0>, lds);
         hipLaunchKernelGGL((k_int_rows2<W, 0>), dim3(grid), dim3(C::THREADS), lds, s, w, colk, kin, kout, rescount, H,
                            nb, Zt, tw, seam, per);
     } else if (kmode == 1) {
-        if (C::SEAM) {
-            if (!seam) throw std::runtime_error("int_rows: the seam census needs a seam buffer");
-            grid = (int)((items + per - 1) / per);
-        }
+        if (!seam) throw std::runtime_error("int_rows: the seam census needs a seam buffer");
+        grid = (int)((items + per - 1) / per);
         set_lds(k_int_rows2<W, 1>, lds);
         hipLaunchKernelGGL((k_int_rows2<W, 1>), dim3(grid), dim3(C::THREADS), lds, s, w, colk, kin, kout, rescount, H,
                            nb, Zt, tw, seam, per);
-        if (C::SEAM && grid > 1) {
+        if (grid > 1) {
             FCD_CHECK_LAUNCH();
             hipLaunchKernelGGL(k_ir_seam_check<W>, dim3((unsigned)((grid - 1 + 3) / 4)), dim3(256), 0, s, seam, H, nb,
                                per, grid, rescount);
@@ -810,7 +764,7 @@ template <int H>
 static void launch_int_cols(const float2* Zt, int W, int nb, const IntegCoef& c, float2* Ht, const float2* tw,
                             hipStream_t s, const int* colk) {
     using C = IntColsCfg<H>;
-    const size_t lds = (size_t)C::NLEN * 8 + (size_t)C::TEAMS * C::ROW * 8 + (C::KY_LDS ? (size_t)H * 8 : 0);
+    const size_t lds = (size_t)C::NLEN * 8 + (size_t)C::TEAMS * C::ROW * 8 + (size_t)H * 8;
     set_lds(k_int_cols<H>, lds);
     const int grid = grid_for(((long)nb * (W / 2 + 1) + C::TEAMS - 1) / C::TEAMS, 4);
     const int zt = zt_rows(W);

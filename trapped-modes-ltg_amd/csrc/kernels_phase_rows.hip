@@ -47,15 +47,6 @@ constexpr int PR_B = 128;             // band window
 #define FCD_PR_ROWS 8
 #endif
 constexpr int PR_ROWS = FCD_PR_ROWS;  // rows per tile (one wave each)
-#ifndef FCD_PR_PAIRED
-#define FCD_PR_PAIRED 1  // both carriers' band transforms in lockstep
-#endif
-#ifndef FCD_PR_THETA_LATE
-#define FCD_PR_THETA_LATE 1  // paired path: reference angles loaded after the transforms (register pressure)
-#endif
-#ifndef FCD_PR_PKUNWRAP
-#define FCD_PR_PKUNWRAP 1  // unwrap / census on packed pairs of both maps (0: the integer-code form)
-#endif
 #if !defined(FCD_DIAGNOSTIC) && defined(FCD_PR_ABL)
 #error "FCD_PR_ABL ablations are diagnostic-only: build with -DFCD_DIAGNOSTIC"
 #endif
@@ -64,11 +55,9 @@ constexpr int PR_ROWS = FCD_PR_ROWS;  // rows per tile (one wave each)
                       // 4 no band transforms, 8 no atan2 / wrap, 16 no z-row FFT
 #endif
 #ifndef FCD_PR_ATAN_N
-#define FCD_PR_ATAN_N 2  // pixel pairs per carrier in one interleaved atan2 group (0: the per-pair form)
+#define FCD_PR_ATAN_N 2  // pixel pairs per carrier in one interleaved atan2 group
 #endif
-#ifndef FCD_PR_ATAN_GROUP
-#define FCD_PR_ATAN_GROUP 4  // atan2 chains per scheduling group (0: unbounded)
-#endif
+static_assert(FCD_PR_ATAN_N > 0 && 16 % (2 * FCD_PR_ATAN_N) == 0, "atan2 groups tile the 16 values");
 constexpr int PR_ZT = FCD_ZT_1024;    // Zt tile height (int_rows.inc zt_rows(1024))
 static_assert(PR_ZT % PR_ROWS == 0, "a tile covers part of one Zt tile");
 constexpr int PR_WAVES = PR_ROWS;     // one wave per row
@@ -91,13 +80,6 @@ static_assert(2 * PR_L * GSched<PR_B>::REGION <= 2 * PR_SLOT, "paired float-half
 
 constexpr float kTwoPiF = 6.28318530717959f;
 constexpr float kPR_VLim = 3.14159265f - 4e-3f;
-
-__device__ __forceinline__ int fw_amb(float a, float b, int& amb) {
-    constexpr float P = 3.14159274f;  // fl(M_PI)
-    const float d = a - b;
-    amb |= fabsf(d) == P;
-    return d > P ? -1 : (d < -P ? 1 : 0);
-}
 
 __device__ __forceinline__ int fw_exact(float a, float b) {
     const double d = (double)a - (double)b;
@@ -232,11 +214,6 @@ __global__ __launch_bounds__(PR_THREADS, FCD_PR_MINB) void k_phase_rows(
                     for (int k = 0; k < 4; ++k) th4[c][k] = tp[k];
                 }
             };
-#if FCD_PR_PAIRED && FCD_PR_THETA_LATE
-#else
-            load_theta();
-#endif
-#if FCD_PR_PAIRED
             // both carriers' transforms in lockstep (GroupFFTTab2): float-half
             // exchange regions of the two carriers side by side in the slot
             float2 x0[16], x1[16];
@@ -251,10 +228,7 @@ __global__ __launch_bounds__(PR_THREADS, FCD_PR_MINB) void k_phase_rows(
             GroupFFTTab2<PR_B>::template run_half<true>(x0, x1, sx + g * GSched<PR_B>::REGION,
                                                        sx + (PR_L + g) * GSched<PR_B>::REGION, t, btab);
             PR_STAMP(3);
-#if FCD_PR_THETA_LATE
-            load_theta();
-#endif
-#if FCD_PR_ATAN_N > 0
+            load_theta();  // after the transforms: register pressure
             // FCD_PR_ATAN_N pixel pairs of each carrier per interleaved group
             // (wrapped_phase_pkn: 2 * FCD_PR_ATAN_N independent chains)
 #pragma unroll
@@ -288,53 +262,7 @@ __global__ __launch_bounds__(PR_THREADS, FCD_PR_MINB) void k_phase_rows(
                     w1[q + 1] = wq[2 * m + 1].y;
                 }
             }
-#else
-#pragma unroll
-            for (int q = 0; q < 16; q += 2) {  // pixel pairs: packed atan2 / wrap
-                if (FCD_PR_ATAN_GROUP && q % FCD_PR_ATAN_GROUP == 0) __builtin_amdgcn_sched_barrier(0);
-                const int k = q / 4, e = q % 4;
-                const fv2 t0 = e == 0 ? fv2{th4[0][k].x, th4[0][k].y} : fv2{th4[0][k].z, th4[0][k].w};
-                const fv2 t1 = e == 0 ? fv2{th4[1][k].x, th4[1][k].y} : fv2{th4[1][k].z, th4[1][k].w};
-                const fv2 a0 = wrapped_phase_pk(t0, x0[q], x0[q + 1]);
-                const fv2 a1 = wrapped_phase_pk(t1, x1[q], x1[q + 1]);
-                w0[q] = a0.x;
-                w0[q + 1] = a0.y;
-                w1[q] = a1.x;
-                w1[q + 1] = a1.y;
-            }
-#endif
             PR_STAMP(4);
-#else
-#pragma unroll
-            for (int c = 0; c < 2; ++c) {
-                float th[16];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    th[4 * k] = th4[c][k].x;
-                    th[4 * k + 1] = th4[c][k].y;
-                    th[4 * k + 2] = th4[c][k].z;
-                    th[4 * k + 3] = th4[c][k].w;
-                }
-                float2 x[16];
-#pragma unroll
-                for (int q = 0; q < 16; ++q)
-                    x[q] = cmul(stage[(c * PR_B + t + PR_G * q) * PR_SROW + wave], ptl[q * 64 + lane]);
-                GroupFFTTab<PR_B>::template run<true>(x, slot + g * GSched<PR_B>::REGION, t, btab);
-#pragma unroll
-                for (int q = 0; q < 16; q += 2) {  // pixel pairs: packed atan2 / wrap
-                    if (FCD_PR_ATAN_GROUP && q % FCD_PR_ATAN_GROUP == 0) __builtin_amdgcn_sched_barrier(0);
-                    const fv2 wq = wrapped_phase_pk(fv2{th[q], th[q + 1]}, x[q], x[q + 1]);
-                    if (c == 0) {
-                        w0[q] = wq.x;
-                        w0[q + 1] = wq.y;
-                    } else {
-                        w1[q] = wq.x;
-                        w1[q + 1] = wq.y;
-                    }
-                }
-                PR_STAMP(3 + c);
-            }
-#endif
         }
         // ---- natural strided -> blocked through the slot
         wave_sync();
@@ -358,7 +286,6 @@ __global__ __launch_bounds__(PR_THREADS, FCD_PR_MINB) void k_phase_rows(
                 col0[((long)f * 2 + 1) * H + r] = v[0].y;
             }
             if constexpr (UNWRAP) {
-#if FCD_PR_PKUNWRAP
                 // both maps as packed pairs: dd = -find_wrap(w(j), w(j+1)) = rint((w(j) -
                 // w(j+1)) / 2 pi) for every f32 difference except +-fl(pi) (exhaustively
                 // checked against the comparison form; +-fl(pi) is flagged ambiguous as
@@ -389,34 +316,6 @@ __global__ __launch_bounds__(PR_THREADS, FCD_PR_MINB) void k_phase_rows(
                     acc += dd[j];
                 }
                 bad |= amb;
-#else
-                int amb = 0, hb0 = 0, hb1 = 0;  // 2-bit codes of h + 1
-#pragma unroll
-                for (int j = 0; j < 16; ++j) {
-                    const bool in = j0 + j + 1 < PR_W;
-                    const int h0 = in ? fw_amb(v[j].x, v[j + 1].x, amb) : 0;
-                    const int h1 = in ? fw_amb(v[j].y, v[j + 1].y, amb) : 0;
-                    hb0 |= (h0 + 1) << (2 * j);
-                    hb1 |= (h1 + 1) << (2 * j);
-                }
-                int run0 = 0, run1 = 0;  // (1 - h) increments of the segment
-#pragma unroll
-                for (int j = 0; j < 16; ++j) {
-                    run0 += 2 - ((hb0 >> (2 * j)) & 3);
-                    run1 += 2 - ((hb1 >> (2 * j)) & 3);
-                }
-                const int incl0 = team_scan_incl_dpp<64>(run0);
-                const int incl1 = team_scan_incl_dpp<64>(run1);
-                int acc0 = incl0 - run0 - j0, acc1 = incl1 - run1 - j0;  // k' at the segment start
-                wave_sync();  // every lane has read its neighbour's first value
-#pragma unroll
-                for (int j = 0; j < 16; ++j) {
-                    slot[pad(j0 + j)] = make_float2(fmaf((float)acc0, kTwoPiF, v[j].x), fmaf((float)acc1, kTwoPiF, v[j].y));
-                    acc0 -= ((hb0 >> (2 * j)) & 3) - 1;
-                    acc1 -= ((hb1 >> (2 * j)) & 3) - 1;
-                }
-                bad |= amb;
-#endif
             }
         }
         if constexpr (UNWRAP) {  // first and last unwrapped rows of the tile -> seam buffer (k_seam_check)
@@ -443,7 +342,6 @@ __global__ __launch_bounds__(PR_THREADS, FCD_PR_MINB) void k_phase_rows(
                 const float2 a0 = a_row[0], b0 = nx[0];  // phi'(r, 0) = w(r, 0)
                 const float d0 = kTwoPiF * (float)(-fw_exact(a0.x, b0.x));
                 const float d1 = kTwoPiF * (float)(-fw_exact(a0.y, b0.y));
-#if FCD_PR_PKUNWRAP
                 // largest |b - a + d| of both maps (packed differences, one max3 per pixel)
                 float m = 0.f;
 #pragma unroll
@@ -452,13 +350,6 @@ __global__ __launch_bounds__(PR_THREADS, FCD_PR_MINB) void k_phase_rows(
                     m = fmaxf(m, fmaxf(fabsf(e.x), fabsf(e.y)));
                 }
                 bad |= (int)(m > kPR_VLim);
-#else
-#pragma unroll
-                for (int j = 0; j < 16; ++j) {
-                    const float2 a = a_row[pad(j0 + j)], b = nx[pad(j0 + j)];
-                    bad |= (int)(fabsf(b.x - a.x + d0) > kPR_VLim) | (int)(fabsf(b.y - a.y + d1) > kPR_VLim);
-                }
-#endif
             }
             if (__any(bad) && lane == 0) atomicOr(flags + f * 2, 1);
             PR_STAMP(7);
@@ -491,7 +382,7 @@ __global__ __launch_bounds__(PR_THREADS, FCD_PR_MINB) void k_phase_rows(
             const float2* src = row_slot(rl, par ^ 1);
 #pragma unroll 4
             for (int k = 0; k < PR_W / 64; ++k) {
-                const float2 v = src[pad(zt_col_inv(c0 + 64 * k, PR_W))];
+                const float2 v = src[pad(c0 + 64 * k)];
                 if (!(FCD_PR_ABL & 2) || v.x == 1234.5f) st_stream(dst + (c0 + 64 * k) * PR_ZT + rl, v);  // 2: no Zt stores
             }
         }

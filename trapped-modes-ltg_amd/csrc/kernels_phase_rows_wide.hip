@@ -385,7 +385,6 @@ __global__ __launch_bounds__(WideCfg<W>::THREADS, 1) void k_phase_rows_wide(
         __syncthreads();
         // ---- Zt: this tile's rows of the Zt tiles' column runs; the radix-NWR join
         // X[k + 1024 j] = sum_h W_NWR^(h j) w^(h k) Y_h[k] on the way out
-        static_assert(!FCD_ZT_PAIRED, "the join writes columns k + 1024 j together");
         {
             const int r0 = rb * ROWS;
             float2* dst = Zt + (long)f * H * W + (long)(r0 / C::ZT) * W * C::ZT + (r0 % C::ZT);
