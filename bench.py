@@ -33,11 +33,11 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
 def load_traffic(n, chunk):
-    """HBM bytes per demod launch group from the committed PMC summary
-    (profiles/traffic_latest.json, written by tools/traffic_summary.py from two
-    rocprofv3 --pmc passes, FETCH_SIZE and WRITE_SIZE, over this bench command),
-    if it was measured for the same frame size and chunk."""
-    p = os.path.join(ROOT, "profiles", "traffic_latest.json")
+    """HBM bytes per demod launch group from the committed PMC summary of this frame
+    size (profiles/traffic_<n>.json, written by tools/traffic_summary.py from two
+    rocprofv3 --pmc passes, FETCH_SIZE and WRITE_SIZE, over this bench command at that
+    size), if one was measured."""
+    p = os.path.join(ROOT, "profiles", f"traffic_{n}.json")
     try:
         with open(p) as f:
             t = json.load(f)

@@ -95,7 +95,7 @@ lines += ["", f"Roofline pass (single stream, {chunk:g}-frame launch groups, {le
           f"**{prof_bench['roofline']['us_per_launch']} us per launch**.", "",
           "Bench line of the profiled command:", "", "```json", json.dumps(prof_bench), "```", "",
           "Unprofiled `python bench.py` on the same box:", "", "```json", bench.strip(), "```", ""]
-tp = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles", "traffic_latest.json")
+tp = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles", "traffic_1024.json")
 if os.path.exists(tp):
     t = json.load(open(tp))
     lines += ["PMC traffic (rocprofv3 `--pmc FETCH_SIZE` / `--pmc WRITE_SIZE`, separate passes over `bench.py --steps 2`; "

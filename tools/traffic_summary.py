@@ -7,8 +7,8 @@ streaming read; other widths uncalibrated): the membench copies move a known
 512 MiB per launch at 4, 8 and 16 B per lane, which gives the FETCH_SIZE and
 WRITE_SIZE scale of each width on this pool.  The engine's kernels are scaled
 with the factor of the width their dominant stream uses (measured, printed).
-Writes profiles/traffic_latest.json for bench.py (roofline.traffic) and prints
-a per-kernel table.
+Writes profiles/traffic_<frame>.json for bench.py (roofline.traffic at that frame
+size) and prints a per-kernel table.
 """
 import argparse
 import csv
@@ -19,7 +19,9 @@ import statistics
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-DEMOD = ("k_demod_rows", "k_demod_cols", "k_band_phase")
+# the demod launch group of bench.py's roofline pass: the band kernel up to 2048-point
+# rows, the full-length inverse k_demod_phase at 4096 (512-bin carrier windows)
+DEMOD = ("k_demod_rows", "k_demod_cols", "k_band_phase", "k_demod_phase")
 # the heights-only headline path (fused band transform + unwrap + row FFT)
 HEADLINE = ("k_demod_rows", "k_demod_cols", "k_phase_rows", "k_colk", "k_seam_check", "k_int_cols", "k_int_c2r")
 CHAIN = DEMOD + ("k_phase_rows", "k_seam_check", "k_colk", "k_int_rows2", "k_int_cols", "k_int_c2r")
@@ -45,10 +47,10 @@ def short(n):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
-    ap.add_argument("--frame", type=int, default=1024)
+    ap.add_argument("--frame", type=int, default=None, help="frame size (default: from the bench line)")
     ap.add_argument("--chunk", type=int, default=None, help="frames per launch (kbench runs: tools/traffic_kb.sh)")
-    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
-                    help="where to write the summary (bench.py reads profiles/traffic_latest.json: 1024^2 only)")
+    ap.add_argument("--out", default=None,
+                    help="where to write the summary (default profiles/traffic_<frame>.json, which bench.py reads)")
     a = ap.parse_args()
     known = 512 << 20
     cal = {}
@@ -76,7 +78,7 @@ def main():
             top = max(vals[k][c])
             vals[k][c] = [v for v in vals[k][c] if v >= 0.9 * top]
     # demod_rows / band_phase stream 4-B lanes (frame, theta, phases); demod_cols 8-B tiles
-    factor = {"k_demod_rows": fetch_f, "k_band_phase": fetch_f, "k_demod_cols": fetch_f8}
+    factor = {"k_demod_rows": fetch_f, "k_band_phase": fetch_f, "k_demod_phase": fetch_f, "k_demod_cols": fetch_f8}
     table = {}
     for k in CHAIN:
         if k not in vals:
@@ -93,6 +95,8 @@ def main():
             b = json.loads(line)
             if chunk is None:
                 chunk = int(round(b["roofline"]["frames_per_launch"]))
+            if a.frame is None:
+                a.frame = int(b["config"]["frame"])
             streams = int(b["config"].get("streams_per_chunk", 1))
     # frames per kept launch: the largest launches of every kernel are whole chunks (the
     # roofline pass for the demod kernels; bench.py's stage-timed headline pass runs each
@@ -115,6 +119,8 @@ def main():
                      f"{'tools/kbench' if a.chunk else 'bench.py'}, largest launches per kernel); "
                      "FETCH scaled by the membench 4/8-B-lane calibration, WRITE by the 4-B-lane one"}
     print(json.dumps(res, indent=1))
+    if a.out is None:
+        a.out = os.path.join(ROOT, "profiles", f"traffic_{a.frame}.json")
     with open(a.out, "w") as f:
         json.dump(res, f, indent=1)
 
