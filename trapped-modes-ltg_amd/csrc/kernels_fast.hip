@@ -438,12 +438,17 @@ __global__ __launch_bounds__(IntColsCfg<H>::THREADS, IntColsCfg<H>::V) void k_in
     };
     // Items are codes: frame code / CW, column code % CW (valid below NCH).
     //
-    // Each block walks a CONTIGUOUS range of columns: Zt's 8-row tiles hold a
-    // column's rows in 64 bytes, half a 128-byte line whose other half is the
-    // neighbouring column; the mirror columns W - c of consecutive items pair up
-    // off by one, so grid-striding fetched every mirror line twice (1.5x the
-    // compulsory Zt bytes).  In a contiguous range the neighbour is the next
-    // iteration's item and its half line is still in L2.
+    // Zt's 8-row tiles hold a column's rows in 64 bytes, half a 128-byte line whose
+    // other half is the neighbouring column, and items c, c + 1 always share one line
+    // (c even: their direct columns; c odd: their mirror columns W - c - 1, W - c).  So
+    // adjacent items must be read while both halves sit in one XCD's L2.  XCD-AWARE
+    // (dispatch deals block b to XCD b % 8): the items are cut into 8 contiguous
+    // regions, one per XCD, and XCD x's blocks walk its region iteration-major -- at
+    // iteration i its blocks take consecutive TEAMS-item groups of one stretch of
+    // (blocks per XCD) x TEAMS items -- so neighbouring items run on the same XCD at the
+    // same time (a contiguous range per block shared its edge lines with the block's
+    // previous iteration, by then evicted: 1.58x the compulsory Zt reads, PMC r03zm).
+    // kbench r04d: 2.63-2.69 -> 2.53 us/frame at 1024^2 x 256, 11.98 -> 11.67 at 2048^2 x 64.
     //
     // With 4-row Zt tiles (4096-point rows) a 128-byte line holds 4 columns x 4 rows,
     // and a block's next column came too late: its lines had left the XCD's L2
@@ -451,9 +456,10 @@ __global__ __launch_bounds__(IntColsCfg<H>::THREADS, IntColsCfg<H>::V) void k_in
     // the 4 blocks of a group sit on one XCD (dispatch deals block b to XCD b % 8)
     // and take columns 4k, 4k + 1, 4k + 2, 4k + 3 of the same quad at the same time.
     const bool quad = zts == 2 && TEAMS == 1 && gridDim.x % 32 == 0 && FCD_INTCOLS_QUADS;
+    const bool xcd = !quad && gridDim.x % 8 == 0;
     const int NQ = (NCH + 3) / 4;
     const int CW = quad ? 4 * NQ : NCH;
-    int c0, cstep, cend;
+    int c0, cstep, cend, bstride;  // first item, item step between teams, end, step between iterations
     if (quad) {
         const int q = blockIdx.x / 8, j = q % 4;
         const int grp = blockIdx.x % 8 + 8 * (q / 4), ngrp = gridDim.x / 4;
@@ -462,11 +468,21 @@ __global__ __launch_bounds__(IntColsCfg<H>::THREADS, IntColsCfg<H>::V) void k_in
         c0 = 4 * Q0 + j;
         cstep = 4;
         cend = 4 * Q1;
+        bstride = TEAMS * cstep;
+    } else if (xcd) {
+        const int bpx = gridDim.x / 8;                      // blocks per XCD
+        const int region = (items + 7) / 8;                 // items per XCD
+        const int r0 = min((int)(blockIdx.x % 8) * region, items);
+        c0 = r0 + (int)(blockIdx.x / 8) * TEAMS;
+        cstep = 1;
+        cend = min(r0 + region, items);
+        bstride = bpx * TEAMS;
     } else {
         const int per = (items + gridDim.x - 1) / gridDim.x;
         c0 = min(blockIdx.x * per, items);
         cstep = 1;
         cend = min(c0 + per, items);
+        bstride = TEAMS;
     }
     auto fetch_col = [&](int code, bool mirror, float2 (&v)[E]) {
         const bool valid = code < cend && code % CW < NCH;
@@ -477,7 +493,7 @@ __global__ __launch_bounds__(IntColsCfg<H>::THREADS, IntColsCfg<H>::V) void k_in
         fetch_col(code, false, px);
     };
     fetch(c0 + team * cstep);
-    for (int base = c0; base < cend; base += TEAMS * cstep) {
+    for (int base = c0; base < cend; base += bstride) {
         const int item = base + team * cstep;
         const bool valid = item < cend && item % CW < NCH;
         const int f = valid ? item / CW : 0, col = valid ? item % CW : 0;
@@ -507,7 +523,7 @@ __global__ __launch_bounds__(IntColsCfg<H>::THREADS, IntColsCfg<H>::V) void k_in
         // 3.94 vs 3.32 us/frame, kbench r02l; the next item's loads issued between them
         // hide better.  Pairing k_demod_cols' two inverse transforms: no change, r02m)
         fft.template run<true>(y, s, t);
-        if (base + TEAMS * cstep < cend) fetch(base + (TEAMS + team) * cstep);
+        if (base + bstride < cend) fetch(base + bstride + team * cstep);
         fft.template run<false>(x, s, t);
         const float kx = c.kxe[col], kx2 = c.kx2[col];
         const float hnorm = 0.5f * c.norm;
