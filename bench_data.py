@@ -20,8 +20,9 @@ SQUARE_SIZE = 0.001  # physical square side for calibration (any value; only sca
 AMP = 0.2  # bump amplitude / sigma^2 (peak strain)
 
 
-def checkerboard(n, rotate_deg=0.0, dtype=np.float32):
-    y, x = np.mgrid[0:n, 0:n].astype(np.float64)
+def checkerboard(n, rotate_deg=0.0, dtype=np.float32, cols=None):
+    """n x n board (n x cols when cols is given)."""
+    y, x = np.mgrid[0:n, 0:n if cols is None else cols].astype(np.float64)
     if rotate_deg:
         th = np.deg2rad(rotate_deg)
         x, y = x * np.cos(th) + y * np.sin(th), -x * np.sin(th) + y * np.cos(th)
@@ -29,11 +30,14 @@ def checkerboard(n, rotate_deg=0.0, dtype=np.float32):
     return (cell * 65535.0).astype(dtype)
 
 
-def bumps(n, seed, count=6):
+def bumps(n, seed, count=6, cols=None):
+    """Bump centres, widths and amplitudes for an n x n frame (n x cols: centres over each
+    axis, widths from the shorter side)."""
     rng = np.random.default_rng(seed)
+    m = n if cols is None else cols
     cy = rng.uniform(0.2 * n, 0.8 * n, count)
-    cx = rng.uniform(0.2 * n, 0.8 * n, count)
-    sg = rng.uniform(0.05 * n, 0.15 * n, count)
+    cx = rng.uniform(0.2 * m, 0.8 * m, count)
+    sg = rng.uniform(0.05 * min(n, m), 0.15 * min(n, m), count)
     amp = rng.choice([-1.0, 1.0], count) * AMP * sg * sg
     return cy, cx, sg, amp
 
@@ -50,17 +54,17 @@ def taper(n, xp=np):
     return t, dt
 
 
-def displacement_numpy(n, seed):
-    """T * grad(h) with h the bump sum and T(y, x) = t(y) t(x)."""
-    y, x = np.mgrid[0:n, 0:n].astype(np.float64)
-    hy = np.zeros((n, n))
-    hx = np.zeros((n, n))
-    for cy, cx, sg, a in zip(*bumps(n, seed)):
+def displacement_numpy(n, seed, cols=None):
+    """T * grad(h) with h the bump sum and T(y, x) = t(y) t(x) (n x n, or n x cols)."""
+    m = n if cols is None else cols
+    y, x = np.mgrid[0:n, 0:m].astype(np.float64)
+    hy = np.zeros((n, m))
+    hx = np.zeros((n, m))
+    for cy, cx, sg, a in zip(*bumps(n, seed, cols=cols)):
         e = a * np.exp(-((y - cy) ** 2 + (x - cx) ** 2) / (2 * sg * sg))
         hy -= (y - cy) * e / (sg * sg)
         hx -= (x - cx) * e / (sg * sg)
-    t, dt = taper(n)
-    ty, tx = t[:, None], t[None, :]
+    ty, tx = taper(n)[0][:, None], taper(m)[0][None, :]
     return hy * ty * tx, hx * ty * tx
 
 
@@ -86,19 +90,20 @@ def make_frames_numpy(n, count, seed=0, rotate_deg=0.0):
     return ref, frames
 
 
-def dislocation_displacement(n, pairs, length=200):
+def dislocation_displacement(n, pairs, length=200, cols=None):
     """u_x of edge-dislocation pairs, sum over (y0, x0) of
     P / (2 pi) * (atan2(y - y0, x - x0) - atan2(y - y0, x - x0 - length)), P = 20 px (the
     board's period, so the cut between the two cores is invisible): both carrier phases
     wind by +-2 pi around each core, i.e. a residue pair on row ~y0."""
-    y, x = np.mgrid[0:n, 0:n].astype(np.float64)
-    ux = np.zeros((n, n))
+    m = n if cols is None else cols
+    y, x = np.mgrid[0:n, 0:m].astype(np.float64)
+    ux = np.zeros((n, m))
     for y0, x0 in pairs:
         ux += (2 * SQUARE_PX / (2 * np.pi)) * (np.arctan2(y - y0, x - x0) - np.arctan2(y - y0, x - x0 - length))
     return ux
 
 
-def make_residue_frame(n, pairs, seed=None, rotate_deg=0.0, length=200, quantum=None):
+def make_residue_frame(n, pairs, seed=None, rotate_deg=0.0, length=200, quantum=None, cols=None):
     """One frame whose wrapped maps carry residues: the board warped by the bump field of
     `seed` (none if None) plus the dislocation pairs' u_x (the exact-unwrap workload of
     camera frames at the c3 / c5 sizes).
@@ -108,12 +113,13 @@ def make_residue_frame(n, pairs, seed=None, rotate_deg=0.0, length=200, quantum=
     (numpy 1.26 and 2.2 disagree on 4096^2 grids); after the rounding the frame is made of
     IEEE +, *, floor only, so the same bytes come out of the reference's interpreter, this
     one and the GPU box's (the golden fixtures store the frame's digest)."""
-    ref = checkerboard(n, rotate_deg)
+    ref = checkerboard(n, rotate_deg, cols=cols)
+    m = n if cols is None else cols
     if seed is None:
-        gy, gx = np.zeros((n, n)), np.zeros((n, n))
+        gy, gx = np.zeros((n, m)), np.zeros((n, m))
     else:
-        gy, gx = displacement_numpy(n, seed)
-    gx = gx + dislocation_displacement(n, pairs, length)
+        gy, gx = displacement_numpy(n, seed, cols=cols)
+    gx = gx + dislocation_displacement(n, pairs, length, cols=cols)
     if quantum:
         gy, gx = np.round(gy * quantum) / quantum, np.round(gx * quantum) / quantum
     return ref, warp_numpy(ref, gy, gx)

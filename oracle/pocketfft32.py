@@ -42,8 +42,24 @@ def twiddle(n, m):
     return f32(math.cos(a)), f32(math.sin(a))
 
 
+def _odd_factors(f, left):
+    """The odd part of pocketfft's factorize: divisors 3, 5, 7, ... in turn, the rest last.
+    Only 3 and 5 have passes here (5-smooth lengths); others raise."""
+    d = 3
+    while d * d <= left:
+        while left % d == 0:
+            f.append(d)
+            left //= d
+        d += 2
+    if left > 1:
+        f.append(left)
+    if any(p not in (2, 3, 4, 5, 8) for p in f):
+        raise ValueError("lengths with prime factors above 5 are not restated")
+    return f
+
+
 def rfactors(n):
-    """rfftp::factorize: 4s first, a single 2 moved to the front."""
+    """rfftp::factorize: 4s first, a single 2 moved to the front, then 3s, 5s."""
     f, left = [], n
     while left % 4 == 0:
         f.append(4)
@@ -52,13 +68,11 @@ def rfactors(n):
         left //= 2
         f.append(2)
         f[0], f[-1] = f[-1], f[0]
-    if left != 1:
-        raise ValueError("powers of two only")
-    return f
+    return _odd_factors(f, left)
 
 
 def cfactors(n):
-    """cfftp::factorize: 8s, then 4s, a single 2 moved to the front."""
+    """cfftp::factorize: 8s, then 4s, a single 2 moved to the front, then 3s, 5s."""
     f, left = [], n
     while left & 7 == 0:
         f.append(8)
@@ -70,9 +84,7 @@ def cfactors(n):
         left >>= 1
         f.append(2)
         f[0], f[-1] = f[-1], f[0]
-    if left != 1:
-        raise ValueError("powers of two only")
-    return f
+    return _odd_factors(f, left)
 
 
 def rtwiddles(n, fact):
@@ -182,6 +194,100 @@ def _radf4(ido, l1, cc, ch, wa):
             CH(ic, 1, k, tr4 - ti3)
 
 
+TAUR = f32(-0.5)
+TAUI = f32(0.8660254037844386467637231707529362)
+TR11 = f32(0.3090169943749474241022934171828191)
+TI11 = f32(0.9510565162951535721164393333793821)
+TR12 = f32(-0.8090169943749474241022934171828191)
+TI12 = f32(0.5877852522924731291687059546390728)
+
+
+def _radf3(ido, l1, cc, ch, wa):
+    CC = lambda a, b, c: cc[:, a + ido * (b + l1 * c)]  # noqa: E731
+    WA = lambda x, i: wa[i + x * (ido - 1)]  # noqa: E731
+
+    def CH(a, b, c, v):
+        ch[:, a + ido * (b + 3 * c)] = v
+    for k in range(l1):
+        cr2 = CC(0, k, 1) + CC(0, k, 2)
+        CH(0, 0, k, CC(0, k, 0) + cr2)
+        CH(0, 2, k, TAUI * (CC(0, k, 2) - CC(0, k, 1)))
+        CH(ido - 1, 1, k, CC(0, k, 0) + TAUR * cr2)
+    if ido == 1:
+        return
+    for k in range(l1):
+        for i in range(2, ido, 2):
+            ic = ido - i
+            dr2 = WA(0, i - 2) * CC(i - 1, k, 1) + WA(0, i - 1) * CC(i, k, 1)
+            di2 = WA(0, i - 2) * CC(i, k, 1) - WA(0, i - 1) * CC(i - 1, k, 1)
+            dr3 = WA(1, i - 2) * CC(i - 1, k, 2) + WA(1, i - 1) * CC(i, k, 2)
+            di3 = WA(1, i - 2) * CC(i, k, 2) - WA(1, i - 1) * CC(i - 1, k, 2)
+            cr2 = dr2 + dr3
+            ci2 = di2 + di3
+            CH(i - 1, 0, k, CC(i - 1, k, 0) + cr2)
+            CH(i, 0, k, CC(i, k, 0) + ci2)
+            tr2 = CC(i - 1, k, 0) + TAUR * cr2
+            ti2 = CC(i, k, 0) + TAUR * ci2
+            tr3 = TAUI * (di2 - di3)
+            ti3 = TAUI * (dr3 - dr2)
+            CH(i - 1, 2, k, tr2 + tr3)
+            CH(ic - 1, 1, k, tr2 - tr3)
+            CH(i, 2, k, ti3 + ti2)
+            CH(ic, 1, k, ti3 - ti2)
+
+
+def _radf5(ido, l1, cc, ch, wa):
+    CC = lambda a, b, c: cc[:, a + ido * (b + l1 * c)]  # noqa: E731
+    WA = lambda x, i: wa[i + x * (ido - 1)]  # noqa: E731
+
+    def CH(a, b, c, v):
+        ch[:, a + ido * (b + 5 * c)] = v
+    for k in range(l1):
+        cr2, ci5 = CC(0, k, 4) + CC(0, k, 1), CC(0, k, 4) - CC(0, k, 1)
+        cr3, ci4 = CC(0, k, 3) + CC(0, k, 2), CC(0, k, 3) - CC(0, k, 2)
+        CH(0, 0, k, CC(0, k, 0) + cr2 + cr3)
+        CH(ido - 1, 1, k, CC(0, k, 0) + TR11 * cr2 + TR12 * cr3)
+        CH(0, 2, k, TI11 * ci5 + TI12 * ci4)
+        CH(ido - 1, 3, k, CC(0, k, 0) + TR12 * cr2 + TR11 * cr3)
+        CH(0, 4, k, TI12 * ci5 - TI11 * ci4)
+    if ido == 1:
+        return
+    for k in range(l1):
+        for i in range(2, ido, 2):
+            ic = ido - i
+            dr2 = WA(0, i - 2) * CC(i - 1, k, 1) + WA(0, i - 1) * CC(i, k, 1)
+            di2 = WA(0, i - 2) * CC(i, k, 1) - WA(0, i - 1) * CC(i - 1, k, 1)
+            dr3 = WA(1, i - 2) * CC(i - 1, k, 2) + WA(1, i - 1) * CC(i, k, 2)
+            di3 = WA(1, i - 2) * CC(i, k, 2) - WA(1, i - 1) * CC(i - 1, k, 2)
+            dr4 = WA(2, i - 2) * CC(i - 1, k, 3) + WA(2, i - 1) * CC(i, k, 3)
+            di4 = WA(2, i - 2) * CC(i, k, 3) - WA(2, i - 1) * CC(i - 1, k, 3)
+            dr5 = WA(3, i - 2) * CC(i - 1, k, 4) + WA(3, i - 1) * CC(i, k, 4)
+            di5 = WA(3, i - 2) * CC(i, k, 4) - WA(3, i - 1) * CC(i - 1, k, 4)
+            cr2, ci5 = dr5 + dr2, dr5 - dr2
+            ci2, cr5 = di2 + di5, di2 - di5
+            cr3, ci4 = dr4 + dr3, dr4 - dr3
+            ci3, cr4 = di3 + di4, di3 - di4
+            CH(i - 1, 0, k, CC(i - 1, k, 0) + cr2 + cr3)
+            CH(i, 0, k, CC(i, k, 0) + ci2 + ci3)
+            tr2 = CC(i - 1, k, 0) + TR11 * cr2 + TR12 * cr3
+            ti2 = CC(i, k, 0) + TR11 * ci2 + TR12 * ci3
+            tr3 = CC(i - 1, k, 0) + TR12 * cr2 + TR11 * cr3
+            ti3 = CC(i, k, 0) + TR12 * ci2 + TR11 * ci3
+            tr5, tr4 = cr5 * TI11 + cr4 * TI12, cr5 * TI12 - cr4 * TI11
+            ti5, ti4 = ci5 * TI11 + ci4 * TI12, ci5 * TI12 - ci4 * TI11
+            CH(i - 1, 2, k, tr2 + tr5)
+            CH(ic - 1, 1, k, tr2 - tr5)
+            CH(i, 2, k, ti5 + ti2)
+            CH(ic, 1, k, ti5 - ti2)
+            CH(i - 1, 4, k, tr3 + tr4)
+            CH(ic - 1, 3, k, tr3 - tr4)
+            CH(i, 4, k, ti4 + ti3)
+            CH(ic, 3, k, ti4 - ti3)
+
+
+_RADF = {2: _radf2, 3: _radf3, 4: _radf4, 5: _radf5}
+
+
 def rfft_rows(x):
     """pocketfft r2c (forward) of every row of float32 [rows, n] -> complex64 [rows, n/2+1]."""
     p1 = np.array(x, np.float32, copy=True, order="C")
@@ -194,13 +300,14 @@ def rfft_rows(x):
         ip = fact[k]
         ido = n // l1
         l1 //= ip
-        (_radf4 if ip == 4 else _radf2)(ido, l1, p1, p2, tws[k])
+        _RADF[ip](ido, l1, p1, p2, tws[k])
         p1, p2 = p2, p1
     out = np.zeros((rows, n // 2 + 1), np.complex64)  # halfcomplex r0, r1, i1, r2, i2, ... -> complex
     out.real[:, 0] = p1[:, 0]
-    out.real[:, 1:n // 2] = p1[:, 1:n - 1:2]
-    out.imag[:, 1:n // 2] = p1[:, 2:n - 1:2]
-    out.real[:, n // 2] = p1[:, n - 1]
+    out.real[:, 1:(n + 1) // 2] = p1[:, 1:n - 1 + n % 2:2]
+    out.imag[:, 1:(n + 1) // 2] = p1[:, 2:n:2]
+    if n % 2 == 0:
+        out.real[:, n // 2] = p1[:, n - 1]
     return out
 
 
@@ -243,6 +350,34 @@ def _cpass(ip, ido, l1, c1, c2, tw):
             def put(m, v):
                 o = i + ido * (k + l1 * m)
                 r2[o], i2[o] = v
+            if ip == 3:  # pass3
+                t0 = C[0]
+                t1, t2 = _add(C[1], C[2]), _sub(C[1], C[2])
+                put(0, _add(t0, t1))
+                ca = (t0[0] + t1[0] * TAUR, t0[1] + t1[1] * TAUR)
+                cb = (-(t2[1] * -TAUI), t2[0] * -TAUI)
+                if i == 0:
+                    put(1, _add(ca, cb))
+                    put(2, _sub(ca, cb))
+                else:
+                    put(1, _mulc(_add(ca, cb), WA(0, i)))
+                    put(2, _mulc(_sub(ca, cb), WA(1, i)))
+                continue
+            if ip == 5:  # pass5
+                t0 = C[0]
+                t1, t4 = _add(C[1], C[4]), _sub(C[1], C[4])
+                t2, t3 = _add(C[2], C[3]), _sub(C[2], C[3])
+                put(0, (t0[0] + t1[0] + t2[0], t0[1] + t1[1] + t2[1]))
+                for u1, u2, twar, twbr, twai, twbi in ((1, 4, TR11, TR12, -TI11, -TI12), (2, 3, TR12, TR11, -TI12, TI11)):
+                    ca = (t0[0] + twar * t1[0] + twbr * t2[0], t0[1] + twar * t1[1] + twbr * t2[1])
+                    cb = (-(twai * t4[1] + twbi * t3[1]), twai * t4[0] + twbi * t3[0])
+                    if i == 0:
+                        put(u1, _add(ca, cb))
+                        put(u2, _sub(ca, cb))
+                    else:
+                        put(u1, _mulc(_add(ca, cb), WA(u1 - 1, i)))
+                        put(u2, _mulc(_sub(ca, cb), WA(u2 - 1, i)))
+                continue
             if ip == 2:
                 put(0, _add(C[0], C[1]))
                 d = _sub(C[0], C[1])

@@ -33,6 +33,8 @@ Fixtures (all under tests/golden/):
                      rotated-board frame and one with residues (bump field + edge-dislocation
                      pairs), the reference's carrier picks, heights, wrapped phases and FULL
                      unwrap k-fields (bench_data.make_residue_frame, frame digests stored)
+  mixed.npz          frame sides that are not powers of two (1024 x 1280, 1536 x 2048, a
+                     960-row camera crop): as large.npz, plus fft2 digests of 5-smooth shapes
   analyze_ref.npz    pydata/analyze.py ITSELF (imported with a placeholder `cv2` module
                      whose every attribute access raises: cv2 is only used on the polar
                      paths, analyze.py:237-241, 674-676, which are not run): analyze.mask /
@@ -471,6 +473,78 @@ def make_large():
     np.savez_compressed(os.path.join(OUT, "large.npz"), **out)
 
 
+# Frame sides that are not powers of two (the engine's mixed-radix generic chain): camera
+# formats 1280 x 1024 (here 1024 rows x 1280 columns) and 2048 x 1536, a residue frame, and
+# a 960-row crop of the 10-bit camera pair (real_df.npz's reference and frame 0, rows
+# 32..991: every map carries residues).
+MIXED_CASES = {
+    "s1024x1280": dict(rows=1024, cols=1280, seed=31, pairs=[]),
+    "r1024x1280": dict(rows=1024, cols=1280, seed=32, pairs=[(300.3, 500.4), (700.6, 900.2)]),
+    "s1536x2048": dict(rows=1536, cols=2048, seed=33, pairs=[]),
+    "c960x1024": dict(crop=(32, 992)),
+}
+
+
+def mixed_case_frames(spec):
+    if "crop" in spec:
+        r0, r1 = spec["crop"]
+        ref = load_raw("reference_df.tif").astype(np.float32)[r0:r1]
+        frame = load_raw("prueba1_20250317_122608_C1S0001000001.tif").astype(np.float32)[r0:r1]
+        return np.ascontiguousarray(ref), np.ascontiguousarray(frame), 0.002
+    sys.path.insert(0, os.path.dirname(os.path.dirname(OUT)))
+    from bench_data import make_residue_frame
+    ref, frame = make_residue_frame(spec["rows"], spec["pairs"], seed=spec["seed"], rotate_deg=5.0, quantum=4096,
+                                    cols=spec["cols"])
+    return ref, frame, 0.001
+
+
+def make_mixed():
+    """mixed.npz: as large.npz for MIXED_CASES (heights on a ~256-wide sub-grid, wrapped
+    phases on a ~128-wide one, the full k-fields), plus sha256 digests of scipy's fft2 of
+    each reference and of seeded integer-valued images of other 5-smooth shapes (the
+    restated radix-3 / radix-5 pocketfft passes)."""
+    import hashlib
+    out = {"versions": VERSIONS, "cases": np.array(list(MIXED_CASES))}
+    for tag, spec in MIXED_CASES.items():
+        ref, frame, sq = mixed_case_frames(spec)
+        rows, cols = ref.shape
+        r = run_pair(ref, frame, sq, height=1.0)
+        locs, thr = peak_locations(ref)
+        k = np.stack([kfield(w, p) for w, p in zip(r["wrapped"], r["phases"])])
+        assert np.abs(k).max() < 127
+        hs, ws = max(1, cols // 256), max(1, cols // 128)
+        out.update({
+            f"{tag}_shape": np.array([rows, cols]), f"{tag}_sq": sq,
+            f"{tag}_seed": spec.get("seed", -1),
+            f"{tag}_pairs": np.array(spec.get("pairs", []), np.float64).reshape(-1, 2),
+            f"{tag}_ref_sha": hashlib.sha256(ref.tobytes()).hexdigest(),
+            f"{tag}_frame_sha": hashlib.sha256(frame.tobytes()).hexdigest(),
+            f"{tag}_ref_fft2_sha": hashlib.sha256(fft2(ref).tobytes()).hexdigest(),
+            f"{tag}_peaks": r["peaks"], f"{tag}_cf": r["cf"], f"{tag}_radius": r["radius"],
+            f"{tag}_freqs": r["freqs"], f"{tag}_mask_count": r["mask_count"],
+            f"{tag}_blob_peaks": locs, f"{tag}_threshold": thr,
+            f"{tag}_height_step": hs, f"{tag}_wrapped_step": ws,
+            f"{tag}_height_sub": r["height"][::hs, ::hs].astype(np.float32),
+            f"{tag}_height_stats": stats(r["height"]),
+            f"{tag}_wrapped_sub": r["wrapped"][:, ::ws, ::ws],
+            f"{tag}_k": k.astype(np.int8),
+            f"{tag}_residues": np.array([residue_count(w) for w in r["wrapped"]]),
+        })
+        print("mixed", tag, ref.shape, r["peaks"].tolist(), r["cf"], "residues", out[f"{tag}_residues"].tolist(),
+              flush=True)
+    rng = np.random.default_rng(4242)
+    shapes = [(192, 320), (320, 192), (576, 960), (128, 384)]
+    for (h, w) in shapes:
+        u = rng.integers(0, 1024, (h, w)).astype(np.uint16)
+        img = u.astype(np.float32) * np.float32(0.37)
+        out[f"rand_{h}x{w}_u16"] = u
+        out[f"rand_{h}x{w}_fft2_sha"] = hashlib.sha256(fft2(img).tobytes()).hexdigest()
+        out[f"rand_{h}x{w}_mean"] = np.float32(np.mean(img))
+        out[f"rand_{h}x{w}_spec_sha"] = hashlib.sha256(np.fft.fftshift(np.abs(fft2(img - np.mean(img)))).tobytes()).hexdigest()
+    out["rand_shapes"] = np.array(shapes)
+    np.savez_compressed(os.path.join(OUT, "mixed.npz"), **out)
+
+
 def import_reference_analyze():
     """/root/reference/pydata/analyze.py, imported as the reference ships it.  Its module
     top level does `import cv2` (analyze.py:21), absent here; cv2 is used only by the
@@ -600,7 +674,7 @@ def make_analyze_ref():
 
 if __name__ == "__main__":
     which = sys.argv[1:] or ["real_pair", "real_df", "unwrap", "synthetic", "integrate", "val", "ingest",
-                             "bench_board", "analyze_ref", "spectrum", "large"]
+                             "bench_board", "analyze_ref", "spectrum", "large", "mixed"]
     if "real_pair" in which:
         make_real_pair()
     if "real_df" in which:
@@ -623,3 +697,5 @@ if __name__ == "__main__":
         make_spectrum()
     if "large" in which:
         make_large()
+    if "mixed" in which:
+        make_mixed()

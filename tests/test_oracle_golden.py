@@ -177,3 +177,48 @@ def test_oracle_large_frames_vs_reference_run(golden, tag):
     sub = n // 256
     hs = h[::sub, ::sub]
     assert np.linalg.norm(hs - g[f"{tag}_height_sub"]) / np.linalg.norm(g[f"{tag}_height_sub"]) < 1e-5
+
+
+def test_pocketfft32_mixed_radix_digests(golden):
+    """oracle/pocketfft32.py's radf3 / radf5 / pass3 / pass5 (5-smooth shapes) against
+    scipy 1.7.1's float32 fft2, numpy's mean and the find_peaks spectrum, by digest."""
+    import hashlib
+    from oracle import pocketfft32 as P
+    g = golden("mixed")
+    for h, w in g["rand_shapes"]:
+        img = g[f"rand_{h}x{w}_u16"].astype(np.float32) * np.float32(0.37)
+        assert hashlib.sha256(P.fft2(img).tobytes()).hexdigest() == str(g[f"rand_{h}x{w}_fft2_sha"]), (h, w)
+        assert P.mean_f32(img) == g[f"rand_{h}x{w}_mean"]
+        assert hashlib.sha256(P.find_peaks_spectrum(img).tobytes()).hexdigest() == str(g[f"rand_{h}x{w}_spec_sha"])
+
+
+@pytest.mark.parametrize("tag", ["r1024x1280", "c960x1024"])
+def test_oracle_mixed_frames_vs_reference_run(golden, tag):
+    """The oracle on frames whose sides are not powers of two against the reference's own
+    run (mixed.npz): setup bit-exact, k-fields exact up to the anchor off the border ring
+    (the camera crop: off the pixels next to residues on the border), heights at
+    float32-FFT tolerance."""
+    import hashlib
+    g = golden("mixed")
+    if tag.startswith("c"):
+        d = golden("real_df")
+        ref = np.ascontiguousarray(d["ref_u16"][32:992].astype(np.float32))
+        frame = np.ascontiguousarray(d["frames_u16"][0][32:992].astype(np.float32))
+    else:
+        from bench_data import make_residue_frame
+        rows, cols = (int(v) for v in g[f"{tag}_shape"])
+        ref, frame = make_residue_frame(rows, [tuple(p) for p in g[f"{tag}_pairs"]], seed=int(g[f"{tag}_seed"]),
+                                        rotate_deg=5.0, quantum=4096, cols=cols)
+    assert hashlib.sha256(frame.tobytes()).hexdigest() == str(g[f"{tag}_frame_sha"])
+    sq = float(g[f"{tag}_sq"])
+    h, ph, cf, ex = O.compute_height_map(ref, frame, sq, height=1.0)
+    assert cf == float(g[f"{tag}_cf"])
+    assert np.array_equal([np.asarray(c.pixels) for c in ex["carriers"]], g[f"{tag}_peaks"])
+    for m in range(2):
+        d = ex["k"][m].astype(np.int64) - g[f"{tag}_k"][m]
+        inner = d[1:-1, 1:-1]
+        bad = inner != inner.flat[0]
+        assert bad.sum() <= (0 if not tag.startswith("c") else 16), int(bad.sum())
+    hs = int(g[f"{tag}_height_step"])
+    sub = g[f"{tag}_height_sub"]
+    assert np.linalg.norm(h[::hs, ::hs] - sub) / np.linalg.norm(sub) < (1e-5 if not tag.startswith("c") else 1e-4)

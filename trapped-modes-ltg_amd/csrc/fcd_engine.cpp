@@ -184,6 +184,11 @@ struct PinBuf {
 
 struct fcd_ctx {
     int device = 0, H = 0, W = 0;
+    // a side is not a power of two: every per-frame call takes the generic chain on the
+    // mixed-radix transforms (kernels_mr.hip), the reference's own sequence of 2-D FFTs
+    bool generic = false;
+    fcdk::MrPlan mr_row{}, mr_col{};
+    DevBuf mr_scratch;  // the mixed-radix column transforms' transposed copy (chunk frames)
     hipStream_t own = nullptr;
     DevBuf tw_row, tw_col;        // plain tables exp(-2 pi i m / n) (generic LDS FFT kernels)
     DevBuf twp_row, twp_col;      // pass-major tables (register FFT kernels)
@@ -339,11 +344,30 @@ fcdk::MstWork mst_work(fcd_ctx* c) {
     return m;
 }
 
+// Row / column transforms of the generic chain: the power-of-two LDS FFTs of
+// kernels_fft.hip, or the mixed-radix ones of kernels_mr.hip for other sides.
+void rows_fft(fcd_ctx* c, bool inv, fcdk::RowIn im, fcdk::RowOut om, const void* in, void* out, long nrows, float sub,
+              const fcdk::PhaseOut* ph, hipStream_t s) {
+    if (c->generic)
+        fcdk::mr_rows(c->mr_row, inv, im, om, in, out, nrows, c->H, sub, c->tw_row.as<float2>(), ph, s);
+    else
+        fcdk::row_fft(c->W, inv, im, om, in, out, nrows, c->H, sub, c->tw_row.as<float2>(), ph, s);
+}
+
+void cols_fft(fcd_ctx* c, bool inv, float2* data, int nb, hipStream_t s) {
+    if (c->generic) {
+        if ((size_t)nb * c->hw() * sizeof(float2) > c->mr_scratch.bytes)
+            throw FcdError(FCD_E_INTERNAL, "mixed-radix scratch too small");
+        fcdk::mr_cols(c->mr_col, c->W, inv, data, nb, c->tw_col.as<float2>(), c->mr_scratch.as<float2>(), s);
+    } else {
+        fcdk::col_fft(c->H, c->W, inv, data, nb, c->tw_col.as<float2>(), s);
+    }
+}
+
 // 2-D forward FFT of nb real images (row pass from real input) into `out`.
 void fft2_real(fcd_ctx* c, const float* in, float2* out, int nb, float sub, hipStream_t s) {
-    fcdk::row_fft(c->W, false, fcdk::ROW_IN_REAL, fcdk::ROW_OUT_COMPLEX, in, out, (long)nb * c->H, c->H, sub,
-                  c->tw_row.as<float2>(), nullptr, s);
-    fcdk::col_fft(c->H, c->W, false, out, nb, c->tw_col.as<float2>(), s);
+    rows_fft(c, false, fcdk::ROW_IN_REAL, fcdk::ROW_OUT_COMPLEX, in, out, (long)nb * c->H, sub, nullptr, s);
+    cols_fft(c, false, out, nb, s);
 }
 
 // Wrapped phases of nb spectra (in `spec`) for both carriers, fcd.py:116-118.
@@ -352,10 +376,9 @@ void demod_phases(fcd_ctx* c, const float2* spec, int nb, float* wrapped, hipStr
     for (int car = 0; car < 2; ++car) {
         fcdk::DiskTable t{c->disk_rows.as<int>() + (size_t)car * 2 * c->W};
         fcdk::disk_mask(spec, A, nb, c->H, c->W, t, s);
-        fcdk::col_fft(c->H, c->W, true, A, nb, c->tw_col.as<float2>(), s);
+        cols_fft(c, true, A, nb, s);
         fcdk::PhaseOut ph{c->theta.as<float>() + (size_t)car * c->hw(), wrapped, car};
-        fcdk::row_fft(c->W, true, fcdk::ROW_IN_COMPLEX, fcdk::ROW_OUT_PHASE, A, nullptr, (long)nb * c->H, c->H, 0.f,
-                      c->tw_row.as<float2>(), &ph, s);
+        rows_fft(c, true, fcdk::ROW_IN_COMPLEX, fcdk::ROW_OUT_PHASE, A, nullptr, (long)nb * c->H, 0.f, &ph, s);
     }
 }
 
@@ -546,13 +569,11 @@ fcdk::IntegCoef integ_coef(fcd_ctx* c, double a0, double b0, double a1, double b
 void integrate_z(fcd_ctx* c, int nb, const fcdk::IntegCoef& k, float* h_out, hipStream_t s) {
     float2* Z = c->spec.as<float2>();
     float2* Hh = c->work.as<float2>();
-    fcdk::row_fft(c->W, false, fcdk::ROW_IN_COMPLEX, fcdk::ROW_OUT_COMPLEX, Z, Z, (long)nb * c->H, c->H, 0.f,
-                  c->tw_row.as<float2>(), nullptr, s);
-    fcdk::col_fft(c->H, c->W, false, Z, nb, c->tw_col.as<float2>(), s);
+    rows_fft(c, false, fcdk::ROW_IN_COMPLEX, fcdk::ROW_OUT_COMPLEX, Z, Z, (long)nb * c->H, 0.f, nullptr, s);
+    cols_fft(c, false, Z, nb, s);
     fcdk::integ_multiply(Z, Hh, nb, c->H, c->W, k, s);
-    fcdk::col_fft(c->H, c->W, true, Hh, nb, c->tw_col.as<float2>(), s);
-    fcdk::row_fft(c->W, true, fcdk::ROW_IN_COMPLEX, fcdk::ROW_OUT_REAL, Hh, h_out, (long)nb * c->H, c->H, 0.f,
-                  c->tw_row.as<float2>(), nullptr, s);
+    cols_fft(c, true, Hh, nb, s);
+    rows_fft(c, true, fcdk::ROW_IN_COMPLEX, fcdk::ROW_OUT_REAL, Hh, h_out, (long)nb * c->H, 0.f, nullptr, s);
 }
 
 // The column kernels' pass-major tables (their element counts may differ from fft_elems)
@@ -632,6 +653,11 @@ void build_demod_tables(fcd_ctx* c, hipStream_t s) {
     c->NC = (int)hc_list.size();
     c->NCA = std::max(std::max(c->NCc[0], c->NCc[1]), 1);
     if (c->NC == 0) throw FcdError(FCD_E_NOPEAKS, "carrier disks are empty");
+    if (c->generic) {  // no band-pruned fast path: the generic chain needs no tables
+        c->band_B = c->fused_B = 0;
+        c->fused_ok = false;
+        return;
+    }
     c->dt_hc.ensure(hc_list.size() * sizeof(int));
     c->dt_nouts.ensure(nouts.size() * sizeof(int));
     c->dt_outs.ensure(outs.size() * sizeof(int4));
@@ -772,9 +798,8 @@ void reference_state(fcd_ctx* c, const float* dref0, const float* dref1, hipStre
             float2* R = c->refsig.as<float2>() + q * hw;
             fcdk::DiskTable t{c->disk_rows.as<int>() + (size_t)q * 2 * c->W};
             fcdk::disk_mask(F, R, 1, c->H, c->W, t, s);
-            fcdk::col_fft(c->H, c->W, true, R, 1, c->tw_col.as<float2>(), s);
-            fcdk::row_fft(c->W, true, fcdk::ROW_IN_COMPLEX, fcdk::ROW_OUT_COMPLEX, R, R, c->H, c->H, 0.f,
-                          c->tw_row.as<float2>(), nullptr, s);
+            cols_fft(c, true, R, 1, s);
+            rows_fft(c, true, fcdk::ROW_IN_COMPLEX, fcdk::ROW_OUT_COMPLEX, R, R, c->H, 0.f, nullptr, s);
             fcdk::angle(R, c->theta.as<float>() + q * hw, hw, s);
         }
         const size_t tb = (size_t)hw * sizeof(float), rb = (size_t)hw * sizeof(float2);
@@ -907,9 +932,10 @@ FCD_API int fcd_create(int device, int rows, int cols, fcd_ctx** out) {
     FCD_TRY({
         if (!out) throw FcdError(FCD_E_INVALID, "out is null");
         *out = nullptr;
-        if (!fcdk::fft_size_supported(rows) || !fcdk::fft_size_supported(cols))
-            throw FcdError(FCD_E_UNSUPPORTED, "rows and cols must be powers of two in [64, 4096], got " +
-                                                  std::to_string(rows) + "x" + std::to_string(cols));
+        const bool pow2 = fcdk::fft_size_supported(rows) && fcdk::fft_size_supported(cols);
+        if (!pow2 && !(fcdk::mr_supported(rows) && fcdk::mr_supported(cols)))
+            throw FcdError(FCD_E_UNSUPPORTED, "rows and cols must be multiples of 64 in [64, 4096] of the form "
+                                              "2^a 3^b 5^c, got " + std::to_string(rows) + "x" + std::to_string(cols));
         int ndev = 0;
         HIPCHK(hipGetDeviceCount(&ndev));
         if (device < 0 || device >= ndev) throw FcdError(FCD_E_INVALID, "bad device ordinal");
@@ -923,6 +949,11 @@ FCD_API int fcd_create(int device, int rows, int cols, fcd_ctx** out) {
         c->pr_dynamic = fcd_env_int("FCD_PR_DYNAMIC", 0) != 0;
         c->H = rows;
         c->W = cols;
+        c->generic = !pow2;
+        if (c->generic) {
+            c->mr_row = fcdk::mr_plan(cols);
+            c->mr_col = fcdk::mr_plan(rows);
+        }
         HIPCHK(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking));
         c->pr_ctr.ensure(4 * sizeof(unsigned));
         HIPCHK(hipMemset(c->pr_ctr.p, 0, 4 * sizeof(unsigned)));
@@ -931,12 +962,14 @@ FCD_API int fcd_create(int device, int rows, int cols, fcd_ctx** out) {
         c->tw_col.ensure(tc.size() * sizeof(float2));
         HIPCHK(hipMemcpy(c->tw_row.p, tr.data(), tr.size() * sizeof(float2), hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(c->tw_col.p, tc.data(), tc.size() * sizeof(float2), hipMemcpyHostToDevice));
-        const std::vector<float2> pr = pass_twiddles(cols), pc = pass_twiddles(rows);
-        c->twp_row.ensure(pr.size() * sizeof(float2));
-        c->twp_col.ensure(pc.size() * sizeof(float2));
-        HIPCHK(hipMemcpy(c->twp_row.p, pr.data(), pr.size() * sizeof(float2), hipMemcpyHostToDevice));
-        HIPCHK(hipMemcpy(c->twp_col.p, pc.data(), pc.size() * sizeof(float2), hipMemcpyHostToDevice));
-        if (fcdk::int_cols_elems(rows) == 16 || fcdk::demod_cols_elems(rows) == 16) {
+        if (!c->generic) {  // the register FFTs' pass-major tables (power-of-two fast path)
+            const std::vector<float2> pr = pass_twiddles(cols), pc = pass_twiddles(rows);
+            c->twp_row.ensure(pr.size() * sizeof(float2));
+            c->twp_col.ensure(pc.size() * sizeof(float2));
+            HIPCHK(hipMemcpy(c->twp_row.p, pr.data(), pr.size() * sizeof(float2), hipMemcpyHostToDevice));
+            HIPCHK(hipMemcpy(c->twp_col.p, pc.data(), pc.size() * sizeof(float2), hipMemcpyHostToDevice));
+        }
+        if (!c->generic && (fcdk::int_cols_elems(rows) == 16 || fcdk::demod_cols_elems(rows) == 16)) {
             const std::vector<float2> pi = pass_twiddles(rows, 16);
             c->twp_col16.ensure(pi.size() * sizeof(float2));
             HIPCHK(hipMemcpy(c->twp_col16.p, pi.data(), pi.size() * sizeof(float2), hipMemcpyHostToDevice));
@@ -951,9 +984,13 @@ FCD_API int fcd_create(int device, int rows, int cols, fcd_ctx** out) {
             HIPCHK(hipMemcpy(c->pf_ctw.p, ctw.data(), ctw.size() * sizeof(float), hipMemcpyHostToDevice));
         }
         // chunk: ~48 B of workspace per pixel per frame; keep the working set near the 256 MiB MALL
+        // (the generic chain streams every stage through HBM anyway: up to 32 frames
+        // in 4 GiB, its transposes' scratch included)
         const long per_frame = 48L * rows * cols;
-        c->chunk = (int)std::max(1L, std::min(64L, (256L << 20) / per_frame));
+        c->chunk = c->generic ? (int)std::max(1L, std::min(32L, (4L << 30) / (per_frame + 8L * rows * cols)))
+                              : (int)std::max(1L, std::min(64L, (256L << 20) / per_frame));
         ensure_chunk_buffers(c.get());
+        if (c->generic) c->mr_scratch.ensure((size_t)c->chunk * c->hw() * sizeof(float2));
         c->scalar.ensure(64);
         *out = c.release();
     })
@@ -1322,6 +1359,68 @@ void stage_frames(fcd_ctx* c, const void* frames, int format, bool dev, const in
     (void)hw;
 }
 
+// The generic chain (a frame side that is not a power of two): per chunk of c->chunk
+// frames the reference's own sequence -- fft2 of the frames (fcd.py:28), per carrier the
+// disk mask, ifft2 and phase step (fcd.py:116-118), the unwrap of both maps (fcd.py:119:
+// residue census, scan or exact MST), phi0 + i phi1 and its spectral integration with the
+// displacement solve folded in (fcd.py:30-33, fourier.py:115-137) -- on the mixed-radix
+// transforms.  Synchronous on `s`.
+int process_generic(fcd_ctx* c, const void* frames, int format, int n_frames, bool dev, bool unwrap,
+                    const fcdk::IntegCoef& coef, float* height_out, float* wrapped_out, int32_t* k_out, hipStream_t s) {
+    const long hw = c->hw();
+    const hipMemcpyKind kind = dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+    c->frames_in.ensure((size_t)c->chunk * hw * sizeof(float));
+    c->out_h.ensure((size_t)c->chunk * hw * sizeof(float));
+    const auto t0 = std::chrono::steady_clock::now();
+    long nres = 0;
+    for (int f0 = 0; f0 < n_frames; f0 += c->chunk) {
+        const int nb = std::min(c->chunk, n_frames - f0);
+        const float* fr = reinterpret_cast<const float*>(frames) + (size_t)f0 * hw;
+        if (!dev || format != FCD_FMT_F32) {
+            std::vector<int> idx(nb);
+            std::iota(idx.begin(), idx.end(), f0);
+            stage_frames(c, frames, format, dev, idx.data(), nb, s);
+            fr = c->frames_in.as<float>();
+        }
+        if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
+        float2* spec = c->spec.as<float2>();
+        float* w = c->wrapped.as<float>();
+        fft2_real(c, fr, spec, nb, 0.f, s);
+        demod_phases(c, spec, nb, w, s);
+        if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
+        int32_t* k = nullptr;
+        if (unwrap) {
+            std::vector<int> counts(2 * (size_t)nb);
+            k = c->kbuf.as<int32_t>();
+            unwrap_maps(c, w, 2 * nb, k, counts.data(), s);
+            for (int i = 0; i < nb; ++i) nres += counts[2 * (size_t)i] || counts[2 * (size_t)i + 1];
+        }
+        if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
+        fcdk::make_z(w, k, spec, nb, c->H, c->W, s);
+        float* hdst = dev && height_out ? height_out + (size_t)f0 * hw : c->out_h.as<float>();
+        integrate_z(c, nb, coef, hdst, s);
+        if (c->profiling) {
+            HIPCHK(hipEventRecord(c->next_event(), s));
+            c->prof_frames += nb;
+        }
+        if (height_out && !dev) HIPCHK(hipMemcpyAsync(height_out + (size_t)f0 * hw, hdst, (size_t)nb * hw * 4, kind, s));
+        if (wrapped_out)
+            HIPCHK(hipMemcpyAsync(wrapped_out + (size_t)f0 * 2 * hw, w, (size_t)nb * 2 * hw * 4, kind, s));
+        if (k_out && k) {
+            HIPCHK(hipMemcpyAsync(k_out + (size_t)f0 * 2 * hw, k, (size_t)nb * 2 * hw * 4, kind, s));
+        } else if (k_out) {
+            if (dev) HIPCHK(hipMemsetAsync(k_out + (size_t)f0 * 2 * hw, 0, (size_t)nb * 2 * hw * 4, s));
+            else std::memset(k_out + (size_t)f0 * 2 * hw, 0, (size_t)nb * 2 * hw * 4);
+        }
+        HIPCHK(hipStreamSynchronize(s));  // the chunk's workspace is reused by the next
+    }
+    if (c->profiling) {  // frames with residues (their maps took the exact MST unwrap)
+        c->prof_fix_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        c->prof_fix_frames += nres;
+    }
+    return FCD_OK;
+}
+
 int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int flags, double height, int unwrap,
                  float* height_out, float* wrapped_out, int32_t* k_out, void* stream) {
     check_ctx(c, false);
@@ -1344,6 +1443,8 @@ int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int f
     // h_hat = i/k^2 [(kx f1[0] - ky f1[1]) Phi0 + (ky f0[1] - kx f0[0]) Phi1] / (det * height)
     const fcdk::IntegCoef coef = integ_coef(c, in.frequencies[1][0] * sc, -in.frequencies[1][1] * sc,
                                             -in.frequencies[0][0] * sc, in.frequencies[0][1] * sc);
+    if (c->generic)
+        return process_generic(c, frames, format, n_frames, dev, unwrap != 0, coef, height_out, wrapped_out, k_out, s);
     const int nbmax = c->fchunk;
     c->frames_in.ensure((size_t)nbmax * hw * sizeof(float));
     c->out_h.ensure((size_t)nbmax * hw * sizeof(float));

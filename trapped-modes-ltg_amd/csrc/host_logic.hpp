@@ -55,7 +55,8 @@ inline std::vector<double> wavenumber(int n, double cf, bool shifted) {
 
 // scipy 1.7.1 pocketfft plans (kernels_pocketfft.hip; restated in oracle/pocketfft32.py):
 // rfftp factors 4, 4, ... with a single 2 moved to the front; cfftp 8s, then 4s, a single
-// 2 first; twiddles (cos, sin)(2 pi m / n) rounded to float (sincos_2pibyn<float>).
+// 2 first; then both take 3s and 5s (larger odd factors are not restated); twiddles
+// (cos, sin)(2 pi m / n) rounded to float (sincos_2pibyn<float>).
 inline std::pair<float, float> pf_twiddle(int n, long m) {
     const double a = 2 * kPi * (double)m / (double)n;
     return {(float)std::cos(a), (float)std::sin(a)};
@@ -78,6 +79,11 @@ inline std::vector<int> pf_factors(int n, bool real) {
         f.push_back(2);
         std::swap(f.front(), f.back());
     }
+    for (int d : {3, 5})
+        while (left % d == 0) {
+            f.push_back(d);
+            left /= d;
+        }
     if (left != 1 || f.size() > 8) throw std::runtime_error("pocketfft plan: unsupported length");
     return f;
 }

@@ -118,6 +118,22 @@ void row_fft(int W, bool inverse, RowIn in_mode, RowOut out_mode, const void* in
              int H, float sub, const float2* tw, const PhaseOut* ph, hipStream_t s);
 // In-place batched column FFT of nbatch [H][W] complex arrays.
 void col_fft(int H, int W, bool inverse, float2* data, int nbatch, const float2* tw, hipStream_t s);
+// Mixed-radix row / column transforms (kernels_mr.hip) of the generic chain for sides that
+// are not powers of two: n = 2^a 3^b 5^c, a multiple of 64 in [64, 4096].
+struct MrPlan {
+    int n, nf;
+    int fct[8];  // radices in pass order: 8s, 4s, then 3s, 5s
+};
+bool mr_supported(int n);
+MrPlan mr_plan(int n);
+// as row_fft (same modes; tw: exp(-2 pi i m / n), m < n)
+void mr_rows(const MrPlan& p, bool inverse, RowIn in_mode, RowOut out_mode, const void* in, void* out, long nrows,
+             int H, float sub, const float2* tw, const PhaseOut* ph, hipStream_t s);
+// [nb][R][C] -> [nb][C][R]
+void mr_transpose(const float2* in, float2* out, int nb, int R, int C, hipStream_t s);
+// in-place column transforms of [nb][p.n][W] (through scratch: nb * p.n * W complex)
+void mr_cols(const MrPlan& p, int W, bool inverse, float2* data, int nb, const float2* tw, float2* scratch,
+             hipStream_t s);
 
 // out[b] = in[b] * disk (unshifted spectrum index)
 void disk_mask(const float2* in, float2* out, int nbatch, int H, int W, DiskTable t, hipStream_t s);

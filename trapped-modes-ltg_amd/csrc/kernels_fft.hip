@@ -222,7 +222,7 @@ __global__ void k_disk_mask(const float2* __restrict__ in, float2* __restrict__ 
     if (idx >= n) return;
     const long p = idx % ((long)H * W);
     const int i = (int)(p / W), j = (int)(p % W);
-    const int si = (i + H / 2) & (H - 1), sj = (j + W / 2) & (W - 1);
+    const int si = (i + H / 2) % H, sj = (j + W / 2) % W;  // (any even side: the generic chain too)
     const int2 rr = reinterpret_cast<const int2*>(t.rows)[sj];
     const bool inside = si >= rr.x && si <= rr.y;
     out[idx] = inside ? in[idx] : make_float2(0.f, 0.f);
@@ -319,8 +319,8 @@ __global__ void k_spectrum_mag_b(const float2* __restrict__ F, float* __restrict
     if (gidx < n) {
         const long idx = gidx - b * hw;
         const int si = (int)(idx / W), sj = (int)(idx % W);
-        int i = (si + H / 2) & (H - 1), j = (sj + W / 2) & (W - 1);
-        const int mi = (H - i) & (H - 1), mj = (W - j) & (W - 1);  // one canonical bin per Hermitian pair
+        int i = (si + H / 2) % H, j = (sj + W / 2) % W;
+        const int mi = (H - i) % H, mj = (W - j) % W;  // one canonical bin per Hermitian pair
         if (mi < i || (mi == i && mj < j)) {
             i = mi;
             j = mj;

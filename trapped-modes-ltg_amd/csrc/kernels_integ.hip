@@ -74,7 +74,7 @@ __global__ void k_integ_multiply(const float2* __restrict__ Z, float2* __restric
     const long hw = (long)H * W;
     const long b = idx / hw, p = idx % hw;
     const int r = (int)(p / W), q = (int)(p % W);
-    const int rm = (H - r) & (H - 1), qm = (W - q) & (W - 1);
+    const int rm = (H - r) % H, qm = (W - q) % W;
     const float2 z = Z[idx];
     const float2 zm = Z[b * hw + (long)rm * W + qm];
     // Phi0 = (Z(k) + conj Z(-k)) / 2 ; Phi1 = (Z(k) - conj Z(-k)) / (2i)

@@ -1,0 +1,261 @@
+// Mixed-radix transforms for frame sides that are not powers of two.
+//
+// The reference takes frames of any shape (scipy.fft.fft2 at fcd.py:28, fourier.py:18,
+// fourier.py:134; ifft2 at fcd.py:118, carriers.py:23-24, fourier.py:137).  Camera
+// sensors are often 1280 x 1024, 1920 x 1536, 2048 x 1536 ...: this file gives the
+// engine's generic chain (fcd_engine.cpp: fft2_real / demod_phases / integrate_z /
+// reference_state) its row and column transforms at every side n = 2^a 3^b 5^c with n a
+// multiple of 64 in [64, 4096] (the multiple of 64 keeps the unwrap's 64 x 64 MST tiles
+// and 16-byte residue loads as they are).
+//
+// One workgroup per row, the row in LDS, Stockham passes of radix 8 / 4 (the power of
+// two, in 8s then 4s) then 3s and 5s, each pass reading one LDS buffer and writing the
+// other (one barrier per pass), twiddles exp(-+2 pi i m / n) from the context's plain
+// table (computed in f64 on the host).  Columns go through a tiled transpose, the row
+// transform of length H, and the transpose back.  These are the generic-chain
+// transforms, not the band-pruned register FFTs of the power-of-two fast path: a frame
+// costs ~15 streaming passes over 16 bytes per pixel.
+#include <hip/hip_runtime.h>
+
+#include <stdexcept>
+#include <string>
+
+#include "fft_lds.hpp"
+#include "kernels.hpp"
+
+namespace fcdk {
+
+#define FCD_HIPCHK(x)                                                               \
+    do {                                                                            \
+        hipError_t e_ = (x);                                                        \
+        if (e_ != hipSuccess) throw std::runtime_error(std::string(#x ": ") + hipGetErrorString(e_)); \
+    } while (0)
+#define FCD_CHECK_LAUNCH()                                                          \
+    do {                                                                            \
+        hipError_t e_ = hipGetLastError();                                          \
+        if (e_ != hipSuccess) throw std::runtime_error(std::string("kernel launch: ") + hipGetErrorString(e_)); \
+    } while (0)
+
+namespace {
+
+constexpr int MR_THREADS = 256;
+constexpr float kPiF = 3.14159265358979f;
+constexpr float kTwoPiF = 6.28318530717959f;
+// radix-3 / radix-5 DFT constants
+constexpr float kS3 = 0.866025403784438647f;                                  // sin(2 pi / 3)
+constexpr float kC51 = 0.309016994374947424f, kS51 = 0.951056516295153572f;   // cos, sin(2 pi / 5)
+constexpr float kC52 = -0.809016994374947424f, kS52 = 0.587785252292473129f;  // cos, sin(4 pi / 5)
+
+template <bool INV>
+__device__ __forceinline__ void dft3(float2* a) {
+    const float2 t1 = cadd(a[1], a[2]), t2 = csub(a[1], a[2]);
+    const float2 m = make_float2(a[0].x - 0.5f * t1.x, a[0].y - 0.5f * t1.y);
+    // forward: y1 = m - i s3 t2, y2 = m + i s3 t2 (W3 = exp(-2 pi i / 3))
+    const float sg = INV ? -kS3 : kS3;
+    const float2 u = make_float2(sg * t2.y, -sg * t2.x);  // -i sg t2
+    a[0] = cadd(a[0], t1);
+    a[1] = cadd(m, u);
+    a[2] = csub(m, u);
+}
+
+template <bool INV>
+__device__ __forceinline__ void dft5(float2* a) {
+    const float2 t1 = cadd(a[1], a[4]), t4 = csub(a[1], a[4]);
+    const float2 t2 = cadd(a[2], a[3]), t3 = csub(a[2], a[3]);
+    const float2 c1 = make_float2(a[0].x + kC51 * t1.x + kC52 * t2.x, a[0].y + kC51 * t1.y + kC52 * t2.y);
+    const float2 c2 = make_float2(a[0].x + kC52 * t1.x + kC51 * t2.x, a[0].y + kC52 * t1.y + kC51 * t2.y);
+    const float sg = INV ? -1.f : 1.f;
+    // forward: y1 = c1 - i (s51 t4 + s52 t3), y2 = c2 - i (s52 t4 - s51 t3); y4, y3 the conjugate pairs
+    const float2 d1 = make_float2(sg * (kS51 * t4.x + kS52 * t3.x), sg * (kS51 * t4.y + kS52 * t3.y));
+    const float2 d2 = make_float2(sg * (kS52 * t4.x - kS51 * t3.x), sg * (kS52 * t4.y - kS51 * t3.y));
+    a[0] = make_float2(a[0].x + t1.x + t2.x, a[0].y + t1.y + t2.y);
+    a[1] = make_float2(c1.x + d1.y, c1.y - d1.x);
+    a[4] = make_float2(c1.x - d1.y, c1.y + d1.x);
+    a[2] = make_float2(c2.x + d2.y, c2.y - d2.x);
+    a[3] = make_float2(c2.x - d2.y, c2.y + d2.x);
+}
+
+template <int R, bool INV>
+__device__ __forceinline__ void dft_any(float2* a) {
+    if constexpr (R == 3) dft3<INV>(a);
+    else if constexpr (R == 5) dft5<INV>(a);
+    else dft_reg<R, INV>(a);
+}
+
+// One Stockham pass: src -> dst, L = product of the radices already applied.
+template <int R, bool INV>
+__device__ __forceinline__ void mr_pass(const float2* src, float2* dst, int n, int L, const float2* __restrict__ tw) {
+    const int nb = n / R, step = n / (L * R);
+    for (int j = threadIdx.x; j < nb; j += MR_THREADS) {
+        const int k = j % L;
+        float2 a[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) a[r] = src[j + r * nb];
+        if (L > 1) {
+#pragma unroll
+            for (int r = 1; r < R; ++r) a[r] = cmul_dir<INV>(a[r], tw[r * k * step]);
+        }
+        dft_any<R, INV>(a);
+        const int base = (j - k) * R + k;
+#pragma unroll
+        for (int r = 0; r < R; ++r) dst[base + r * L] = a[r];
+    }
+}
+
+template <bool INV, int IN, int OUT>
+__global__ __launch_bounds__(MR_THREADS) void k_mr_rows(const void* __restrict__ in, void* __restrict__ out, long nrows,
+                                                        int H, float sub, MrPlan p, const float2* __restrict__ tw,
+                                                        PhaseOut ph) {
+    extern __shared__ __attribute__((aligned(16))) float2 mr_lds[];
+    const int n = p.n;
+    const long row = blockIdx.x;
+    float2* b0 = mr_lds;
+    float2* b1 = mr_lds + n;
+    for (int i = threadIdx.x; i < n; i += MR_THREADS) {
+        float2 v;
+        if constexpr (IN == ROW_IN_REAL) {
+            v = make_float2(static_cast<const float*>(in)[row * n + i] - sub, 0.f);
+        } else {
+            v = static_cast<const float2*>(in)[row * n + i];
+        }
+        b0[i] = v;
+    }
+    __syncthreads();
+    int L = 1;
+    for (int f = 0; f < p.nf; ++f) {
+        const int R = p.fct[f];
+        if (R == 8) mr_pass<8, INV>(b0, b1, n, L, tw);
+        else if (R == 4) mr_pass<4, INV>(b0, b1, n, L, tw);
+        else if (R == 3) mr_pass<3, INV>(b0, b1, n, L, tw);
+        else mr_pass<5, INV>(b0, b1, n, L, tw);
+        __syncthreads();
+        float2* t = b0;
+        b0 = b1;
+        b1 = t;
+        L *= R;
+    }
+    if constexpr (OUT == ROW_OUT_COMPLEX) {
+        for (int i = threadIdx.x; i < n; i += MR_THREADS) static_cast<float2*>(out)[row * n + i] = b0[i];
+    } else if constexpr (OUT == ROW_OUT_REAL) {
+        for (int i = threadIdx.x; i < n; i += MR_THREADS) static_cast<float*>(out)[row * n + i] = b0[i].x;
+    } else {
+        // w = wrap(theta - angle(A)) == -angle(A * conj(R)) of fcd.py:118 (as k_row_fft)
+        const long b = row / H, r = row % H;
+        const float* th = ph.theta + r * n;
+        float* wo = ph.wrapped + ((b * 2 + ph.carrier) * H + r) * (long)n;
+        for (int i = threadIdx.x; i < n; i += MR_THREADS) {
+            const float2 a = b0[i];
+            float d = th[i] - atan2f(a.y, a.x);
+            if (d > kPiF) d -= kTwoPiF;
+            else if (d < -kPiF) d += kTwoPiF;
+            wo[i] = d;
+        }
+    }
+}
+
+// [nb][R][C] -> [nb][C][R], 32 x 32 tiles through LDS (odd pitch)
+__global__ __launch_bounds__(256) void k_mr_transpose(const float2* __restrict__ in, float2* __restrict__ out, int R,
+                                                      int C) {
+    __shared__ float2 tile[32][33];
+    const long b = blockIdx.z;
+    const int r0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
+    const float2* src = in + b * (long)R * C;
+    float2* dst = out + b * (long)R * C;
+    const int tx = threadIdx.x % 32, ty = threadIdx.x / 32;
+    for (int y = ty; y < 32; y += 8)
+        if (r0 + y < R && c0 + tx < C) tile[y][tx] = src[(long)(r0 + y) * C + c0 + tx];
+    __syncthreads();
+    for (int y = ty; y < 32; y += 8)
+        if (c0 + y < C && r0 + tx < R) dst[(long)(c0 + y) * R + r0 + tx] = tile[tx][y];
+}
+
+template <bool INV, int IN, int OUT>
+void launch_mr(const MrPlan& p, const void* in, void* out, long nrows, int H, float sub, const float2* tw,
+               const PhaseOut* ph, hipStream_t s) {
+    PhaseOut q{};
+    if (ph) q = *ph;
+    const size_t lds = 2 * (size_t)p.n * sizeof(float2);
+    static bool attr = false;
+    if (!attr) {
+        FCD_HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mr_rows<INV, IN, OUT>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024));
+        attr = true;
+    }
+    hipLaunchKernelGGL((k_mr_rows<INV, IN, OUT>), dim3((unsigned)nrows), dim3(MR_THREADS), lds, s, in, out, nrows, H,
+                       sub, p, tw, q);
+    FCD_CHECK_LAUNCH();
+}
+
+}  // namespace
+
+bool mr_supported(int n) {
+    if (n < 64 || n > 4096 || n % 64 != 0) return false;
+    int m = n;
+    for (int d : {2, 3, 5})
+        while (m % d == 0) m /= d;
+    return m == 1;
+}
+
+MrPlan mr_plan(int n) {
+    if (!mr_supported(n)) throw std::runtime_error("mixed-radix plan: unsupported length " + std::to_string(n));
+    MrPlan p{};
+    p.n = n;
+    int m = n, two = 0;
+    while (m % 2 == 0) {
+        m /= 2;
+        ++two;
+    }
+    auto add = [&](int r) { p.fct[p.nf++] = r; };
+    while (two >= 3 && two != 4) {  // 8s, leaving 0, 2 or 4 twos for 4s
+        add(8);
+        two -= 3;
+    }
+    while (two >= 2) {
+        add(4);
+        two -= 2;
+    }
+    while (m % 3 == 0) {
+        add(3);
+        m /= 3;
+    }
+    while (m % 5 == 0) {
+        add(5);
+        m /= 5;
+    }
+    if (two != 0 || m != 1 || p.nf > 8) throw std::runtime_error("mixed-radix plan: bad factorisation");
+    return p;
+}
+
+void mr_rows(const MrPlan& p, bool inverse, RowIn im, RowOut om, const void* in, void* out, long nrows, int H,
+             float sub, const float2* tw, const PhaseOut* ph, hipStream_t s) {
+    if (nrows <= 0) return;
+    if (!inverse && im == ROW_IN_REAL && om == ROW_OUT_COMPLEX)
+        launch_mr<false, ROW_IN_REAL, ROW_OUT_COMPLEX>(p, in, out, nrows, H, sub, tw, ph, s);
+    else if (!inverse && im == ROW_IN_COMPLEX && om == ROW_OUT_COMPLEX)
+        launch_mr<false, ROW_IN_COMPLEX, ROW_OUT_COMPLEX>(p, in, out, nrows, H, sub, tw, ph, s);
+    else if (inverse && im == ROW_IN_COMPLEX && om == ROW_OUT_COMPLEX)
+        launch_mr<true, ROW_IN_COMPLEX, ROW_OUT_COMPLEX>(p, in, out, nrows, H, sub, tw, ph, s);
+    else if (inverse && im == ROW_IN_COMPLEX && om == ROW_OUT_REAL)
+        launch_mr<true, ROW_IN_COMPLEX, ROW_OUT_REAL>(p, in, out, nrows, H, sub, tw, ph, s);
+    else if (inverse && im == ROW_IN_COMPLEX && om == ROW_OUT_PHASE)
+        launch_mr<true, ROW_IN_COMPLEX, ROW_OUT_PHASE>(p, in, out, nrows, H, sub, tw, ph, s);
+    else
+        throw std::runtime_error("mr_rows: unsupported mode combination");
+}
+
+void mr_transpose(const float2* in, float2* out, int nb, int R, int C, hipStream_t s) {
+    if (nb <= 0) return;
+    hipLaunchKernelGGL(k_mr_transpose, dim3((unsigned)((C + 31) / 32), (unsigned)((R + 31) / 32), (unsigned)nb),
+                       dim3(256), 0, s, in, out, R, C);
+    FCD_CHECK_LAUNCH();
+}
+
+void mr_cols(const MrPlan& p, int W, bool inverse, float2* data, int nb, const float2* tw, float2* scratch,
+             hipStream_t s) {
+    const int H = p.n;
+    mr_transpose(data, scratch, nb, H, W, s);
+    mr_rows(p, inverse, ROW_IN_COMPLEX, ROW_OUT_COMPLEX, scratch, scratch, (long)nb * W, W, 0.f, tw, nullptr, s);
+    mr_transpose(scratch, data, nb, W, H, s);
+}
+
+}  // namespace fcdk

@@ -6,10 +6,12 @@
 //  * np.mean of float32: 8192-element chunks, each summed pairwise (8 accumulators over
 //    128-element blocks, blocks combined in halves), chunk sums accumulated in order,
 //    one float32 division (k_pf_chunk_sums, k_pf_center);
-//  * scipy.fft.fft2 of a real float32 image: FFTPACK radf4 / radf2 passes over every
-//    row (rfftp, factors 4... with a single 2 first), cfftp pass8 / pass4 / pass2
-//    forward over every column of the half spectrum, the rest filled as conjugate
-//    mirrors (k_pf_rows, k_pf_cols, k_pf_mirror);
+//  * scipy.fft.fft2 of a real float32 image: FFTPACK radf4 / radf2 / radf3 / radf5
+//    passes over every row (rfftp, factors 4... with a single 2 first, then 3s, 5s),
+//    cfftp pass8 / pass4 / pass2 / pass3 / pass5 forward over every column of the half
+//    spectrum, the rest filled as conjugate mirrors (k_pf_rows, k_pf_cols, k_pf_mirror);
+//    even lengths whose odd part is 5-smooth (longer prime factors take pocketfft's
+//    generic / Bluestein passes, not restated);
 //  * np.abs of complex64: larger * sqrt(fma(r, r, 1)), r = smaller / larger (its
 //    AVX512F loop; pf_cabs, used by the candidate kernel in kernels_fft.hip).
 //
@@ -43,11 +45,17 @@ namespace fcdk {
 namespace {
 
 constexpr float kHsqt2 = 0.707106781186547524400844362104849f;  // pocketfft's hsqt2 (T0 = float)
+// radf3 / pass3 and radf5 / pass5 constants (T0 = float)
+constexpr float kTaur = -0.5f, kTaui = 0.8660254037844386467637231707529362f;
+constexpr float kTr11 = 0.3090169943749474241022934171828191f, kTi11 = 0.9510565162951535721164393333793821f;
+constexpr float kTr12 = -0.8090169943749474241022934171828191f, kTi12 = 0.5877852522924731291687059546390728f;
 constexpr int PF_THREADS = 256;
 
 // ------------------------------------------------------------------ np.mean (float32)
 // One workgroup per (8192-element chunk, image): thread t sums 128-element block t with
 // numpy's 8 accumulators, then the blocks combine pairwise (left + right) up the tree.
+// Frame sides are multiples of 64, so every chunk is 8192 elements except a last one of
+// 4096: both 2^k blocks of 128, where numpy's recursive halving is exactly this tree.
 __global__ __launch_bounds__(64) void k_pf_chunk_sums(const float* __restrict__ img, long hw, int nchunks,
                                                        float* __restrict__ sums) {
     __shared__ float blk[64];
@@ -161,6 +169,86 @@ __device__ void radf4(int ido, int l1, const float* cc, float* ch, const float* 
     }
 #undef WA
 #undef CH
+}
+
+__device__ void radf3(int ido, int l1, const float* cc, float* ch, const float* wa) {
+#define CH(a, b, c) ch[(a) + ido * ((b) + 3 * (c))]
+#define WA(x, i) wa[(i) + (x) * (ido - 1)]
+    for (int k = threadIdx.x; k < l1; k += blockDim.x) {
+        const float cr2 = CC(0, k, 1) + CC(0, k, 2);
+        CH(0, 0, k) = CC(0, k, 0) + cr2;
+        CH(0, 2, k) = kTaui * (CC(0, k, 2) - CC(0, k, 1));
+        CH(ido - 1, 1, k) = CC(0, k, 0) + kTaur * cr2;
+    }
+    if (ido == 1) return;
+    const int m = (ido - 1) / 2;
+    for (int it = threadIdx.x; it < l1 * m; it += blockDim.x) {
+        const int k = it / m, i = 2 + 2 * (it % m), ic = ido - i;
+        const float dr2 = WA(0, i - 2) * CC(i - 1, k, 1) + WA(0, i - 1) * CC(i, k, 1);
+        const float di2 = WA(0, i - 2) * CC(i, k, 1) - WA(0, i - 1) * CC(i - 1, k, 1);
+        const float dr3 = WA(1, i - 2) * CC(i - 1, k, 2) + WA(1, i - 1) * CC(i, k, 2);
+        const float di3 = WA(1, i - 2) * CC(i, k, 2) - WA(1, i - 1) * CC(i - 1, k, 2);
+        const float cr2 = dr2 + dr3, ci2 = di2 + di3;
+        CH(i - 1, 0, k) = CC(i - 1, k, 0) + cr2;
+        CH(i, 0, k) = CC(i, k, 0) + ci2;
+        const float tr2 = CC(i - 1, k, 0) + kTaur * cr2, ti2 = CC(i, k, 0) + kTaur * ci2;
+        const float tr3 = kTaui * (di2 - di3), ti3 = kTaui * (dr3 - dr2);
+        CH(i - 1, 2, k) = tr2 + tr3;
+        CH(ic - 1, 1, k) = tr2 - tr3;
+        CH(i, 2, k) = ti3 + ti2;
+        CH(ic, 1, k) = ti3 - ti2;
+    }
+#undef WA
+#undef CH
+}
+
+__device__ void radf5(int ido, int l1, const float* cc, float* ch, const float* wa) {
+#define CH(a, b, c) ch[(a) + ido * ((b) + 5 * (c))]
+#define WA(x, i) wa[(i) + (x) * (ido - 1)]
+    for (int k = threadIdx.x; k < l1; k += blockDim.x) {
+        const float cr2 = CC(0, k, 4) + CC(0, k, 1), ci5 = CC(0, k, 4) - CC(0, k, 1);
+        const float cr3 = CC(0, k, 3) + CC(0, k, 2), ci4 = CC(0, k, 3) - CC(0, k, 2);
+        CH(0, 0, k) = CC(0, k, 0) + cr2 + cr3;
+        CH(ido - 1, 1, k) = CC(0, k, 0) + kTr11 * cr2 + kTr12 * cr3;
+        CH(0, 2, k) = kTi11 * ci5 + kTi12 * ci4;
+        CH(ido - 1, 3, k) = CC(0, k, 0) + kTr12 * cr2 + kTr11 * cr3;
+        CH(0, 4, k) = kTi12 * ci5 - kTi11 * ci4;
+    }
+    if (ido == 1) return;
+    const int m = (ido - 1) / 2;
+    for (int it = threadIdx.x; it < l1 * m; it += blockDim.x) {
+        const int k = it / m, i = 2 + 2 * (it % m), ic = ido - i;
+        const float dr2 = WA(0, i - 2) * CC(i - 1, k, 1) + WA(0, i - 1) * CC(i, k, 1);
+        const float di2 = WA(0, i - 2) * CC(i, k, 1) - WA(0, i - 1) * CC(i - 1, k, 1);
+        const float dr3 = WA(1, i - 2) * CC(i - 1, k, 2) + WA(1, i - 1) * CC(i, k, 2);
+        const float di3 = WA(1, i - 2) * CC(i, k, 2) - WA(1, i - 1) * CC(i - 1, k, 2);
+        const float dr4 = WA(2, i - 2) * CC(i - 1, k, 3) + WA(2, i - 1) * CC(i, k, 3);
+        const float di4 = WA(2, i - 2) * CC(i, k, 3) - WA(2, i - 1) * CC(i - 1, k, 3);
+        const float dr5 = WA(3, i - 2) * CC(i - 1, k, 4) + WA(3, i - 1) * CC(i, k, 4);
+        const float di5 = WA(3, i - 2) * CC(i, k, 4) - WA(3, i - 1) * CC(i - 1, k, 4);
+        const float cr2 = dr5 + dr2, ci5 = dr5 - dr2;
+        const float ci2 = di2 + di5, cr5 = di2 - di5;
+        const float cr3 = dr4 + dr3, ci4 = dr4 - dr3;
+        const float ci3 = di3 + di4, cr4 = di3 - di4;
+        CH(i - 1, 0, k) = CC(i - 1, k, 0) + cr2 + cr3;
+        CH(i, 0, k) = CC(i, k, 0) + ci2 + ci3;
+        const float tr2 = CC(i - 1, k, 0) + kTr11 * cr2 + kTr12 * cr3;
+        const float ti2 = CC(i, k, 0) + kTr11 * ci2 + kTr12 * ci3;
+        const float tr3 = CC(i - 1, k, 0) + kTr12 * cr2 + kTr11 * cr3;
+        const float ti3 = CC(i, k, 0) + kTr12 * ci2 + kTr11 * ci3;
+        const float tr5 = cr5 * kTi11 + cr4 * kTi12, tr4 = cr5 * kTi12 - cr4 * kTi11;
+        const float ti5 = ci5 * kTi11 + ci4 * kTi12, ti4 = ci5 * kTi12 - ci4 * kTi11;
+        CH(i - 1, 2, k) = tr2 + tr5;
+        CH(ic - 1, 1, k) = tr2 - tr5;
+        CH(i, 2, k) = ti5 + ti2;
+        CH(ic, 1, k) = ti5 - ti2;
+        CH(i - 1, 4, k) = tr3 + tr4;
+        CH(ic - 1, 3, k) = tr3 - tr4;
+        CH(i, 4, k) = ti4 + ti3;
+        CH(ic, 3, k) = ti4 - ti3;
+    }
+#undef WA
+#undef CH
 #undef CC
 }
 
@@ -180,8 +268,12 @@ __global__ __launch_bounds__(PF_THREADS) void k_pf_rows(const float* __restrict_
         l1 /= ip;
         if (ip == 4)
             radf4(ido, l1, p1, p2, tw + plan.tw[k]);
-        else
+        else if (ip == 2)
             radf2(ido, l1, p1, p2, tw + plan.tw[k]);
+        else if (ip == 3)
+            radf3(ido, l1, p1, p2, tw + plan.tw[k]);
+        else
+            radf5(ido, l1, p1, p2, tw + plan.tw[k]);
         __syncthreads();
         float* t = p1;
         p1 = p2;
@@ -221,7 +313,40 @@ __device__ void cpass(int ip, int ido, int l1, const float2* cc, float2* ch, con
 #define WA(x, i) wa[(i) - 1 + (x) * (ido - 1)]
     for (int it = threadIdx.x; it < l1 * ido; it += blockDim.x) {
         const int k = it / ido, i = it % ido;
-        if (ip == 2) {
+        if (ip == 3) {  // pass3<fwd>: tw1r = -1/2, tw1i = -sqrt(3)/2
+            const float2 t0 = CC(i, 0, k), t1 = cadd(CC(i, 1, k), CC(i, 2, k)), t2 = csub(CC(i, 1, k), CC(i, 2, k));
+            CH(i, k, 0) = cadd(t0, t1);
+            const float tw1i = -kTaui;
+            const float2 ca = make_float2(t0.x + t1.x * kTaur, t0.y + t1.y * kTaur);
+            const float2 cb = make_float2(-(t2.y * tw1i), t2.x * tw1i);
+            if (i == 0) {
+                CH(i, k, 1) = cadd(ca, cb);
+                CH(i, k, 2) = csub(ca, cb);
+            } else {
+                CH(i, k, 1) = cmulc(cadd(ca, cb), WA(0, i));
+                CH(i, k, 2) = cmulc(csub(ca, cb), WA(1, i));
+            }
+        } else if (ip == 5) {  // pass5<fwd>: tw1i = -sin(2 pi / 5), tw2i = -sin(4 pi / 5)
+            const float2 t0 = CC(i, 0, k);
+            const float2 t1 = cadd(CC(i, 1, k), CC(i, 4, k)), t4 = csub(CC(i, 1, k), CC(i, 4, k));
+            const float2 t2 = cadd(CC(i, 2, k), CC(i, 3, k)), t3 = csub(CC(i, 2, k), CC(i, 3, k));
+            CH(i, k, 0) = make_float2(t0.x + t1.x + t2.x, t0.y + t1.y + t2.y);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {  // (u1, u2) = (1, 4), then (2, 3)
+                const int u1 = h ? 2 : 1, u2 = h ? 3 : 4;
+                const float twar = h ? kTr12 : kTr11, twbr = h ? kTr11 : kTr12;
+                const float twai = h ? -kTi12 : -kTi11, twbi = h ? kTi11 : -kTi12;
+                const float2 ca = make_float2(t0.x + twar * t1.x + twbr * t2.x, t0.y + twar * t1.y + twbr * t2.y);
+                const float2 cb = make_float2(-(twai * t4.y + twbi * t3.y), twai * t4.x + twbi * t3.x);
+                if (i == 0) {
+                    CH(i, k, u1) = cadd(ca, cb);
+                    CH(i, k, u2) = csub(ca, cb);
+                } else {
+                    CH(i, k, u1) = cmulc(cadd(ca, cb), WA(u1 - 1, i));
+                    CH(i, k, u2) = cmulc(csub(ca, cb), WA(u2 - 1, i));
+                }
+            }
+        } else if (ip == 2) {
             CH(i, k, 0) = cadd(CC(i, 0, k), CC(i, 1, k));
             const float2 d = csub(CC(i, 0, k), CC(i, 1, k));
             CH(i, k, 1) = i == 0 ? d : cmulc(d, WA(0, i));
@@ -328,7 +453,7 @@ __global__ void k_pf_mirror(float2* __restrict__ F, int H, int W, long n) {
     const int i = (int)(idx / W), j = (int)(idx % W);
     float2* f = F + b * hw;
     if (j > W / 2) {
-        const float2 v = f[(long)((H - i) & (H - 1)) * W + (W - j)];
+        const float2 v = f[(long)((H - i) % H) * W + (W - j)];
         f[idx] = make_float2(v.x, -v.y);
     } else if (j == 0 || j == W / 2) {
         if (i > H / 2) {
