@@ -767,7 +767,8 @@ def test_device_labelling_matches_host(lib, monkeypatch, golden):
 
 @pytest.mark.parametrize("rows,cols", [(512, 1024), (1024, 512), (256, 128)])
 def test_non_square_frames_vs_oracle(lib, golden, rows, cols):
-    """H != W (the reference takes any frame shape; the engine any power-of-two pair): a
+    """H != W (the reference takes any frame shape; the engine any pair of 5-smooth multiples
+    of 64, powers of two here; test_gpu_mixed.py for the others): a
     crop of the 10-bit camera pair through the whole pipeline against the oracle."""
     from oracle import fcd_oracle as O
     from pyfcd.fcd import fcd
