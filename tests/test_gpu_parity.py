@@ -222,7 +222,18 @@ def test_unwrap_two_level_equals_pixel_rounds(lib, monkeypatch, shape):
         k1, _ = eng.unwrap(w)
         assert np.array_equal(k1, k2), (tile, "boundary lists")
         monkeypatch.delenv("FCD_MST_LEVEL")
+        monkeypatch.setenv("FCD_T0_ROUNDS", "1")  # the capped tile pass on the other shapes
+        k1, _ = eng.unwrap(w)
+        assert np.array_equal(k1, k2), (tile, "capped")
+        monkeypatch.delenv("FCD_T0_ROUNDS")
     monkeypatch.delenv("FCD_MST_TILE")
+    # tile passes capped after 0 / 1 / 2 hook rounds (the noisiest maps' tiles keep going
+    # until they hold at most cg_ccap components) and uncapped
+    for cap in ("0", "1", "2", "99"):
+        monkeypatch.setenv("FCD_T0_ROUNDS", cap)
+        k1, _ = eng.unwrap(w)
+        assert np.array_equal(k1, k2), ("cap", cap)
+    monkeypatch.delenv("FCD_T0_ROUNDS")
     for level in ("0", "1", "2"):  # all-pixel rounds; pixel round / tiles before the list rounds
         monkeypatch.setenv("FCD_MST_LEVEL", level)
         k1, _ = eng.unwrap(w)

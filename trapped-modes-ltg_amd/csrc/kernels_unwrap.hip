@@ -47,6 +47,9 @@ constexpr double kBorderRel = 9999999.0;
 #ifndef FCD_MST_TILE_DEFAULT
 #define FCD_MST_TILE_DEFAULT 64  // tile pass shape code (mst_tile_shape)
 #endif
+#ifndef FCD_T0_ROUNDS_DEFAULT
+#define FCD_T0_ROUNDS_DEFAULT 2  // tile hook rounds before the cap (k_mst_tile0); large: none
+#endif
 
 // find_wrap of the reference unwrapper: -1 if w1 - w2 > pi, +1 if < -pi.
 __device__ __forceinline__ int find_wrap(float a, float b) {
@@ -78,38 +81,58 @@ __device__ __forceinline__ int find_wrap_f(float a, float b, bool& amb) {
     return d > P ? -1 : (d < -P ? 1 : 0);
 }
 
-// Residue count per map: 4 plaquettes per thread (4 pixels of a row and the next row, 16-
-// byte loads), 1024 pixels per block, blockIdx.y = map.
+// Residue count per map: each thread walks a strip of kResRows plaquette rows down 4
+// columns (16-byte loads of each row once, the next row's loads issued before the
+// current pair's tests), blockIdx.y = map.
+constexpr int kResRows = 16;
+__device__ __forceinline__ int residues_quad(const float (&ra)[5], const float (&rc)[5], int nk) {
+    bool amb = false;
+    int r = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        // plaquette (i, j + k): a -> b -> c -> d -> a, a = (i, j+k), b = (i, j+k+1), c = (i+1, j+k+1), d = (i+1, j+k)
+        const int s = find_wrap_f(ra[k], ra[k + 1], amb) + find_wrap_f(ra[k + 1], rc[k + 1], amb) +
+                      find_wrap_f(rc[k + 1], rc[k], amb) + find_wrap_f(rc[k], ra[k], amb);
+        r += k < nk && s != 0;
+    }
+    if (amb) {  // some difference is exactly fl(pi) apart: the f64 tests for this quad
+        r = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            r += k < nk && (find_wrap(ra[k], ra[k + 1]) + find_wrap(ra[k + 1], rc[k + 1]) + find_wrap(rc[k + 1], rc[k]) +
+                            find_wrap(rc[k], ra[k])) != 0;
+    }
+    return r;
+}
+
 __global__ __launch_bounds__(256) void k_residues(const float* __restrict__ w, int H, int W, int* counts) {
     const int map = blockIdx.y;
-    // XCD-aware: consecutive row blocks on one XCD (xcd_block), so the row a block shares
-    // with the next one comes from that XCD's L2
-    const unsigned G = gridDim.x, bx = blockIdx.x;
-    const int vb = (G % 8 == 0) ? (int)((bx % 8) * (G / 8) + bx / 8) : (int)bx;
-    const int p = vb * 1024 + 4 * threadIdx.x;  // first pixel of this thread (W % 4 == 0)
-    const int i = p / W, j = p % W;
+    const int q = W / 4;  // column quads per row (W % 4 == 0)
+    const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+    const int strip = (int)(idx / q), j = (int)(idx % q) * 4;
+    const int i0 = strip * kResRows, i1 = min(i0 + kResRows, H - 1);  // plaquette rows [i0, i1)
     int r = 0;
-    if (p < H * W && i < H - 1) {
-        const float* m = w + (long)map * H * W + p;
-        const float4 a = *reinterpret_cast<const float4*>(m), c = *reinterpret_cast<const float4*>(m + W);
+    if (i0 < i1) {
+        const float* m = w + (long)map * H * W + (long)i0 * W + j;
         const bool last = j + 4 >= W;  // the row's last plaquette column is j + 2
-        const float an = last ? 0.f : m[4], cn = last ? 0.f : m[W + 4];
-        const float ra[5] = {a.x, a.y, a.z, a.w, an}, rc[5] = {c.x, c.y, c.z, c.w, cn};
         const int nk = last ? 3 : 4;
-        bool amb = false;
+        auto load = [&](const float* p, float (&v)[5]) {
+            const float4 a = *reinterpret_cast<const float4*>(p);
+            v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+            v[4] = last ? 0.f : p[4];
+        };
+        float ra[5], rc[5], rn[5] = {};
+        load(m, ra);
+        load(m + W, rc);
+        for (int i = i0; i < i1; ++i) {
+            if (i + 2 <= i1) load(m + 2L * W, rn);  // row i + 2 (the next pair's lower row)
+            r += residues_quad(ra, rc, nk);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            // plaquette (i, j + k): a -> b -> c -> d -> a, a = (i, j+k), b = (i, j+k+1), c = (i+1, j+k+1), d = (i+1, j+k)
-            const int s = find_wrap_f(ra[k], ra[k + 1], amb) + find_wrap_f(ra[k + 1], rc[k + 1], amb) +
-                          find_wrap_f(rc[k + 1], rc[k], amb) + find_wrap_f(rc[k], ra[k], amb);
-            r += k < nk && s != 0;
-        }
-        if (amb) {  // some difference is exactly fl(pi) apart: the f64 tests for this thread
-            r = 0;
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                r += k < nk && (find_wrap(ra[k], ra[k + 1]) + find_wrap(ra[k + 1], rc[k + 1]) + find_wrap(rc[k + 1], rc[k]) +
-                                find_wrap(rc[k], ra[k])) != 0;
+            for (int k = 0; k < 5; ++k) {
+                ra[k] = rc[k];
+                rc[k] = rn[k];
+            }
+            m += W;
         }
     }
     // one atomic per block with residues: a map's count word takes one add per block
@@ -128,7 +151,8 @@ __global__ __launch_bounds__(256) void k_residues(const float* __restrict__ w, i
 void residues(const float* w, int nmaps, int H, int W, int* counts, hipStream_t s) {
     FCD_HIPCHK(hipMemsetAsync(counts, 0, sizeof(int) * nmaps, s));
     if (W % 4 != 0) throw std::runtime_error("residues: W must be a multiple of 4");
-    hipLaunchKernelGGL(k_residues, dim3((unsigned)(((long)H * W + 1023) / 1024), (unsigned)nmaps), dim3(256), 0, s, w, H, W,
+    const long threads = (long)(H - 1 + kResRows - 1) / kResRows * (W / 4);
+    hipLaunchKernelGGL(k_residues, dim3((unsigned)((threads + 255) / 256), (unsigned)nmaps), dim3(256), 0, s, w, H, W,
                        counts);
     FCD_CHECK_LAUNCH();
 }
@@ -851,10 +875,11 @@ __device__ __forceinline__ int t0_off(unsigned l) { return (int)(short)(l & 0xff
 // components only the lightest (weight, edge index) can be in it, by the cycle property
 // of the contracted graph).  When a tile's Boruvka stops, every component's lightest
 // edge leaves the tile, so every component holds a tile-border pixel: V <= 2 (TW + TH) - 4
-// components, and the contracted tile graph is planar, so at most 3 V - 6 distinct
-// adjacent pairs inside the tile, plus the TH + TW edges leaving it to the right and
-// downwards (the other two sides are the neighbours' right / down edges).  Hence the
-// fixed per-tile capacities below and an LDS hash table that never fills.
+// components (a tile stopped by the round cap checks V <= cg_ccap itself), and the
+// contracted tile graph is planar, so at most 3 V - 6 distinct adjacent pairs inside the
+// tile, plus the TH + TW edges leaving it to the right and downwards (the other two sides
+// are the neighbours' right / down edges).  Hence the fixed per-tile capacities below and
+// an LDS hash table that never fills.
 //
 // Per tile tg (= blockIdx.x of the tile pass): components tg * cg_ccap + rank, edges in
 // [tg * cg_ecap, + cg_ecnt[tg]) as records (ea, eb, weight bits, global edge index,
@@ -921,8 +946,9 @@ __device__ __forceinline__ void tile0_graph(unsigned char* pool, const unsigned 
     const long eb0 = tg * ECAP;
     const int nh = H * (W - 1);
     // Round 0 of the component-graph rounds comes out of the tile's last round: every
-    // component's lightest outgoing edge (all of them leave the tile) is its minimum
-    // (bw, be) there, be as a local edge code (t0_hcode / t0_vcode).
+    // component's lightest outgoing edge (after a full run all of them leave the tile;
+    // after a capped one some end inside it) is its minimum (bw, be) there, be as a local
+    // edge code (t0_hcode / t0_vcode).
     const unsigned long long* const bw = reinterpret_cast<const unsigned long long*>(pool);
     const int* const be = reinterpret_cast<const int*>(pool + 8 * T0N);
     unsigned long long rbw[4];
@@ -1071,9 +1097,19 @@ __device__ __forceinline__ void tile0_graph(unsigned char* pool, const unsigned 
     }
 }
 
+// cap (CG only): after `cap` hook rounds the tile stops as soon as it holds at most
+// cg_ccap components, its last candidates (every component's lightest edge, inside the
+// tile or leaving it) becoming round 0 of the component-graph rounds.  The components
+// are MST subtrees after any number of rounds, so the tree is the same; the late tile
+// rounds (few hooks, a full round's barriers and atomics each) move to the contracted
+// graph, which is then only a few per cent larger (tools/diag/t0_rounds_sim.py on the
+// camera frames: 17.0 k components and 32 k tile pairs per map after the full run,
+// 17.6 k / 33 k after 3 rounds, 20.5 k / 42 k after 2).  At most cg_ccap components
+// keep the capacities: the contracted tile graph is planar (a minor of the grid), so
+// at most 3 V - 6 pairs.
 template <int TW, int TH, bool CG>
 __global__ __launch_bounds__(TW * TH / 4, 4) void k_mst_tile0(const float* __restrict__ w, const int* __restrict__ map_ids,
-                                                          int nact, int H, int W, MstWork m) {
+                                                          int nact, int H, int W, MstWork m, int cap) {
     constexpr int T0N = TW * TH;  // pixels per tile
     constexpr int T0W = TW + 4;   // wrapped-phase image with a 2-pixel halo
     constexpr int T0R = TW + 2;   // reliabilities with a 1-pixel halo
@@ -1174,11 +1210,14 @@ __global__ __launch_bounds__(TW * TH / 4, 4) void k_mst_tile0(const float* __res
         bw[i] = 0x7ff0000000000000ull;
         be[i] = 0x7fffffff;
     }
+    __shared__ int t0roots[2];  // the capped rounds' component counts (by round parity)
+    if (threadIdx.x == 0) t0roots[0] = t0roots[1] = 0;
     __syncthreads();
     T0_STAMP(1);
     [[maybe_unused]] int nrounds = 0;
     for (;;) {
         ++nrounds;
+        const bool capped = CG && nrounds > cap;  // block-uniform
         // (a) each pixel's lightest edge to another tile component or out of the tile
         // (the five component labels loaded unconditionally, then selects)
         unsigned long long key[4];
@@ -1216,6 +1255,13 @@ __global__ __launch_bounds__(TW * TH / 4, 4) void k_mst_tile0(const float* __res
             // 13.67 -> 13.9 ms per 96 frames, r03cg6)
             if (bk != ~0ull) atomicMin(bw + c, bk);
         }
+        if (capped) {  // count this round's components (one LDS atomic per wave)
+            int tot = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) tot += __popcll(__ballot(cs[k] == (int)threadIdx.x + NT * k));
+            if ((threadIdx.x & 63) == 0) atomicAdd(&t0roots[nrounds & 1], tot);
+            if (threadIdx.x == 0) t0roots[(nrounds + 1) & 1] = 0;  // read two rounds ago, added to next round
+        }
         __syncthreads();
         T0_STAMP(2);
 #pragma unroll
@@ -1223,6 +1269,8 @@ __global__ __launch_bounds__(TW * TH / 4, 4) void k_mst_tile0(const float* __res
             if (key[k] != ~0ull && key[k] == bw[cs[k]]) atomicMin(be + cs[k], ke[k]);
         __syncthreads();
         T0_STAMP(3);
+        // (the minima are final: with few enough components they are round 0 of the graph)
+        if (capped && t0roots[nrounds & 1] <= cg_ccap(TW, TH)) break;
         // (c) hooks: the pixel holding its component's lightest edge (unique: weight,
         // then edge code) decides, if that edge ends inside the tile, and leaves the link
         // in the component's (no longer needed) minimum slot, marked by bit 63 (a weight's
@@ -1503,7 +1551,10 @@ void mst_tile_level0(const float* w, const int* map_ids, int nact, int H, int W,
     if (!tw) throw std::runtime_error("mst_tile_level0: frame not a multiple of the tile");
     const dim3 g((unsigned)((long)nact * (H / th) * (W / tw)));
     const dim3 b((unsigned)(tw * th / 4));
-#define FCD_T0_LAUNCH(TW, TH, CG) hipLaunchKernelGGL((k_mst_tile0<TW, TH, CG>), g, b, 0, s, w, map_ids, nact, H, W, m)
+    // FCD_T0_ROUNDS (A/B override, read per call): the tile rounds before the cap applies
+    const char* e = std::getenv("FCD_T0_ROUNDS");
+    const int cap = e ? std::atoi(e) : FCD_T0_ROUNDS_DEFAULT;
+#define FCD_T0_LAUNCH(TW, TH, CG) hipLaunchKernelGGL((k_mst_tile0<TW, TH, CG>), g, b, 0, s, w, map_ids, nact, H, W, m, cap)
     if (tw == 64 && th == 64) {
         if (graph) FCD_T0_LAUNCH(64, 64, true);
         else FCD_T0_LAUNCH(64, 64, false);
