@@ -38,6 +38,10 @@
 #include "gfft.hpp"
 #include "kernels.hpp"
 
+#ifndef FCD_WIDE_ZT_NT
+#define FCD_WIDE_ZT_NT 0  // A/B: streaming Zt stores at 4096 too
+#endif
+
 namespace fcdk {
 
 namespace {
@@ -392,13 +396,20 @@ __global__ __launch_bounds__(WideCfg<W>::THREADS, 1) void k_phase_rows_wide(
             const int c0 = threadIdx.x / ROWS, rl = threadIdx.x % ROWS;
             const float2* src = row_slot(rl, par ^ 1);
             constexpr int JU = NWR == 2 ? 2 : 1;  // join columns in flight (VGPRs at 4096)
+            auto zst = [](float2* p, float2 v) {
+                // at 4096 a tile's part of a Zt column run is 16 bytes (2 of the 4 rows):
+                // streaming stores write each half-run on its own (PMC: 279 MB written per
+                // 134 MB of Zt); plain stores let the L2 join it with the next tile's half
+                if constexpr (C::ROWS * 8 >= 32 || FCD_WIDE_ZT_NT) st_stream(p, v);
+                else *p = v;
+            };
 #pragma unroll JU
             for (int k = 0; k < 1024 / CPP; ++k) {
                 const int c = c0 + CPP * k;
                 if constexpr (NWR == 2) {
                     const float2 e = src[pad(c)], o = cmul(src[C::HALF + pad(c)], ctw[c]);
-                    st_stream(dst + c * C::ZT + rl, cadd(e, o));
-                    st_stream(dst + (c + 1024) * C::ZT + rl, csub(e, o));
+                    zst(dst + c * C::ZT + rl, cadd(e, o));
+                    zst(dst + (c + 1024) * C::ZT + rl, csub(e, o));
                 } else {
                     const float2 y0 = src[pad(c)];
                     const float2 y1 = cmul(src[C::HALF + pad(c)], ctw[c]);
@@ -406,10 +417,10 @@ __global__ __launch_bounds__(WideCfg<W>::THREADS, 1) void k_phase_rows_wide(
                     const float2 y3 = cmul(src[3 * C::HALF + pad(c)], ctw[2048 + c]);
                     const float2 a = cadd(y0, y2), b = csub(y0, y2), d = cadd(y1, y3), e = csub(y1, y3);
                     const float2 ie = make_float2(e.y, -e.x);  // -i e
-                    st_stream(dst + c * C::ZT + rl, cadd(a, d));
-                    st_stream(dst + (c + 1024) * C::ZT + rl, cadd(b, ie));
-                    st_stream(dst + (c + 2048) * C::ZT + rl, csub(a, d));
-                    st_stream(dst + (c + 3072) * C::ZT + rl, csub(b, ie));
+                    zst(dst + c * C::ZT + rl, cadd(a, d));
+                    zst(dst + (c + 1024) * C::ZT + rl, cadd(b, ie));
+                    zst(dst + (c + 2048) * C::ZT + rl, csub(a, d));
+                    zst(dst + (c + 3072) * C::ZT + rl, csub(b, ie));
                 }
             }
         }
