@@ -317,6 +317,8 @@ fcdk::MstWork mst_work(fcd_ctx* c) {
     fcdk::MstWork m;
     m.comp = c->mst_comp.as<int>();
     m.off = c->mst_off.as<int>();
+    m.crank = c->mst_comp.as<unsigned char>();
+    m.coff = c->mst_off.as<short>();
     m.rel = c->mst_rel.as<double>();
     m.cand_w = c->mst_cw.as<double>();
     m.cand_e = c->mst_ce.as<int>();
@@ -467,7 +469,7 @@ void unwrap_maps(fcd_ctx* c, const float* w, int nmaps, int32_t* k, int* res_hos
         }
         if (fits) {
             if (rounds >= max_rounds) throw FcdError(FCD_E_INTERNAL, "unwrap: Boruvka did not converge");
-            fcdk::mst_level_finalize(c->mst_ids.as<int>(), nact, c->H, c->W, m, k, s);
+            fcdk::mst_cg_finalize(c->mst_ids.as<int>(), nact, c->H, c->W, m, k, s);
             return;
         }
         level = 2;  // the boundary-list rounds need no capacity bound

@@ -188,6 +188,9 @@ struct MstWork {
     // contracted-edge count, the edge records (SoA) in per-tile segments; nhooks[1]:
     // set if a tile's graph did not fit (never, by the planar bound; the host falls back)
     int* cg_ncomp; int* cg_ecnt; int* cg_ea; int* cg_eb; unsigned long long* cg_ew; int* cg_ec; int* cg_ed;
+    // the component-graph path's level-0 labels, compact (aliases of comp / off): per pixel
+    // its component's rank in its tile (< cg_ccap <= 256) and K(pixel) - K(component)
+    unsigned char* crank; short* coff;
 };
 // Maps listed in map_ids (device int[nact]) of the wrapped stack w.
 void mst_init(const float* w, const int* map_ids, int nact, int H, int W, MstWork m, hipStream_t s);
@@ -210,6 +213,8 @@ long mst_cg_edge_capacity(long nv);  // edge records for nv vertices (any tile s
 // Round r of the component-graph Boruvka (r = 0: the candidates come from the tile pass; its
 // hooks resolve the cross-tile edges).
 void mst_cg_round(int nact, int H, int W, MstWork m, int r, hipStream_t s);
+// k of the component-graph path (every level-0 component's offk final)
+void mst_cg_finalize(const int* map_ids, int nact, int H, int W, MstWork m, int32_t* k, hipStream_t s);
 void mst_level_setup(int nact, int H, int W, MstWork m, hipStream_t s);
 void mst_level_round(const float* w, const int* map_ids, int nact, int H, int W, MstWork m, int r, hipStream_t s);
 void mst_level_finalize(const int* map_ids, int nact, int H, int W, MstWork m, int32_t* k, hipStream_t s);

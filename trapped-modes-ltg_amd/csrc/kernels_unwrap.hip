@@ -1070,8 +1070,8 @@ __device__ __forceinline__ void tile0_graph(unsigned char* pool, const unsigned 
         const long v = vbase + (long)(gi0 + li) * W + gj0 + lj;
         const int c = lc[i];
         const int id = cb + rk[c];
-        m.comp[v] = id;
-        m.off[v] = lo[i];
+        m.crank[v] = (unsigned char)rk[c];  // (a rank >= 256 sets the overflow flag below)
+        m.coff[v] = lo[i];
         if (c == i) {  // (its round-0 minimum is written above)
             m.rootof[id] = id;
             m.offk[id] = 0;
@@ -1440,8 +1440,27 @@ __global__ __launch_bounds__(256) void k_cg_cand2(MstWork m, int ntiles, int eca
 // of a mutual pair the larger root hooks onto the smaller.
 // FIRST (round 0, whose minima the tile pass wrote): the edges into a neighbour tile
 // are resolved here (and written back) instead of in k_cg_cand.
+// A pixel's level-0 component id in the component-graph path: its tile's segment base
+// plus its rank there (crank).
+struct CgGeom {
+    int W, tw, th, tiles_x, tiles, ccap;
+    long hw;
+    __device__ __forceinline__ int tile_of(long v) const {
+        const int slot = (int)(v / hw), p = (int)(v % hw);
+        return slot * tiles + (p / W) / th * tiles_x + (p % W) / tw;
+    }
+    __device__ __forceinline__ int comp_of(const MstWork& m, long v) const { return tile_of(v) * ccap + m.crank[v]; }
+};
+
+static CgGeom cg_geom(int H, int W) {
+    int th = 0;
+    const int tw = mst_tile_shape(H, W, &th);
+    if (!tw) throw std::runtime_error("component graph: frame not a multiple of the tile");
+    return CgGeom{W, tw, th, W / tw, (H / th) * (W / tw), cg_ccap(tw, th), (long)H * W};
+}
+
 template <bool FIRST>
-__global__ __launch_bounds__(256) void k_cg_hook(MstWork m, int ntiles, int ecap) {
+__global__ __launch_bounds__(256) void k_cg_hook(MstWork m, int ntiles, int ecap, CgGeom geo) {
     for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const int n = m.cg_ecnt[t];
         const long b0 = (long)t * ecap;
@@ -1455,8 +1474,8 @@ __global__ __launch_bounds__(256) void k_cg_hook(MstWork m, int ntiles, int ecap
                 int ed = m.cg_ed[b0 + i];
                 if (FIRST && b < 0) {
                     const long y = -1 - (long)b;
-                    b = m.comp[y];
-                    ed += m.off[y];
+                    b = geo.comp_of(m, y);
+                    ed += m.coff[y];
                     m.cg_eb[b0 + i] = b;
                     m.cg_ed[b0 + i] = ed;
                 }
@@ -1517,20 +1536,44 @@ void mst_cg_round(int nact, int H, int W, MstWork m, int r, hipStream_t s) {
     if (!tw) throw std::runtime_error("mst_cg_round: frame not a multiple of the tile");
     const int ntiles = nact * (H / th) * (W / tw);
     const int ecap = cg_ecap(tw, th), ccap = cg_ccap(tw, th);
+    const CgGeom geo = cg_geom(H, W);
     FCD_HIPCHK(hipMemsetAsync(m.nhooks, 0, sizeof(int), s));
     const dim3 g((unsigned)std::min(ntiles, 4096)), b(256);
     if (r == 0) {  // the candidates of round 0 came with the tile pass
-        hipLaunchKernelGGL(k_cg_hook<true>, g, b, 0, s, m, ntiles, ecap);
+        hipLaunchKernelGGL(k_cg_hook<true>, g, b, 0, s, m, ntiles, ecap, geo);
         FCD_CHECK_LAUNCH();
     } else {
         hipLaunchKernelGGL(k_cg_cand, g, b, 0, s, m, ntiles, ecap);
         FCD_CHECK_LAUNCH();
         hipLaunchKernelGGL(k_cg_cand2, g, b, 0, s, m, ntiles, ecap);
         FCD_CHECK_LAUNCH();
-        hipLaunchKernelGGL(k_cg_hook<false>, g, b, 0, s, m, ntiles, ecap);
+        hipLaunchKernelGGL(k_cg_hook<false>, g, b, 0, s, m, ntiles, ecap, geo);
         FCD_CHECK_LAUNCH();
     }
     hipLaunchKernelGGL(k_cg_relabel, g, b, 0, s, m, ntiles, ccap);
+    FCD_CHECK_LAUNCH();
+}
+
+// k(v) = K[component] + off(v) - (the same at the map's pixel 0): 4 pixels per thread.
+__global__ __launch_bounds__(256) void k_cg_finalize(const int* __restrict__ map_ids, int nact, MstWork m, CgGeom geo,
+                                                     int32_t* __restrict__ k) {
+    const long v = 4 * ((long)blockIdx.x * blockDim.x + threadIdx.x);
+    if (v >= nact * geo.hw) return;
+    const int slot = (int)(v / geo.hw);
+    const long base = slot * geo.hw;
+    const int kb = m.offk[geo.comp_of(m, base)] + m.coff[base];
+    const int cb = geo.tile_of(v) * geo.ccap;  // 4 pixels of one row of one tile (tw % 4 == 0)
+    const uchar4 r = *reinterpret_cast<const uchar4*>(m.crank + v);
+    const short4 o = *reinterpret_cast<const short4*>(m.coff + v);
+    const int4 kv = make_int4(m.offk[cb + r.x] + o.x - kb, m.offk[cb + r.y] + o.y - kb, m.offk[cb + r.z] + o.z - kb,
+                              m.offk[cb + r.w] + o.w - kb);
+    *reinterpret_cast<int4*>(k + (long)map_ids[slot] * geo.hw + (v - base)) = kv;
+}
+
+void mst_cg_finalize(const int* map_ids, int nact, int H, int W, MstWork m, int32_t* k, hipStream_t s) {
+    const CgGeom geo = cg_geom(H, W);
+    const long n4 = (long)nact * H * W / 4;
+    hipLaunchKernelGGL(k_cg_finalize, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, map_ids, nact, m, geo, k);
     FCD_CHECK_LAUNCH();
 }
 
