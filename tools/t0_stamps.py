@@ -23,14 +23,15 @@ def main():
     eng.process_device(fr.data_ptr(), len(frames), 1.0, True, h.data_ptr())
     torch.cuda.synchronize()
     lib = _lib.load_library()
-    buf = (ctypes.c_ulonglong * (256 * 9))()
+    buf = (ctypes.c_ulonglong * (256 * 13))()
     assert lib.fcd_debug_t0_stamps(buf) == 0
-    a = np.array(buf, dtype=np.float64).reshape(256, 9)
-    names = ["load+rel", "keys+init", "(a) cand", "(b) tie", "(c) hook", "(d) resolve", "(e) relabel", "store"]
-    tot = a[:, :8].sum(axis=1).mean()
+    a = np.array(buf, dtype=np.float64).reshape(256, 13)
+    names = ["load+rel", "keys+init", "(a) cand", "(b) tie", "(c) hook", "(d) resolve", "(e) relabel",
+             "g: minima+hash init", "g: roots", "g: probes+min", "g: code+append", "g: global writes"]
+    tot = a[:, :12].sum(axis=1).mean()
     for i, n in enumerate(names):
         print(f"{n:12s} {a[:, i].mean():10.0f} cycles  {100 * a[:, i].mean() / tot:5.1f} %")
-    print("rounds: mean %.2f min %d max %d" % (a[:, 8].mean(), a[:, 8].min(), a[:, 8].max()))
+    print("rounds: mean %.2f min %d max %d" % (a[:, 12].mean(), a[:, 12].min(), a[:, 12].max()))
 
 
 if __name__ == "__main__":

@@ -50,9 +50,11 @@ struct DemodTables {
 
 // Zt (row spectra of phi0 + i phi1) tile height at W <= 1024: every column
 // segment of a tile is one run of FCD_ZT_1024 * 8 bytes (shared by the fused
-// kernel's write-out, k_int_rows2 and the column kernels).
+// kernel's write-out, k_int_rows2 and the column kernels).  16 rows: a run is one
+// 128-byte line, so k_int_cols reads each line once (8 rows: two columns per line,
+// 1.45x the compulsory reads, PMC r04e; 1.00x with 16, r04n, same step time).
 #ifndef FCD_ZT_1024
-#define FCD_ZT_1024 8
+#define FCD_ZT_1024 16
 #endif
 // Zt keeps the natural column order inside a tile.  (A mirror-paired order, every
 // column next to its Hermitian mirror so that a 128-byte line is exactly the pair one

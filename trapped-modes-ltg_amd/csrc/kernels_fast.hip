@@ -438,10 +438,13 @@ __global__ __launch_bounds__(IntColsCfg<H>::THREADS, IntColsCfg<H>::V) void k_in
     };
     // Items are codes: frame code / CW, column code % CW (valid below NCH).
     //
-    // Zt's 8-row tiles hold a column's rows in 64 bytes, half a 128-byte line whose
-    // other half is the neighbouring column, and items c, c + 1 always share one line
-    // (c even: their direct columns; c odd: their mirror columns W - c - 1, W - c).  So
-    // adjacent items must be read while both halves sit in one XCD's L2.  XCD-AWARE
+    // With 8-row Zt tiles (2048-point columns; 1024 until r04n) a column's rows fill 64
+    // bytes, half a 128-byte line whose other half is the neighbouring column, and items
+    // c, c + 1 always share one line (c even: their direct columns; c odd: their mirror
+    // columns W - c - 1, W - c).  So adjacent items must be read while both halves sit in
+    // one XCD's L2; even so the reads were 1.45x the compulsory bytes at 1024 (PMC r04e),
+    // and 1024-point columns now have 16-row Zt tiles (whole lines per column: 1.00x,
+    // PMC r04n, at the same step time).  XCD-AWARE
     // (dispatch deals block b to XCD b % 8): the items are cut into 8 contiguous
     // regions, one per XCD, and XCD x's blocks walk its region iteration-major -- at
     // iteration i its blocks take consecutive TEAMS-item groups of one stretch of

@@ -850,12 +850,26 @@ void mst_level_finalize(const int* map_ids, int nact, int H, int W, MstWork m, i
 // Tiles of TW x TH = 64 x 64 (4096 pixels, 1024 threads, 65 KB of LDS: one workgroup
 // per CU at 128 VGPRs), 64 x 32 (512 threads, 33 KB: two) or 32 x 32 (256 threads, 17 KB:
 // four); 4 pixels per thread.
+// diagnostic (FCD_T0_STAMPS builds): per-phase cycles of the first 256 tiles (thread 0)
+// and their round counts; phases 7-11 split the graph write-out
 #ifdef FCD_T0_STAMPS
-// diagnostic: per-phase cycles of the first 256 tiles (thread 0) and their round counts
-__device__ unsigned long long g_t0_stamps[256 * 9];
+constexpr int kT0Phases = 12;
+__device__ unsigned long long g_t0_stamps[256 * (kT0Phases + 1)];
 extern "C" __attribute__((visibility("default"))) int fcd_debug_t0_stamps(unsigned long long* out) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_t0_stamps), sizeof(g_t0_stamps)) == hipSuccess ? 0 : -1;
 }
+struct T0Clock {
+    unsigned long long tprev = __builtin_readcyclecounter(), ph[kT0Phases] = {};
+    __device__ __forceinline__ void stamp(int i) {
+        const unsigned long long t = __builtin_readcyclecounter();
+        ph[i] += t - tprev;
+        tprev = t;
+    }
+};
+#else
+struct T0Clock {
+    __device__ __forceinline__ void stamp(int) {}
+};
 #endif
 // Edges of a tile by a local code that keeps the global edge order (horizontal edges
 // first, each kind row-major; li in [-1, TH], lj in [-1, TW] relative to the tile origin):
@@ -928,7 +942,7 @@ __device__ __forceinline__ void wave_append(const bool (&pred)[N], int* lds_coun
 // After the tile's rounds: lc / lo (labels, offsets) valid, the rest of the pool free.
 template <int TW, int TH>
 __device__ __forceinline__ void tile0_graph(unsigned char* pool, const unsigned long long (&ekey)[4][4], unsigned incs,
-                                            int H, int W, int gi0, int gj0, long vbase, MstWork& m) {
+                                            int H, int W, int gi0, int gj0, long vbase, MstWork& m, T0Clock& clk) {
     constexpr int T0N = TW * TH, NT = T0N / 4;
     constexpr int HS = T0N / 2;  // hash slots: >= 2.7x the pairs a tile can have
     constexpr int HB = HS == 2048 ? 11 : (HS == 1024 ? 10 : 9);
@@ -969,6 +983,7 @@ __device__ __forceinline__ void tile0_graph(unsigned char* pool, const unsigned 
         hwt[i] = ~0ull;
     }
     __syncthreads();
+    clk.stamp(7);
     {
         bool root[4];
         int r[4];
@@ -990,6 +1005,7 @@ __device__ __forceinline__ void tile0_graph(unsigned char* pool, const unsigned 
         }
     }
     __syncthreads();
+    clk.stamp(8);
     // Every global store of the write-out comes after the last barrier: a barrier is a
     // workgroup release and would wait for the stores in flight (about a quarter of the
     // tile's time when the comp / off stores preceded the hash phases).
@@ -1047,6 +1063,7 @@ __device__ __forceinline__ void tile0_graph(unsigned char* pool, const unsigned 
     };
     wave_append(cross, &ncnt[1], pos);
     __syncthreads();
+    clk.stamp(9);
 #pragma unroll
     for (int j = 0; j < 8; ++j)
         if (slot[j] >= 0 && hwt[slot[j]] == ekey[j >> 1][2 * (j & 1)]) atomicMin(hcode + slot[j], (unsigned)code_of(j));
@@ -1063,6 +1080,7 @@ __device__ __forceinline__ void tile0_graph(unsigned char* pool, const unsigned 
             if (win[j]) pos[j] = wpos[j];  // an edge is either inside the tile or leaves it
     }
     __syncthreads();
+    clk.stamp(10);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int i = threadIdx.x + NT * k;
@@ -1095,6 +1113,7 @@ __device__ __forceinline__ void tile0_graph(unsigned char* pool, const unsigned 
         m.cg_ecnt[tg] = min(ncnt[1], ECAP);
         if (ncnt[1] > ECAP || ncnt[0] > cg_ccap(TW, TH)) atomicOr(m.nhooks + 1, 1);
     }
+    clk.stamp(11);
 }
 
 // cap (CG only): after `cap` hook rounds the tile stops as soon as it holds at most
@@ -1127,19 +1146,8 @@ __global__ __launch_bounds__(TW * TH / 4, 4) void k_mst_tile0(const float* __res
     float* const ws = reinterpret_cast<float*>(pool);
     double* const rs = reinterpret_cast<double*>(pool + ((T0W * (TH + 4) * 4 + 15) & ~15));
     static_assert(((T0W * (TH + 4) * 4 + 15) & ~15) + T0R * (TH + 2) * 8 <= 16 * T0N, "phases + reliabilities fit the pool");
-#ifdef FCD_T0_STAMPS
-    unsigned long long tprev = __builtin_readcyclecounter(), ph[8] = {};
-#define T0_STAMP(i)                                                \
-    do {                                                           \
-        const unsigned long long t_ = __builtin_readcyclecounter(); \
-        ph[(i)] += t_ - tprev;                                     \
-        tprev = t_;                                                \
-    } while (0)
-#else
-#define T0_STAMP(i) \
-    do {            \
-    } while (0)
-#endif
+    T0Clock clk;
+#define T0_STAMP(i) clk.stamp(i)
     const long hw = (long)H * W;
     const int tiles_x = W / TW, tiles = (H / TH) * tiles_x;
     const int slot = blockIdx.x / tiles, tile = blockIdx.x % tiles;
@@ -1343,7 +1351,7 @@ __global__ __launch_bounds__(TW * TH / 4, 4) void k_mst_tile0(const float* __res
         T0_STAMP(6);
     }
     if constexpr (CG) {
-        tile0_graph<TW, TH>(pool, ekey, incs, H, W, gi0, gj0, vbase, m);
+        tile0_graph<TW, TH>(pool, ekey, incs, H, W, gi0, gj0, vbase, m, clk);
     } else {
     // level-0 components: global ids of the tile roots, offsets to them; candidate
     // slots of every pixel reset for the level rounds
@@ -1360,10 +1368,10 @@ __global__ __launch_bounds__(TW * TH / 4, 4) void k_mst_tile0(const float* __res
     }
     }
 #ifdef FCD_T0_STAMPS
-    T0_STAMP(7);
+    if constexpr (!CG) T0_STAMP(7);
     if (blockIdx.x < 256 && threadIdx.x == 0) {
-        for (int i = 0; i < 8; ++i) g_t0_stamps[blockIdx.x * 9 + i] = ph[i];
-        g_t0_stamps[blockIdx.x * 9 + 8] = nrounds;
+        for (int i = 0; i < kT0Phases; ++i) g_t0_stamps[blockIdx.x * (kT0Phases + 1) + i] = clk.ph[i];
+        g_t0_stamps[blockIdx.x * (kT0Phases + 1) + kT0Phases] = nrounds;
     }
 #endif
 }
