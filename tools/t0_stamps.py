@@ -23,15 +23,16 @@ def main():
     eng.process_device(fr.data_ptr(), len(frames), 1.0, True, h.data_ptr())
     torch.cuda.synchronize()
     lib = _lib.load_library()
-    buf = (ctypes.c_ulonglong * (256 * 13))()
+    buf = (ctypes.c_ulonglong * (256 * 14))()
     assert lib.fcd_debug_t0_stamps(buf) == 0
-    a = np.array(buf, dtype=np.float64).reshape(256, 13)
-    names = ["load+rel", "keys+init", "(a) cand", "(b) tie", "(c) hook", "(d) resolve", "(e) relabel",
-             "g: minima+hash init", "g: roots", "g: probes+min", "g: code+append", "g: global writes"]
-    tot = a[:, :12].sum(axis=1).mean()
+    a = np.array(buf, dtype=np.float64).reshape(256, 14)
+    names = ["reliabilities", "keys+init", "(a) cand", "(b) tie", "(c) hook", "(d) resolve", "(e) relabel",
+             "g: minima+hash init", "g: roots", "g: probes+min", "g: code+append", "g: global writes",
+             "phase loads"]
+    tot = a[:, :12].sum(axis=1).mean() + a[:, 12].mean()
     for i, n in enumerate(names):
         print(f"{n:12s} {a[:, i].mean():10.0f} cycles  {100 * a[:, i].mean() / tot:5.1f} %")
-    print("rounds: mean %.2f min %d max %d" % (a[:, 12].mean(), a[:, 12].min(), a[:, 12].max()))
+    print("rounds: mean %.2f min %d max %d" % (a[:, 13].mean(), a[:, 13].min(), a[:, 13].max()))
 
 
 if __name__ == "__main__":

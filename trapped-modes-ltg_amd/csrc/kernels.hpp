@@ -56,6 +56,17 @@ struct DemodTables {
 #ifndef FCD_ZT_1024
 #define FCD_ZT_1024 16
 #endif
+// Zt layout tile at 4096-point rows (rows per column run; k_int_rows2 holds 4 rows per
+// tile in LDS, the fused wide kernel 2).  16 makes k_int_cols read whole 128-byte lines
+// (1.37x -> 1.00x the compulsory reads, int_cols + c2r 123.6 -> 107.7 us/frame), but the
+// fused wide kernel then writes 16-byte pieces of 8-tile runs: plain stores read every
+// line back (152.9 -> 202.7 us/frame), streaming ones crawl (396.9); c5 3.14k -> 2.83k /
+// 1.78k frames/s (r04q / r04r).  So 4.
+#ifndef FCD_ZT_4096
+#define FCD_ZT_4096 4
+#endif
+// Zt layout: rows per column run at row length W
+__host__ __device__ constexpr int zt_layout(int W) { return W <= 1024 ? FCD_ZT_1024 : (W == 2048 ? 8 : FCD_ZT_4096); }
 // Zt keeps the natural column order inside a tile.  (A mirror-paired order, every
 // column next to its Hermitian mirror so that a 128-byte line is exactly the pair one
 // k_int_cols item reads, cut Zt reads by 30 % but measured slower: kbench r03k1, int_cols

@@ -786,7 +786,7 @@ static void launch_int_cols(const float2* Zt, int W, int nb, const IntegCoef& c,
     const size_t lds = (size_t)C::NLEN * 8 + (size_t)C::TEAMS * C::ROW * 8 + (size_t)H * 8;
     set_lds(k_int_cols<H>, lds);
     const int grid = grid_for(((long)nb * (W / 2 + 1) + C::TEAMS - 1) / C::TEAMS, 4);
-    const int zt = zt_rows(W);
+    const int zt = zt_layout(W);
     const int zts = zt == 16 ? 4 : (zt == 8 ? 3 : 2);
     hipLaunchKernelGGL(k_int_cols<H>, dim3(grid), dim3(C::THREADS), lds, s, Zt, W, nb, c, Ht, tw, zts, colk);
     FCD_CHECK_LAUNCH();

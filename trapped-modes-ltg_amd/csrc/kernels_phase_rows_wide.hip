@@ -24,7 +24,7 @@
 //     wave-local 1024-point group FFT), and the Zt write-out joins the NWR outputs with
 //     one radix-NWR pass, X[k + 1024 j] = sum_h W_NWR^(h j) w^(h k) Y_h[k];
 //   * Zt: the tile writes its rows' parts of the Zt tiles' column runs (8-row Zt tiles
-//     at 2048, 4-row at 4096, int_rows.inc zt_rows); the next tile of the block's
+//     at 2048, FCD_ZT_4096-row at 4096, kernels.hpp zt_layout); the next tiles of the block's
 //     contiguous range writes the rest right after.
 //
 // REF = true (4096 only, once per reference): the band transforms of the reference's
@@ -55,7 +55,7 @@ struct WideCfg {
     static constexpr int ROWS = W == 2048 ? 4 : 2;  // rows per tile
     static constexpr int THREADS = ROWS * RL;       // 512
     static constexpr int G = B / 16, L = W / B;
-    static constexpr int ZT = W == 2048 ? 8 : 4;    // Zt tile height (int_rows.inc zt_rows)
+    static constexpr int ZT = zt_layout(W);         // Zt layout tile height (kernels.hpp)
     static constexpr int SLOT = padded_len(W) + 2;  // row slot (float2), 16-byte multiple
     static constexpr int HALF = padded_len(1024);   // one wave's 1024-point region; pad(k + 1024 h) = pad(k) + h HALF
     static constexpr int SROW = ROWS + 1;           // staged band rows (odd pitch)
@@ -397,10 +397,13 @@ __global__ __launch_bounds__(WideCfg<W>::THREADS, 1) void k_phase_rows_wide(
             const float2* src = row_slot(rl, par ^ 1);
             constexpr int JU = NWR == 2 ? 2 : 1;  // join columns in flight (VGPRs at 4096)
             auto zst = [](float2* p, float2 v) {
-                // at 4096 a tile's part of a Zt column run is 16 bytes (2 of the 4 rows):
-                // streaming stores write each half-run on its own (PMC: 279 MB written per
-                // 134 MB of Zt); plain stores let the L2 join it with the next tile's half
-                if constexpr (C::ROWS * 8 >= 32 || FCD_WIDE_ZT_NT) st_stream(p, v);
+                // at 4096 a tile's part of a Zt column run is 16 bytes (2 rows): streaming
+                // stores write each piece on its own (PMC r04i: 279 MB written per 134 MB of
+                // Zt).  With 4-row runs plain stores let the L2 join it with the next tile's
+                // half (3.09k -> 3.15k frames/s, r04j); with 16-row runs (eight tiles per
+                // line) plain stores cost a read of every line (r04q: reads 206 -> 279 MB),
+                // so those stay streaming
+                if constexpr (C::ROWS * 8 >= 32 || C::ZT != 2 * C::ROWS || FCD_WIDE_ZT_NT) st_stream(p, v);
                 else *p = v;
             };
 #pragma unroll JU

@@ -853,7 +853,7 @@ void mst_level_finalize(const int* map_ids, int nact, int H, int W, MstWork m, i
 // diagnostic (FCD_T0_STAMPS builds): per-phase cycles of the first 256 tiles (thread 0)
 // and their round counts; phases 7-11 split the graph write-out
 #ifdef FCD_T0_STAMPS
-constexpr int kT0Phases = 12;
+constexpr int kT0Phases = 13;
 __device__ unsigned long long g_t0_stamps[256 * (kT0Phases + 1)];
 extern "C" __attribute__((visibility("default"))) int fcd_debug_t0_stamps(unsigned long long* out) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_t0_stamps), sizeof(g_t0_stamps)) == hipSuccess ? 0 : -1;
@@ -1160,6 +1160,7 @@ __global__ __launch_bounds__(TW * TH / 4, 4) void k_mst_tile0(const float* __res
         ws[i] = (gi >= 0 && gi < H && gj >= 0 && gj < W) ? mw[(long)gi * W + gj] : 0.f;
     }
     __syncthreads();
+    T0_STAMP(12);
     // reliabilities of the tile and its 1-pixel halo (k_mst_rel's operation order)
     for (int i = threadIdx.x; i < T0R * (TH + 2); i += NT) {
         const int li = i / T0R, lj = i % T0R;  // ws index (li + 1, lj + 1)
