@@ -149,7 +149,8 @@ void mr_cols(const MrPlan& p, int W, bool inverse, float2* data, int nb, const f
              hipStream_t s);
 
 // out[b] = in[b] * disk (unshifted spectrum index)
-void disk_mask(const float2* in, float2* out, int nbatch, int H, int W, DiskTable t, hipStream_t s);
+// transposed: in / out column-major per image ([b][j][i]: the generic chain's transposed spectra)
+void disk_mask(const float2* in, float2* out, int nbatch, int H, int W, DiskTable t, hipStream_t s, bool transposed = false);
 // theta = atan2(R)  (reference carrier angle)
 void angle(const float2* in, float* out, long n, hipStream_t s);
 // Batched reference setup (fourier.find_peaks for nb images): out[b] = img[b] - mean(img[b])
@@ -237,7 +238,8 @@ void mst_level_finalize(const int* map_ids, int nact, int H, int W, MstWork m, i
 void make_z(const float* w, const int32_t* k, float2* z, int nbatch, int H, int W, hipStream_t s);
 // z = gx + i gy
 void pack_z(const float* gx, const float* gy, float2* z, long n, hipStream_t s);
-void integ_multiply(const float2* Z, float2* Hh, int nbatch, int H, int W, IntegCoef c, hipStream_t s);
+void integ_multiply(const float2* Z, float2* Hh, int nbatch, int H, int W, IntegCoef c, hipStream_t s,
+                    bool transposed = false);
 // phases f32 = w + 2pi k
 void compose_phase(const float* w, const int32_t* k, float* out, long n, hipStream_t s);
 

@@ -217,20 +217,20 @@ void col_fft(int H, int W, bool inverse, float2* data, int nbatch, const float2*
 // mask = ifftshift(disk(peak, R)): unshifted (i, j) is inside iff the shifted
 // (i+H/2, j+W/2) lies in the skimage disk raster (carriers.py:17-20).
 __global__ void k_disk_mask(const float2* __restrict__ in, float2* __restrict__ out, long n, int H, int W,
-                            DiskTable t) {
+                            DiskTable t, bool tr) {
     const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= n) return;
     const long p = idx % ((long)H * W);
-    const int i = (int)(p / W), j = (int)(p % W);
+    const int i = tr ? (int)(p % H) : (int)(p / W), j = tr ? (int)(p / H) : (int)(p % W);
     const int si = (i + H / 2) % H, sj = (j + W / 2) % W;  // (any even side: the generic chain too)
     const int2 rr = reinterpret_cast<const int2*>(t.rows)[sj];
     const bool inside = si >= rr.x && si <= rr.y;
     out[idx] = inside ? in[idx] : make_float2(0.f, 0.f);
 }
 
-void disk_mask(const float2* in, float2* out, int nbatch, int H, int W, DiskTable t, hipStream_t s) {
+void disk_mask(const float2* in, float2* out, int nbatch, int H, int W, DiskTable t, hipStream_t s, bool transposed) {
     const long n = (long)nbatch * H * W;
-    hipLaunchKernelGGL(k_disk_mask, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, in, out, n, H, W, t);
+    hipLaunchKernelGGL(k_disk_mask, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, in, out, n, H, W, t, transposed);
     FCD_CHECK_LAUNCH();
 }
 

@@ -67,16 +67,17 @@ void pack_z(const float* gx, const float* gy, float2* z, long n, hipStream_t s) 
     FCD_CHECK_LAUNCH();
 }
 
+// tr: Z and Hh column-major per image ([b][q][r], the generic chain's transposed spectra)
 __global__ void k_integ_multiply(const float2* __restrict__ Z, float2* __restrict__ Hh, int H, int W, long n,
-                                 IntegCoef c) {
+                                 IntegCoef c, bool tr) {
     const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= n) return;
     const long hw = (long)H * W;
     const long b = idx / hw, p = idx % hw;
-    const int r = (int)(p / W), q = (int)(p % W);
+    const int r = tr ? (int)(p % H) : (int)(p / W), q = tr ? (int)(p / H) : (int)(p % W);
     const int rm = (H - r) % H, qm = (W - q) % W;
     const float2 z = Z[idx];
-    const float2 zm = Z[b * hw + (long)rm * W + qm];
+    const float2 zm = Z[b * hw + (tr ? (long)qm * H + rm : (long)rm * W + qm)];
     // Phi0 = (Z(k) + conj Z(-k)) / 2 ; Phi1 = (Z(k) - conj Z(-k)) / (2i)
     const float2 f0 = make_float2(0.5f * (z.x + zm.x), 0.5f * (z.y - zm.y));
     const float2 dd = make_float2(z.x - zm.x, z.y + zm.y);
@@ -93,9 +94,9 @@ __global__ void k_integ_multiply(const float2* __restrict__ Z, float2* __restric
     Hh[idx] = make_float2(-im, re);
 }
 
-void integ_multiply(const float2* Z, float2* Hh, int nbatch, int H, int W, IntegCoef c, hipStream_t s) {
+void integ_multiply(const float2* Z, float2* Hh, int nbatch, int H, int W, IntegCoef c, hipStream_t s, bool transposed) {
     const long n = (long)nbatch * H * W;
-    hipLaunchKernelGGL(k_integ_multiply, dim3(nblk(n)), dim3(256), 0, s, Z, Hh, H, W, n, c);
+    hipLaunchKernelGGL(k_integ_multiply, dim3(nblk(n)), dim3(256), 0, s, Z, Hh, H, W, n, c, transposed);
     FCD_CHECK_LAUNCH();
 }
 
