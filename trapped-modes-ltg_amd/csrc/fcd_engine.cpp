@@ -189,6 +189,8 @@ struct fcd_ctx {
     bool generic = false;
     fcdk::MrPlan mr_row{}, mr_col{};
     DevBuf mr_scratch;  // the mixed-radix column transforms' transposed copy (chunk frames)
+    DevBuf gb_tables;   // generic chain's band columns (build_demod_tables)
+    int gb_NU = 0;      // columns in either carrier's disk
     hipStream_t own = nullptr;
     DevBuf tw_row, tw_col;        // plain tables exp(-2 pi i m / n) (generic LDS FFT kernels)
     DevBuf twp_row, twp_col;      // pass-major tables (register FFT kernels)
@@ -572,34 +574,56 @@ fcdk::IntegCoef integ_coef(fcd_ctx* c, double a0, double b0, double a1, double b
 // columns and a transpose back, so a transposed spectrum saves half the transposes (10 ->
 // 5 per chunk).  Same transforms, same arithmetic as fft2_real / demod_phases / integrate_z.
 // Buffers: spec (row layout), mr_scratch (transposed spectrum), work.
+// Forward 2-D FFT of the frames kept at the band columns only (the union of both
+// carriers' disk columns, NU of W): rows, gather-transpose of those columns, their column
+// transforms: specT [nb][NU][H].  The demodulation reads no other column of the spectrum.
 void generic_fft2_t(fcd_ctx* c, const float* in, int nb, float2* specT, hipStream_t s) {
     float2* tmp = c->spec.as<float2>();
+    const int* ucols = c->gb_tables.as<int>();
     rows_fft(c, false, fcdk::ROW_IN_REAL, fcdk::ROW_OUT_COMPLEX, in, tmp, (long)nb * c->H, 0.f, nullptr, s);
-    fcdk::mr_transpose(tmp, specT, nb, c->H, c->W, s);
-    fcdk::mr_rows(c->mr_col, false, fcdk::ROW_IN_COMPLEX, fcdk::ROW_OUT_COMPLEX, specT, specT, (long)nb * c->W, c->W, 0.f,
-                  c->tw_col.as<float2>(), nullptr, s);
+    fcdk::mr_gather_cols(tmp, specT, nb, c->H, c->W, ucols, c->gb_NU, s);
+    fcdk::mr_rows(c->mr_col, false, fcdk::ROW_IN_COMPLEX, fcdk::ROW_OUT_COMPLEX, specT, specT, (long)nb * c->gb_NU, c->gb_NU,
+                  0.f, c->tw_col.as<float2>(), nullptr, s);
 }
 
+// Per carrier: the disk-masked band columns [nb][NCc][H], their inverse column
+// transforms, then the inverse row transforms with the phase, whose loads gather the band
+// columns of their row (the other columns of ifft_cols(D * mask) are zero).
 void generic_demod_t(fcd_ctx* c, const float2* specT, int nb, float* wrapped, hipStream_t s) {
     float2* AT = c->work.as<float2>();
-    float2* A = c->spec.as<float2>();
+    const int* g = c->gb_tables.as<int>();
+    const int NU = c->gb_NU, n0 = c->NCc[0], n1 = c->NCc[1];
+    const int* cols[2] = {g + NU, g + NU + n0};
+    const int* uslot[2] = {g + NU + n0 + n1, g + NU + 2 * n0 + n1};
+    const int* colslot = g + NU + 2 * (n0 + n1);
     for (int car = 0; car < 2; ++car) {
+        const int nc = c->NCc[car];
         fcdk::DiskTable t{c->disk_rows.as<int>() + (size_t)car * 2 * c->W};
-        fcdk::disk_mask(specT, AT, nb, c->H, c->W, t, s, true);
-        fcdk::mr_rows(c->mr_col, true, fcdk::ROW_IN_COMPLEX, fcdk::ROW_OUT_COMPLEX, AT, AT, (long)nb * c->W, c->W, 0.f,
-                      c->tw_col.as<float2>(), nullptr, s);
-        fcdk::mr_transpose(AT, A, nb, c->W, c->H, s);
+        fcdk::disk_band_t(specT, AT, nb, c->H, c->W, NU, cols[car], uslot[car], nc, t, s);
+        if (nc > 0)
+            fcdk::mr_rows(c->mr_col, true, fcdk::ROW_IN_COMPLEX, fcdk::ROW_OUT_COMPLEX, AT, AT, (long)nb * nc, nc, 0.f,
+                          c->tw_col.as<float2>(), nullptr, s);
         fcdk::PhaseOut ph{c->theta.as<float>() + (size_t)car * c->hw(), wrapped, car};
-        rows_fft(c, true, fcdk::ROW_IN_COMPLEX, fcdk::ROW_OUT_PHASE, A, nullptr, (long)nb * c->H, 0.f, &ph, s);
+        // the inverse rows gather their band columns themselves (scattering the band into
+        // zero-filled rows first measured 7.68 k vs 8.18 k frames/s at 1024 x 1280, r04w)
+        ph.bslot = colslot + (size_t)car * c->W;
+        ph.bnc = nc;
+        fcdk::mr_rows(c->mr_row, true, fcdk::ROW_IN_BAND, fcdk::ROW_OUT_PHASE, AT, nullptr, (long)nb * c->H, c->H, 0.f,
+                      c->tw_row.as<float2>(), &ph, s);
     }
 }
 
-void generic_integrate_t(fcd_ctx* c, int nb, const fcdk::IntegCoef& k, float* h_out, hipStream_t s) {
+// z of the maps (w + 2 pi k, make_z's arithmetic) built in the row transform's load
+void generic_integrate_t(fcd_ctx* c, int nb, const float* w, const int32_t* kf, const fcdk::IntegCoef& k, float* h_out,
+                         hipStream_t s) {
     float2* Z = c->spec.as<float2>();
     float2* ZT = c->mr_scratch.as<float2>();
     float2* HT = c->work.as<float2>();
     const float2* twc = c->tw_col.as<float2>();
-    rows_fft(c, false, fcdk::ROW_IN_COMPLEX, fcdk::ROW_OUT_COMPLEX, Z, Z, (long)nb * c->H, 0.f, nullptr, s);
+    fcdk::PhaseOut zin{};
+    zin.kin = kf;
+    fcdk::mr_rows(c->mr_row, false, fcdk::ROW_IN_Z, fcdk::ROW_OUT_COMPLEX, w, Z, (long)nb * c->H, c->H, 0.f,
+                  c->tw_row.as<float2>(), &zin, s);
     fcdk::mr_transpose(Z, ZT, nb, c->H, c->W, s);
     fcdk::mr_rows(c->mr_col, false, fcdk::ROW_IN_COMPLEX, fcdk::ROW_OUT_COMPLEX, ZT, ZT, (long)nb * c->W, c->W, 0.f, twc,
                   nullptr, s);
@@ -698,9 +722,34 @@ void build_demod_tables(fcd_ctx* c, hipStream_t s) {
     c->NC = (int)hc_list.size();
     c->NCA = std::max(std::max(c->NCc[0], c->NCc[1]), 1);
     if (c->NC == 0) throw FcdError(FCD_E_NOPEAKS, "carrier disks are empty");
-    if (c->generic) {  // no band-pruned fast path: the generic chain needs no tables
+    if (c->generic) {  // no band-pruned fast path; the generic chain's column subsets
         c->band_B = c->fused_B = 0;
         c->fused_ok = false;
+        // [NU union columns][carrier 0 columns][carrier 1 columns][their union slots (2)]
+        // [colslot: 2 x W] (generic_demod_t)
+        std::vector<int> uslot_of(W, -1), ucols, cols[2], uslot[2];
+        for (int uc = 0; uc < W; ++uc)
+            if (colslot[uc] >= 0 || colslot[(size_t)W + uc] >= 0) {
+                uslot_of[uc] = (int)ucols.size();
+                ucols.push_back(uc);
+            }
+        for (int q = 0; q < 2; ++q) {
+            cols[q].assign(c->NCc[q], 0);
+            uslot[q].assign(c->NCc[q], 0);
+            for (int uc = 0; uc < W; ++uc) {
+                const int n = colslot[(size_t)q * W + uc];
+                if (n < 0) continue;
+                cols[q][n] = uc;
+                uslot[q][n] = uslot_of[uc];
+            }
+        }
+        c->gb_NU = (int)ucols.size();
+        std::vector<int> gb(ucols);
+        for (int q = 0; q < 2; ++q) gb.insert(gb.end(), cols[q].begin(), cols[q].end());
+        for (int q = 0; q < 2; ++q) gb.insert(gb.end(), uslot[q].begin(), uslot[q].end());
+        gb.insert(gb.end(), colslot.begin(), colslot.end());
+        c->gb_tables.ensure(gb.size() * sizeof(int));
+        upload(c->gb_tables.p, gb.data(), gb.size() * sizeof(int), s);
         return;
     }
     c->dt_hc.ensure(hc_list.size() * sizeof(int));
@@ -1428,7 +1477,6 @@ int process_generic(fcd_ctx* c, const void* frames, int format, int n_frames, bo
             fr = c->frames_in.as<float>();
         }
         if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
-        float2* spec = c->spec.as<float2>();
         float* w = c->wrapped.as<float>();
         if ((size_t)nb * hw * sizeof(float2) > c->mr_scratch.bytes)
             throw FcdError(FCD_E_INTERNAL, "mixed-radix scratch too small");
@@ -1444,9 +1492,8 @@ int process_generic(fcd_ctx* c, const void* frames, int format, int n_frames, bo
             for (int i = 0; i < nb; ++i) nres += counts[2 * (size_t)i] || counts[2 * (size_t)i + 1];
         }
         if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
-        fcdk::make_z(w, k, spec, nb, c->H, c->W, s);
         float* hdst = dev && height_out ? height_out + (size_t)f0 * hw : c->out_h.as<float>();
-        generic_integrate_t(c, nb, coef, hdst, s);
+        generic_integrate_t(c, nb, w, k, coef, hdst, s);
         if (c->profiling) {
             HIPCHK(hipEventRecord(c->next_event(), s));
             c->prof_frames += nb;

@@ -12,13 +12,20 @@
 namespace fcdk {
 
 // Row-FFT input / output modes.
-enum RowIn { ROW_IN_COMPLEX = 0, ROW_IN_REAL = 1 };
+// ROW_IN_Z (mr_rows only): z = (w0 + 2 pi k0) + i (w1 + 2 pi k1) of the two maps' rows, in =
+// wrapped [nb][2][H][W], PhaseOut::kin the k-fields (null: none), as make_z
+// ROW_IN_BAND (mr_rows only): row (b, i) of the band columns held transposed, in = [nb][bnc][H]
+// complex, column j = in[b][bslot[j]][i] (bslot[j] < 0: zero)
+enum RowIn { ROW_IN_COMPLEX = 0, ROW_IN_REAL = 1, ROW_IN_Z = 2, ROW_IN_BAND = 3 };
 enum RowOut { ROW_OUT_COMPLEX = 0, ROW_OUT_REAL = 1, ROW_OUT_PHASE = 2 };
 
 struct PhaseOut {          // ROW_OUT_PHASE: w = wrap(theta - atan2(A))
     const float* theta;    // [H][W] reference angle of this carrier
     float* wrapped;        // output base; row r of batch b -> wrapped + ((b*2 + carrier)*H + r)*W
     int carrier;
+    const int32_t* kin = nullptr;  // ROW_IN_Z's k-fields
+    const int* bslot = nullptr;    // ROW_IN_BAND's column slots [W] and their count
+    int bnc = 0;
 };
 
 // Disk band-pass of one carrier (skimage.draw.disk raster in fftshifted
@@ -144,11 +151,17 @@ void mr_rows(const MrPlan& p, bool inverse, RowIn in_mode, RowOut out_mode, cons
              int H, float sub, const float2* tw, const PhaseOut* ph, hipStream_t s);
 // [nb][R][C] -> [nb][C][R]
 void mr_transpose(const float2* in, float2* out, int nb, int R, int C, hipStream_t s);
+// column subset: [nb][R][C] -> [nb][NS][R] (columns cols[])
+void mr_gather_cols(const float2* in, float2* out, int nb, int R, int C, const int* cols, int NS, hipStream_t s);
 // in-place column transforms of [nb][p.n][W] (through scratch: nb * p.n * W complex)
 void mr_cols(const MrPlan& p, int W, bool inverse, float2* data, int nb, const float2* tw, float2* scratch,
              hipStream_t s);
 
 // out[b] = in[b] * disk (unshifted spectrum index)
+// the generic chain's band columns: out[b][k][i] = spec_t[b][uslot[k]][i] inside carrier's disk
+// at unshifted column cols[k], else 0 (spec_t: [nb][NU][H] transposed band spectra)
+void disk_band_t(const float2* spec_t, float2* out, int nbatch, int H, int W, int NU, const int* cols,
+                 const int* uslot, int nc, DiskTable t, hipStream_t s);
 // transposed: in / out column-major per image ([b][j][i]: the generic chain's transposed spectra)
 void disk_mask(const float2* in, float2* out, int nbatch, int H, int W, DiskTable t, hipStream_t s, bool transposed = false);
 // theta = atan2(R)  (reference carrier angle)

@@ -234,6 +234,29 @@ void disk_mask(const float2* in, float2* out, int nbatch, int H, int W, DiskTabl
     FCD_CHECK_LAUNCH();
 }
 
+__global__ void k_disk_band_t(const float2* __restrict__ spec_t, float2* __restrict__ out, long n, int H, int W, int NU,
+                              const int* __restrict__ cols, const int* __restrict__ uslot, int nc, DiskTable t) {
+    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= n) return;
+    const long per = (long)nc * H;
+    const long b = idx / per, p = idx % per;
+    const int k = (int)(p / H), i = (int)(p % H);
+    const int j = cols[k];
+    const int si = (i + H / 2) % H, sj = (j + W / 2) % W;
+    const int2 rr = reinterpret_cast<const int2*>(t.rows)[sj];
+    const bool inside = si >= rr.x && si <= rr.y;
+    out[idx] = inside ? spec_t[(b * NU + uslot[k]) * H + i] : make_float2(0.f, 0.f);
+}
+
+void disk_band_t(const float2* spec_t, float2* out, int nbatch, int H, int W, int NU, const int* cols, const int* uslot,
+                 int nc, DiskTable t, hipStream_t s) {
+    const long n = (long)nbatch * nc * H;
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_disk_band_t, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, spec_t, out, n, H, W, NU, cols,
+                       uslot, nc, t);
+    FCD_CHECK_LAUNCH();
+}
+
 __global__ void k_angle(const float2* __restrict__ in, float* __restrict__ out, long n) {
     const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx < n) out[idx] = atan2f(in[idx].y, in[idx].x);

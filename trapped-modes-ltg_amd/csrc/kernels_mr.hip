@@ -115,6 +115,19 @@ __global__ __launch_bounds__(MR_THREADS) void k_mr_rows(const void* __restrict__
         float2 v;
         if constexpr (IN == ROW_IN_REAL) {
             v = make_float2(static_cast<const float*>(in)[row * n + i] - sub, 0.f);
+        } else if constexpr (IN == ROW_IN_Z) {  // k_make_z's arithmetic
+            const long b = row / H, r = row % H;
+            const long i0 = ((2 * b) * H + r) * n + i, i1 = ((2 * b + 1) * H + r) * n + i;
+            float p0 = static_cast<const float*>(in)[i0], p1 = static_cast<const float*>(in)[i1];
+            if (ph.kin) {
+                p0 = (float)((double)p0 + 6.283185307179586 * (double)ph.kin[i0]);
+                p1 = (float)((double)p1 + 6.283185307179586 * (double)ph.kin[i1]);
+            }
+            v = make_float2(p0, p1);
+        } else if constexpr (IN == ROW_IN_BAND) {
+            const long b = row / H, r = row % H;
+            const int sl = ph.bslot[i];
+            v = sl >= 0 ? static_cast<const float2*>(in)[(b * ph.bnc + sl) * H + r] : make_float2(0.f, 0.f);
         } else {
             v = static_cast<const float2*>(in)[row * n + i];
         }
@@ -233,12 +246,16 @@ void mr_rows(const MrPlan& p, bool inverse, RowIn im, RowOut om, const void* in,
         launch_mr<false, ROW_IN_REAL, ROW_OUT_COMPLEX>(p, in, out, nrows, H, sub, tw, ph, s);
     else if (!inverse && im == ROW_IN_COMPLEX && om == ROW_OUT_COMPLEX)
         launch_mr<false, ROW_IN_COMPLEX, ROW_OUT_COMPLEX>(p, in, out, nrows, H, sub, tw, ph, s);
+    else if (!inverse && im == ROW_IN_Z && om == ROW_OUT_COMPLEX)
+        launch_mr<false, ROW_IN_Z, ROW_OUT_COMPLEX>(p, in, out, nrows, H, sub, tw, ph, s);
     else if (inverse && im == ROW_IN_COMPLEX && om == ROW_OUT_COMPLEX)
         launch_mr<true, ROW_IN_COMPLEX, ROW_OUT_COMPLEX>(p, in, out, nrows, H, sub, tw, ph, s);
     else if (inverse && im == ROW_IN_COMPLEX && om == ROW_OUT_REAL)
         launch_mr<true, ROW_IN_COMPLEX, ROW_OUT_REAL>(p, in, out, nrows, H, sub, tw, ph, s);
     else if (inverse && im == ROW_IN_COMPLEX && om == ROW_OUT_PHASE)
         launch_mr<true, ROW_IN_COMPLEX, ROW_OUT_PHASE>(p, in, out, nrows, H, sub, tw, ph, s);
+    else if (inverse && im == ROW_IN_BAND && om == ROW_OUT_PHASE)
+        launch_mr<true, ROW_IN_BAND, ROW_OUT_PHASE>(p, in, out, nrows, H, sub, tw, ph, s);
     else
         throw std::runtime_error("mr_rows: unsupported mode combination");
 }
@@ -247,6 +264,31 @@ void mr_transpose(const float2* in, float2* out, int nb, int R, int C, hipStream
     if (nb <= 0) return;
     hipLaunchKernelGGL(k_mr_transpose, dim3((unsigned)((C + 31) / 32), (unsigned)((R + 31) / 32), (unsigned)nb),
                        dim3(256), 0, s, in, out, R, C);
+    FCD_CHECK_LAUNCH();
+}
+
+// Column subset (the generic chain's band-pruned column passes): gather [nb][R][C] ->
+// [nb][NS][R] for the columns cols[0..NS), 32 x 32 tiles through LDS.
+__global__ __launch_bounds__(256) void k_mr_gather_cols(const float2* __restrict__ in, float2* __restrict__ out, int R,
+                                                        int C, const int* __restrict__ cols, int NS) {
+    __shared__ float2 tile[32][33];
+    const long b = blockIdx.z;
+    const int r0 = blockIdx.y * 32, s0 = blockIdx.x * 32;
+    const float2* src = in + b * (long)R * C;
+    float2* dst = out + b * (long)NS * R;
+    const int tx = threadIdx.x % 32, ty = threadIdx.x / 32;
+    const int col = s0 + tx < NS ? cols[s0 + tx] : 0;
+    for (int y = ty; y < 32; y += 8)
+        if (r0 + y < R && s0 + tx < NS) tile[y][tx] = src[(long)(r0 + y) * C + col];
+    __syncthreads();
+    for (int y = ty; y < 32; y += 8)
+        if (s0 + y < NS && r0 + tx < R) dst[(long)(s0 + y) * R + r0 + tx] = tile[tx][y];
+}
+
+void mr_gather_cols(const float2* in, float2* out, int nb, int R, int C, const int* cols, int NS, hipStream_t s) {
+    if (nb <= 0 || NS <= 0) return;
+    hipLaunchKernelGGL(k_mr_gather_cols, dim3((unsigned)((NS + 31) / 32), (unsigned)((R + 31) / 32), (unsigned)nb),
+                       dim3(256), 0, s, in, out, R, C, cols, NS);
     FCD_CHECK_LAUNCH();
 }
 
