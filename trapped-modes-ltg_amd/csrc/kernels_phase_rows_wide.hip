@@ -38,10 +38,6 @@
 #include "gfft.hpp"
 #include "kernels.hpp"
 
-#ifndef FCD_WIDE_ZT_NT
-#define FCD_WIDE_ZT_NT 0  // A/B: streaming Zt stores at 4096 too
-#endif
-
 namespace fcdk {
 
 namespace {
@@ -403,7 +399,7 @@ __global__ __launch_bounds__(WideCfg<W>::THREADS, 1) void k_phase_rows_wide(
                 // half (3.09k -> 3.15k frames/s, r04j); with 16-row runs (eight tiles per
                 // line) plain stores cost a read of every line (r04q: reads 206 -> 279 MB),
                 // so those stay streaming
-                if constexpr (C::ROWS * 8 >= 32 || C::ZT != 2 * C::ROWS || FCD_WIDE_ZT_NT) st_stream(p, v);
+                if constexpr (C::ROWS * 8 >= 32 || C::ZT != 2 * C::ROWS) st_stream(p, v);
                 else *p = v;
             };
 #pragma unroll JU

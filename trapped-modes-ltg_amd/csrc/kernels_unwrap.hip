@@ -47,9 +47,6 @@ constexpr double kBorderRel = 9999999.0;
 #ifndef FCD_MST_TILE_DEFAULT
 #define FCD_MST_TILE_DEFAULT 64  // tile pass shape code (mst_tile_shape)
 #endif
-#ifndef FCD_T0_BATCH_LOADS
-#define FCD_T0_BATCH_LOADS 1  // A/B: the tile's phase loads issued together (0: one per loop trip)
-#endif
 #ifndef FCD_T0_REL_UNROLL
 #define FCD_T0_REL_UNROLL 2  // reliability loop trips unrolled (A/B r04t: 1 8.46-8.50k, 2 8.56k, 5 8.39-8.44k frames/s)
 #endif
@@ -1171,28 +1168,21 @@ __global__ __launch_bounds__(TW * TH / 4, 4) void k_mst_tile0(const float* __res
     // All of a thread's loads are issued before the first LDS store (clamped addresses,
     // unconditional loads): as a loop, each trip waited for its load (vmcnt(0) before
     // the ds_write), five HBM round trips in a row, 11 % of the tile (stamps r04p).
-    if constexpr (FCD_T0_BATCH_LOADS) {
-        constexpr int NL = (T0W * (TH + 4) + NT - 1) / NT;
-        float v[NL];
+    constexpr int NL = (T0W * (TH + 4) + NT - 1) / NT;
+    float v[NL];
 #pragma unroll
-        for (int u = 0; u < NL; ++u) {
-            const int i = threadIdx.x + u * NT;
-            const int gi = gi0 - 2 + i / T0W, gj = gj0 - 2 + i % T0W;
-            const int ci = min(max(gi, 0), H - 1), cj = min(max(gj, 0), W - 1);
-            v[u] = mw[(long)ci * W + cj];
-        }
+    for (int u = 0; u < NL; ++u) {
+        const int i = threadIdx.x + u * NT;
+        const int gi = gi0 - 2 + i / T0W, gj = gj0 - 2 + i % T0W;
+        const int ci = min(max(gi, 0), H - 1), cj = min(max(gj, 0), W - 1);
+        v[u] = mw[(long)ci * W + cj];
+    }
 #pragma unroll
-        for (int u = 0; u < NL; ++u) asm volatile("" ::"v"(v[u]));  // (keeps the last load up here)
+    for (int u = 0; u < NL; ++u) asm volatile("" ::"v"(v[u]));  // (keeps the last load up here)
 #pragma unroll
-        for (int u = 0; u < NL; ++u) {
-            const int i = threadIdx.x + u * NT;
-            if (i < T0W * (TH + 4)) ws[i] = v[u];
-        }
-    } else {
-        for (int i = threadIdx.x; i < T0W * (TH + 4); i += NT) {
-            const int gi = gi0 - 2 + i / T0W, gj = gj0 - 2 + i % T0W;
-            ws[i] = (gi >= 0 && gi < H && gj >= 0 && gj < W) ? mw[(long)gi * W + gj] : 0.f;
-        }
+    for (int u = 0; u < NL; ++u) {
+        const int i = threadIdx.x + u * NT;
+        if (i < T0W * (TH + 4)) ws[i] = v[u];
     }
     __syncthreads();
     T0_STAMP(12);
