@@ -564,10 +564,9 @@ def residue_rows(w):
 
 
 # (y0, x0) of dislocation pairs whose residues all fall on plaquette rows 8k - 1,
-# i.e. between two 8-row tiles of the fused kernel, in both carrier maps (found by running
-# the oracle over candidate placements; rechecked on the engine's own phases below).  At
-# 1024 the unfused k_int_rows2 tiles are 16 rows (FCD_ZT_1024): the pairs on rows 207 and
-# 319 sit on its tile edges too.
+# i.e. between two 8-row tiles of the fused kernel and of k_int_rows2, in both carrier maps
+# (found by running the oracle over candidate placements; rechecked on the engine's own
+# phases below)
 SEAM_PAIRS = {1024: [(206.75, 307.2), (207.0, 307.2), (319.5, 358.4), (319.75, 358.4), (487.0, 435.2)],
               2048: [(487.0, 870.4)],
               4096: [(487.0, 870.4), (607.0, 870.4)]}  # 4-row tiles at 4096: rows 4k - 1
