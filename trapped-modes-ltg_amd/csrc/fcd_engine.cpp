@@ -190,6 +190,7 @@ struct fcd_ctx {
     fcdk::MrPlan mr_row{}, mr_col{};
     DevBuf mr_scratch;  // the mixed-radix column transforms' transposed copy (chunk frames)
     DevBuf gb_tables;   // generic chain's band columns (build_demod_tables)
+    DevBuf mst_slot;    // map -> MST slot (-1: not in it) for k_int_rows2 kmode 3
     int gb_NU = 0;      // columns in either carrier's disk
     hipStream_t own = nullptr;
     DevBuf tw_row, tw_col;        // plain tables exp(-2 pi i m / n) (generic LDS FFT kernels)
@@ -399,8 +400,11 @@ int mst_level() {
 // all_mst: every map goes through the MST pass without a residue count (the
 // exact fix-up of frames already known to carry residues; on a residue-free map
 // the MST integration equals the scan, k(0, 0) = 0 in both).
+// mk (nullable): when the component-graph MST runs, its maps' k is left to the caller
+// through *mk (k_int_rows2 kmode 3, no k-field pass; mk->map_slot null otherwise)
 void unwrap_maps(fcd_ctx* c, const float* w, int nmaps, int32_t* k, int* res_host, hipStream_t s,
-                 bool all_mst = false) {
+                 bool all_mst = false, fcdk::MstK* mk = nullptr) {
+    if (mk) mk->map_slot = nullptr;
     std::vector<int> active;
     if (all_mst) {
         for (int i = 0; i < nmaps; ++i) active.push_back(i);
@@ -471,6 +475,14 @@ void unwrap_maps(fcd_ctx* c, const float* w, int nmaps, int32_t* k, int* res_hos
         }
         if (fits) {
             if (rounds >= max_rounds) throw FcdError(FCD_E_INTERNAL, "unwrap: Boruvka did not converge");
+            if (mk) {
+                std::vector<int> slot(nmaps, -1);
+                for (int i = 0; i < nact; ++i) slot[active[i]] = i;
+                c->mst_slot.ensure(slot.size() * sizeof(int));
+                upload(c->mst_slot.p, slot.data(), slot.size() * sizeof(int), s);
+                *mk = fcdk::MstK{m.crank, m.coff, m.offk, c->mst_slot.as<int>(), fcdk::mst_cg_geom(c->H, c->W)};
+                return;
+            }
             fcdk::mst_cg_finalize(c->mst_ids.as<int>(), nact, c->H, c->W, m, k, s);
             return;
         }
@@ -1573,9 +1585,10 @@ int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int f
             fast_demod(c, fr, nb, s);
             int32_t* kf = dev && k_out ? k_out + (size_t)f0 * 2 * hw : c->fk.as<int32_t>();
             counts.assign((size_t)2 * nb, 0);
-            unwrap_maps(c, c->wrapped.as<float>(), 2 * nb, kf, counts.data(), s);
-            fcdk::int_rows(c->W, 2, c->wrapped.as<float>(), nullptr, kf, nullptr, nullptr, c->H, nb, c->Zt.as<float2>(),
-                           c->twp_row.as<float2>(), nullptr, s);
+            fcdk::MstK mk{};
+            unwrap_maps(c, c->wrapped.as<float>(), 2 * nb, kf, counts.data(), s, false, k_out ? nullptr : &mk);
+            fcdk::int_rows(c->W, mk.map_slot ? 3 : 2, c->wrapped.as<float>(), nullptr, kf, nullptr, nullptr, c->H, nb,
+                           c->Zt.as<float2>(), c->twp_row.as<float2>(), nullptr, s, mk.map_slot ? &mk : nullptr);
             fcdk::int_cols(c->H, c->Zt.as<float2>(), c->W, nb, coef, c->Ht.as<float2>(), ic_tw(c), s);
             float* hdst = dev && height_out ? height_out + (size_t)f0 * hw : c->out_h.as<float>();
             fcdk::int_c2r(c->W, c->Ht.as<float2>(), c->H, nb, hdst, c->twp_row.as<float2>(), s);

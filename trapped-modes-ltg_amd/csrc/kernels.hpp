@@ -93,7 +93,8 @@ void demod_phase(int W, const float2* Ab, int H, int nb, int NCA, const DemodTab
 // seam: kmode 1's buffer of the tile ranges' first / last unwrapped rows
 // (int_rows_seam_bytes(W, H, nb) bytes; may be null for kmodes 0 and 2)
 void int_rows(int W, int kmode, const float* w, const int* colk, const int32_t* kin, int32_t* kout, int* rescount,
-              int H, int nb, float2* Zt, const float2* tw, float2* seam, hipStream_t s);
+              int H, int nb, float2* Zt, const float2* tw, float2* seam, hipStream_t s,
+              const struct MstK* mk = nullptr);
 size_t int_rows_seam_bytes(int W, int H, int nb);
 struct IntegCoef;
 // colk (nullable): per (frame, map, row) column-0 unwrap offsets still to be
@@ -203,6 +204,26 @@ inline bool fcd_fused_env(const char* name) {  // FCD_FUSED_2048 / FCD_FUSED_409
 void residues(const float* w, int nmaps, int H, int W, int* counts, hipStream_t s);
 void unwrap_scan(const float* w, int nmaps, int H, int W, int* colk, int32_t* k, hipStream_t s);
 
+// The component-graph path's tile geometry: level-0 component of pixel v (vertex id slot *
+// H * W + pixel) = tile_of(v) * ccap + crank[v]
+struct CgGeom {
+    int W, tw, th, tiles_x, tiles, ccap;
+    long hw;
+    __host__ __device__ __forceinline__ int tile_of(long v) const {
+        const int slot = (int)(v / hw), p = (int)(v % hw);
+        return slot * tiles + (p / W) / th * tiles_x + (p % W) / tw;
+    }
+};
+// k of the maps the component-graph MST unwrapped, read where it is used (k_int_rows2
+// kmode 3) instead of a k-field pass: k(v) = offk[comp(v)] + coff[v] - (the same at the
+// map's pixel 0); map_slot[map] = its MST slot or -1 (then k comes from kin)
+struct MstK {
+    const unsigned char* crank;
+    const short* coff;
+    const int* offk;
+    const int* map_slot;
+    CgGeom geo;
+};
 struct MstWork {
     int* comp; int* off; double* rel; double* cand_w; int* cand_e;
     unsigned long long* best_w; int* best_e; unsigned long long* link; int* nhooks;
@@ -242,6 +263,7 @@ long mst_cg_edge_capacity(long nv);  // edge records for nv vertices (any tile s
 void mst_cg_round(int nact, int H, int W, MstWork m, int r, hipStream_t s);
 // k of the component-graph path (every level-0 component's offk final)
 void mst_cg_finalize(const int* map_ids, int nact, int H, int W, MstWork m, int32_t* k, hipStream_t s);
+CgGeom mst_cg_geom(int H, int W);
 void mst_level_setup(int nact, int H, int W, MstWork m, hipStream_t s);
 void mst_level_round(const float* w, const int* map_ids, int nact, int H, int W, MstWork m, int r, hipStream_t s);
 void mst_level_finalize(const int* map_ids, int nact, int H, int W, MstWork m, int32_t* k, hipStream_t s);

@@ -745,7 +745,11 @@ static int int_rows_grid(int H, int nb) {
 
 template <int W>
 static void launch_int_rows(int kmode, const float* w, const int* colk, const int32_t* kin, int32_t* kout,
-                            int* rescount, int H, int nb, float2* Zt, const float2* tw, float2* seam, hipStream_t s) {
+                            int* rescount, int H, int nb, float2* Zt, const float2* tw, float2* seam, hipStream_t s,
+                            const MstK* mkp) {
+    MstK mk{};
+    if (mkp) mk = *mkp;
+    if (kmode == 3 && !mkp) throw std::runtime_error("int_rows: kmode 3 needs the MST labels");
     using C = IRCfg<W>;
     const size_t lds = C::LDS_BYTES;
     int grid = int_rows_grid<W>(H, nb);
@@ -754,22 +758,26 @@ static void launch_int_rows(int kmode, const float* w, const int* colk, const in
     if (kmode == 0) {
         set_lds(k_int_rows2<W, 0>, lds);
         hipLaunchKernelGGL((k_int_rows2<W, 0>), dim3(grid), dim3(C::THREADS), lds, s, w, colk, kin, kout, rescount, H,
-                           nb, Zt, tw, seam, per);
+                           nb, Zt, tw, seam, per, mk);
     } else if (kmode == 1) {
         if (!seam) throw std::runtime_error("int_rows: the seam census needs a seam buffer");
         grid = (int)((items + per - 1) / per);
         set_lds(k_int_rows2<W, 1>, lds);
         hipLaunchKernelGGL((k_int_rows2<W, 1>), dim3(grid), dim3(C::THREADS), lds, s, w, colk, kin, kout, rescount, H,
-                           nb, Zt, tw, seam, per);
+                           nb, Zt, tw, seam, per, mk);
         if (grid > 1) {
             FCD_CHECK_LAUNCH();
             hipLaunchKernelGGL(k_ir_seam_check<W>, dim3((unsigned)((grid - 1 + 3) / 4)), dim3(256), 0, s, seam, H, nb,
                                per, grid, rescount);
         }
-    } else {
+    } else if (kmode == 2) {
         set_lds(k_int_rows2<W, 2>, lds);
         hipLaunchKernelGGL((k_int_rows2<W, 2>), dim3(grid), dim3(C::THREADS), lds, s, w, colk, kin, kout, rescount, H,
-                           nb, Zt, tw, seam, per);
+                           nb, Zt, tw, seam, per, mk);
+    } else {
+        set_lds(k_int_rows2<W, 3>, lds);
+        hipLaunchKernelGGL((k_int_rows2<W, 3>), dim3(grid), dim3(C::THREADS), lds, s, w, colk, kin, kout, rescount, H,
+                           nb, Zt, tw, seam, per, mk);
     }
     FCD_CHECK_LAUNCH();
 }
@@ -818,8 +826,8 @@ void demod_phase(int W, const float2* Ab, int H, int nb, int NCA, const DemodTab
     FCD_SIZE_SWITCH(W, launch_demod_phase, Ab, H, nb, NCA, T, theta, wrapped, tw, s);
 }
 void int_rows(int W, int kmode, const float* w, const int* colk, const int32_t* kin, int32_t* kout, int* rescount,
-              int H, int nb, float2* Zt, const float2* tw, float2* seam, hipStream_t s) {
-    FCD_SIZE_SWITCH(W, launch_int_rows, kmode, w, colk, kin, kout, rescount, H, nb, Zt, tw, seam, s);
+              int H, int nb, float2* Zt, const float2* tw, float2* seam, hipStream_t s, const MstK* mk) {
+    FCD_SIZE_SWITCH(W, launch_int_rows, kmode, w, colk, kin, kout, rescount, H, nb, Zt, tw, seam, s, mk);
 }
 size_t int_rows_seam_bytes(int W, int H, int nb) {
     size_t b = 0;

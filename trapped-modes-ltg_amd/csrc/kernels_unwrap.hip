@@ -1489,17 +1489,7 @@ __global__ __launch_bounds__(256) void k_cg_cand2(MstWork m, int ntiles, int eca
 // are resolved here (and written back) instead of in k_cg_cand.
 // A pixel's level-0 component id in the component-graph path: its tile's segment base
 // plus its rank there (crank).
-struct CgGeom {
-    int W, tw, th, tiles_x, tiles, ccap;
-    long hw;
-    __device__ __forceinline__ int tile_of(long v) const {
-        const int slot = (int)(v / hw), p = (int)(v % hw);
-        return slot * tiles + (p / W) / th * tiles_x + (p % W) / tw;
-    }
-    __device__ __forceinline__ int comp_of(const MstWork& m, long v) const { return tile_of(v) * ccap + m.crank[v]; }
-};
-
-static CgGeom cg_geom(int H, int W) {
+CgGeom mst_cg_geom(int H, int W) {
     int th = 0;
     const int tw = mst_tile_shape(H, W, &th);
     if (!tw) throw std::runtime_error("component graph: frame not a multiple of the tile");
@@ -1521,16 +1511,17 @@ __global__ __launch_bounds__(256) void k_cg_hook(MstWork m, int ntiles, int ecap
                 int ed = m.cg_ed[b0 + i];
                 if (FIRST && b < 0) {
                     const long y = -1 - (long)b;
-                    b = geo.comp_of(m, y);
+                    b = geo.tile_of(y) * geo.ccap + m.crank[y];
                     ed += m.coff[y];
                     m.cg_eb[b0 + i] = b;
                     m.cg_ed[b0 + i] = ed;
                 }
-                const int ra = m.rootof[a], rb = m.rootof[b];
+                // (round 0: every level-0 component is its own root, offset 0)
+                const int ra = FIRST ? a : m.rootof[a], rb = FIRST ? b : m.rootof[b];
                 const bool wa = m.best_w[ra] == w && m.best_e[ra] == c;
                 const bool wb = m.best_w[rb] == w && m.best_e[rb] == c;
                 if (wa || wb) {
-                    const int kab = ed - m.offk[a] + m.offk[b];  // K_ra - K_rb
+                    const int kab = FIRST ? ed : ed - m.offk[a] + m.offk[b];  // K_ra - K_rb
                     if (wa && (!wb || ra > rb)) m.link[ra] = pack_link(rb, kab);
                     else m.link[rb] = pack_link(ra, -kab);
                     hooked = true;
@@ -1583,7 +1574,7 @@ void mst_cg_round(int nact, int H, int W, MstWork m, int r, hipStream_t s) {
     if (!tw) throw std::runtime_error("mst_cg_round: frame not a multiple of the tile");
     const int ntiles = nact * (H / th) * (W / tw);
     const int ecap = cg_ecap(tw, th), ccap = cg_ccap(tw, th);
-    const CgGeom geo = cg_geom(H, W);
+    const CgGeom geo = mst_cg_geom(H, W);
     FCD_HIPCHK(hipMemsetAsync(m.nhooks, 0, sizeof(int), s));
     const dim3 g((unsigned)std::min((ntiles + 3) / 4, 4096)), b(256);  // 4 tiles per block at a time
     if (r == 0) {  // the candidates of round 0 came with the tile pass
@@ -1608,7 +1599,7 @@ __global__ __launch_bounds__(256) void k_cg_finalize(const int* __restrict__ map
     if (v >= nact * geo.hw) return;
     const int slot = (int)(v / geo.hw);
     const long base = slot * geo.hw;
-    const int kb = m.offk[geo.comp_of(m, base)] + m.coff[base];
+    const int kb = m.offk[geo.tile_of(base) * geo.ccap + m.crank[base]] + m.coff[base];
     const int cb = geo.tile_of(v) * geo.ccap;  // 4 pixels of one row of one tile (tw % 4 == 0)
     const uchar4 r = *reinterpret_cast<const uchar4*>(m.crank + v);
     const short4 o = *reinterpret_cast<const short4*>(m.coff + v);
@@ -1618,7 +1609,7 @@ __global__ __launch_bounds__(256) void k_cg_finalize(const int* __restrict__ map
 }
 
 void mst_cg_finalize(const int* map_ids, int nact, int H, int W, MstWork m, int32_t* k, hipStream_t s) {
-    const CgGeom geo = cg_geom(H, W);
+    const CgGeom geo = mst_cg_geom(H, W);
     const long n4 = (long)nact * H * W / 4;
     hipLaunchKernelGGL(k_cg_finalize, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, map_ids, nact, m, geo, k);
     FCD_CHECK_LAUNCH();
