@@ -1422,13 +1422,40 @@ __global__ __launch_bounds__(TW * TH / 4, 4) void k_mst_tile0(const float* __res
 // weight into both roots; the segment is compacted in place (edges inside a root are
 // gone for good).
 constexpr int CGW_U = 8;  // edges per lane per pass: 512 of a segment
+// Each wave first takes its segment's minima per root in a small LDS table (the segment's
+// edges meet a few dozen roots; the global 64-bit atomics of later rounds queue on those
+// roots), then one global atomicMin per table entry.
+constexpr int CGH = 256;  // root slots per wave
 __global__ __launch_bounds__(256) void k_cg_cand(MstWork m, int ntiles, int ecap) {
     const unsigned long long lt = (1ull << (threadIdx.x & 63)) - 1;
+    __shared__ unsigned hkey_s[4][CGH];  // root + 1, 0: empty
+    __shared__ unsigned long long hval_s[4][CGH];
+    unsigned* const hk = hkey_s[(threadIdx.x >> 6) & 3];
+    unsigned long long* const hv = hval_s[(threadIdx.x >> 6) & 3];
+    auto root_min = [&](int r, unsigned long long w) {
+        const unsigned key = (unsigned)r + 1u;
+        unsigned h = (key * 2654435761u) >> 24;
+        for (int probe = 0; probe < 8; ++probe) {
+            const unsigned cur = atomicCAS(hk + h, 0u, key);
+            if (cur == 0u || cur == key) {
+                atomicMin(hv + h, w);
+                return;
+            }
+            h = (h + 1) & (CGH - 1);
+        }
+        atomicMin(m.best_w + r, w);  // a crowded table: straight to the root's minimum
+    };
     CG_TILES_LOOP(t) {
         const int n = m.cg_ecnt[t];
         if (n == 0) continue;  // wave-uniform: a finished tile costs one load per round
         const long b0 = (long)t * ecap;
         int nout = 0;
+#pragma unroll
+        for (int q = 0; q < CGH / 64; ++q) {
+            hk[lane + 64 * q] = 0u;
+            hv[lane + 64 * q] = ~0ull;
+        }
+        __builtin_amdgcn_wave_barrier();
         for (int base = 0; base < n; base += 64 * CGW_U) {
             int ea[CGW_U], eb[CGW_U], ec[CGW_U], ed[CGW_U], ra[CGW_U], rb[CGW_U];
             unsigned long long ew[CGW_U];
@@ -1462,10 +1489,17 @@ __global__ __launch_bounds__(256) void k_cg_cand(MstWork m, int ntiles, int ecap
                 nout += __popcll(bal);
                 if (!keep[u]) continue;
                 if (pos != base + u * 64 + lane) cg_write_edge(m, b0 + pos, ea[u], eb[u], ew[u], ec[u], ed[u]);
-                atomicMin(m.best_w + ra[u], ew[u]);
-                atomicMin(m.best_w + rb[u], ew[u]);
+                root_min(ra[u], ew[u]);
+                root_min(rb[u], ew[u]);
             }
         }
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int q = 0; q < CGH / 64; ++q) {
+            const unsigned key = hk[lane + 64 * q];
+            if (key) atomicMin(m.best_w + (key - 1u), hv[lane + 64 * q]);
+        }
+        __builtin_amdgcn_wave_barrier();
         if (lane == 0) m.cg_ecnt[t] = nout;
     }
 }
