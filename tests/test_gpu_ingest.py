@@ -280,6 +280,26 @@ def test_exact_first_mode_for_residue_heavy_batches(df, monkeypatch):
     st, _ = eng.stage_times()
     assert st["launches"] == 0 and int(st["fixup_frames"]) == 3  # no fused first pass ran
     assert np.array_equal(hd.cpu().numpy()[real_idx], out["0"][real_idx])
+    # with the k-fields requested the exact chain writes them (k_cg_finalize) instead of
+    # reading the MST labels inside k_int_rows2: a fresh engine's first call (two passes)
+    # and its second (exact chain) give the same heights and k-fields
+    e2 = _engine(ref, sq)
+    e2.profile(True)
+    ks, hs = [], []
+    for call in range(2):
+        hk = torch.empty_like(fd)
+        kk = torch.empty((len(frames), 2) + ref.shape, dtype=torch.int32, device=dev)
+        e2.process_device(fd.data_ptr(), len(frames), 1.0, True, hk.data_ptr(), k_ptr=kk.data_ptr())
+        torch.cuda.synchronize()
+        st, _ = e2.stage_times()
+        assert (st["launches"] == 0) == (call == 1), (call, st)  # the second call: exact chain
+        hs.append(hk.cpu().numpy())
+        ks.append(kk.cpu().numpy())
+    assert np.array_equal(hs[0][real_idx], hs[1][real_idx])
+    for f in real_idx:
+        for m in range(2):
+            d = ks[1][f, m].astype(np.int64) - ks[0][f, m]
+            assert np.all(d == d.flat[0]), (f, m)
     # a residue-free call (the reference repeated) switches back after it
     fr = torch.from_numpy(np.stack([ref] * 4)).to(dev)
     eng.process_device(fr.data_ptr(), 4, 1.0, True, hd.data_ptr())

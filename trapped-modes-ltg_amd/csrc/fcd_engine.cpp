@@ -1568,7 +1568,7 @@ int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int f
     // demod, residue count, the scan unwrap for residue-free maps and the MST for the
     // others, integration.  Same kernels and k-fields as pass 2 (bit-identical heights);
     // FCD_EXACT_FIRST=0 / 1 forces either mode.
-    static const int ef_env = fcd_env_int("FCD_EXACT_FIRST", -1);
+    const int ef_env = fcd_env_int("FCD_EXACT_FIRST", -1);  // (read per call: tests switch it)
     if (unwrap && !wrapped_out && (ef_env >= 0 ? ef_env == 1 : c->exact_first)) {
         const auto t0 = std::chrono::steady_clock::now();
         long nres = 0;

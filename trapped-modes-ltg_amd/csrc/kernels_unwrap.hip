@@ -1337,8 +1337,10 @@ __global__ __launch_bounds__(TW * TH / 4, 4) void k_mst_tile0(const float* __res
         }
         __syncthreads();
         T0_STAMP(4);
-        // (d) every hooked root to its final root, publishing the shortcuts as it walks
-        // (a root's link is one 32-bit word, so parent and offset are read together)
+        // (d) every hooked root to its final root (a root's link is one 32-bit word, so
+        // parent and offset are read together)
+        // each root walks to its final root, publishing the shortcuts as it goes (lockstep
+        // pointer jumping with a barrier per pass measured 9.0 k vs 9.9 k frames/s, r04aj)
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int c = threadIdx.x + NT * k;
