@@ -212,6 +212,26 @@ def test_gloo_two_rank_shard_gather():
     assert tmax == 2.0 and total == 7.0
 
 
+def test_gather_stack_one_rank_passes_through():
+    """A one-rank group (bench.py --gather at N=1, a one-GPU node) has no peers: the
+    shard comes back as the stack, no empty send/recv batch is posted."""
+    import torch
+    import torch.distributed as dist
+    from pyfcd.dist import free_port, gather_stack
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        local = torch.arange(12, dtype=torch.float32).reshape(2, 2, 3)
+        assert gather_stack(local, 2) is local
+        try:
+            gather_stack(local, 3)
+            raise AssertionError("gather_stack accepted a short shard")
+        except ValueError:
+            pass
+    finally:
+        dist.destroy_process_group()
+
+
 def test_bench_launches_its_own_ranks():
     """`python bench.py --gpus 2` with no launcher around it starts two rank
     processes itself (torch.distributed.run, 127.0.0.1) before any GPU call; each

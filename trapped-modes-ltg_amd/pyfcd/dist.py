@@ -95,6 +95,8 @@ def gather_stack(local, total_frames):
     a0, b0 = shard_range(total_frames, rank, world)
     if local.shape[0] != b0 - a0:
         raise ValueError(f"rank {rank}: shard of {local.shape[0]} frames, expected {b0 - a0}")
+    if world == 1:  # no peers: an empty point-to-point batch is an error in torch.distributed
+        return local
     if rank != 0:
         ops = [dist.P2POp(dist.isend, local.contiguous(), 0)]
         out = None
