@@ -401,16 +401,18 @@ int mst_level() {
 // exact fix-up of frames already known to carry residues; on a residue-free map
 // the MST integration equals the scan, k(0, 0) = 0 in both).
 // mk (nullable): when the component-graph MST runs, its maps' k is left to the caller
-// through *mk (k_int_rows2 kmode 3, no k-field pass; mk->map_slot null otherwise)
+// through *mk (k_int_rows2 kmode 3, no k-field pass; mk->map_slot null otherwise).
+// any_res: the residue counts only as "has residues" (> 0), which lets the count skip
+// the rest of a map once it has found one
 void unwrap_maps(fcd_ctx* c, const float* w, int nmaps, int32_t* k, int* res_host, hipStream_t s,
-                 bool all_mst = false, fcdk::MstK* mk = nullptr) {
+                 bool all_mst = false, fcdk::MstK* mk = nullptr, bool any_res = false) {
     if (mk) mk->map_slot = nullptr;
     std::vector<int> active;
     if (all_mst) {
         for (int i = 0; i < nmaps; ++i) active.push_back(i);
     } else {
         int* res = c->rescnt.as<int>();
-        fcdk::residues(w, nmaps, c->H, c->W, res, s);
+        fcdk::residues(w, nmaps, c->H, c->W, res, s, any_res);
         std::vector<int> counts(nmaps);
         HIPCHK(hipMemcpyAsync(counts.data(), res, sizeof(int) * nmaps, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
@@ -1500,7 +1502,7 @@ int process_generic(fcd_ctx* c, const void* frames, int format, int n_frames, bo
         if (unwrap) {
             std::vector<int> counts(2 * (size_t)nb);
             k = c->kbuf.as<int32_t>();
-            unwrap_maps(c, w, 2 * nb, k, counts.data(), s);
+            unwrap_maps(c, w, 2 * nb, k, counts.data(), s, false, nullptr, true);
             for (int i = 0; i < nb; ++i) nres += counts[2 * (size_t)i] || counts[2 * (size_t)i + 1];
         }
         if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
@@ -1586,7 +1588,7 @@ int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int f
             int32_t* kf = dev && k_out ? k_out + (size_t)f0 * 2 * hw : c->fk.as<int32_t>();
             counts.assign((size_t)2 * nb, 0);
             fcdk::MstK mk{};
-            unwrap_maps(c, c->wrapped.as<float>(), 2 * nb, kf, counts.data(), s, false, k_out ? nullptr : &mk);
+            unwrap_maps(c, c->wrapped.as<float>(), 2 * nb, kf, counts.data(), s, false, k_out ? nullptr : &mk, true);
             fcdk::int_rows(c->W, mk.map_slot ? 3 : 2, c->wrapped.as<float>(), nullptr, kf, nullptr, nullptr, c->H, nb,
                            c->Zt.as<float2>(), c->twp_row.as<float2>(), nullptr, s, mk.map_slot ? &mk : nullptr);
             fcdk::int_cols(c->H, c->Zt.as<float2>(), c->W, nb, coef, c->Ht.as<float2>(), ic_tw(c), s);

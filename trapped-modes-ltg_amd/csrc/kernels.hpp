@@ -201,7 +201,9 @@ inline bool fcd_fused_env(const char* name) {  // FCD_FUSED_2048 / FCD_FUSED_409
 }
 
 // ---- unwrap ----
-void residues(const float* w, int nmaps, int H, int W, int* counts, hipStream_t s);
+// counts[m] = residues of map m; any_only: counts[m] > 0 iff map m has residues (blocks of
+// an already-counted map skip their strips)
+void residues(const float* w, int nmaps, int H, int W, int* counts, hipStream_t s, bool any_only = false);
 void unwrap_scan(const float* w, int nmaps, int H, int W, int* colk, int32_t* k, hipStream_t s);
 
 // The component-graph path's tile geometry: level-0 component of pixel v (vertex id slot *

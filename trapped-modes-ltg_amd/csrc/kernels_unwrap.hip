@@ -108,10 +108,16 @@ __device__ __forceinline__ int residues_quad(const float (&ra)[5], const float (
     return r;
 }
 
-__global__ __launch_bounds__(256) void k_residues(const float* __restrict__ w, int H, int W, int* counts) {
-    const int map = blockIdx.y;
+// Blocks are numbered map-fastest (block b: map b % nmaps, strip block b / nmaps), so the
+// first blocks in flight sample every map.  any_only: a map's count is then only "> 0 iff
+// it has residues", and a block whose map is already counted skips its strip (camera
+// frames: most blocks, their maps flagged by the first wave of blocks).
+__global__ __launch_bounds__(256) void k_residues(const float* __restrict__ w, int H, int W, int nmaps, int* counts,
+                                                  bool any_only) {
+    const int map = (int)(blockIdx.x % (unsigned)nmaps);
+    if (any_only && __hip_atomic_load(counts + map, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > 0) return;
     const int q = W / 4;  // column quads per row (W % 4 == 0)
-    const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+    const long idx = (long)(blockIdx.x / (unsigned)nmaps) * 256 + threadIdx.x;
     const int strip = (int)(idx / q), j = (int)(idx % q) * 4;
     const int i0 = strip * kResRows, i1 = min(i0 + kResRows, H - 1);  // plaquette rows [i0, i1)
     int r = 0;
@@ -151,12 +157,13 @@ __global__ __launch_bounds__(256) void k_residues(const float* __restrict__ w, i
     if (threadIdx.x == 0 && bc) atomicAdd(counts + map, bc);
 }
 
-void residues(const float* w, int nmaps, int H, int W, int* counts, hipStream_t s) {
+void residues(const float* w, int nmaps, int H, int W, int* counts, hipStream_t s, bool any_only) {
     FCD_HIPCHK(hipMemsetAsync(counts, 0, sizeof(int) * nmaps, s));
     if (W % 4 != 0) throw std::runtime_error("residues: W must be a multiple of 4");
     const long threads = (long)(H - 1 + kResRows - 1) / kResRows * (W / 4);
-    hipLaunchKernelGGL(k_residues, dim3((unsigned)((threads + 255) / 256), (unsigned)nmaps), dim3(256), 0, s, w, H, W,
-                       counts);
+    const long blocks = (threads + 255) / 256 * nmaps;
+    if (blocks > 0x7fffffffL) throw std::runtime_error("residues: too many maps in one launch");
+    hipLaunchKernelGGL(k_residues, dim3((unsigned)blocks), dim3(256), 0, s, w, H, W, nmaps, counts, any_only);
     FCD_CHECK_LAUNCH();
 }
 
