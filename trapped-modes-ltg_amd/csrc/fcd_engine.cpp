@@ -299,7 +299,7 @@ void ensure_mst(fcd_ctx* c, int nact) {
     c->mst_bw.ensure(nv * 8);
     c->mst_be.ensure(nv * 4);
     c->mst_link.ensure(nv * 8);
-    c->mst_hooks.ensure(2 * sizeof(int));  // hooks this round; component-graph overflow flag
+    c->mst_hooks.ensure((2 + fcdk::kCgRounds) * sizeof(int));  // hooks this round; graph overflow; graph rounds' hooks
     // edge records for any tile side (FCD_MST_TILE may change between calls on the same buffers)
     const size_t ne = (size_t)fcdk::mst_cg_edge_capacity((long)nv);
     const size_t nt = (size_t)nact * c->hw() / 1024 + 1;  // tiles (32 x 32 at the smallest)
@@ -436,7 +436,7 @@ void unwrap_maps(fcd_ctx* c, const float* w, int nmaps, int32_t* k, int* res_hos
     int tile_h = 0;
     const int tile_w = fcdk::mst_tile_shape(c->H, c->W, &tile_h);
     if (level == 3 && tile_w > 0) {
-        HIPCHK(hipMemsetAsync(m.nhooks + 1, 0, sizeof(int), s));
+        HIPCHK(hipMemsetAsync(m.nhooks + 1, 0, (1 + fcdk::kCgRounds) * sizeof(int), s));
         fcdk::mst_tile_level0(w, c->mst_ids.as<int>(), nact, c->H, c->W, m, s, true);
         bool fits = true;
         static const bool cg_dbg = std::getenv("FCD_MST_DEBUG") != nullptr;
@@ -460,20 +460,22 @@ void unwrap_maps(fcd_ctx* c, const float* w, int nmaps, int32_t* k, int* res_hos
         // the first check after FCD_CG_FIRST rounds (camera frames converge in 7-9, and a
         // round of finished tiles costs one load per tile), then every third: each check
         // is a host round trip with the GPU idle
-        static const int first = std::max(1, fcd_env_int("FCD_CG_FIRST", 9));
+        static const int first = std::min(std::max(1, fcd_env_int("FCD_CG_FIRST", 9)), 64);  // (rounds < kCgRounds)
         for (int step = first; rounds < max_rounds; rounds += step, step = 3) {
             for (int g = 0; g < step; ++g) {
                 if (cg_dbg) cg_dump(rounds + g);
                 fcdk::mst_cg_round(nact, c->H, c->W, m, rounds + g, s);
             }
-            int flags[2] = {0, 0};  // hooks in the last round, a tile graph over its capacity
-            HIPCHK(hipMemcpyAsync(flags, m.nhooks, sizeof(flags), hipMemcpyDeviceToHost, s));
+            // nhooks[1]: a tile graph over its capacity; nhooks[2 + r]: hooks in round r
+            const int last = rounds + step - 1;
+            int flags[2 + fcdk::kCgRounds] = {};
+            HIPCHK(hipMemcpyAsync(flags, m.nhooks, (3 + last) * sizeof(int), hipMemcpyDeviceToHost, s));
             HIPCHK(hipStreamSynchronize(s));
             if (flags[1]) {
                 fits = false;
                 break;
             }
-            if (flags[0] == 0) break;
+            if (flags[2 + last] == 0) break;
         }
         if (fits) {
             if (rounds >= max_rounds) throw FcdError(FCD_E_INTERNAL, "unwrap: Boruvka did not converge");

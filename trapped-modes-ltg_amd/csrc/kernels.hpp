@@ -236,7 +236,9 @@ struct MstWork {
     unsigned char* maskB[2];  // per boundary entry: its neighbours still outside its component
     // component-graph rounds (mst_cg_round): per tile its level-0 component count and
     // contracted-edge count, the edge records (SoA) in per-tile segments; nhooks[1]:
-    // set if a tile's graph did not fit (never, by the planar bound; the host falls back)
+    // set if a tile's graph did not fit (never, by the planar bound; the host falls back);
+    // nhooks[2 + r]: hooks in graph round r (r < kCgRounds; zeroed once per MST pass, so
+    // the rounds need no per-round reset)
     int* cg_ncomp; int* cg_ecnt; int* cg_ea; int* cg_eb; unsigned long long* cg_ew; int* cg_ec; int* cg_ed;
     // the component-graph path's level-0 labels, compact (aliases of comp / off): per pixel
     // its component's rank in its tile (< cg_ccap <= 256) and K(pixel) - K(component)
@@ -262,6 +264,7 @@ void mst_tile_level0(const float* w, const int* map_ids, int nact, int H, int W,
 long mst_cg_edge_capacity(long nv);  // edge records for nv vertices (any tile side)
 // Round r of the component-graph Boruvka (r = 0: the candidates come from the tile pass; its
 // hooks resolve the cross-tile edges).
+constexpr int kCgRounds = 72;
 void mst_cg_round(int nact, int H, int W, MstWork m, int r, hipStream_t s);
 // k of the component-graph path (every level-0 component's offk final)
 void mst_cg_finalize(const int* map_ids, int nact, int H, int W, MstWork m, int32_t* k, hipStream_t s);

@@ -1540,7 +1540,7 @@ CgGeom mst_cg_geom(int H, int W) {
 }
 
 template <bool FIRST>
-__global__ __launch_bounds__(256) void k_cg_hook(MstWork m, int ntiles, int ecap, CgGeom geo) {
+__global__ __launch_bounds__(256) void k_cg_hook(MstWork m, int ntiles, int ecap, CgGeom geo, int* hflag) {
     CG_TILES_LOOP(t) {
         const int n = m.cg_ecnt[t];
         const long b0 = (long)t * ecap;
@@ -1570,7 +1570,7 @@ __global__ __launch_bounds__(256) void k_cg_hook(MstWork m, int ntiles, int ecap
                     hooked = true;
                 }
             }
-            count_hook(hooked, m.nhooks);
+            count_hook(hooked, hflag);
         }
     }
 }
@@ -1618,17 +1618,18 @@ void mst_cg_round(int nact, int H, int W, MstWork m, int r, hipStream_t s) {
     const int ntiles = nact * (H / th) * (W / tw);
     const int ecap = cg_ecap(tw, th), ccap = cg_ccap(tw, th);
     const CgGeom geo = mst_cg_geom(H, W);
-    FCD_HIPCHK(hipMemsetAsync(m.nhooks, 0, sizeof(int), s));
+    if (r >= kCgRounds) throw std::runtime_error("mst_cg_round: round past the hook-flag slots");
+    int* const hflag = m.nhooks + 2 + r;  // zeroed with the MST pass (no per-round reset)
     const dim3 g((unsigned)std::min((ntiles + 3) / 4, 4096)), b(256);  // 4 tiles per block at a time
     if (r == 0) {  // the candidates of round 0 came with the tile pass
-        hipLaunchKernelGGL(k_cg_hook<true>, g, b, 0, s, m, ntiles, ecap, geo);
+        hipLaunchKernelGGL(k_cg_hook<true>, g, b, 0, s, m, ntiles, ecap, geo, hflag);
         FCD_CHECK_LAUNCH();
     } else {
         hipLaunchKernelGGL(k_cg_cand, g, b, 0, s, m, ntiles, ecap);
         FCD_CHECK_LAUNCH();
         hipLaunchKernelGGL(k_cg_cand2, g, b, 0, s, m, ntiles, ecap);
         FCD_CHECK_LAUNCH();
-        hipLaunchKernelGGL(k_cg_hook<false>, g, b, 0, s, m, ntiles, ecap, geo);
+        hipLaunchKernelGGL(k_cg_hook<false>, g, b, 0, s, m, ntiles, ecap, geo, hflag);
         FCD_CHECK_LAUNCH();
     }
     hipLaunchKernelGGL(k_cg_relabel, g, b, 0, s, m, ntiles, ccap);
