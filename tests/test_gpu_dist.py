@@ -118,3 +118,38 @@ def test_two_ranks_shard_and_gather_equal_one_process():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert ok
+
+
+def _rank_rccl_one(rank, world, port, q):
+    """A one-rank RCCL group on the box's GPU: the device-tensor collectives bench.py's
+    ranks use (the step-time max, a sum) and gather_stack's one-rank pass-through. Two
+    ranks cannot share one device under RCCL; the N-rank exchange runs on the driver's
+    8-GPU node (bench.py --gpus N --gather)."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "trapped-modes-ltg_amd")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        from pyfcd.dist import gather_stack, max_over_ranks, sum_over_ranks
+        ok = dist.get_backend() == "nccl"
+        ok = ok and max_over_ranks(2.5, device=dev) == 2.5 and sum_over_ranks(3.0, device=dev) == 3.0
+        t = torch.arange(24, dtype=torch.float32, device=dev).reshape(2, 3, 4)
+        dist.all_reduce(t)  # one rank: unchanged, but through RCCL on the device
+        torch.cuda.synchronize(dev)
+        ok = ok and bool(torch.equal(t.cpu(), torch.arange(24, dtype=torch.float32).reshape(2, 3, 4)))
+        ok = ok and gather_stack(t, 2) is t
+        q.put(ok)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_one_rank_group():
+    assert _run_ranks(_rank_rccl_one, world=1)
+
