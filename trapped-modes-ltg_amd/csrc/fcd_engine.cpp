@@ -251,7 +251,7 @@ struct fcd_ctx {
     // MST workspace
     DevBuf mst_comp, mst_off, mst_rel, mst_cw, mst_ce, mst_bw, mst_be, mst_link, mst_hooks, mst_ids;
     DevBuf mst_rootof, mst_offk, mst_lb0, mst_lb1, mst_lr0, mst_lr1, mst_ll0, mst_cnt, mst_mb0, mst_mb1;  // two-level rounds
-    DevBuf cg_ncomp, cg_ecnt, cg_ea, cg_eb, cg_ew, cg_ec, cg_ed;  // component-graph rounds
+    DevBuf cg_ncomp, cg_ecnt, cg_ea, cg_eb, cg_ew, cg_ec, cg_ed, cg_lcol;  // component-graph rounds
     size_t mst_cap = 0;
 
     // stage timing: 4 events per chunk (start, after demod, after unwrap, after integrate)
@@ -304,6 +304,7 @@ void ensure_mst(fcd_ctx* c, int nact) {
     const size_t ne = (size_t)fcdk::mst_cg_edge_capacity((long)nv);
     const size_t nt = (size_t)nact * c->hw() / 1024 + 1;  // tiles (32 x 32 at the smallest)
     c->cg_ncomp.ensure(nt * 4);
+    c->cg_lcol.ensure(nt * 64 * 4);  // tile height <= 64
     c->cg_ecnt.ensure(nt * 4);
     for (DevBuf* b : {&c->cg_ea, &c->cg_eb, &c->cg_ec, &c->cg_ed}) b->ensure(ne * 4);
     c->cg_ew.ensure(ne * 8);
@@ -340,6 +341,7 @@ fcdk::MstWork mst_work(fcd_ctx* c) {
     m.maskB[0] = c->mst_mb0.as<unsigned char>();
     m.maskB[1] = c->mst_mb1.as<unsigned char>();
     m.cg_ncomp = c->cg_ncomp.as<int>();
+    m.cg_lcol = c->cg_lcol.as<unsigned>();
     m.cg_ecnt = c->cg_ecnt.as<int>();
     m.cg_ea = c->cg_ea.as<int>();
     m.cg_eb = c->cg_eb.as<int>();

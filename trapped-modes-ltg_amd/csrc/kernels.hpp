@@ -240,6 +240,10 @@ struct MstWork {
     // nhooks[2 + r]: hooks in graph round r (r < kCgRounds; zeroed once per MST pass, so
     // the rounds need no per-round reset)
     int* cg_ncomp; int* cg_ecnt; int* cg_ea; int* cg_eb; unsigned long long* cg_ew; int* cg_ec; int* cg_ed;
+    // per tile its column-0 pixels' labels, row by row (rank | offset << 16): the far ends
+    // of the edges into a tile from its left neighbour, read as one run instead of one
+    // cache line per row of crank / coff
+    unsigned* cg_lcol;
     // the component-graph path's level-0 labels, compact (aliases of comp / off): per pixel
     // its component's rank in its tile (< cg_ccap <= 256) and K(pixel) - K(component)
     unsigned char* crank; short* coff;

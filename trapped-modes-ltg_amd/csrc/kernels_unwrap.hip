@@ -1107,6 +1107,7 @@ __device__ __forceinline__ void tile0_graph(unsigned char* pool, const unsigned 
         const int id = cb + rk[c];
         m.crank[v] = (unsigned char)rk[c];  // (a rank >= 256 sets the overflow flag below)
         m.coff[v] = lo[i];
+        if (lj == 0) m.cg_lcol[tg * TH + li] = ((unsigned)rk[c] & 0xffu) | ((unsigned)(unsigned short)lo[i] << 16);
         if (c == i) {  // (its round-0 minimum is written above)
             m.rootof[id] = id;
             m.offk[id] = 0;
@@ -1553,9 +1554,24 @@ __global__ __launch_bounds__(256) void k_cg_hook(MstWork m, int ntiles, int ecap
                 int b = m.cg_eb[b0 + i];
                 int ed = m.cg_ed[b0 + i];
                 if (FIRST && b < 0) {
+                    // the far end y of an edge into the right / lower neighbour tile: a
+                    // column-0 pixel from that tile's cg_lcol run (the right-hand edges of a
+                    // tile then read 256 contiguous bytes, not 64 cache lines of crank and
+                    // of coff: ~2/3 of this kernel's 1.2 GB per 96 frames, PMC r04ay)
                     const long y = -1 - (long)b;
-                    b = geo.tile_of(y) * geo.ccap + m.crank[y];
-                    ed += m.coff[y];
+                    const int tl = geo.tile_of(y);
+                    const int p = (int)(y % geo.hw), py = p / geo.W, px = p - py * geo.W;
+                    int rk, of;
+                    if (px % geo.tw == 0) {
+                        const unsigned lv = m.cg_lcol[(long)tl * geo.th + py % geo.th];
+                        rk = (int)(lv & 0xffu);
+                        of = (int)(short)(lv >> 16);
+                    } else {
+                        rk = m.crank[y];
+                        of = m.coff[y];
+                    }
+                    b = tl * geo.ccap + rk;
+                    ed += of;
                     m.cg_eb[b0 + i] = b;
                     m.cg_ed[b0 + i] = ed;
                 }
