@@ -1,6 +1,6 @@
 # rocprof kernel stats of the real-frame pass for two library builds (FCD_LIB), hook kernels
 set -o pipefail
-out=gpurun_out/r04ba
+out=gpurun_out/${TAG:-r04ba}
 mkdir -p $out
 export TMPDIR=/tmp
 for v in base new; do
