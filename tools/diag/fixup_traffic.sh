@@ -1,5 +1,5 @@
 set -o pipefail
-out=gpurun_out/r04ay
+out=gpurun_out/${TAG:-r04ay}
 mkdir -p $out
 export TMPDIR=/tmp
 for c in FETCH_SIZE WRITE_SIZE; do

@@ -1,5 +1,5 @@
 """PMC bytes of the real-frame (exact MST) pass per kernel: FETCH_SIZE / WRITE_SIZE passes
-over tools/fixup_bench.py 96 (tools/diag/r04ay_fixup_traffic.sh), scaled by the membench
+over tools/fixup_bench.py 96 (tools/diag/fixup_traffic.sh), scaled by the membench
 calibration of the same run (FETCH x counter ratio at 4-B lanes, WRITE x its own), with
 the kernel durations of the counter runs (serialised dispatches: the bytes are the figure
 to read; the rate is against the unprofiled rocprof durations in r04au_fixup_kernel_stats).
