@@ -1322,7 +1322,9 @@ __global__ __launch_bounds__(TW * TH / 4, 4) void k_mst_tile0(const float* __res
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int i = threadIdx.x + NT * k, c = cs[k];
-            if (key[k] == ~0ull || key[k] != bw[c] || ke[k] != be[c]) continue;
+            // the component's lightest edge by its (tile-unique) code alone: an edge has one
+            // end in c, so no other pixel of c holds it as a candidate
+            if (key[k] == ~0ull || ke[k] != be[c]) continue;
             const int li = i / TW, lj = i % TW, d = kd[k];
             const int ni = li + (d == 2) - (d == 3), nj = lj + (d == 0) - (d == 1);
             if (!(ni >= 0 && ni < TH && nj >= 0 && nj < TW)) continue;  // leaves the tile: the level rounds take it
