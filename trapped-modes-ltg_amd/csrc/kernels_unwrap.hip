@@ -1338,10 +1338,11 @@ __global__ __launch_bounds__(TW * TH / 4, 4) void k_mst_tile0(const float* __res
         }
         const int any = __syncthreads_or(hooked);
         if (!any) break;
+        // (this thread's pixels' labels are still cs[]: lc changes only in the relabel step)
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int c = threadIdx.x + NT * k;
-            if (lc[c] != c) continue;
+            if (cs[k] != c) continue;
             const unsigned long long v = bw[c];
             lnk[c] = (v >> 63) ? (unsigned)v : t0_link(c, 0);
         }
@@ -1354,7 +1355,7 @@ __global__ __launch_bounds__(TW * TH / 4, 4) void k_mst_tile0(const float* __res
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int c = threadIdx.x + NT * k;
-            if (lc[c] != c) continue;
+            if (cs[k] != c) continue;
             const unsigned l = __hip_atomic_load(lnk + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             int p = t0_parent(l), o = t0_off(l);
             if (p == c) continue;
@@ -1373,7 +1374,7 @@ __global__ __launch_bounds__(TW * TH / 4, 4) void k_mst_tile0(const float* __res
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int i = threadIdx.x + NT * k;
-            const unsigned l = lnk[lc[i]];
+            const unsigned l = lnk[cs[k]];
             nc[k] = t0_parent(l);
             no[k] = lo[i] + t0_off(l);
         }
