@@ -1258,6 +1258,7 @@ __global__ __launch_bounds__(TW * TH / 4, 4) void k_mst_tile0(const float* __res
     __syncthreads();
     T0_STAMP(1);
     [[maybe_unused]] int nrounds = 0;
+    int lor[4] = {0, 0, 0, 0};  // this thread's pixels' lo (LDS keeps the copy the others read)
     for (;;) {
         ++nrounds;
         const bool capped = CG && nrounds > cap;  // block-uniform
@@ -1333,7 +1334,7 @@ __global__ __launch_bounds__(TW * TH / 4, 4) void k_mst_tile0(const float* __res
             const int delta = (d == 0 || d == 2) ? -inc : inc;  // k(y) - k(i) across the edge
             const int dr = lc[y];
             if (be[dr] == ke[k] && c < dr) continue;  // mutual pair: the smaller root stays
-            bw[c] = (1ull << 63) | t0_link(dr, lo[y] - lo[i] - delta);  // K_c - K_dr
+            bw[c] = (1ull << 63) | t0_link(dr, lo[y] - lor[k] - delta);  // K_c - K_dr
             hooked = 1;
         }
         const int any = __syncthreads_or(hooked);
@@ -1373,10 +1374,9 @@ __global__ __launch_bounds__(TW * TH / 4, 4) void k_mst_tile0(const float* __res
         int nc[4], no[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const int i = threadIdx.x + NT * k;
             const unsigned l = lnk[cs[k]];
             nc[k] = t0_parent(l);
-            no[k] = lo[i] + t0_off(l);
+            no[k] = lor[k] + t0_off(l);
         }
         __syncthreads();
 #pragma unroll
@@ -1384,6 +1384,7 @@ __global__ __launch_bounds__(TW * TH / 4, 4) void k_mst_tile0(const float* __res
             const int i = threadIdx.x + NT * k;
             lc[i] = (short)nc[k];
             lo[i] = (short)no[k];
+            lor[k] = (short)no[k];
             bw[i] = 0x7ff0000000000000ull;
             be[i] = 0x7fffffff;
         }
