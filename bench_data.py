@@ -157,3 +157,33 @@ def make_frames_torch(n, count, seed=0, rotate_deg=0.0, device="cuda", chunk=64)
                             align_corners=True)
         frames[b0:b0 + nb] = out[:, 0]
     return ref, frames
+
+
+def hash_image(h, w, seed=0, levels=1024):
+    """Deterministic pseudo-random integer image (uint16 in [0, levels)) from an integer hash
+    of (row, col, seed): identical under every numpy version (unsigned 64-bit arithmetic
+    only), so the fixtures of tests/golden/shapes.npz store the recipe, not the pixels."""
+    i = np.arange(h, dtype=np.uint64)[:, None]
+    j = np.arange(w, dtype=np.uint64)[None, :]
+    m = np.uint64(0xFFFFFFFF)
+    x = (i * np.uint64(0x9E3779B1) + j * np.uint64(0x85EBCA77) + np.uint64(seed) * np.uint64(0xC2B2AE3D)) & m
+    x = x ^ (x >> np.uint64(15))
+    x = (x * np.uint64(0x2C1B3C6D)) & m
+    x = x ^ (x >> np.uint64(12))
+    x = (x * np.uint64(0x297A2D39)) & m
+    x = x ^ (x >> np.uint64(15))
+    return (x % np.uint64(levels)).astype(np.uint16)
+
+
+def sine_board(rows, cols, n_rows, n_cols=None):
+    """pyval/val.py:96-98's float64 pattern I0 = 0.5 + (sin(X kx) * sin(Y ky)) / 2 on a
+    rows x cols grid ('ij' meshgrid of the pixel indices, k = 2 pi n / N per axis), built
+    from its two 1-D sine tables (returned too) so that tests rebuild it exactly."""
+    n_cols = n_rows if n_cols is None else n_cols
+    sx = np.sin(np.arange(rows, dtype=np.float64) * (2 * np.pi * n_rows / rows))
+    sy = np.sin(np.arange(cols, dtype=np.float64) * (2 * np.pi * n_cols / cols))
+    return board_from_tables(sx, sy), sx, sy
+
+
+def board_from_tables(sx, sy):
+    return 0.5 + (sx[:, None] * sy[None, :]) / 2

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define FCD_ABI_VERSION 6
+#define FCD_ABI_VERSION 7
 
 enum {
     FCD_OK = 0,
@@ -53,6 +53,15 @@ enum { FCD_HOST_PTRS = 0, FCD_DEVICE_PTRS = 1 };
  * scipy / numpy unchanged (analyze.py:486-527), so it is not rounded to float32
  * on the way in. */
 enum { FCD_STACK_F64 = 2 };
+
+/* Flag bit of fcd_set_reference / fcd_find_peaks / fcd_fft2 (OR-ed into flags): the
+ * images are float64 instead of float32.  The reference computes find_peaks' spectrum in
+ * the image's own precision (fourier.py:18: a float64 image -> complex128 FFTs, as
+ * pyval/val.py:98 hands compute_height_map), so the carrier picks of a float64 reference
+ * come from the float64 spectrum, bit for bit; fcd_fft2 then writes complex128.  The
+ * per-frame demodulation of fcd_process stays float32 (the reference image rounded to
+ * float32 for the carrier signals). */
+enum { FCD_IMG_F64 = 4 };
 
 /* Frame sample formats (fcd_process_raw).  The reference decodes every frame
  * to float32 on the host (analyze.load_image, analyze.py:25-40); these let the
@@ -76,7 +85,8 @@ typedef struct {
     int32_t mask_count[2];      /* pixels inside each disk band-pass (carriers.py:17-20) */
     int32_t n_blobs;            /* blobs kept by find_peak_locations (<= 4, fourier.py:166-168) */
     int64_t blob_peaks[4][2];   /* their peak pixels, ascending intensity */
-    float threshold;            /* 0.5 * max |F| after the high-pass (fourier.py:35) */
+    double threshold;           /* 0.5 * max |F| after the high-pass (fourier.py:35; a float32 value for
+                                   float32 images, float64 for FCD_IMG_F64) */
 } fcd_ref_info;
 
 int fcd_abi_version(void);

@@ -91,9 +91,16 @@ def find_peak_locations(image, threshold, no_peaks):
     return [p[1] for p in peaks[:no_peaks]]
 
 
-def find_peaks(image):
-    """fourier.find_peaks (fourier.py:7-41)."""
-    spec = np.fft.fftshift(np.abs(fft2(image - np.mean(image))))
+def find_peaks(image, exact=False):
+    """fourier.find_peaks (fourier.py:7-41).  exact: the spectrum with the reference's own
+    rounding in the image's precision (oracle/pocketfft.py: scipy 1.7.1's pocketfft, numpy
+    1.26.4's mean and abs), which decides the picks where blobs tie in exact arithmetic;
+    otherwise the interpreter's scipy.fft (a faster stand-in for the CPU baseline)."""
+    if exact:
+        from oracle import pocketfft
+        spec = pocketfft.find_peaks_spectrum(image)
+    else:
+        spec = np.fft.fftshift(np.abs(fft2(image - np.mean(image))))
     kr, kc = wavenumber_meshgrid(spec.shape, shifted=True)
     kmin = 4 * np.pi / min(image.shape)
     spec *= (kr ** 2 + kc ** 2) > kmin ** 2
@@ -115,9 +122,9 @@ def find_peaks(image):
     return right, perp
 
 
-def calibration_factor(square_size, reference):
+def calibration_factor(square_size, reference, exact=False):
     """fcd.compute_calibration_factor (fcd.py:72-101): 2*sq / (2pi / mean|k_pix|)."""
-    peaks = find_peaks(reference)
+    peaks = find_peaks(reference, exact)
     kp = np.array([pixel_to_wavenumber(reference.shape, p) for p in peaks])
     pixel_wavelength = 2 * np.pi / np.mean(np.abs(kp))
     return 2 * square_size / pixel_wavelength, peaks

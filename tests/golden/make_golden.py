@@ -35,6 +35,10 @@ Fixtures (all under tests/golden/):
                      unwrap k-fields (bench_data.make_residue_frame, frame digests stored)
   mixed.npz          frame sides that are not powers of two (1024 x 1280, 1536 x 2048, a
                      960-row camera crop): as large.npz, plus fft2 digests of 5-smooth shapes
+  shapes.npz         any frame shape and float64 images: fft2 / mean / spectrum digests of
+                     hashed integer images (bench_data.hash_image) at odd, prime, Bluestein
+                     and camera shapes in float32 and float64, and the reference's carrier
+                     picks for float64 references (pyval's tie-prone sine board I0 among them)
   analyze_ref.npz    pydata/analyze.py ITSELF (imported with a placeholder `cv2` module
                      whose every attribute access raises: cv2 is only used on the polar
                      paths, analyze.py:237-241, 674-676, which are not run): analyze.mask /
@@ -545,6 +549,76 @@ def make_mixed():
     np.savez_compressed(os.path.join(OUT, "mixed.npz"), **out)
 
 
+# Frame shapes for the exact reference spectrum (scipy's fft2 in the image's precision):
+# powers of two, 5-smooth, 7 / 11 / larger primes (rfftp radfg, cfftp pass7 / pass11 /
+# passg), Bluestein sides (1021, 4099, 257 ...), odd sides and camera formats.
+SHAPES_FFT = [(64, 64), (63, 64), (64, 63), (93, 186), (100, 75), (189, 256), (257, 251), (343, 121), (17, 2),
+              (1, 64), (1023, 1021), (1021, 1023), (1080, 1920), (1000, 1000), (600, 2448), (4099, 40), (50, 4097)]
+# float64 references (the reference computes find_peaks' spectrum in complex128 for them,
+# fourier.py:18; pyval/val.py:98 hands compute_height_map a float64 I0): pyval's own
+# unrotated sine board (tie-prone: its four blobs tie in exact arithmetic), the pattern.py
+# board as float64, and sine boards of other shapes.
+F64_REFS = {
+    "val1024": dict(kind="sine", rows=1024, cols=1024, n=60),
+    "val512": dict(kind="sine", rows=512, cols=512, n=30),
+    "val600x800": dict(kind="sine", rows=600, cols=800, n=37, n_cols=49),
+    "val1021x1023": dict(kind="sine", rows=1021, cols=1023, n=57, n_cols=61),
+    "flat1024": dict(kind="board", rows=1024, rot=0.0),
+    "rot768x1280": dict(kind="board", rows=768, cols=1280, rot=5.0),
+}
+
+
+def f64_reference(spec):
+    sys.path.insert(0, os.path.dirname(os.path.dirname(OUT)))
+    from bench_data import checkerboard, sine_board
+    if spec["kind"] == "sine":
+        img, sx, sy = sine_board(spec["rows"], spec["cols"], spec["n"], spec.get("n_cols"))
+        return img, {"sx": sx, "sy": sy}
+    return checkerboard(spec["rows"], spec["rot"], cols=spec.get("cols")).astype(np.float64), {}
+
+
+def make_shapes():
+    """shapes.npz: digests of scipy's fft2, np.mean and the find_peaks spectrum for hashed
+    integer images (bench_data.hash_image) of SHAPES_FFT in float32 and float64, and the
+    reference's carrier picks (find_peaks, compute_calibration_factor) for the float64
+    references of F64_REFS."""
+    import hashlib
+    sys.path.insert(0, os.path.dirname(os.path.dirname(OUT)))
+    from bench_data import hash_image
+    out = {"versions": VERSIONS, "fft_shapes": np.array(SHAPES_FFT), "f64_refs": np.array(list(F64_REFS))}
+    for k, (h, w) in enumerate(SHAPES_FFT):
+        u = hash_image(h, w, seed=k)
+        out[f"{h}x{w}_u16_sha"] = hashlib.sha256(u.tobytes()).hexdigest()
+        for T, tag in ((np.float32, "f32"), (np.float64, "f64")):
+            img = u.astype(T) * T(0.37)
+            F = fft2(img)
+            assert F.dtype == (np.complex64 if T == np.float32 else np.complex128)
+            m = np.mean(img)
+            out[f"{h}x{w}_{tag}_fft2_sha"] = hashlib.sha256(F.tobytes()).hexdigest()
+            out[f"{h}x{w}_{tag}_mean"] = np.asarray(m, T)
+            out[f"{h}x{w}_{tag}_spec_sha"] = hashlib.sha256(np.fft.fftshift(np.abs(fft2(img - m))).tobytes()).hexdigest()
+    for tag, spec in F64_REFS.items():
+        img, tables = f64_reference(spec)
+        assert img.dtype == np.float64
+        sq = 0.001
+        cf, (p0, p1) = fcd.compute_calibration_factor(sq, img)
+        locs, thr = peak_locations(img)
+        out[f"{tag}_sha"] = hashlib.sha256(img.tobytes()).hexdigest()
+        out[f"{tag}_peaks"] = np.array([np.asarray(p0), np.asarray(p1)], np.int64)
+        out[f"{tag}_cf"] = cf
+        out[f"{tag}_blob_peaks"] = locs
+        out[f"{tag}_threshold"] = thr
+        # the picks of the same image rounded to float32 (what an engine demodulating the
+        # float32 rounding would have picked)
+        c32, (q0, q1) = fcd.compute_calibration_factor(sq, img.astype(np.float32))
+        out[f"{tag}_peaks_f32"] = np.array([np.asarray(q0), np.asarray(q1)], np.int64)
+        for k, v in tables.items():
+            out[f"{tag}_{k}"] = v
+        print("shapes f64 ref", tag, img.shape, out[f"{tag}_peaks"].tolist(), "f32 picks", out[f"{tag}_peaks_f32"].tolist(),
+              locs.tolist(), thr, flush=True)
+    np.savez_compressed(os.path.join(OUT, "shapes.npz"), **out)
+
+
 def import_reference_analyze():
     """/root/reference/pydata/analyze.py, imported as the reference ships it.  Its module
     top level does `import cv2` (analyze.py:21), absent here; cv2 is used only by the
@@ -674,7 +748,7 @@ def make_analyze_ref():
 
 if __name__ == "__main__":
     which = sys.argv[1:] or ["real_pair", "real_df", "unwrap", "synthetic", "integrate", "val", "ingest",
-                             "bench_board", "analyze_ref", "spectrum", "large", "mixed"]
+                             "bench_board", "analyze_ref", "spectrum", "large", "mixed", "shapes"]
     if "real_pair" in which:
         make_real_pair()
     if "real_df" in which:
@@ -699,3 +773,5 @@ if __name__ == "__main__":
         make_large()
     if "mixed" in which:
         make_mixed()
+    if "shapes" in which:
+        make_shapes()

@@ -28,7 +28,7 @@ def test_library_exports_every_header_symbol():
     lib = _lib.load_library()
     for name in header_symbols():
         assert hasattr(lib, name), name
-    assert lib.fcd_abi_version() == 6
+    assert lib.fcd_abi_version() == 7
 
 
 def test_library_is_gfx950_code_object():

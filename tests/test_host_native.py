@@ -106,25 +106,38 @@ def test_no_blobs_is_an_error(hlt):
     assert out.startswith("error -5")  # FCD_E_NOPEAKS, as the reference's min() of an empty list raises
 
 
-@pytest.mark.parametrize("n", [64, 128, 1024, 2048, 4096])
+PF_LENGTHS = [1, 2, 3, 5, 7, 8, 11, 12, 13, 17, 31, 49, 60, 64, 93, 121, 128, 186, 189, 227, 257, 289, 343, 377,
+              1000, 1021, 1023, 1080, 1920, 2048, 2448]
+
+
+@pytest.mark.parametrize("f64", [0, 1])
 @pytest.mark.parametrize("real", [1, 0])
-def test_pocketfft_plans_match_oracle(hlt, n, real):
-    """rfftp / cfftp factorisation and twiddle tables (sincos_2pibyn<float>), as
-    oracle/pocketfft32.py states them (itself pinned to scipy's outputs)."""
-    from oracle import pocketfft32 as P
-    lines = hlt("pfplan", stdin=f"{n} {real}\n").splitlines()
-    plan = [tuple(int(v) for v in t.split(":")) for t in lines[0].split()]
-    tw = np.array([float.fromhex(v) for v in lines[1:]], np.float64).astype(np.float32)
-    fact = P.rfactors(n) if real else P.cfactors(n)
-    assert [f for f, _ in plan] == fact
-    if real:
-        want = np.concatenate(P.rtwiddles(n, fact))
-    else:
-        want = np.concatenate([np.stack([tr, ti], 1).ravel() for tr, ti in P.ctwiddles(n, fact)])
-    assert np.array_equal(tw, want)
-    offs = np.cumsum([0] + [len(t) if real else len(t[0]) for t in (P.rtwiddles(n, fact) if real else
-                                                                      P.ctwiddles(n, fact))])[:-1]
-    assert [o for _, o in plan] == offs.tolist()
+def test_pocketfft_passes_match_oracle(hlt, real, f64):
+    """csrc/pocketfft.hpp -- the exact passes the device runs (rfftp radf2/3/4/5/g, cfftp
+    pass2/3/4/5/7/8/11/g, Bluestein), its plans and sincos_2pibyn twiddles -- run on the
+    host under the sanitizers, bit for bit against oracle/pocketfft.py (itself pinned to
+    scipy 1.7.1 on every length 1..400, tests/golden/shapes.npz) in both precisions."""
+    from oracle import pocketfft as P
+    T = np.float64 if f64 else np.float32
+    rng = np.random.default_rng(11 + real + 2 * f64)
+    for n in PF_LENGTHS:
+        rows = 2
+        if real:
+            x = rng.standard_normal((rows, n)).astype(T)
+            want_r, want_i = P.rfft_rows(x, T)
+            vals = x.astype(np.float64).ravel()
+        else:
+            z = (rng.standard_normal((rows, n)) + 1j * rng.standard_normal((rows, n)))
+            zr, zi = z.real.astype(T), z.imag.astype(T)
+            want_r, want_i = P.cfft((zr.copy(), zi.copy()), True, T)
+            vals = np.stack([zr, zi], -1).astype(np.float64).ravel()
+        stdin = f"{n} {real} {f64} {rows}\n" + " ".join(float(v).hex() for v in vals) + "\n"
+        lines = hlt("pfrun", stdin=stdin).splitlines()
+        blue, n2, nf = (int(v) for v in lines[0].split()[1:])
+        assert bool(blue) == P.use_bluestein(n, bool(real)), n
+        got = np.array([[float.fromhex(a) for a in ln.split()] for ln in lines[1:]], np.float64).astype(T)
+        got = got.reshape(rows, -1, 2)
+        assert np.array_equal(got[..., 0], want_r) and np.array_equal(got[..., 1], want_i), (n, real, f64)
 
 
 @pytest.mark.parametrize("nbytes", [0, 1, 4095, 8 << 20, (8 << 20) + 7, 77_777_777])

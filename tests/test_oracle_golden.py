@@ -5,6 +5,8 @@ the golden vectors the reference produced (tests/golden/make_golden.py):
 bit-exact peaks / calibration factor / unwrap k-fields, and float32-FFT
 tolerance on phases and heights.
 """
+import hashlib
+
 import numpy as np
 import pytest
 
@@ -222,3 +224,49 @@ def test_oracle_mixed_frames_vs_reference_run(golden, tag):
     hs = int(g[f"{tag}_height_step"])
     sub = g[f"{tag}_height_sub"]
     assert np.linalg.norm(h[::hs, ::hs] - sub) / np.linalg.norm(sub) < (1e-5 if not tag.startswith("c") else 1e-4)
+
+
+def test_pocketfft_any_shape_and_float64_digests(golden):
+    """oracle/pocketfft.py against scipy 1.7.1 / numpy 1.26.4 themselves (shapes.npz): fft2,
+    mean and the find_peaks spectrum of hashed integer images at odd, prime (radfg, pass7 /
+    pass11 / passg), Bluestein and camera shapes, float32 and float64, bit for bit."""
+    from bench_data import hash_image
+    from oracle import pocketfft as P
+    g = golden("shapes")
+    for k, (h, w) in enumerate(g["fft_shapes"]):
+        u = hash_image(int(h), int(w), seed=k)
+        assert hashlib.sha256(u.tobytes()).hexdigest() == str(g[f"{h}x{w}_u16_sha"]), (h, w)
+        for T, tag in ((np.float32, "f32"), (np.float64, "f64")):
+            img = u.astype(T) * T(0.37)
+            assert hashlib.sha256(P.fft2(img).tobytes()).hexdigest() == str(g[f"{h}x{w}_{tag}_fft2_sha"]), (h, w, tag)
+            assert P.mean_T(img, T) == g[f"{h}x{w}_{tag}_mean"], (h, w, tag)
+            spec = P.find_peaks_spectrum(img)
+            assert hashlib.sha256(spec.tobytes()).hexdigest() == str(g[f"{h}x{w}_{tag}_spec_sha"]), (h, w, tag)
+
+
+def f64_reference_image(g, tag):
+    """The float64 references of shapes.npz, rebuilt exactly (make_golden.py F64_REFS)."""
+    from bench_data import board_from_tables, checkerboard
+    if f"{tag}_sx" in g:
+        img = board_from_tables(g[f"{tag}_sx"], g[f"{tag}_sy"])
+    else:
+        spec = {"flat1024": (1024, 0.0, None), "rot768x1280": (768, 5.0, 1280)}[tag]
+        img = checkerboard(spec[0], spec[1], cols=spec[2]).astype(np.float64)
+    assert hashlib.sha256(img.tobytes()).hexdigest() == str(g[f"{tag}_sha"]), tag
+    return img
+
+
+def test_oracle_float64_reference_picks(golden):
+    """find_peaks of a float64 reference decides its carriers from the complex128 spectrum
+    (fourier.py:18; pyval/val.py:98): the oracle's exact spectrum reproduces the
+    reference's picks, blobs and threshold in float64, and the different picks of the same
+    image rounded to float32 (flat1024, val600x800)."""
+    from oracle import fcd_oracle as O
+    g = golden("shapes")
+    for tag in g["f64_refs"]:
+        img = f64_reference_image(g, str(tag))
+        cf, peaks = O.calibration_factor(0.001, img, exact=True)
+        assert np.array_equal(np.array(peaks), g[f"{tag}_peaks"]), tag
+        assert cf == float(g[f"{tag}_cf"]), tag
+        _, p32 = O.calibration_factor(0.001, img.astype(np.float32), exact=True)
+        assert np.array_equal(np.array(p32), g[f"{tag}_peaks_f32"]), tag

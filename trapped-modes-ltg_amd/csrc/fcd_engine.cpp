@@ -241,8 +241,12 @@ struct fcd_ctx {
     int chunk = 1;
     DevBuf spec, work, wrapped, kbuf, colk, rescnt, frames_in, out_h, scalar;
     DevBuf cand_idx, cand_val, pk_small, pk_F, pk_work;  // reference setup: candidates, scalars, spectra
-    fcdk::PfPlan pf_row{}, pf_col{};  // scipy pocketfft's plans for the exact reference spectrum
-    DevBuf pf_rtw, pf_ctw, pf_sums;   // their twiddles; numpy's float32 chunk sums
+    pf::Plan pf_row{}, pf_col{};      // scipy pocketfft's plans of the exact reference spectrum (float32)
+    DevBuf pf_rtw, pf_ctw, pf_sums;   // their tables; numpy's chunk sums
+    pf::Plan pf_row64{}, pf_col64{};  // the same for float64 images (FCD_IMG_F64), built on first use
+    DevBuf pf_rtw64, pf_ctw64, pf_scratch;
+    bool pf64_ready = false;
+    DevBuf ref32;                     // a float64 reference rounded to float32 (the per-frame carriers)
     DevBuf fix_raw;  // raw samples of the frames redone by the exact pass
     // temporal analysis: staged block, exp table, bins, partial sums, output, window
     DevBuf t_stage, t_tab, t_bins, t_part, t_out, t_win, t_wsum, t_slices;
@@ -938,80 +942,117 @@ void reference_state(fcd_ctx* c, const float* dref0, const float* dref1, hipStre
     HIPCHK(hipStreamSynchronize(s));
 }
 
-// fourier.find_peaks + compute_calibration_factor + the carrier disks for nb
-// device-resident images (fcd.py:53-101, fourier.py:7-41), every image-sized stage
-// batched on the device: means, centring, FFT, |F| * highpass and its maximum, the
-// above-threshold candidates, the 8-connected labelling and the 4-blob pick
-// (kernels_fft.hip); the host finishes each image from its <= 4 peaks.  c->info and
-// c->disk_rows_host end up describing the last image; infos[i] (nullable) gets each.
-// Workspace: pk_* (16 bytes per pixel per image) + candidates (8 bytes per kept slot).
-// candidates kept per image (the device labels up to 4096 of them): never more than the
-// image has pixels
-long find_peaks_cap(const fcd_ctx* c) { return std::min(1L << 16, c->hw()); }
-int find_peaks_batch_max(const fcd_ctx* c) {
-    return (int)std::max(1L, (512L << 20) / (16L * c->hw() + 8L * find_peaks_cap(c)));
+// The float64 plans (FCD_IMG_F64 images), built on first use.
+void ensure_pf64(fcd_ctx* c) {
+    if (c->pf64_ready) return;
+    std::vector<double> rtw, ctw;
+    c->pf_row64 = pf::make_plan<double>(c->W, true, rtw);
+    c->pf_col64 = pf::make_plan<double>(c->H, false, ctw);
+    c->pf_rtw64.ensure(rtw.size() * sizeof(double));
+    c->pf_ctw64.ensure(ctw.size() * sizeof(double));
+    HIPCHK(hipMemcpy(c->pf_rtw64.p, rtw.data(), rtw.size() * sizeof(double), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->pf_ctw64.p, ctw.data(), ctw.size() * sizeof(double), hipMemcpyHostToDevice));
+    c->pf64_ready = true;
 }
 
-void find_peaks_batch(fcd_ctx* c, const float* dimgs, int nb, double square_size, fcd_ref_info* infos, hipStream_t s) {
+// scipy.fft.fft2 of nb device-resident real images (float32 -> complex64, float64 ->
+// complex128) with the reference's own rounding (kernels_pocketfft.hip).
+void exact_fft2(fcd_ctx* c, const void* in, bool f64, int nb, void* F, hipStream_t s) {
+    if (f64) ensure_pf64(c);
+    const pf::Plan& rp = f64 ? c->pf_row64 : c->pf_row;
+    const pf::Plan& cp = f64 ? c->pf_col64 : c->pf_col;
+    c->pf_scratch.ensure(std::max<size_t>(fcdk::pf_scratch_bytes(rp, cp, f64), 16));
+    fcdk::pf_fft2(in, f64, nb, c->H, c->W, rp, f64 ? c->pf_rtw64.p : c->pf_rtw.p, cp, f64 ? c->pf_ctw64.p : c->pf_ctw.p,
+                  F, c->pf_scratch.p, s);
+}
+
+// fourier.find_peaks + compute_calibration_factor + the carrier disks for nb
+// device-resident images (fcd.py:53-101, fourier.py:7-41), every image-sized stage
+// batched on the device in the image's precision: numpy's mean and centring, scipy's
+// fft2 (kernels_pocketfft.hip), |F| * highpass and its maximum, the above-threshold
+// candidates (any number: every pixel has a slot), and for float32 spectra the
+// 8-connected labelling and the 4-blob pick (kernels_fft.hip); the host finishes each
+// image from its <= 4 peaks.  Images whose candidates exceed the device labelling's
+// capacity (4096), and float64 spectra, are labelled on the host from their candidate
+// list (host_logic.hpp).  c->info and c->disk_rows_host end up describing the last image;
+// infos[i] (nullable) gets each.
+int find_peaks_batch_max(const fcd_ctx* c, bool f64) {
+    const long es = f64 ? 8 : 4;
+    const long per = c->hw() * (2 * es + 2 * es + 4 + es);  // spectrum, centred + |F|, candidates
+    return (int)std::max(1L, (512L << 20) / per);
+}
+
+void find_peaks_batch(fcd_ctx* c, const void* dimgs, bool f64, int nb, double square_size, fcd_ref_info* infos,
+                      hipStream_t s) {
     const long hw = c->hw();
     const int H = c->H, W = c->W;
     if (nb <= 0) return;
-    const int cap = (int)find_peaks_cap(c);
-    c->pk_F.ensure((size_t)nb * hw * sizeof(float2));
-    c->pk_work.ensure((size_t)nb * hw * 2 * sizeof(float));
-    float2* F = c->pk_F.as<float2>();
-    float* centered = c->pk_work.as<float>();
-    float* mag = centered + (size_t)nb * hw;
-    c->pk_small.ensure((size_t)nb * (8 + 4 + 4 + 32) + (size_t)(H + W) * 8);
-    double* sums = c->pk_small.as<double>();
-    unsigned* maxbits = reinterpret_cast<unsigned*>(sums + nb);
-    int* counts = reinterpret_cast<int*>(maxbits + nb);
+    const size_t es = f64 ? sizeof(double) : sizeof(float);
+    const long cap = hw;  // every pixel may be above the threshold (fourier.py:152)
+    c->pk_F.ensure((size_t)nb * hw * 2 * es);
+    c->pk_work.ensure((size_t)nb * hw * 2 * es);
+    char* centered = static_cast<char*>(c->pk_work.p);
+    char* mag = centered + (size_t)nb * hw * es;
+    c->pk_small.ensure((size_t)nb * (8 + 4 + 32) + (size_t)(H + W) * 8 + 64);
+    unsigned long long* maxbits = c->pk_small.as<unsigned long long>();
+    double* ktab = reinterpret_cast<double*>(maxbits + nb);
+    int* counts = reinterpret_cast<int*>(ktab + H + W);
     int* res = counts + nb;
-    double* ktab = reinterpret_cast<double*>(res + 8 * (size_t)nb);
     const std::vector<double> krs = wavenumber(H, 1.0, true), kcs = wavenumber(W, 1.0, true);
     upload(ktab, krs.data(), H * sizeof(double), s);
     upload(ktab + H, kcs.data(), W * sizeof(double), s);
     c->cand_idx.ensure((size_t)nb * cap * sizeof(int));
-    c->cand_val.ensure((size_t)nb * cap * sizeof(float));
+    c->cand_val.ensure((size_t)nb * cap * es);
     const double kmin = 4 * kPi / (double)std::min(H, W);  // fourier.py:22
-    (void)sums;
-    // image - np.mean(image) and scipy's fft2 with the reference's own float32 rounding
+    // image - np.mean(image) and scipy's fft2 with the reference's own rounding
     // (kernels_pocketfft.hip): exact ties between carrier blobs break as they do there
-    c->pf_sums.ensure((size_t)nb * fcdk::pf_chunk_count(hw) * sizeof(float));
-    fcdk::pf_center(dimgs, nb, hw, c->pf_sums.as<float>(), centered, s);
-    fcdk::pf_fft2(centered, nb, H, W, c->pf_row, c->pf_rtw.as<float>(), c->pf_col, c->pf_ctw.as<float2>(), F, s);
-    fcdk::spectrum_candidates_b(F, nb, H, W, ktab, ktab + H, kmin * kmin, mag, maxbits, counts, c->cand_idx.as<int>(),
-                                c->cand_val.as<float>(), cap, s);
-    fcdk::label_peaks(counts, c->cand_idx.as<int>(), c->cand_val.as<float>(), cap, nb, H, W, res, s);
-    std::vector<unsigned> mb(nb);
-    std::vector<int> rs((size_t)nb * 8);
-    HIPCHK(hipMemcpyAsync(mb.data(), maxbits, nb * sizeof(unsigned), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(rs.data(), res, rs.size() * sizeof(int), hipMemcpyDeviceToHost, s));
+    c->pf_sums.ensure((size_t)nb * fcdk::pf_chunk_count(hw) * es);
+    fcdk::pf_center(dimgs, f64, nb, hw, c->pf_sums.p, centered, s);
+    exact_fft2(c, centered, f64, nb, c->pk_F.p, s);
+    fcdk::spectrum_candidates_b(c->pk_F.p, f64, nb, H, W, ktab, ktab + H, kmin * kmin, mag, maxbits, counts,
+                                c->cand_idx.as<int>(), c->cand_val.p, cap, s);
+    if (!f64) fcdk::label_peaks(counts, c->cand_idx.as<int>(), c->cand_val.as<float>(), cap, nb, H, W, res, s);
+    std::vector<unsigned long long> mb(nb);
+    std::vector<int> rs((size_t)nb * 8, 0), cnt(nb);
+    HIPCHK(hipMemcpyAsync(mb.data(), maxbits, nb * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(cnt.data(), counts, nb * sizeof(int), hipMemcpyDeviceToHost, s));
+    if (!f64) HIPCHK(hipMemcpyAsync(rs.data(), res, rs.size() * sizeof(int), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     const bool host_label = std::getenv("FCD_HOST_LABEL") != nullptr;  // A/B: the host labelling for all
     for (int b = 0; b < nb; ++b) {
-        float mx;
-        std::memcpy(&mx, &mb[b], 4);
+        double mx;
+        if (f64) {
+            std::memcpy(&mx, &mb[b], 8);
+        } else {
+            float m32;
+            const unsigned u = (unsigned)mb[b];
+            std::memcpy(&m32, &u, 4);
+            mx = m32;
+        }
         const int* r = rs.data() + (size_t)b * 8;
         std::vector<Blob> blobs;
-        if (r[0] != 0 || host_label) {
-            const int ncand = r[0] != 0 ? r[1] : -1;
-            int n = ncand;
-            if (n < 0) HIPCHK(hipMemcpy(&n, counts + b, sizeof(int), hipMemcpyDeviceToHost));
-            if (n > cap) throw FcdError(FCD_E_UNSUPPORTED, "find_peaks: too many pixels above threshold");
+        if (f64 || r[0] != 0 || host_label) {
+            const int n = cnt[b];  // <= cap = H * W
             std::vector<int> cidx(n);
-            std::vector<float> cval(n);
+            std::vector<double> cval(n);
             if (n) {
                 HIPCHK(hipMemcpy(cidx.data(), c->cand_idx.as<int>() + (size_t)b * cap, n * sizeof(int),
                                  hipMemcpyDeviceToHost));
-                HIPCHK(hipMemcpy(cval.data(), c->cand_val.as<float>() + (size_t)b * cap, n * sizeof(float),
-                                 hipMemcpyDeviceToHost));
+                if (f64) {
+                    HIPCHK(hipMemcpy(cval.data(), c->cand_val.as<double>() + (size_t)b * cap, n * sizeof(double),
+                                     hipMemcpyDeviceToHost));
+                } else {
+                    std::vector<float> v32(n);
+                    HIPCHK(hipMemcpy(v32.data(), c->cand_val.as<float>() + (size_t)b * cap, n * sizeof(float),
+                                     hipMemcpyDeviceToHost));
+                    std::copy(v32.begin(), v32.end(), cval.begin());
+                }
             }
             blobs = label_candidates_host(H, W, cidx, cval);
         } else {
-            for (int e = 0; e < r[2]; ++e) blobs.push_back(Blob{r[3 + e], r[3 + e], 0.f});
+            for (int e = 0; e < r[2]; ++e) blobs.push_back(Blob{r[3 + e], r[3 + e], 0.0});
         }
-        fcdh::carriers_from_blobs(H, W, c->info, c->disk_rows_host, blobs, 0.5f * mx, square_size);
+        fcdh::carriers_from_blobs(H, W, c->info, c->disk_rows_host, blobs, 0.5 * mx, square_size);
         if (infos) infos[b] = c->info;
     }
 }
@@ -1087,9 +1128,9 @@ FCD_API int fcd_create(int device, int rows, int cols, fcd_ctx** out) {
             HIPCHK(hipMemcpy(c->twp_col16.p, pi.data(), pi.size() * sizeof(float2), hipMemcpyHostToDevice));
         }
         {
-            std::vector<float> rtw, ctw;  // ctw: (cos, sin) pairs = float2 on the device
-            fcdh::pf_row_plan(cols, c->pf_row, rtw);
-            fcdh::pf_col_plan(rows, c->pf_col, ctw);
+            std::vector<float> rtw, ctw;  // the plans' tables (complex entries as (re, im) pairs)
+            c->pf_row = pf::make_plan<float>(cols, true, rtw);
+            c->pf_col = pf::make_plan<float>(rows, false, ctw);
             c->pf_rtw.ensure(rtw.size() * sizeof(float));
             c->pf_ctw.ensure(ctw.size() * sizeof(float));
             HIPCHK(hipMemcpy(c->pf_rtw.p, rtw.data(), rtw.size() * sizeof(float), hipMemcpyHostToDevice));
@@ -1147,17 +1188,27 @@ FCD_API int fcd_set_reference(fcd_ctx* c, const float* reference, int flags, dou
     FCD_TRY({
         check_ctx(c);
         if (!reference) throw FcdError(FCD_E_INVALID, "reference is null");
+        if (flags & ~(FCD_DEVICE_PTRS | FCD_IMG_F64)) throw FcdError(FCD_E_INVALID, "bad flags");
         hipStream_t s = c->own;
         const long hw = c->hw();
+        const bool f64 = flags & FCD_IMG_F64;
+        const size_t es = f64 ? sizeof(double) : sizeof(float);
         c->has_ref = false;
-        const float* dref = reference;
-        if (flags != FCD_DEVICE_PTRS) {
-            c->frames_in.ensure(hw * sizeof(float));
-            upload(c->frames_in.p, reference, hw * sizeof(float), s);
-            dref = c->frames_in.as<float>();
+        const void* dref = reference;
+        if (!(flags & FCD_DEVICE_PTRS)) {
+            c->frames_in.ensure(hw * es);
+            upload(c->frames_in.p, reference, hw * es, s);
+            dref = c->frames_in.p;
         }
-        find_peaks_batch(c, dref, 1, square_size, nullptr, s);
-        reference_state(c, dref, dref, s);
+        // the carrier picks from the reference's own precision (fourier.py:18)
+        find_peaks_batch(c, dref, f64, 1, square_size, nullptr, s);
+        const float* dref32 = static_cast<const float*>(dref);
+        if (f64) {  // the per-frame demodulation's carrier signals from its float32 rounding
+            c->ref32.ensure(hw * sizeof(float));
+            fcdk::convert_f64(static_cast<const double*>(dref), hw, c->ref32.as<float>(), s);
+            dref32 = c->ref32.as<float>();
+        }
+        reference_state(c, dref32, dref32, s);
         c->has_ref = true;
         if (info) *info = c->info;
     })
@@ -1209,8 +1260,11 @@ FCD_API int fcd_find_peaks(fcd_ctx* c, const float* images, int n, int flags, do
     FCD_TRY({
         check_ctx(c);
         if (!images || !infos || n < 0) throw FcdError(FCD_E_INVALID, "bad arguments");
+        if (flags & ~(FCD_DEVICE_PTRS | FCD_IMG_F64)) throw FcdError(FCD_E_INVALID, "bad flags");
         hipStream_t s = c->own;
         const long hw = c->hw();
+        const bool f64 = flags & FCD_IMG_F64;
+        const size_t es = f64 ? sizeof(double) : sizeof(float);
         // the context's reference (if any) is kept: its per-reference host state is
         // restored afterwards; the device state find_peaks_batch touches is workspace
         const fcd_ref_info keep_info = c->info;
@@ -1224,16 +1278,16 @@ FCD_API int fcd_find_peaks(fcd_ctx* c, const float* images, int n, int flags, do
                 c->disk_rows_host = rows;
             }
         } restore{c, keep_info, keep_rows};
-        const int bmax = find_peaks_batch_max(c);
+        const int bmax = find_peaks_batch_max(c, f64);
         for (int i0 = 0; i0 < n; i0 += bmax) {
             const int nb = std::min(bmax, n - i0);
-            const float* img = images + (size_t)i0 * hw;
-            if (flags != FCD_DEVICE_PTRS) {
-                c->frames_in.ensure((size_t)nb * hw * sizeof(float));
-                upload(c->frames_in.p, img, (size_t)nb * hw * sizeof(float), s);
-                img = c->frames_in.as<float>();
+            const void* img = reinterpret_cast<const char*>(images) + (size_t)i0 * hw * es;
+            if (!(flags & FCD_DEVICE_PTRS)) {
+                c->frames_in.ensure((size_t)nb * hw * es);
+                upload(c->frames_in.p, img, (size_t)nb * hw * es, s);
+                img = c->frames_in.p;
             }
-            find_peaks_batch(c, img, nb, square_size, infos + i0, s);
+            find_peaks_batch(c, img, f64, nb, square_size, infos + i0, s);
         }
     })
 }
@@ -1949,22 +2003,27 @@ FCD_API int fcd_fft2(fcd_ctx* c, const float* in, int n, int flags, float* out, 
     FCD_TRY({
         check_ctx(c);
         if (!in || !out || n < 0) throw FcdError(FCD_E_INVALID, "bad arguments");
+        if (flags & ~(FCD_DEVICE_PTRS | FCD_IMG_F64)) throw FcdError(FCD_E_INVALID, "bad flags");
         hipStream_t s = c->pick(stream);
         const long hw = c->hw();
-        const bool dev = flags == FCD_DEVICE_PTRS;
-        if (!dev) c->frames_in.ensure((size_t)c->chunk * hw * 4);
+        const bool dev = flags & FCD_DEVICE_PTRS, f64 = flags & FCD_IMG_F64;
+        const size_t es = f64 ? sizeof(double) : sizeof(float);
+        if (!dev) {
+            c->frames_in.ensure((size_t)c->chunk * hw * es);
+            c->pk_F.ensure((size_t)c->chunk * hw * 2 * es);
+        }
         for (int f0 = 0; f0 < n; f0 += c->chunk) {
             const int nb = std::min(c->chunk, n - f0);
-            const float* x = in + (size_t)f0 * hw;
+            const void* x = reinterpret_cast<const char*>(in) + (size_t)f0 * hw * es;
             if (!dev) {
-                upload(c->frames_in.p, x, (size_t)nb * hw * 4, s);
-                x = c->frames_in.as<float>();
+                upload(c->frames_in.p, x, (size_t)nb * hw * es, s);
+                x = c->frames_in.p;
             }
-            float2* dst = dev ? reinterpret_cast<float2*>(out) + (size_t)f0 * hw : c->spec.as<float2>();
-            fcdk::pf_fft2(x, nb, c->H, c->W, c->pf_row, c->pf_rtw.as<float>(), c->pf_col, c->pf_ctw.as<float2>(), dst,
-                          s);
+            void* dst = dev ? reinterpret_cast<char*>(out) + (size_t)f0 * hw * 2 * es : c->pk_F.p;
+            exact_fft2(c, x, f64, nb, dst, s);
             if (!dev) {
-                HIPCHK(hipMemcpyAsync(out + (size_t)f0 * hw * 2, dst, (size_t)nb * hw * 8, hipMemcpyDeviceToHost, s));
+                HIPCHK(hipMemcpyAsync(reinterpret_cast<char*>(out) + (size_t)f0 * hw * 2 * es, dst,
+                                      (size_t)nb * hw * 2 * es, hipMemcpyDeviceToHost, s));
                 HIPCHK(hipStreamSynchronize(s));
             }
         }

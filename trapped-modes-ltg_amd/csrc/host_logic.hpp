@@ -18,17 +18,8 @@
 #include <vector>
 
 #include "../../include/fcd.h"
+#include "pocketfft.hpp"
 
-namespace fcdk {
-// scipy pocketfft plan of the exact reference spectrum (kernels_pocketfft.hip): the
-// factor sequence of rfftp (rows) / cfftp (columns) and each pass's offset into its
-// twiddle table (float (cos, sin) pairs; complex entries for the columns)
-struct PfPlan {
-    int nf;
-    int fct[8];
-    int tw[8];
-};
-}  // namespace fcdk
 
 namespace fcdh {
 
@@ -53,103 +44,24 @@ inline std::vector<double> wavenumber(int n, double cf, bool shifted) {
     return k;
 }
 
-// scipy 1.7.1 pocketfft plans (kernels_pocketfft.hip; restated in oracle/pocketfft32.py):
-// rfftp factors 4, 4, ... with a single 2 moved to the front; cfftp 8s, then 4s, a single
-// 2 first; then both take 3s and 5s (larger odd factors are not restated); twiddles
-// (cos, sin)(2 pi m / n) rounded to float (sincos_2pibyn<float>).
-inline std::pair<float, float> pf_twiddle(int n, long m) {
-    const double a = 2 * kPi * (double)m / (double)n;
-    return {(float)std::cos(a), (float)std::sin(a)};
-}
-
-inline std::vector<int> pf_factors(int n, bool real) {
-    std::vector<int> f;
-    int left = n;
-    if (!real)
-        while ((left & 7) == 0) {
-            f.push_back(8);
-            left >>= 3;
-        }
-    while ((left & 3) == 0) {
-        f.push_back(4);
-        left >>= 2;
-    }
-    if ((left & 1) == 0) {
-        left >>= 1;
-        f.push_back(2);
-        std::swap(f.front(), f.back());
-    }
-    for (int d : {3, 5})
-        while (left % d == 0) {
-            f.push_back(d);
-            left /= d;
-        }
-    if (left != 1 || f.size() > 8) throw std::runtime_error("pocketfft plan: unsupported length");
-    return f;
-}
-
-inline void pf_row_plan(int n, fcdk::PfPlan& p, std::vector<float>& tw) {  // rfftp::comp_twiddle
-    const std::vector<int> f = pf_factors(n, true);
-    p.nf = (int)f.size();
-    long l1 = 1;
-    for (int k = 0; k < p.nf; ++k) {
-        const int ip = f[k];
-        const long ido = n / (l1 * ip);
-        p.fct[k] = ip;
-        p.tw[k] = (int)tw.size();
-        const size_t len = (size_t)std::max<long>((ip - 1) * (ido - 1), 1);
-        tw.resize(tw.size() + len, 0.f);
-        if (k < p.nf - 1)
-            for (int j = 1; j < ip; ++j)
-                for (long i = 1; i <= (ido - 1) / 2; ++i) {
-                    const auto w = pf_twiddle(n, j * l1 * i);
-                    tw[p.tw[k] + (j - 1) * (ido - 1) + 2 * i - 2] = w.first;
-                    tw[p.tw[k] + (j - 1) * (ido - 1) + 2 * i - 1] = w.second;
-                }
-        l1 *= ip;
-    }
-}
-
-// cfftp::comp_twiddle; tw holds (cos, sin) float pairs (the device reads them as float2)
-inline void pf_col_plan(int n, fcdk::PfPlan& p, std::vector<float>& tw) {
-    const std::vector<int> f = pf_factors(n, false);
-    p.nf = (int)f.size();
-    long l1 = 1;
-    for (int k = 0; k < p.nf; ++k) {
-        const int ip = f[k];
-        const long ido = n / (l1 * ip);
-        p.fct[k] = ip;
-        p.tw[k] = (int)(tw.size() / 2);  // offset in (cos, sin) pairs
-        const size_t len = (size_t)std::max<long>((ip - 1) * (ido - 1), 1);
-        tw.resize(tw.size() + 2 * len, 0.f);
-        for (int j = 1; j < ip; ++j)
-            for (long i = 1; i < ido; ++i) {
-                const auto w = pf_twiddle(n, j * l1 * i);
-                const size_t o = 2 * ((size_t)p.tw[k] + (j - 1) * (ido - 1) + i - 1);
-                tw[o] = w.first;
-                tw[o + 1] = w.second;
-            }
-        l1 *= ip;
-    }
-}
-
 struct Blob {
     int first;     // raster index of its first pixel (skimage label order)
     int peak;      // raster index of its max pixel (first in row-major on ties)
-    float value;
+    double value;  // |F| at the peak (float32 or float64 spectrum, exact in double)
 };
 
 
 // fourier.find_peak_locations (fourier.py:139-168) on the host, from an image's
 // candidate list: the images whose above-threshold set exceeds the device labelling
 // kernel's capacity (fcdk::label_peaks).  Returns the 4 dimmest blobs in order.
-inline std::vector<Blob> label_candidates_host(int H, int W, const std::vector<int>& idx_in, const std::vector<float>& val_in) {
+inline std::vector<Blob> label_candidates_host(int H, int W, const std::vector<int>& idx_in,
+                                               const std::vector<double>& val_in) {
     const size_t n = idx_in.size();
     std::vector<size_t> order(n);
     std::iota(order.begin(), order.end(), 0);
     std::sort(order.begin(), order.end(), [&](size_t a, size_t b) { return idx_in[a] < idx_in[b]; });
     std::vector<int> idx(n);
-    std::vector<float> val(n);
+    std::vector<double> val(n);
     for (size_t i = 0; i < n; ++i) {
         idx[i] = idx_in[order[i]];
         val[i] = val_in[order[i]];
@@ -263,7 +175,7 @@ inline void carrier_geometry(int H, int W, fcd_ref_info& info, std::vector<int>&
 // from the 4 dimmest blobs (fourier.py:38-39, fcd.py:53-101): sets info and
 // disk_rows_host.
 inline void carriers_from_blobs(int H, int W, fcd_ref_info& info, std::vector<int>& disk_rows_host,
-                                const std::vector<Blob>& blobs, float thr, double square_size) {
+                                const std::vector<Blob>& blobs, double thr, double square_size) {
     if (blobs.size() < 1) throw FcdError(FCD_E_NOPEAKS, "find_peaks: no spectral peaks above threshold");
 
     const std::vector<double> kr = wavenumber(H, 1.0, true), kc = wavenumber(W, 1.0, true);

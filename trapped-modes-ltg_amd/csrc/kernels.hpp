@@ -7,7 +7,7 @@
 #include <cstdlib>
 #include <vector>
 
-#include "host_logic.hpp"  // fcdk::PfPlan
+#include "pocketfft.hpp"  // pf::Plan
 
 namespace fcdk {
 
@@ -82,6 +82,8 @@ bool fft_size_supported(int n);
 // frame ingest (kernels_ingest.hip): raw samples (FCD_FMT_*) -> float32 frames
 size_t raw_frame_bytes(int format, int H, int W);
 void ingest(int format, const void* raw, int nframes, int H, int W, float* out, hipStream_t s);
+// float64 -> float32, rounded to nearest (numpy astype)
+void convert_f64(const double* in, long n, float* out, hipStream_t s);
 
 // ---- band-pruned per-frame pipeline (kernels_fast.hip) ----
 void demod_rows(int W, const float* frames, int H, int nb, const DemodTables& T, float2* Xb, const float2* tw,
@@ -167,25 +169,25 @@ void disk_band_t(const float2* spec_t, float2* out, int nbatch, int H, int W, in
 void disk_mask(const float2* in, float2* out, int nbatch, int H, int W, DiskTable t, hipStream_t s, bool transposed = false);
 // theta = atan2(R)  (reference carrier angle)
 void angle(const float2* in, float* out, long n, hipStream_t s);
-// Batched reference setup (fourier.find_peaks for nb images): out[b] = img[b] - mean(img[b])
-// (f64 mean, f32 difference; the exact numpy mean is pf_center); |F| (np.abs's float32
-// formula) * highpass per image with its maximum and the
-// above-threshold candidates (cap per image, border excluded); 8-connected labelling and
-// the 4 dimmest blobs' peaks per image (res: 8 ints per image, see kernels_fft.hip).
-void center_images(const float* img, int nb, long hw, double* sums, float* out, hipStream_t s);
-void spectrum_candidates_b(const float2* F, int nb, int H, int W, const double* krow_s, const double* kcol_s,
-                           double kmin2, float* mag, unsigned* maxbits, int* count, int* idx, float* val, int cap,
-                           hipStream_t s);
-void label_peaks(const int* counts, const int* idx, const float* val, int cap, int nb, int H, int W, int* res,
+// Batched reference setup (fourier.find_peaks for nb images): |F| (np.abs's formula for
+// complex64 / complex128) * highpass per image with its maximum (as unsigned bits of the
+// float / double, zero-extended) and the above-threshold candidates (cap per image,
+// border excluded); 8-connected labelling and the 4 dimmest blobs' peaks per image for
+// float32 spectra (res: 8 ints per image, see kernels_fft.hip).
+void spectrum_candidates_b(const void* F, bool f64, int nb, int H, int W, const double* krow_s, const double* kcol_s,
+                           double kmin2, void* mag, unsigned long long* maxbits, int* count, int* idx, void* val,
+                           long cap, hipStream_t s);
+void label_peaks(const int* counts, const int* idx, const float* val, long cap, int nb, int H, int W, int* res,
                  hipStream_t s);
-// The reference's float32 spectrum bit for bit (kernels_pocketfft.hip): numpy's float32
-// mean and centring, scipy 1.7.1 pocketfft's fft2 of real float32 images.  Plans: the
-// factor sequence of rfftp (rows) / cfftp (columns) and each pass's offset into its
-// twiddle table (float cos / sin pairs for rows, float2 for columns), built on the host.
-int pf_chunk_count(long hw);  // sums: nb * pf_chunk_count(hw) floats
-void pf_center(const float* img, int nb, long hw, float* sums, float* out, hipStream_t s);
-void pf_fft2(const float* in, int nb, int H, int W, const PfPlan& rows, const float* rtw, const PfPlan& cols,
-             const float2* ctw, float2* F, hipStream_t s);
+// The reference's spectrum bit for bit (kernels_pocketfft.hip, pocketfft.hpp): numpy's
+// mean and centring, scipy 1.7.1 pocketfft's fft2 of real images of any shape, float32
+// or float64 (f64).  Plans and tables from pf::make_plan (rows real, columns complex).
+int pf_chunk_count(long hw);  // sums: nb * pf_chunk_count(hw) elements
+// global scratch the transforms need when a row's / column's buffers exceed LDS
+size_t pf_scratch_bytes(const pf::Plan& rows, const pf::Plan& cols, bool f64);
+void pf_center(const void* img, bool f64, int nb, long hw, void* sums, void* out, hipStream_t s);
+void pf_fft2(const void* in, bool f64, int nb, int H, int W, const pf::Plan& rows, const void* rtab, const pf::Plan& cols,
+             const void* ctab, void* F, void* scratch, hipStream_t s);
 
 // kernels_phase_rows_wide.hip: the fused kernel at 2048- and 4096-point rows, and its
 // REF mode (4096: the reference's band angles into theta_b, [2][H][W])

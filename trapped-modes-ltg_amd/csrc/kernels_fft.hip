@@ -268,40 +268,10 @@ void angle(const float2* in, float* out, long n, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------ batched reference setup
-// fourier.find_peaks (fourier.py:7-41) for nb images at once, every stage on the
-// device: f64 image means, (image - mean) in f32 (the row FFT's input), |F| * highpass
-// with a per-image maximum, the above-threshold candidates per image, and the
-// 8-connected labelling with the peak pick (k_label_peaks).
-__global__ void k_mean_b(const float* __restrict__ img, long hw, double* sums) {
-    __shared__ double part[256];
-    const float* p = img + (long)blockIdx.y * hw;
-    double acc = 0.0;
-    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < hw; i += (long)gridDim.x * blockDim.x)
-        acc += (double)p[i];
-    part[threadIdx.x] = acc;
-    __syncthreads();
-    for (int st = 128; st > 0; st >>= 1) {
-        if ((int)threadIdx.x < st) part[threadIdx.x] += part[threadIdx.x + st];
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) atomicAdd(sums + blockIdx.y, part[0]);
-}
-
-__global__ void k_center_b(const float* __restrict__ img, long hw, long n, const double* __restrict__ sums,
-                           float* __restrict__ out) {
-    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= n) return;
-    out[idx] = img[idx] - (float)(sums[idx / hw] / (double)hw);  // image - mean, fourier.py:18
-}
-
-void center_images(const float* img, int nb, long hw, double* sums, float* out, hipStream_t s) {
-    FCD_HIPCHK(hipMemsetAsync(sums, 0, sizeof(double) * nb, s));
-    hipLaunchKernelGGL(k_mean_b, dim3(256, nb), dim3(256), 0, s, img, hw, sums);
-    FCD_CHECK_LAUNCH();
-    const long n = (long)nb * hw;
-    hipLaunchKernelGGL(k_center_b, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, img, hw, n, sums, out);
-    FCD_CHECK_LAUNCH();
-}
+// fourier.find_peaks (fourier.py:7-41) for nb images at once: |F| * highpass of the
+// reference's own spectrum (kernels_pocketfft.hip) with a per-image maximum, the
+// above-threshold candidates per image, and the 8-connected labelling with the peak pick
+// (k_label_peaks, float32 spectra).
 
 // Correctly rounded float32 square root of a positive normal x.  v_sqrt_f32 (what
 // sqrtf / __fsqrt_rn lower to here) is within 1 ulp but not correctly rounded; the
@@ -319,11 +289,12 @@ __device__ __forceinline__ float sqrt_rn(float x) {
     return s;
 }
 
-// np.abs of a complex64 value as numpy 1.26.4 computes it (its AVX512F loop,
+// np.abs of a complex value as numpy 1.26.4 computes it (its AVX512F loop,
 // loops_unary_complex: larger * sqrt(fma(r, r, 1)) with r = smaller / larger, inf / NaN
 // cases first); this file is compiled without FMA contraction, the one FMA is explicit,
-// the division is the IEEE sequence (v_div_scale / fmas / fixup).
-__device__ __forceinline__ float np_cabsf(float2 f) {
+// the division is the IEEE sequence (v_div_scale / fmas / fixup).  The float64 square
+// root is __dsqrt_rn (correctly rounded).
+__device__ __forceinline__ float np_cabs(float2 f) {
     const float re = fabsf(f.x), im = fabsf(f.y);
     if (re == INFINITY || im == INFINITY) return INFINITY;
     if (re != re || im != im) return NAN;
@@ -331,47 +302,64 @@ __device__ __forceinline__ float np_cabsf(float2 f) {
     const float r = big == 0.f ? 0.f : __fdiv_rn(small, big);
     return __fmul_rn(sqrt_rn(__fmaf_rn(r, r, 1.0f)), big);
 }
+__device__ __forceinline__ double np_cabs(double2 f) {
+    const double re = fabs(f.x), im = fabs(f.y);
+    if (re == INFINITY || im == INFINITY) return INFINITY;
+    if (re != re || im != im) return NAN;
+    const double big = fmax(re, im), small = fmin(im, re);
+    const double r = big == 0.0 ? 0.0 : __ddiv_rn(small, big);
+    return __dmul_rn(__dsqrt_rn(__fma_rn(r, r, 1.0)), big);
+}
+__device__ __forceinline__ unsigned long long order_bits(float m) { return __float_as_uint(m); }
+__device__ __forceinline__ unsigned long long order_bits(double m) { return (unsigned long long)__double_as_longlong(m); }
+__device__ __forceinline__ float from_bits(unsigned long long u, float) { return __uint_as_float((unsigned)u); }
+__device__ __forceinline__ double from_bits(unsigned long long u, double) { return __longlong_as_double((long long)u); }
 
-__global__ void k_spectrum_mag_b(const float2* __restrict__ F, float* __restrict__ mag, unsigned* maxbits, int H,
+template <class T, class C>
+__global__ void k_spectrum_mag_b(const C* __restrict__ F, T* __restrict__ mag, unsigned long long* maxbits, int H,
                                  int W, long n, const double* __restrict__ krow_s, const double* __restrict__ kcol_s,
                                  double kmin2) {
     const long gidx = (long)blockIdx.x * blockDim.x + threadIdx.x;
     const long hw = (long)H * W;
-    float m = 0.f;
-    const long b = gidx / hw;  // H * W is a multiple of 64: a wave stays in one image
+    T m = T(0);
+    const long b = gidx / hw;
     if (gidx < n) {
         const long idx = gidx - b * hw;
         const int si = (int)(idx / W), sj = (int)(idx % W);
-        int i = (si + H / 2) % H, j = (sj + W / 2) % W;
-        const int mi = (H - i) % H, mj = (W - j) % W;  // one canonical bin per Hermitian pair
+        int i = (si + H / 2) % H, j = (sj + W / 2) % W;  // fftshift: shifted (si, sj) <- unshifted (i, j)
+        const int mi = (H - i) % H, mj = (W - j) % W;   // one canonical bin per Hermitian pair
         if (mi < i || (mi == i && mj < j)) {
             i = mi;
             j = mj;
         }
-        const float2 f = F[b * hw + (long)i * W + j];
-        m = np_cabsf(f);
+        m = np_cabs(F[b * hw + (long)i * W + j]);
         const double kr = krow_s[si], kc = kcol_s[sj];
         const double k2 = __dadd_rn(__dmul_rn(kr, kr), __dmul_rn(kc, kc));
-        if (!(k2 > kmin2)) m = 0.f;
+        if (!(k2 > kmin2)) m = T(0);  // image_fft *= highpass_mask() (fourier.py:20-23, 34)
         mag[gidx] = m;
     }
-    unsigned u = __float_as_uint(m);
+    // the per-image maximum (a wave may span two images when H * W is not a multiple of 64)
+    const unsigned long long u = order_bits(m);
+    const long b0 = __shfl(b, 0, 64);
+    unsigned long long uw = b == b0 ? u : 0ull;
     for (int o = 32; o > 0; o >>= 1) {
-        const unsigned v = __shfl_xor(u, o, 64);
-        u = v > u ? v : u;
+        const unsigned long long v = __shfl_xor(uw, o, 64);
+        uw = v > uw ? v : uw;
     }
-    if ((threadIdx.x & 63) == 0 && b * hw < n) atomicMax(maxbits + b, u);
+    if ((threadIdx.x & 63) == 0 && b0 * hw < n) atomicMax(maxbits + b0, uw);
+    if (b != b0 && gidx < n) atomicMax(maxbits + b, u);
 }
 
-__global__ void k_candidates_b(const float* __restrict__ mag, const unsigned* __restrict__ maxbits, int H, int W,
-                               long n, int* count, int* idx_out, float* val_out, int cap) {
+template <class T>
+__global__ void k_candidates_b(const T* __restrict__ mag, const unsigned long long* __restrict__ maxbits, int H, int W,
+                               long n, int* count, int* idx_out, T* val_out, long cap) {
     const long gidx = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (gidx >= n) return;
     const long hw = (long)H * W, b = gidx / hw, idx = gidx - b * hw;
     const int si = (int)(idx / W), sj = (int)(idx % W);
     if (si == 0 || sj == 0 || si == H - 1 || sj == W - 1) return;  // fourier.py:154-158
-    const float thr = 0.5f * __uint_as_float(maxbits[b]);           // fourier.py:35
-    const float m = mag[gidx];
+    const T thr = T(0.5) * from_bits(maxbits[b], T(0));             // fourier.py:35 (exact)
+    const T m = mag[gidx];
     if (m > thr) {
         const int slot = atomicAdd(count + b, 1);
         if (slot < cap) {
@@ -381,18 +369,29 @@ __global__ void k_candidates_b(const float* __restrict__ mag, const unsigned* __
     }
 }
 
-void spectrum_candidates_b(const float2* F, int nb, int H, int W, const double* krow_s, const double* kcol_s,
-                           double kmin2, float* mag, unsigned* maxbits, int* count, int* idx, float* val, int cap,
-                           hipStream_t s) {
+template <class T, class C>
+void candidates_t(const C* F, int nb, int H, int W, const double* krow_s, const double* kcol_s, double kmin2, T* mag,
+                  unsigned long long* maxbits, int* count, int* idx, T* val, long cap, hipStream_t s) {
     const long n = (long)nb * H * W;
-    FCD_HIPCHK(hipMemsetAsync(maxbits, 0, sizeof(unsigned) * nb, s));
+    FCD_HIPCHK(hipMemsetAsync(maxbits, 0, sizeof(unsigned long long) * nb, s));
     FCD_HIPCHK(hipMemsetAsync(count, 0, sizeof(int) * nb, s));
-    hipLaunchKernelGGL(k_spectrum_mag_b, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, F, mag, maxbits, H, W, n,
-                       krow_s, kcol_s, kmin2);
+    hipLaunchKernelGGL((k_spectrum_mag_b<T, C>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, F, mag, maxbits, H,
+                       W, n, krow_s, kcol_s, kmin2);
     FCD_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_candidates_b, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, mag, maxbits, H, W, n,
+    hipLaunchKernelGGL((k_candidates_b<T>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, mag, maxbits, H, W, n,
                        count, idx, val, cap);
     FCD_CHECK_LAUNCH();
+}
+
+void spectrum_candidates_b(const void* F, bool f64, int nb, int H, int W, const double* krow_s, const double* kcol_s,
+                           double kmin2, void* mag, unsigned long long* maxbits, int* count, int* idx, void* val,
+                           long cap, hipStream_t s) {
+    if (f64)
+        candidates_t<double, double2>(static_cast<const double2*>(F), nb, H, W, krow_s, kcol_s, kmin2,
+                                      static_cast<double*>(mag), maxbits, count, idx, static_cast<double*>(val), cap, s);
+    else
+        candidates_t<float, float2>(static_cast<const float2*>(F), nb, H, W, krow_s, kcol_s, kmin2,
+                                    static_cast<float*>(mag), maxbits, count, idx, static_cast<float*>(val), cap, s);
 }
 
 // fourier.find_peak_locations (fourier.py:139-168) on one image's candidate list per
@@ -436,7 +435,7 @@ __device__ __forceinline__ void bitonic_lds(T* key, int n2) {
 }
 
 __global__ __launch_bounds__(1024) void k_label_peaks(const int* __restrict__ counts, const int* __restrict__ idxs,
-                                                      const float* __restrict__ vals, int cap, int H, int W,
+                                                      const float* __restrict__ vals, long cap, int H, int W,
                                                       int* __restrict__ res) {
     __shared__ unsigned long long sk[LABEL_CAP];  // (raster index, slot) for the first sort, (max, root) for the second
     __shared__ unsigned long long cm[LABEL_CAP];  // per root: (value bits, ~position) maximum
@@ -529,7 +528,7 @@ __global__ __launch_bounds__(1024) void k_label_peaks(const int* __restrict__ co
     }
 }
 
-void label_peaks(const int* counts, const int* idx, const float* val, int cap, int nb, int H, int W, int* res,
+void label_peaks(const int* counts, const int* idx, const float* val, long cap, int nb, int H, int W, int* res,
                  hipStream_t s) {
     hipLaunchKernelGGL(k_label_peaks, dim3(nb), dim3(1024), 0, s, counts, idx, val, cap, H, W, res);
     FCD_CHECK_LAUNCH();

@@ -23,6 +23,7 @@ FCD_E_INTERNAL = -6
 FCD_HOST_PTRS = 0
 FCD_DEVICE_PTRS = 1
 FCD_STACK_F64 = 2  # temporal calls: float64 samples
+FCD_IMG_F64 = 4  # set_reference / find_peaks / fft2: float64 images (the reference's precision)
 # frame sample formats (fcd_process_raw)
 FCD_FMT_F32 = 0
 FCD_FMT_U8 = 1
@@ -48,7 +49,7 @@ class FcdRefInfo(ctypes.Structure):
         ("mask_count", ctypes.c_int32 * 2),
         ("n_blobs", ctypes.c_int32),
         ("blob_peaks", (ctypes.c_int64 * 2) * 4),
-        ("threshold", ctypes.c_float),
+        ("threshold", ctypes.c_double),
     ]
 
 
@@ -124,6 +125,17 @@ def _f32(a):
     return np.ascontiguousarray(a, dtype=np.float32)
 
 
+def _img(a):
+    """An image in the precision the reference computes its spectrum in (fourier.py:18):
+    float64 stays float64, everything else becomes float32."""
+    a = np.asarray(a)
+    return np.ascontiguousarray(a, dtype=np.float64 if a.dtype == np.float64 else np.float32)
+
+
+def _img_flag(a):
+    return FCD_IMG_F64 if a.dtype == np.float64 else 0
+
+
 def _ptr(a):
     return None if a is None else a.ctypes.data
 
@@ -136,7 +148,7 @@ def _same_image(a, b):
     if a is b:
         return True
     a = np.asarray(a)
-    return a.shape == b.shape and np.array_equal(_f32(a), b)
+    return a.shape == b.shape and np.array_equal(_img(a), b) and _img(a).dtype == b.dtype
 
 
 class Engine:
@@ -178,7 +190,7 @@ class Engine:
 
     # ------------------------------------------------------------ reference
     def set_reference(self, reference, square_size):
-        ref = _f32(reference)
+        ref = _img(reference)
         if ref.shape != self.shape:
             raise ValueError(f"reference shape {ref.shape} != engine shape {self.shape}")
         info = FcdRefInfo()
@@ -187,8 +199,8 @@ class Engine:
         self.ref_copy = None
         self.ref_square_size = None
         self.geometry = None
-        _check(self._lib.fcd_set_reference(self._h, ref.ctypes.data, FCD_HOST_PTRS, float(square_size),
-                                           ctypes.byref(info)))
+        _check(self._lib.fcd_set_reference(self._h, ref.ctypes.data, FCD_HOST_PTRS | _img_flag(ref),
+                                           float(square_size), ctypes.byref(info)))
         self.info = info
         self.ref_copy = ref.copy()
         self.ref_square_size = float(square_size)
@@ -217,8 +229,10 @@ class Engine:
                                           ctypes.byref(info)))
         self.info = info
         self.explicit = True
-        c0 = r0.copy()
-        c1 = c0 if r1 is r0 else r1.copy()
+        # the images as given (their precision identifies them for holds_carriers); the
+        # carrier signals themselves come from the float32 rounding
+        c0 = _img(ref0).copy()
+        c1 = c0 if r1 is r0 else _img(ref1).copy()
         self.geometry = (c0, c1, _peaks_of(info), (float(rad[0]), float(rad[1])), float(calibration_factor))
         return info
 
@@ -237,21 +251,21 @@ class Engine:
     def find_peaks(self, images, square_size=1.0):
         """fcd_find_peaks: FcdRefInfo per image of a [n, H, W] (or [H, W]) stack, the
         context's reference untouched."""
-        imgs = _f32(images)
+        imgs = _img(images)
         if imgs.ndim == 2:
             imgs = imgs[None]
         if imgs.shape[1:] != self.shape:
             raise ValueError(f"image shape {imgs.shape[1:]} != engine shape {self.shape}")
         infos = (FcdRefInfo * max(len(imgs), 1))()
-        _check(self._lib.fcd_find_peaks(self._h, imgs.ctypes.data, len(imgs), FCD_HOST_PTRS, float(square_size),
-                                        infos))
+        _check(self._lib.fcd_find_peaks(self._h, imgs.ctypes.data, len(imgs), FCD_HOST_PTRS | _img_flag(imgs),
+                                        float(square_size), infos))
         return [infos[i] for i in range(len(imgs))]
 
     def matches(self, reference, square_size):
         if self.explicit or self.ref_copy is None or self.ref_square_size != float(square_size):
             return False
-        ref = np.asarray(reference)
-        return ref.shape == self.ref_copy.shape and np.array_equal(_f32(ref), self.ref_copy)
+        ref = _img(reference)
+        return ref.shape == self.ref_copy.shape and ref.dtype == self.ref_copy.dtype and np.array_equal(ref, self.ref_copy)
 
     def carriers_arrays(self):
         h, w = self.shape
@@ -346,12 +360,14 @@ class Engine:
         return h[0] if squeeze else h
 
     def fft2(self, images):
-        x = _f32(images)
+        """scipy.fft.fft2 of real images, bit for bit: float32 -> complex64, float64 -> complex128."""
+        x = _img(images)
         squeeze = x.ndim == 2
         if squeeze:
             x = x[None]
-        out = np.empty(x.shape, np.complex64)
-        _check(self._lib.fcd_fft2(self._h, x.ctypes.data, x.shape[0], FCD_HOST_PTRS, out.ctypes.data, None))
+        out = np.empty(x.shape, np.complex128 if x.dtype == np.float64 else np.complex64)
+        _check(self._lib.fcd_fft2(self._h, x.ctypes.data, x.shape[0], FCD_HOST_PTRS | _img_flag(x), out.ctypes.data,
+                                  None))
         return out[0] if squeeze else out
 
 
