@@ -35,6 +35,8 @@ Fixtures (all under tests/golden/):
                      unwrap k-fields (bench_data.make_residue_frame, frame digests stored)
   mixed.npz          frame sides that are not powers of two (1024 x 1280, 1536 x 2048, a
                      960-row camera crop): as large.npz, plus fft2 digests of 5-smooth shapes
+  anyshape.npz       frame sides of any size (1080 x 1920, 1000 x 1000, prime / Bluestein
+                     sides 1023 x 1021 / 1021 x 1023, a 1000 x 1000 camera crop): as mixed.npz
   shapes.npz         any frame shape and float64 images: fft2 / mean / spectrum digests of
                      hashed integer images (bench_data.hash_image) at odd, prime, Bluestein
                      and camera shapes in float32 and float64, and the reference's carrier
@@ -502,15 +504,38 @@ def mixed_case_frames(spec):
     return ref, frame, 0.001
 
 
-def make_mixed():
+# Frame sides of any size (the generic chain with its radix-7 / generic odd-prime passes,
+# Bluestein sides and frames padded to multiples of 64 for the unwrap): the HD camera format
+# 1080 x 1920, 1000 x 1000 with residues, prime / Bluestein sides 1023 x 1021 and
+# 1021 x 1023 (with residues), and a 1000 x 1000 crop of the 10-bit camera pair.
+ANY_CASES = {
+    "s1080x1920": dict(rows=1080, cols=1920, seed=41, pairs=[]),
+    "r1000x1000": dict(rows=1000, cols=1000, seed=42, pairs=[(300.3, 400.6), (650.2, 700.7)]),
+    "s1023x1021": dict(rows=1023, cols=1021, seed=43, pairs=[]),
+    "r1021x1023": dict(rows=1021, cols=1023, seed=44, pairs=[(410.3, 520.4)]),
+    "c1000x1000": dict(crop=(12, 1012), ccrop=(20, 1020)),
+}
+
+
+def mixed_case_frames_any(spec):
+    if "ccrop" in spec:
+        (r0, r1), (c0, c1) = spec["crop"], spec["ccrop"]
+        ref = load_raw("reference_df.tif").astype(np.float32)[r0:r1, c0:c1]
+        frame = load_raw("prueba1_20250317_122608_C1S0001000001.tif").astype(np.float32)[r0:r1, c0:c1]
+        return np.ascontiguousarray(ref), np.ascontiguousarray(frame), 0.002
+    return mixed_case_frames(spec)
+
+
+def make_mixed(cases=None, name="mixed"):
     """mixed.npz: as large.npz for MIXED_CASES (heights on a ~256-wide sub-grid, wrapped
     phases on a ~128-wide one, the full k-fields), plus sha256 digests of scipy's fft2 of
     each reference and of seeded integer-valued images of other 5-smooth shapes (the
-    restated radix-3 / radix-5 pocketfft passes)."""
+    restated radix-3 / radix-5 pocketfft passes).  anyshape.npz: the same for ANY_CASES."""
     import hashlib
-    out = {"versions": VERSIONS, "cases": np.array(list(MIXED_CASES))}
-    for tag, spec in MIXED_CASES.items():
-        ref, frame, sq = mixed_case_frames(spec)
+    cases = MIXED_CASES if cases is None else cases
+    out = {"versions": VERSIONS, "cases": np.array(list(cases))}
+    for tag, spec in cases.items():
+        ref, frame, sq = mixed_case_frames_any(spec)
         rows, cols = ref.shape
         r = run_pair(ref, frame, sq, height=1.0)
         locs, thr = peak_locations(ref)
@@ -536,6 +561,9 @@ def make_mixed():
         })
         print("mixed", tag, ref.shape, r["peaks"].tolist(), r["cf"], "residues", out[f"{tag}_residues"].tolist(),
               flush=True)
+    if name != "mixed":
+        np.savez_compressed(os.path.join(OUT, name + ".npz"), **out)
+        return
     rng = np.random.default_rng(4242)
     shapes = [(192, 320), (320, 192), (576, 960), (128, 384)]
     for (h, w) in shapes:
@@ -748,7 +776,7 @@ def make_analyze_ref():
 
 if __name__ == "__main__":
     which = sys.argv[1:] or ["real_pair", "real_df", "unwrap", "synthetic", "integrate", "val", "ingest",
-                             "bench_board", "analyze_ref", "spectrum", "large", "mixed", "shapes"]
+                             "bench_board", "analyze_ref", "spectrum", "large", "mixed", "shapes", "anyshape"]
     if "real_pair" in which:
         make_real_pair()
     if "real_df" in which:
@@ -775,3 +803,5 @@ if __name__ == "__main__":
         make_mixed()
     if "shapes" in which:
         make_shapes()
+    if "anyshape" in which:
+        make_mixed(ANY_CASES, "anyshape")

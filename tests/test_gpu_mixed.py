@@ -65,16 +65,6 @@ def test_mixed_fft2_bit_exact_with_scipy(mixed, golden):
         assert hashlib.sha256(F.tobytes()).hexdigest() == str(g[f"{tag}_ref_fft2_sha"]), tag
 
 
-def test_unsupported_shapes_raise():
-    """Sides that are not multiples of 64 with a 5-smooth factorisation stay refused
-    (FCD_E_UNSUPPORTED), e.g. a 7 in the side or a side below 64."""
-    from pyfcd import _lib
-    for shape in ((1024, 7 * 64), (1000, 1024), (32, 64)):
-        with pytest.raises(_lib.FcdError) as e:
-            _lib.Engine(shape)
-        assert e.value.code == _lib.FCD_E_UNSUPPORTED
-
-
 @pytest.mark.parametrize("tag", CASES)
 def test_mixed_frames_match_reference_run(mixed, golden, tag):
     from oracle import fcd_oracle as O

@@ -137,6 +137,9 @@ std::vector<float2> band_pretwiddles(int W, int B) {
     return t;
 }
 
+// the smallest frame side fcd_create accepts (any larger one up to 8192, see mr_supported)
+constexpr int kMinSide = 16;
+
 int fcd_env_int(const char* name, int dflt) {
     const char* v = std::getenv(name);
     return (v && *v) ? std::atoi(v) : dflt;
@@ -191,6 +194,7 @@ struct fcd_ctx {
     DevBuf mr_scratch;  // the mixed-radix column transforms' transposed copy (chunk frames)
     DevBuf gb_tables;   // generic chain's band columns (build_demod_tables)
     DevBuf mst_slot;    // map -> MST slot (-1: not in it) for k_int_rows2 kmode 3
+    DevBuf pad_w, pad_k;  // maps padded to multiples of 64 for the unwrap (unwrap_maps) and their k
     int gb_NU = 0;      // columns in either carrier's disk
     hipStream_t own = nullptr;
     DevBuf tw_row, tw_col;        // plain tables exp(-2 pi i m / n) (generic LDS FFT kernels)
@@ -292,8 +296,8 @@ void ensure_chunk_buffers(fcd_ctx* c) {
     c->rescnt.ensure(n * 2 * sizeof(int));
 }
 
-void ensure_mst(fcd_ctx* c, int nact) {
-    const size_t nv = (size_t)nact * c->hw();
+void ensure_mst(fcd_ctx* c, int nact, long hw) {
+    const size_t nv = (size_t)nact * hw;
     if (nv <= c->mst_cap) return;
     c->mst_comp.ensure(nv * 4);
     c->mst_off.ensure(nv * 4);
@@ -306,7 +310,7 @@ void ensure_mst(fcd_ctx* c, int nact) {
     c->mst_hooks.ensure((2 + fcdk::kCgRounds) * sizeof(int));  // hooks this round; graph overflow; graph rounds' hooks
     // edge records for any tile side (FCD_MST_TILE may change between calls on the same buffers)
     const size_t ne = (size_t)fcdk::mst_cg_edge_capacity((long)nv);
-    const size_t nt = (size_t)nact * c->hw() / 1024 + 1;  // tiles (32 x 32 at the smallest)
+    const size_t nt = (size_t)nact * hw / 1024 + 1;  // tiles (32 x 32 at the smallest)
     c->cg_ncomp.ensure(nt * 4);
     c->cg_lcol.ensure(nt * 64 * 4);  // tile height <= 64
     c->cg_ecnt.ensure(nt * 4);
@@ -352,6 +356,8 @@ fcdk::MstWork mst_work(fcd_ctx* c) {
     m.cg_ew = c->cg_ew.as<unsigned long long>();
     m.cg_ec = c->cg_ec.as<int>();
     m.cg_ed = c->cg_ed.as<int>();
+    m.Hr = c->H;
+    m.Wr = c->W;
     return m;
 }
 
@@ -410,15 +416,18 @@ int mst_level() {
 // through *mk (k_int_rows2 kmode 3, no k-field pass; mk->map_slot null otherwise).
 // any_res: the residue counts only as "has residues" (> 0), which lets the count skip
 // the rest of a map once it has found one
-void unwrap_maps(fcd_ctx* c, const float* w, int nmaps, int32_t* k, int* res_host, hipStream_t s,
-                 bool all_mst = false, fcdk::MstK* mk = nullptr, bool any_res = false) {
+// H x W: the maps' (padded) size, multiples of 64 for the tile passes; Hr x Wr: the
+// frame's own size (the reliabilities' border, MstWork::Hr / Wr).
+void unwrap_core(fcd_ctx* c, const float* w, int nmaps, int H, int W, int Hr, int Wr, int32_t* k, int* res_host,
+                 hipStream_t s, bool all_mst, fcdk::MstK* mk, bool any_res) {
     if (mk) mk->map_slot = nullptr;
+    const long hw = (long)H * W;
     std::vector<int> active;
     if (all_mst) {
         for (int i = 0; i < nmaps; ++i) active.push_back(i);
     } else {
         int* res = c->rescnt.as<int>();
-        fcdk::residues(w, nmaps, c->H, c->W, res, s, any_res);
+        fcdk::residues(w, nmaps, H, W, res, s, any_res);
         std::vector<int> counts(nmaps);
         HIPCHK(hipMemcpyAsync(counts.data(), res, sizeof(int) * nmaps, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
@@ -428,10 +437,12 @@ void unwrap_maps(fcd_ctx* c, const float* w, int nmaps, int32_t* k, int* res_hos
     }
     // the scan unwrap for the residue-free maps (the MST pass overwrites the others);
     // skipped when every map has residues (the fix-up groups of camera frames)
-    if ((int)active.size() < nmaps) fcdk::unwrap_scan(w, nmaps, c->H, c->W, c->colk.as<int>(), k, s);
+    if ((int)active.size() < nmaps) fcdk::unwrap_scan(w, nmaps, H, W, c->colk.as<int>(), k, s);
     if (active.empty()) return;
-    ensure_mst(c, (int)active.size());
+    ensure_mst(c, (int)active.size(), hw);
     fcdk::MstWork m = mst_work(c);
+    m.Hr = Hr;
+    m.Wr = Wr;
     const int nact = (int)active.size();
     upload(c->mst_ids.p, active.data(), sizeof(int) * nact, s);
     const int max_rounds = 64;
@@ -440,14 +451,14 @@ void unwrap_maps(fcd_ctx* c, const float* w, int nmaps, int32_t* k, int* res_hos
     // third round (a round after convergence hooks nothing and changes nothing).
     int level = mst_level();
     int tile_h = 0;
-    const int tile_w = fcdk::mst_tile_shape(c->H, c->W, &tile_h);
+    const int tile_w = fcdk::mst_tile_shape(H, W, &tile_h);
     if (level == 3 && tile_w > 0) {
         HIPCHK(hipMemsetAsync(m.nhooks + 1, 0, (1 + fcdk::kCgRounds) * sizeof(int), s));
-        fcdk::mst_tile_level0(w, c->mst_ids.as<int>(), nact, c->H, c->W, m, s, true);
+        fcdk::mst_tile_level0(w, c->mst_ids.as<int>(), nact, H, W, m, s, true);
         bool fits = true;
         static const bool cg_dbg = std::getenv("FCD_MST_DEBUG") != nullptr;
         auto cg_dump = [&](int r) {  // diagnostic: components and contracted edges entering round r
-            const size_t nt = (size_t)nact * (c->H / tile_h) * (c->W / tile_w);
+            const size_t nt = (size_t)nact * (H / tile_h) * (W / tile_w);
             std::vector<int> nc(nt), ne(nt);
             HIPCHK(hipMemcpyAsync(nc.data(), m.cg_ncomp, nt * 4, hipMemcpyDeviceToHost, s));
             HIPCHK(hipMemcpyAsync(ne.data(), m.cg_ecnt, nt * 4, hipMemcpyDeviceToHost, s));
@@ -470,7 +481,7 @@ void unwrap_maps(fcd_ctx* c, const float* w, int nmaps, int32_t* k, int* res_hos
         for (int step = first; rounds < max_rounds; rounds += step, step = 3) {
             for (int g = 0; g < step; ++g) {
                 if (cg_dbg) cg_dump(rounds + g);
-                fcdk::mst_cg_round(nact, c->H, c->W, m, rounds + g, s);
+                fcdk::mst_cg_round(nact, H, W, m, rounds + g, s);
             }
             // nhooks[1]: a tile graph over its capacity; nhooks[2 + r]: hooks in round r
             const int last = rounds + step - 1;
@@ -490,10 +501,10 @@ void unwrap_maps(fcd_ctx* c, const float* w, int nmaps, int32_t* k, int* res_hos
                 for (int i = 0; i < nact; ++i) slot[active[i]] = i;
                 c->mst_slot.ensure(slot.size() * sizeof(int));
                 upload(c->mst_slot.p, slot.data(), slot.size() * sizeof(int), s);
-                *mk = fcdk::MstK{m.crank, m.coff, m.offk, c->mst_slot.as<int>(), fcdk::mst_cg_geom(c->H, c->W)};
+                *mk = fcdk::MstK{m.crank, m.coff, m.offk, c->mst_slot.as<int>(), fcdk::mst_cg_geom(H, W)};
                 return;
             }
-            fcdk::mst_cg_finalize(c->mst_ids.as<int>(), nact, c->H, c->W, m, k, s);
+            fcdk::mst_cg_finalize(c->mst_ids.as<int>(), nact, H, W, m, k, s);
             return;
         }
         level = 2;  // the boundary-list rounds need no capacity bound
@@ -502,14 +513,14 @@ void unwrap_maps(fcd_ctx* c, const float* w, int nmaps, int32_t* k, int* res_hos
     if (level >= 1) {
         if (level >= 2 && tile_w > 0) {
             // level-0 components from Boruvka inside 32 x 32 tiles (LDS)
-            fcdk::mst_tile_level0(w, c->mst_ids.as<int>(), nact, c->H, c->W, m, s);
+            fcdk::mst_tile_level0(w, c->mst_ids.as<int>(), nact, H, W, m, s);
         } else {
             // one pixel round
-            fcdk::mst_init(w, c->mst_ids.as<int>(), nact, c->H, c->W, m, s);
-            fcdk::mst_round(w, c->mst_ids.as<int>(), nact, c->H, c->W, m, s, true);
+            fcdk::mst_init(w, c->mst_ids.as<int>(), nact, H, W, m, s);
+            fcdk::mst_round(w, c->mst_ids.as<int>(), nact, H, W, m, s, true);
         }
         // then rounds over the boundary / root lists only
-        fcdk::mst_level_setup(nact, c->H, c->W, m, s);
+        fcdk::mst_level_setup(nact, H, W, m, s);
         static const bool dbg = std::getenv("FCD_MST_DEBUG") != nullptr;
         auto dump = [&](int r) {  // diagnostic: list sizes (B, R) entering round r
             std::vector<int> cnt((size_t)fcdk::mst_level_counts());
@@ -519,13 +530,13 @@ void unwrap_maps(fcd_ctx* c, const float* w, int nmaps, int32_t* k, int* res_hos
             long tot[5] = {0, 0, 0, 0, 0};
             for (int l = 0; l < 5; ++l)
                 for (size_t g = 0; g < nb; ++g) tot[l] += cnt[l * nb + g];
-            std::fprintf(stderr, "[mst] nv %ld round %d: B %ld R %ld L0 %ld\n", (long)nact * c->hw(), r,
+            std::fprintf(stderr, "[mst] nv %ld round %d: B %ld R %ld L0 %ld\n", (long)nact * hw, r,
                          tot[r & 1], tot[2 + (r & 1)], tot[4]);
         };
         for (; rounds < max_rounds; rounds += 3) {
             for (int g = 0; g < 3; ++g) {
                 if (dbg) dump(rounds + g);
-                fcdk::mst_level_round(w, c->mst_ids.as<int>(), nact, c->H, c->W, m, rounds + g, s);
+                fcdk::mst_level_round(w, c->mst_ids.as<int>(), nact, H, W, m, rounds + g, s);
             }
             int hooks = 0;
             HIPCHK(hipMemcpyAsync(&hooks, m.nhooks, sizeof(int), hipMemcpyDeviceToHost, s));
@@ -533,20 +544,42 @@ void unwrap_maps(fcd_ctx* c, const float* w, int nmaps, int32_t* k, int* res_hos
             if (hooks == 0) break;
         }
         if (rounds >= max_rounds) throw FcdError(FCD_E_INTERNAL, "unwrap: Boruvka did not converge");
-        fcdk::mst_level_finalize(c->mst_ids.as<int>(), nact, c->H, c->W, m, k, s);
+        fcdk::mst_level_finalize(c->mst_ids.as<int>(), nact, H, W, m, k, s);
         return;
     }
-    fcdk::mst_init(w, c->mst_ids.as<int>(), nact, c->H, c->W, m, s);
+    fcdk::mst_init(w, c->mst_ids.as<int>(), nact, H, W, m, s);
     for (; rounds < max_rounds; rounds += 3) {
         for (int g = 0; g < 3; ++g)
-            fcdk::mst_round(w, c->mst_ids.as<int>(), nact, c->H, c->W, m, s, rounds + g == 0);
+            fcdk::mst_round(w, c->mst_ids.as<int>(), nact, H, W, m, s, rounds + g == 0);
         int hooks = 0;
         HIPCHK(hipMemcpyAsync(&hooks, m.nhooks, sizeof(int), hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
         if (hooks == 0) break;
     }
     if (rounds == max_rounds) throw FcdError(FCD_E_INTERNAL, "unwrap: Boruvka did not converge");
-    fcdk::mst_finalize(c->mst_ids.as<int>(), nact, c->H, c->W, m, k, s);
+    fcdk::mst_finalize(c->mst_ids.as<int>(), nact, H, W, m, k, s);
+}
+
+// k-fields of nmaps wrapped maps of the context's frame size (unwrap_core); a frame whose
+// sides are not multiples of 64 is unwrapped in a copy padded by replicating its last row
+// and column (kernels_unwrap.hip pad_maps: same residues, same k on the frame's pixels).
+void unwrap_maps(fcd_ctx* c, const float* w, int nmaps, int32_t* k, int* res_host, hipStream_t s,
+                 bool all_mst = false, fcdk::MstK* mk = nullptr, bool any_res = false) {
+    const int H = c->H, W = c->W;
+    if (H % 64 == 0 && W % 64 == 0) {
+        unwrap_core(c, w, nmaps, H, W, H, W, k, res_host, s, all_mst, mk, any_res);
+        return;
+    }
+    if (mk) mk->map_slot = nullptr;
+    const int Hp = (H + 63) / 64 * 64, Wp = (W + 63) / 64 * 64;
+    const size_t np = (size_t)nmaps * Hp * Wp;
+    c->pad_w.ensure(np * sizeof(float));
+    c->pad_k.ensure(np * sizeof(int32_t));
+    c->colk.ensure((size_t)nmaps * Hp * sizeof(int));
+    fcdk::pad_maps(w, nmaps, H, W, Hp, Wp, c->pad_w.as<float>(), s);
+    unwrap_core(c, c->pad_w.as<float>(), nmaps, Hp, Wp, H, W, c->pad_k.as<int32_t>(), res_host, s, all_mst, nullptr,
+                any_res);
+    fcdk::unpad_k(c->pad_k.as<int32_t>(), nmaps, Hp, Wp, H, W, k, s);
 }
 
 // Integration tables for calibration factor cf (fourier.py:128-131, 75-92).
@@ -713,7 +746,7 @@ void build_demod_tables(fcd_ctx* c, hipStream_t s) {
         int n = 0;
         for (int sc = 0; sc < W; ++sc) {
             if (rows[2 * sc] > rows[2 * sc + 1]) continue;
-            const int uc = (sc + W / 2) % W;  // ifftshift: shifted column -> unshifted
+            const int uc = (sc + W - W / 2) % W;  // ifftshift: shifted column -> unshifted (any W)
             colslot[(size_t)q * W + uc] = n;
             const int hc = uc <= W / 2 ? uc : W - uc;
             per_hc[hc].push_back(Out{q, n, uc > W / 2 ? 1 : 0, uc, rows[2 * sc], rows[2 * sc + 1]});
@@ -1086,9 +1119,11 @@ FCD_API int fcd_create(int device, int rows, int cols, fcd_ctx** out) {
         if (!out) throw FcdError(FCD_E_INVALID, "out is null");
         *out = nullptr;
         const bool pow2 = fcdk::fft_size_supported(rows) && fcdk::fft_size_supported(cols);
-        if (!pow2 && !(fcdk::mr_supported(rows) && fcdk::mr_supported(cols)))
-            throw FcdError(FCD_E_UNSUPPORTED, "rows and cols must be multiples of 64 in [64, 4096] of the form "
-                                              "2^a 3^b 5^c, got " + std::to_string(rows) + "x" + std::to_string(cols));
+        if (!pow2 && !(rows >= kMinSide && cols >= kMinSide && fcdk::mr_supported(rows) && fcdk::mr_supported(cols)))
+            throw FcdError(FCD_E_UNSUPPORTED, "frame sides must be in [" + std::to_string(kMinSide) +
+                                                  ", 8192] (at most 4096 for a side with a prime factor above " +
+                                                  std::to_string(fcdk::kMrMaxRadix) + "), got " + std::to_string(rows) +
+                                                  "x" + std::to_string(cols));
         int ndev = 0;
         HIPCHK(hipGetDeviceCount(&ndev));
         if (device < 0 || device >= ndev) throw FcdError(FCD_E_INVALID, "bad device ordinal");
@@ -1110,7 +1145,10 @@ FCD_API int fcd_create(int device, int rows, int cols, fcd_ctx** out) {
         HIPCHK(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking));
         c->pr_ctr.ensure(4 * sizeof(unsigned));
         HIPCHK(hipMemset(c->pr_ctr.p, 0, 4 * sizeof(unsigned)));
-        const std::vector<float2> tr = twiddles(cols), tc = twiddles(rows);
+        // plain tables exp(-2 pi i m / n) (power-of-two LDS kernels), or the mixed-radix plans'
+        // tables (with Bluestein's chirp and convolution spectra)
+        const std::vector<float2> tr = c->generic ? fcdk::mr_tables(c->mr_row) : twiddles(cols),
+                                  tc = c->generic ? fcdk::mr_tables(c->mr_col) : twiddles(rows);
         c->tw_row.ensure(tr.size() * sizeof(float2));
         c->tw_col.ensure(tc.size() * sizeof(float2));
         HIPCHK(hipMemcpy(c->tw_row.p, tr.data(), tr.size() * sizeof(float2), hipMemcpyHostToDevice));

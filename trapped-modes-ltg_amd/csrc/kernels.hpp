@@ -142,14 +142,22 @@ void row_fft(int W, bool inverse, RowIn in_mode, RowOut out_mode, const void* in
 // In-place batched column FFT of nbatch [H][W] complex arrays.
 void col_fft(int H, int W, bool inverse, float2* data, int nbatch, const float2* tw, hipStream_t s);
 // Mixed-radix row / column transforms (kernels_mr.hip) of the generic chain for sides that
-// are not powers of two: n = 2^a 3^b 5^c, a multiple of 64 in [64, 4096].
+// are not powers of two: radix 8 / 4 / 2 / 3 / 5 / 7 codelets, a generic pass for odd
+// primes <= kMrMaxRadix, Bluestein (power-of-two M) otherwise.  Sides up to 8192 (4096
+// with Bluestein).
+constexpr int kMrMaxRadix = 61;
 struct MrPlan {
     int n, nf;
-    int fct[8];  // radices in pass order: 8s, 4s, then 3s, 5s
+    int fct[24];  // radices in pass order (of n; of M with Bluestein)
+    int blue, M;  // Bluestein: convolution length
+    int tM, tc, tgf, tgi;  // offsets into the table of mr_tables (Bluestein)
 };
 bool mr_supported(int n);
 MrPlan mr_plan(int n);
-// as row_fft (same modes; tw: exp(-2 pi i m / n), m < n)
+// the plan's table: exp(-2 pi i m / n), m < n, then (Bluestein) the M-point table, the chirp
+// and the convolution kernels' spectra
+std::vector<float2> mr_tables(const MrPlan& p);
+// as row_fft (same modes; tw: mr_tables(p) on the device)
 void mr_rows(const MrPlan& p, bool inverse, RowIn in_mode, RowOut out_mode, const void* in, void* out, long nrows,
              int H, float sub, const float2* tw, const PhaseOut* ph, hipStream_t s);
 // [nb][R][C] -> [nb][C][R]
@@ -207,6 +215,10 @@ inline bool fcd_fused_env(const char* name) {  // FCD_FUSED_2048 / FCD_FUSED_409
 // an already-counted map skip their strips)
 void residues(const float* w, int nmaps, int H, int W, int* counts, hipStream_t s, bool any_only = false);
 void unwrap_scan(const float* w, int nmaps, int H, int W, int* colk, int32_t* k, hipStream_t s);
+// frames whose sides are not multiples of 64: unwrapped in a copy padded to Hp x Wp by
+// replicating the last row / column (kernels_unwrap.hip), k copied back
+void pad_maps(const float* w, int nmaps, int H, int W, int Hp, int Wp, float* out, hipStream_t s);
+void unpad_k(const int32_t* kp, int nmaps, int Hp, int Wp, int H, int W, int32_t* k, hipStream_t s);
 
 // The component-graph path's tile geometry: level-0 component of pixel v (vertex id slot *
 // H * W + pixel) = tile_of(v) * ccap + crank[v]
@@ -249,7 +261,14 @@ struct MstWork {
     // the component-graph path's level-0 labels, compact (aliases of comp / off): per pixel
     // its component's rank in its tile (< cg_ccap <= 256) and K(pixel) - K(component)
     unsigned char* crank; short* coff;
+    // the frame's own size when the maps were padded to multiples of 64 (fcd_engine.cpp
+    // unwrap_maps): the reference's border reliabilities lie on rows / columns 0 and Hr - 1
+    // / Wr - 1, and every pad pixel gets kPadRel, so every edge touching a pad pixel is
+    // heavier than every edge of the frame and the frame's MST is the padded graph's
+    // restricted to the frame (the k-field of the frame's pixels is unchanged)
+    int Hr, Wr;
 };
+constexpr double kPadRel = 1e300;
 // Maps listed in map_ids (device int[nact]) of the wrapped stack w.
 void mst_init(const float* w, const int* map_ids, int nact, int H, int W, MstWork m, hipStream_t s);
 // first: the round right after mst_init (every component a single vertex)

@@ -222,7 +222,7 @@ __global__ void k_disk_mask(const float2* __restrict__ in, float2* __restrict__ 
     if (idx >= n) return;
     const long p = idx % ((long)H * W);
     const int i = tr ? (int)(p % H) : (int)(p / W), j = tr ? (int)(p / H) : (int)(p % W);
-    const int si = (i + H / 2) % H, sj = (j + W / 2) % W;  // (any even side: the generic chain too)
+    const int si = (i + H / 2) % H, sj = (j + W / 2) % W;  // unshifted -> shifted (any side)
     const int2 rr = reinterpret_cast<const int2*>(t.rows)[sj];
     const bool inside = si >= rr.x && si <= rr.y;
     out[idx] = inside ? in[idx] : make_float2(0.f, 0.f);
@@ -326,7 +326,7 @@ __global__ void k_spectrum_mag_b(const C* __restrict__ F, T* __restrict__ mag, u
     if (gidx < n) {
         const long idx = gidx - b * hw;
         const int si = (int)(idx / W), sj = (int)(idx % W);
-        int i = (si + H / 2) % H, j = (sj + W / 2) % W;  // fftshift: shifted (si, sj) <- unshifted (i, j)
+        int i = (si + H - H / 2) % H, j = (sj + W - W / 2) % W;  // fftshift: shifted (si, sj) <- unshifted (i, j)
         const int mi = (H - i) % H, mj = (W - j) % W;   // one canonical bin per Hermitian pair
         if (mi < i || (mi == i && mj < j)) {
             i = mi;

@@ -1,24 +1,33 @@
 // Mixed-radix transforms for frame sides that are not powers of two.
 //
 // The reference takes frames of any shape (scipy.fft.fft2 at fcd.py:28, fourier.py:18,
-// fourier.py:134; ifft2 at fcd.py:118, carriers.py:23-24, fourier.py:137).  Camera
-// sensors are often 1280 x 1024, 1920 x 1536, 2048 x 1536 ...: this file gives the
-// engine's generic chain (fcd_engine.cpp: fft2_real / demod_phases / integrate_z /
-// reference_state) its row and column transforms at every side n = 2^a 3^b 5^c with n a
-// multiple of 64 in [64, 4096] (the multiple of 64 keeps the unwrap's 64 x 64 MST tiles
-// and 16-byte residue loads as they are).
+// fourier.py:134; ifft2 at fcd.py:118, carriers.py:23-24, fourier.py:137): camera sensors
+// deliver 1920 x 1080, 2448 x 2048, 1280 x 1024 ... frames.  This file gives the engine's
+// generic chain (fcd_engine.cpp: fft2_real / demod_phases / integrate_z /
+// reference_state / process_generic) its row and column transforms at every side n:
 //
-// One workgroup per row, the row in LDS, Stockham passes of radix 8 / 4 (the power of
-// two, in 8s then 4s) then 3s and 5s, each pass reading one LDS buffer and writing the
-// other (one barrier per pass), twiddles exp(-+2 pi i m / n) from the context's plain
-// table (computed in f64 on the host).  Columns go through a tiled transpose, the row
-// transform of length H, and the transpose back.  These are the generic-chain
-// transforms, not the band-pruned register FFTs of the power-of-two fast path: a frame
-// costs ~15 streaming passes over 16 bytes per pixel.
+//  * n whose prime factors are at most 61: one workgroup per row, the row in LDS,
+//    Stockham passes of radix 8 / 4 / 2 (the power of two, in 8s then 4s), then 3s, 5s,
+//    7s (register codelets) and any larger odd prime p <= 61 (a generic pass: the
+//    butterfly inputs pre-twiddled in place, then each output an LDS dot product of p
+//    terms), each pass reading one LDS buffer and writing the other; twiddles exp(-+2 pi
+//    i m / n) from the context's table (computed in f64 on the host);
+//  * n with a prime factor above 61 (1021, 2039, 4093 ...): Bluestein's identity, the
+//    length-n DFT as a circular convolution of length M = 2^ceil(log2(2n - 1)) <= 8192:
+//    a chirp c[m] = exp(-i pi (m^2 mod 2n) / n) premultiply, a radix-8/4/2 FFT of length
+//    M, a multiply by the precomputed FFT of the conjugate chirp (1/M folded in), the
+//    inverse FFT, the chirp postmultiply, all in the row's LDS (2 M complex).
+//
+// Columns go through a tiled transpose, the row transform of length H, and the transpose
+// back.  These are the generic-chain transforms, not the band-pruned register FFTs of
+// the power-of-two fast path.  Sides up to 8192 (4096 with Bluestein): a row's two
+// buffers fill at most 128 KB of the 160 KB LDS.
 #include <hip/hip_runtime.h>
 
+#include <complex>
 #include <stdexcept>
 #include <string>
+#include <vector>
 
 #include "fft_lds.hpp"
 #include "kernels.hpp"
@@ -75,10 +84,43 @@ __device__ __forceinline__ void dft5(float2* a) {
     a[3] = make_float2(c2.x - d2.y, c2.y + d2.x);
 }
 
+// radix 7: y_u = a0 + sum_m cos(2 pi u m / 7) s_m -+ i sum_m sin(2 pi u m / 7) d_m,
+// s_m = a_m + a_{7-m}, d_m = a_m - a_{7-m}
+constexpr float kC7[3] = {0.623489801858733530525f, -0.222520933956314404289f, -0.900968867902419126236f};
+constexpr float kS7[3] = {0.781831482468029808708f, 0.974927912181823607018f, 0.433883739117558120475f};
+template <bool INV>
+__device__ __forceinline__ void dft7(float2* a) {
+    float2 sm[3], dm[3];
+#pragma unroll
+    for (int m = 0; m < 3; ++m) {
+        sm[m] = cadd(a[m + 1], a[6 - m]);
+        dm[m] = csub(a[m + 1], a[6 - m]);
+    }
+    const float2 a0 = a[0];
+    a[0] = cadd(cadd(a0, sm[0]), cadd(sm[1], sm[2]));
+#pragma unroll
+    for (int u = 1; u <= 3; ++u) {
+        float2 ca = a0, cb = make_float2(0.f, 0.f);
+#pragma unroll
+        for (int m = 1; m <= 3; ++m) {
+            int q = (u * m) % 7;
+            const float sg = q > 3 ? -1.f : 1.f;
+            q = q > 3 ? 7 - q : q;
+            ca = make_float2(ca.x + kC7[q - 1] * sm[m - 1].x, ca.y + kC7[q - 1] * sm[m - 1].y);
+            cb = make_float2(cb.x + sg * kS7[q - 1] * dm[m - 1].x, cb.y + sg * kS7[q - 1] * dm[m - 1].y);
+        }
+        // forward: y_u = ca - i cb, y_{7-u} = ca + i cb (inverse: the conjugate twiddles)
+        const float2 icb = INV ? make_float2(-cb.y, cb.x) : make_float2(cb.y, -cb.x);
+        a[u] = cadd(ca, icb);
+        a[7 - u] = csub(ca, icb);
+    }
+}
+
 template <int R, bool INV>
 __device__ __forceinline__ void dft_any(float2* a) {
     if constexpr (R == 3) dft3<INV>(a);
     else if constexpr (R == 5) dft5<INV>(a);
+    else if constexpr (R == 7) dft7<INV>(a);
     else dft_reg<R, INV>(a);
 }
 
@@ -102,15 +144,69 @@ __device__ __forceinline__ void mr_pass(const float2* src, float2* dst, int n, i
     }
 }
 
+// Generic odd radix R (a prime <= 61), two steps: the inputs of every butterfly
+// pre-twiddled in place (src is consumed), then each output an R-term dot product with
+// W_R^(r q) = tw[(r q mod R) n / R].
+template <bool INV>
+__device__ __forceinline__ void mr_pass_gen(float2* src, float2* dst, int n, int L, int R, const float2* __restrict__ tw) {
+    const int nb = n / R, step = n / (L * R), wstep = n / R;
+    if (L > 1) {
+        for (int idx = threadIdx.x; idx < n; idx += MR_THREADS) {
+            const int r = idx / nb, j = idx - r * nb;
+            if (r > 0) src[idx] = cmul_dir<INV>(src[idx], tw[r * (j % L) * step]);
+        }
+        __syncthreads();
+    }
+    for (int idx = threadIdx.x; idx < n; idx += MR_THREADS) {
+        const int q = idx / nb, j = idx - q * nb, k = j % L;
+        float2 acc = src[j];
+        int m = 0;
+        for (int r = 1; r < R; ++r) {
+            m += q;
+            if (m >= R) m -= R;
+            const float2 w = tw[m * wstep];
+            const float2 x = src[j + r * nb];
+            acc = cadd(acc, cmul_dir<INV>(x, w));
+        }
+        dst[(j - k) * R + k + q * L] = acc;
+    }
+}
+
+// The plan's passes over len points (b0 holds the input); returns the buffer holding the
+// result.  Every pass ends with a barrier.
+template <bool INV>
+__device__ __forceinline__ float2* mr_run(float2* b0, float2* b1, int len, const int* fct, int nf,
+                                          const float2* __restrict__ tw) {
+    int L = 1;
+    for (int f = 0; f < nf; ++f) {
+        const int R = fct[f];
+        switch (R) {
+            case 8: mr_pass<8, INV>(b0, b1, len, L, tw); break;
+            case 4: mr_pass<4, INV>(b0, b1, len, L, tw); break;
+            case 2: mr_pass<2, INV>(b0, b1, len, L, tw); break;
+            case 3: mr_pass<3, INV>(b0, b1, len, L, tw); break;
+            case 5: mr_pass<5, INV>(b0, b1, len, L, tw); break;
+            case 7: mr_pass<7, INV>(b0, b1, len, L, tw); break;
+            default: mr_pass_gen<INV>(b0, b1, len, L, R, tw);
+        }
+        __syncthreads();
+        float2* t = b0;
+        b0 = b1;
+        b1 = t;
+        L *= R;
+    }
+    return b0;
+}
+
 template <bool INV, int IN, int OUT>
 __global__ __launch_bounds__(MR_THREADS) void k_mr_rows(const void* __restrict__ in, void* __restrict__ out, long nrows,
                                                         int H, float sub, MrPlan p, const float2* __restrict__ tw,
                                                         PhaseOut ph) {
     extern __shared__ __attribute__((aligned(16))) float2 mr_lds[];
-    const int n = p.n;
+    const int n = p.n, len = p.blue ? p.M : n;
     const long row = blockIdx.x;
     float2* b0 = mr_lds;
-    float2* b1 = mr_lds + n;
+    float2* b1 = mr_lds + len;
     for (int i = threadIdx.x; i < n; i += MR_THREADS) {
         float2 v;
         if constexpr (IN == ROW_IN_REAL) {
@@ -131,22 +227,25 @@ __global__ __launch_bounds__(MR_THREADS) void k_mr_rows(const void* __restrict__
         } else {
             v = static_cast<const float2*>(in)[row * n + i];
         }
+        if (p.blue) v = cmul_dir<INV>(v, tw[p.tc + i]);  // Bluestein: the chirp premultiply
         b0[i] = v;
     }
+    for (int i = n + threadIdx.x; i < len; i += MR_THREADS) b0[i] = make_float2(0.f, 0.f);  // (Bluestein) zero padding
     __syncthreads();
-    int L = 1;
-    for (int f = 0; f < p.nf; ++f) {
-        const int R = p.fct[f];
-        if (R == 8) mr_pass<8, INV>(b0, b1, n, L, tw);
-        else if (R == 4) mr_pass<4, INV>(b0, b1, n, L, tw);
-        else if (R == 3) mr_pass<3, INV>(b0, b1, n, L, tw);
-        else mr_pass<5, INV>(b0, b1, n, L, tw);
+    float2* r;
+    if (!p.blue) {
+        r = mr_run<INV>(b0, b1, n, p.fct, p.nf, tw);
+    } else {
+        // y = IFFT_M(FFT_M(a) * G) with G = FFT_M(conj chirp) / M, then the chirp postmultiply
+        r = mr_run<false>(b0, b1, len, p.fct, p.nf, tw + p.tM);
+        const float2* G = tw + (INV ? p.tgi : p.tgf);
+        for (int i = threadIdx.x; i < len; i += MR_THREADS) r[i] = cmul(r[i], G[i]);
         __syncthreads();
-        float2* t = b0;
-        b0 = b1;
-        b1 = t;
-        L *= R;
+        r = mr_run<true>(r, r == b0 ? b1 : b0, len, p.fct, p.nf, tw + p.tM);
+        for (int i = threadIdx.x; i < n; i += MR_THREADS) r[i] = cmul_dir<INV>(r[i], tw[p.tc + i]);
+        __syncthreads();
     }
+    b0 = r;
     if constexpr (OUT == ROW_OUT_COMPLEX) {
         for (int i = threadIdx.x; i < n; i += MR_THREADS) static_cast<float2*>(out)[row * n + i] = b0[i];
     } else if constexpr (OUT == ROW_OUT_REAL) {
@@ -187,11 +286,11 @@ void launch_mr(const MrPlan& p, const void* in, void* out, long nrows, int H, fl
                const PhaseOut* ph, hipStream_t s) {
     PhaseOut q{};
     if (ph) q = *ph;
-    const size_t lds = 2 * (size_t)p.n * sizeof(float2);
+    const size_t lds = 2 * (size_t)(p.blue ? p.M : p.n) * sizeof(float2);
     static bool attr = false;
     if (!attr) {
         FCD_HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mr_rows<INV, IN, OUT>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024));
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         attr = true;
     }
     hipLaunchKernelGGL((k_mr_rows<INV, IN, OUT>), dim3((unsigned)nrows), dim3(MR_THREADS), lds, s, in, out, nrows, H,
@@ -201,25 +300,44 @@ void launch_mr(const MrPlan& p, const void* in, void* out, long nrows, int H, fl
 
 }  // namespace
 
+// largest prime factor of n
+static int mr_lpf(int n) {
+    int res = 1;
+    for (int d = 2; (long)d * d <= n; ++d)
+        while (n % d == 0) {
+            res = d;
+            n /= d;
+        }
+    return n > 1 ? n : res;
+}
+
 bool mr_supported(int n) {
-    if (n < 64 || n > 4096 || n % 64 != 0) return false;
-    int m = n;
-    for (int d : {2, 3, 5})
-        while (m % d == 0) m /= d;
-    return m == 1;
+    if (n < 2) return false;
+    if (mr_lpf(n) <= kMrMaxRadix) return n <= 8192;
+    return n <= 4096;  // Bluestein: M <= 8192
 }
 
 MrPlan mr_plan(int n) {
     if (!mr_supported(n)) throw std::runtime_error("mixed-radix plan: unsupported length " + std::to_string(n));
     MrPlan p{};
     p.n = n;
-    int m = n, two = 0;
+    p.blue = mr_lpf(n) > kMrMaxRadix;
+    int m = n;
+    if (p.blue) {
+        p.M = 1;
+        while (p.M < 2 * n - 1) p.M *= 2;
+        m = p.M;
+    }
+    int two = 0;
     while (m % 2 == 0) {
         m /= 2;
         ++two;
     }
-    auto add = [&](int r) { p.fct[p.nf++] = r; };
-    while (two >= 3 && two != 4) {  // 8s, leaving 0, 2 or 4 twos for 4s
+    auto add = [&](int r) {
+        if (p.nf >= (int)(sizeof(p.fct) / sizeof(p.fct[0]))) throw std::runtime_error("mixed-radix plan: too many passes");
+        p.fct[p.nf++] = r;
+    };
+    while (two >= 3 && two != 4) {  // 8s, leaving 0, 1, 2 or 4 twos for 4s / a 2
         add(8);
         two -= 3;
     }
@@ -227,16 +345,73 @@ MrPlan mr_plan(int n) {
         add(4);
         two -= 2;
     }
-    while (m % 3 == 0) {
-        add(3);
-        m /= 3;
+    if (two == 1) add(2);
+    for (int d = 3; d <= m; d += 2)
+        while (m % d == 0) {
+            add(d);
+            m /= d;
+        }
+    // table layout (mr_tables): [n: exp(-2 pi i j / n)] then, with Bluestein, [M: exp(-2 pi i j / M)]
+    // [n: chirp] [M: G forward] [M: G inverse]
+    if (p.blue) {
+        p.tM = n;
+        p.tc = n + p.M;
+        p.tgf = 2 * n + p.M;
+        p.tgi = 2 * n + 2 * p.M;
     }
-    while (m % 5 == 0) {
-        add(5);
-        m /= 5;
-    }
-    if (two != 0 || m != 1 || p.nf > 8) throw std::runtime_error("mixed-radix plan: bad factorisation");
     return p;
+}
+
+// f64 radix-2 FFT (host; Bluestein's G tables)
+static void fft_f64(std::vector<std::complex<double>>& a) {
+    const size_t n = a.size();
+    for (size_t i = 1, j = 0; i < n; ++i) {
+        size_t bit = n >> 1;
+        for (; j & bit; bit >>= 1) j ^= bit;
+        j ^= bit;
+        if (i < j) std::swap(a[i], a[j]);
+    }
+    const double pi = 3.14159265358979323846;
+    for (size_t len = 2; len <= n; len <<= 1)
+        for (size_t i = 0; i < n; i += len)
+            for (size_t k = 0; k < len / 2; ++k) {
+                const std::complex<double> w = std::polar(1.0, -2.0 * pi * (double)k / (double)len);
+                const std::complex<double> u = a[i + k], v = a[i + k + len / 2] * w;
+                a[i + k] = u + v;
+                a[i + k + len / 2] = u - v;
+            }
+}
+
+std::vector<float2> mr_tables(const MrPlan& p) {
+    const double pi = 3.14159265358979323846;
+    const int n = p.n;
+    auto unit = [&](double a) { return make_float2((float)std::cos(a), (float)std::sin(a)); };
+    std::vector<float2> t((size_t)n);
+    for (int j = 0; j < n; ++j) t[j] = unit(-2.0 * pi * (double)j / (double)n);
+    if (!p.blue) return t;
+    const int M = p.M;
+    t.resize((size_t)2 * n + 3 * (size_t)M);
+    for (int j = 0; j < M; ++j) t[p.tM + j] = unit(-2.0 * pi * (double)j / (double)M);
+    std::vector<std::complex<double>> c(n);
+    for (int j = 0; j < n; ++j) {
+        const long long q = (long long)j * j % (2LL * n);  // exact argument reduction
+        c[j] = std::polar(1.0, -pi * (double)q / (double)n);
+        t[p.tc + j] = make_float2((float)c[j].real(), (float)c[j].imag());
+    }
+    for (int dir = 0; dir < 2; ++dir) {  // G = FFT_M(g) / M, g = conj(chirp) (forward), chirp (inverse)
+        std::vector<std::complex<double>> g(M, 0.0);
+        for (int j = 0; j < n; ++j) {
+            const std::complex<double> v = dir == 0 ? std::conj(c[j]) : c[j];
+            g[j] = v;
+            if (j) g[M - j] = v;
+        }
+        fft_f64(g);
+        for (int j = 0; j < M; ++j) {
+            const std::complex<double> v = g[j] / (double)M;
+            t[(dir == 0 ? p.tgf : p.tgi) + j] = make_float2((float)v.real(), (float)v.imag());
+        }
+    }
+    return t;
 }
 
 void mr_rows(const MrPlan& p, bool inverse, RowIn im, RowOut om, const void* in, void* out, long nrows, int H,

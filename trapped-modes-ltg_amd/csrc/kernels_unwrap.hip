@@ -260,6 +260,44 @@ void unwrap_scan(const float* w, int nmaps, int H, int W, int* colk, int32_t* k,
     FCD_CHECK_LAUNCH();
 }
 
+// ------------------------------------------------------------------ frames padded to multiples of 64
+// The unwrap's tiles, residue strips and row scans work on sides that are multiples of 64;
+// a frame of any other size is unwrapped in a copy padded by replicating its last row /
+// column.  A pad plaquette then has zero wrap circulation (find_wrap is antisymmetric), the
+// residue-free scan integrates the frame's pixels from their own left / upper neighbours
+// only, and the MST pass gives pad pixels the reliability kPadRel (MstWork::Hr / Wr).
+__global__ __launch_bounds__(256) void k_pad_maps(const float* __restrict__ w, long n, int H, int W, int Hp, int Wp,
+                                                  float* __restrict__ out) {
+    for (long g = (long)blockIdx.x * 256 + threadIdx.x; g < n; g += (long)gridDim.x * 256) {
+        const long m = g / ((long)Hp * Wp), p = g - m * Hp * Wp;
+        const int i = (int)(p / Wp), j = (int)(p % Wp);
+        out[g] = w[(m * H + min(i, H - 1)) * W + min(j, W - 1)];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_unpad_k(const int32_t* __restrict__ kp, long n, int H, int W, int Hp, int Wp,
+                                                 int32_t* __restrict__ k) {
+    for (long g = (long)blockIdx.x * 256 + threadIdx.x; g < n; g += (long)gridDim.x * 256) {
+        const long m = g / ((long)H * W), p = g - m * H * W;
+        const int i = (int)(p / W), j = (int)(p % W);
+        k[g] = kp[(m * Hp + i) * Wp + j];
+    }
+}
+
+static unsigned grid_of(long n) { return (unsigned)std::min<long>(std::max<long>((n + 255) / 256, 1), 16384); }
+
+void pad_maps(const float* w, int nmaps, int H, int W, int Hp, int Wp, float* out, hipStream_t s) {
+    const long n = (long)nmaps * Hp * Wp;
+    hipLaunchKernelGGL(k_pad_maps, dim3(grid_of(n)), dim3(256), 0, s, w, n, H, W, Hp, Wp, out);
+    FCD_CHECK_LAUNCH();
+}
+
+void unpad_k(const int32_t* kp, int nmaps, int Hp, int Wp, int H, int W, int32_t* k, hipStream_t s) {
+    const long n = (long)nmaps * H * W;
+    hipLaunchKernelGGL(k_unpad_k, dim3(grid_of(n)), dim3(256), 0, s, kp, n, H, W, Hp, Wp, k);
+    FCD_CHECK_LAUNCH();
+}
+
 // ------------------------------------------------------------------ Boruvka MST path
 // Vertex ids are slot*H*W + pixel for the nact active maps (slot -> map_ids[slot]).
 __device__ __forceinline__ unsigned long long pack_link(int parent, int off) {
@@ -269,7 +307,7 @@ __device__ __forceinline__ int link_parent(unsigned long long l) { return (int)(
 __device__ __forceinline__ int link_off(unsigned long long l) { return (int)(unsigned)(l & 0xffffffffull); }
 
 __global__ void k_mst_rel(const float* __restrict__ w, const int* __restrict__ map_ids, int nact, int H, int W,
-                          double* __restrict__ rel, int* comp, int* off) {
+                          int Hr, int Wr, double* __restrict__ rel, int* comp, int* off) {
     const long hw = (long)H * W;
     const long v = xcd_block() * blockDim.x + threadIdx.x;
     if (v >= nact * hw) return;
@@ -277,8 +315,8 @@ __global__ void k_mst_rel(const float* __restrict__ w, const int* __restrict__ m
     const long p = v % hw;
     const int i = (int)(p / W), j = (int)(p % W);
     const float* m = w + (long)map_ids[slot] * hw;
-    double r = kBorderRel;
-    if (i > 0 && j > 0 && i < H - 1 && j < W - 1) {
+    double r = (i >= Hr || j >= Wr) ? kPadRel : kBorderRel;
+    if (i > 0 && j > 0 && i < Hr - 1 && j < Wr - 1) {
         const double c = m[p];
         const double h = __dsub_rn(wrapd(__dsub_rn((double)m[p - 1], c)), wrapd(__dsub_rn(c, (double)m[p + 1])));
         const double vv = __dsub_rn(wrapd(__dsub_rn((double)m[p - W], c)), wrapd(__dsub_rn(c, (double)m[p + W])));
@@ -458,7 +496,8 @@ static inline unsigned nblk(long n) { return (unsigned)((n + 255) / 256); }
 
 void mst_init(const float* w, const int* map_ids, int nact, int H, int W, MstWork m, hipStream_t s) {
     const long n = (long)nact * H * W;
-    hipLaunchKernelGGL(k_mst_rel, dim3(nblk(n)), dim3(256), 0, s, w, map_ids, nact, H, W, m.rel, m.comp, m.off);
+    hipLaunchKernelGGL(k_mst_rel, dim3(nblk(n)), dim3(256), 0, s, w, map_ids, nact, H, W, m.Hr, m.Wr, m.rel, m.comp,
+                       m.off);
     FCD_CHECK_LAUNCH();
     // no reset of best_w / best_e: the first round (k_mst_cand<true>) writes every
     // vertex's entry before anything reads it
@@ -585,12 +624,12 @@ __global__ __launch_bounds__(256) void k_lvl_setup(int nact, int H, int W, MstWo
 // dependent loads, not bandwidth, bounds this kernel.
 constexpr int LVL_U = 4;
 
-__global__ __launch_bounds__(256) void k_lvl_cand(int lw, int lh, MstWork m, int par, long seg) {
+__global__ __launch_bounds__(256) void k_lvl_cand(int H, int W, MstWork m, int par, long seg) {
     __shared__ int nout;
     if (threadIdx.x == 0) nout = 0;
     __syncthreads();
-    const int W = 1 << lw, H = 1 << lh;
     const int nh = H * (W - 1);
+    const long hw = (long)H * W;
     const long s0 = (long)blockIdx.x * seg;
     const int n = lvl_cnt(m.cnt, par)[blockIdx.x];
     const int* B = m.listB[par] + s0;
@@ -617,8 +656,8 @@ __global__ __launch_bounds__(256) void k_lvl_cand(int lw, int lh, MstWork m, int
         for (int u = 0; u < LVL_U; ++u) {
             // only the neighbours outside v's component when it entered the list: a
             // neighbour inside it stays inside (components only merge)
-            const int p = v[u] & ((1 << (lw + lh)) - 1);
-            const int pi = p >> lw, pj = p & (W - 1);
+            const int p = (int)(v[u] % hw);
+            const int pi = p / W, pj = p - pi * W;
             nb[u][0] = (mk[u] & 1) ? v[u] + 1 : -1;
             nb[u][1] = (mk[u] & 2) ? v[u] - 1 : -1;
             nb[u][2] = (mk[u] & 4) ? v[u] + W : -1;
@@ -832,10 +871,7 @@ void mst_level_round(const float* w, const int* map_ids, int nact, int H, int W,
     const int par = r & 1;
     FCD_HIPCHK(hipMemsetAsync(m.nhooks, 0, sizeof(int), s));
     const dim3 g(LVL_BLOCKS), b(256);
-    int lw = 0, lh = 0;
-    while ((1 << lw) < W) ++lw;
-    while ((1 << lh) < H) ++lh;
-    hipLaunchKernelGGL(k_lvl_cand, g, b, 0, s, lw, lh, m, par, seg);
+    hipLaunchKernelGGL(k_lvl_cand, g, b, 0, s, H, W, m, par, seg);
     FCD_CHECK_LAUNCH();
     hipLaunchKernelGGL(k_lvl_cand2, g, b, 0, s, m, par, seg);
     FCD_CHECK_LAUNCH();
@@ -1199,8 +1235,8 @@ __global__ __launch_bounds__(TW * TH / 4, 4) void k_mst_tile0(const float* __res
     for (int i = threadIdx.x; i < T0R * (TH + 2); i += NT) {
         const int li = i / T0R, lj = i % T0R;  // ws index (li + 1, lj + 1)
         const int gi = gi0 - 1 + li, gj = gj0 - 1 + lj;
-        double r = kBorderRel;
-        if (gi > 0 && gj > 0 && gi < H - 1 && gj < W - 1) {
+        double r = (gi >= m.Hr || gj >= m.Wr) ? kPadRel : kBorderRel;
+        if (gi > 0 && gj > 0 && gi < m.Hr - 1 && gj < m.Wr - 1) {
             const float* q = ws + (li + 1) * T0W + (lj + 1);
             const double c = q[0];
             const double h = __dsub_rn(wrapd(__dsub_rn((double)q[-1], c)), wrapd(__dsub_rn(c, (double)q[1])));
