@@ -76,7 +76,7 @@ def residue_sites(w):
     return np.argwhere(np.abs(c) > 1)
 
 
-def assert_k_equal(k, kref, w, tag, cut_margin=16):
+def assert_k_equal(k, kref, w, tag, cut_margin=16, max_cut=4):
     """The engine's k-field against the reference's, as unwrapped phases w + 2 pi k, up to
     one global 2 pi c, off the border ring.  Two kinds of pixel may differ, and no other:
 
@@ -86,9 +86,10 @@ def assert_k_equal(k, kref, w, tag, cut_margin=16):
       * pixels next to a branch cut between residues: which side of the cut a pixel
         falls on is decided by reliability ORDER, which last-bit differences of the
         wrapped phases can swap.  These must lie within `cut_margin` px of the bounding
-        box of a residue pair (residues closer than 512 px clustered) and are at most
-        1 % of those boxes' pixels.  The exact pass itself is checked against the oracle
-        fed the engine's own phases (bit for bit, test_large_unwrap_equals_oracle_on_engine_phases).
+        box of a residue pair (residues closer than 512 px clustered), and there are at
+        most `max_cut` of them per map (measured: at most 1, at 4096^2).  The exact pass
+        itself is checked against the oracle fed the engine's own phases (bit for bit,
+        test_large_unwrap_equals_oracle_on_engine_phases).
     """
     k = np.asarray(k, np.int64)
     d = k - np.asarray(kref, np.int64)
@@ -101,7 +102,6 @@ def assert_k_equal(k, kref, w, tag, cut_margin=16):
         sites = residue_sites(w)
         assert len(sites) > 0, f"{tag}: {int(bad.sum())} k mismatches in a residue-free map"
         near = np.zeros(d.shape, bool)
-        area = 0
         used = np.zeros(len(sites), bool)
         for i in range(len(sites)):
             if used[i]:
@@ -112,10 +112,9 @@ def assert_k_equal(k, kref, w, tag, cut_margin=16):
             r0, c0 = max(r0 - cut_margin, 0), max(c0 - cut_margin, 0)
             r1, c1 = min(r1 + cut_margin + 1, d.shape[0]), min(c1 + cut_margin + 1, d.shape[1])
             near[r0:r1, c0:c1] = True
-            area += (r1 - r0) * (c1 - c0)
         far = bad & ~near
         assert not far.any(), f"{tag}: {int(far.sum())} k mismatches away from residues, e.g. {np.argwhere(far)[:4].tolist()}"
-        assert bad.sum() <= 0.01 * area, f"{tag}: {int(bad.sum())} k mismatches next to branch cuts (area {area})"
+        assert bad.sum() <= max_cut, f"{tag}: {int(bad.sum())} k mismatches next to branch cuts (cap {max_cut})"
     assert (d[ring] != 0).sum() <= 8, f"{tag}: {int((d[ring] != 0).sum())} border k mismatches"
 
 
@@ -206,11 +205,11 @@ def test_large_chunked_batches_equal_single(large, fresh, monkeypatch, n):
     hs, _, _ = eng.process(sf[None], 1.0, unwrap=True, want_phases=False)
     for i in (0, 2, 4):  # all from the exact pass
         assert np.array_equal(hb[i], hr[0]), i
-    # the residue-free copies came from the fused kernel; the single call after a
-    # residue-heavy one runs the exact chain's scan unwrap (FCD_EXACT_FIRST auto), whose
-    # row FFT rounds differently
+    # the residue-free copies came from the fused kernel, and so does the single call after
+    # a residue-heavy one (FCD_EXACT_FIRST auto: the exact chain redoes residue-free frames
+    # with the first pass's chain), so the heights do not depend on the call history
     assert np.array_equal(hb[1], hb[3])
-    assert rel_l2(hb[1], hs[0]) < 1e-6
+    assert np.array_equal(hb[1], hs[0])
     sub = n // 256
     assert rel_l2(hr[0][::sub, ::sub], g[f"r{n}_height_sub"]) < 1e-5
     assert rel_l2(hs[0][::sub, ::sub], g[f"s{n}_height_sub"]) < 1e-5

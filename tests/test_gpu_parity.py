@@ -367,8 +367,14 @@ def test_real_df_frames(lib, golden):
             assert np.all(diff == diff.flat[0]), (f, i, int((diff != diff.flat[0]).sum()))
 
 
-def test_batch_equals_single(lib, golden):
+@pytest.mark.parametrize("exact_first", ["0", "1", "auto"])
+def test_batch_equals_single(lib, golden, monkeypatch, exact_first):
+    """A batch equals its frames called one by one, bit for bit, in either pass mode
+    (FCD_EXACT_FIRST: the fused first pass, the exact chain first, or chosen from the
+    previous call): the heights are a pure function of the frame (fcd.py:13-35)."""
     from pyfcd.fcd import fcd
+    if exact_first != "auto":
+        monkeypatch.setenv("FCD_EXACT_FIRST", exact_first)
     s = golden("synthetic")
     ref = s["sine256_ref"]
     frames = np.stack([s["sine256_disp"], s["binary256_disp"] / 65535.0, ref])

@@ -252,6 +252,7 @@ struct fcd_ctx {
     bool pf64_ready = false;
     DevBuf ref32;                     // a float64 reference rounded to float32 (the per-frame carriers)
     DevBuf fix_raw;  // raw samples of the frames redone by the exact pass
+    DevBuf fix_h, fix_res;  // first-pass heights / census of an exact-first call's residue-free frames
     // temporal analysis: staged block, exp table, bins, partial sums, output, window
     DevBuf t_stage, t_tab, t_bins, t_part, t_out, t_win, t_wsum, t_slices;
     DevBuf t_chirp, t_bhat, t_work, t_gpart, t_zo, t_bad;  // the FFT path of the mean spectrum
@@ -1575,7 +1576,7 @@ int process_generic(fcd_ctx* c, const void* frames, int format, int n_frames, bo
     const hipMemcpyKind kind = dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
     c->frames_in.ensure((size_t)c->chunk * hw * sizeof(float));
     c->out_h.ensure((size_t)c->chunk * hw * sizeof(float));
-    const auto t0 = std::chrono::steady_clock::now();
+    double unwrap_ms = 0;
     long nres = 0;
     for (int f0 = 0; f0 < n_frames; f0 += c->chunk) {
         const int nb = std::min(c->chunk, n_frames - f0);
@@ -1598,7 +1599,12 @@ int process_generic(fcd_ctx* c, const void* frames, int format, int n_frames, bo
         if (unwrap) {
             std::vector<int> counts(2 * (size_t)nb);
             k = c->kbuf.as<int32_t>();
+            const auto tu = std::chrono::steady_clock::now();
             unwrap_maps(c, w, 2 * nb, k, counts.data(), s, false, nullptr, true);
+            if (c->profiling) {  // the unwrap span (it synchronises), counted as the exact pass's time
+                HIPCHK(hipStreamSynchronize(s));
+                unwrap_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tu).count();
+            }
             for (int i = 0; i < nb; ++i) nres += counts[2 * (size_t)i] || counts[2 * (size_t)i + 1];
         }
         if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
@@ -1619,11 +1625,44 @@ int process_generic(fcd_ctx* c, const void* frames, int format, int n_frames, bo
         }
         HIPCHK(hipStreamSynchronize(s));  // the chunk's workspace is reused by the next
     }
-    if (c->profiling) {  // frames with residues (their maps took the exact MST unwrap)
-        c->prof_fix_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (c->profiling) {  // frames with residues (their maps took the exact MST unwrap) and the unwrap's time
+        c->prof_fix_ms += unwrap_ms;
         c->prof_fix_frames += nres;
     }
     return FCD_OK;
+}
+
+// The first pass's heights (the fused chain when fused_ok, as pass 1 of process_impl runs it)
+// of the frames f0 + idx[i] of a batch, written to hdst + idx[i] * H * W (device) for each
+// frame whose census of that chain is clean; a frame the chain's census flags (a wrapped
+// difference of exactly fl(pi)) keeps the exact chain's heights, as pass 2 would give it.
+void first_pass_heights(fcd_ctx* c, const void* frames, int format, bool dev, int f0, const std::vector<int>& idx,
+                        bool fused_allowed, const fcdk::IntegCoef& coef, float* hdst, hipStream_t s) {
+    const long hw = c->hw();
+    const int n = (int)idx.size();
+    const bool fused = c->fused_ok && fused_allowed && !c->force_unfused;
+    std::vector<int> abs_idx(n);
+    for (int i = 0; i < n; ++i) abs_idx[i] = f0 + idx[i];
+    const bool run = abs_idx[n - 1] - abs_idx[0] == n - 1;
+    const float* fr;
+    if (run && dev && format == FCD_FMT_F32) {
+        fr = reinterpret_cast<const float*>(frames) + (size_t)abs_idx[0] * hw;
+    } else {
+        stage_frames(c, frames, format, dev, abs_idx.data(), n, s);
+        fr = c->frames_in.as<float>();
+    }
+    c->fix_h.ensure((size_t)n * hw * sizeof(float));
+    c->fix_res.ensure((size_t)n * 2 * sizeof(int));
+    int* res = c->fix_res.as<int>();
+    HIPCHK(hipMemsetAsync(res, 0, (size_t)n * 2 * sizeof(int), s));
+    first_pass_chunk(c, fr, n, true, fused, res, c->fix_h.as<float>(), nullptr, coef, s);
+    std::vector<int> flags((size_t)n * 2);
+    HIPCHK(hipMemcpyAsync(flags.data(), res, flags.size() * sizeof(int), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    for (int i = 0; i < n; ++i)
+        if (!flags[2 * (size_t)i] && !flags[2 * (size_t)i + 1])
+            HIPCHK(hipMemcpyAsync(hdst + (size_t)idx[i] * hw, c->fix_h.as<float>() + (size_t)i * hw, hw * sizeof(float),
+                                  hipMemcpyDeviceToDevice, s));
 }
 
 int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int flags, double height, int unwrap,
@@ -1664,8 +1703,10 @@ int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int f
     // frames of the previous call needed the exact pass, the fused first pass would only
     // produce heights that pass 2 throws away, so this call runs the exact chain at once:
     // demod, residue count, the scan unwrap for residue-free maps and the MST for the
-    // others, integration.  Same kernels and k-fields as pass 2 (bit-identical heights);
-    // FCD_EXACT_FIRST=0 / 1 forces either mode.
+    // others, integration.  Frames with residues: the same kernels and k-fields as pass 2
+    // (bit-identical heights); residue-free frames: redone by the first pass's chain
+    // (first_pass_heights), so every frame's heights are those of the two-pass form whatever
+    // the previous call held.  FCD_EXACT_FIRST=0 / 1 forces either mode.
     const int ef_env = fcd_env_int("FCD_EXACT_FIRST", -1);  // (read per call: tests switch it)
     if (unwrap && !wrapped_out && (ef_env >= 0 ? ef_env == 1 : c->exact_first)) {
         const auto t0 = std::chrono::steady_clock::now();
@@ -1690,6 +1731,13 @@ int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int f
             fcdk::int_cols(c->H, c->Zt.as<float2>(), c->W, nb, coef, c->Ht.as<float2>(), ic_tw(c), s);
             float* hdst = dev && height_out ? height_out + (size_t)f0 * hw : c->out_h.as<float>();
             fcdk::int_c2r(c->W, c->Ht.as<float2>(), c->H, nb, hdst, c->twp_row.as<float2>(), s);
+            // The chunk's residue-free frames get the first pass's heights, as when this call
+            // had not followed a residue-heavy one: a frame's heights never depend on what
+            // earlier calls held (the reference is a pure function of its inputs, fcd.py:13-35).
+            std::vector<int> clean;
+            for (int i = 0; i < nb; ++i)
+                if (!counts[2 * (size_t)i] && !counts[2 * (size_t)i + 1]) clean.push_back(i);
+            if (!clean.empty()) first_pass_heights(c, frames, format, dev, f0, clean, k_out == nullptr, coef, hdst, s);
             if (!dev && height_out)
                 HIPCHK(hipMemcpyAsync(height_out + (size_t)f0 * hw, hdst, (size_t)nb * hw * 4, out_kind, s));
             if (!dev && k_out)

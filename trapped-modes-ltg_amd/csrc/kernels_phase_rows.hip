@@ -58,7 +58,8 @@ constexpr int PR_ROWS = FCD_PR_ROWS;  // rows per tile (one wave each)
 #define FCD_PR_ATAN_N 2  // pixel pairs per carrier in one interleaved atan2 group
 #endif
 static_assert(FCD_PR_ATAN_N > 0 && 16 % (2 * FCD_PR_ATAN_N) == 0, "atan2 groups tile the 16 values");
-constexpr int PR_ZT = FCD_ZT_1024;    // Zt tile height (int_rows.inc zt_rows(1024))
+constexpr int PR_ZT = zt_layout(1024);  // Zt tile height (kernels.hpp zt_layout: k_int_cols / k_int_rows2 read it)
+static_assert(PR_ZT == FCD_ZT_1024, "the fused 1024 kernel writes the layout zt_layout(1024) names");
 static_assert(PR_ZT % PR_ROWS == 0, "a tile covers part of one Zt tile");
 constexpr int PR_WAVES = PR_ROWS;     // one wave per row
 constexpr int PR_THREADS = 64 * PR_WAVES;

@@ -88,7 +88,7 @@ def gather_stack(local, total_frames):
     if not (dist.is_available() and dist.is_initialized()):
         return local
     rank, world = dist.get_rank(), dist.get_world_size()
-    if total_frames < world:
+    if world > 1 and total_frames < world:
         # an empty shard would leave its rank out of the grouped send/recv; on RCCL every
         # rank must enter a group's first point-to-point batch
         raise ValueError(f"gather_stack: {total_frames} frames over {world} ranks leaves a rank without frames")
