@@ -197,8 +197,8 @@ def test_unwrap_matches_oracle_random_residues(lib):
 
 @pytest.mark.parametrize("shape", [(256, 256), (128, 512)])
 def test_unwrap_two_level_equals_pixel_rounds(lib, monkeypatch, shape):
-    """The two-level Boruvka (level-0 components from 64 x 64 tiles, 32 x 32 or 64 x 32
-    with FCD_MST_TILE=32 / 6432, then rounds on the contracted component graph; FCD_MST_LEVEL=2: the
+    """The two-level Boruvka (level-0 components from 64 x 64 tiles, then rounds on the
+    contracted component graph; FCD_MST_LEVEL=2: the
     tiles, then block-segmented boundary / root lists; =1: one pixel round, then the
     lists) and the all-pixel rounds (FCD_MST_LEVEL=0) build the same unique MST:
     identical k-fields, bit for bit, over a batch of maps with thousands of residues
@@ -214,19 +214,6 @@ def test_unwrap_two_level_equals_pixel_rounds(lib, monkeypatch, shape):
     eng = lib.Engine(shape)
     k2, res = eng.unwrap(w)
     assert (res > 0).all() and res.sum() > 5000
-    for tile in ("32", "6432"):  # 32 x 32, 64 wide x 32 tall
-        monkeypatch.setenv("FCD_MST_TILE", tile)
-        k1, _ = eng.unwrap(w)
-        assert np.array_equal(k1, k2), tile
-        monkeypatch.setenv("FCD_MST_LEVEL", "2")
-        k1, _ = eng.unwrap(w)
-        assert np.array_equal(k1, k2), (tile, "boundary lists")
-        monkeypatch.delenv("FCD_MST_LEVEL")
-        monkeypatch.setenv("FCD_T0_ROUNDS", "1")  # the capped tile pass on the other shapes
-        k1, _ = eng.unwrap(w)
-        assert np.array_equal(k1, k2), (tile, "capped")
-        monkeypatch.delenv("FCD_T0_ROUNDS")
-    monkeypatch.delenv("FCD_MST_TILE")
     # tile passes capped after 0 / 1 / 2 hook rounds (the noisiest maps' tiles keep going
     # until they hold at most cg_ccap components) and uncapped
     for cap in ("0", "1", "2", "99"):
@@ -244,11 +231,12 @@ def test_unwrap_two_level_equals_pixel_rounds(lib, monkeypatch, shape):
         assert np.all(d == d.flat[0])
 
 
-@pytest.mark.parametrize("shape", [(64, 64), (64, 128), (1024, 1024)])
+@pytest.mark.parametrize("shape", [(64, 64), (64, 128), (1024, 1024), (61, 97), (100, 130)])
 def test_residue_counts_match_oracle(lib, shape):
     """k_residues (4 plaquettes per thread, f32 find_wrap with the exact test at
     |fl(a - b)| = fl(pi)) against the oracle's count on noisy maps, several per batch,
-    including values exactly pi apart."""
+    including values exactly pi apart; widths that are not multiples of 4 (61 x 97:
+    scalar loads, the row's last quad partial) count on the maps themselves."""
     from oracle import fcd_oracle as O
     rng = np.random.default_rng(shape[0] + shape[1])
     maps = []
@@ -262,9 +250,12 @@ def test_residue_counts_match_oracle(lib, shape):
     assert [int(r) for r in res] == [O.count_residues(m) for m in w]
 
 
-def test_unwrap_residue_free_scan(lib):
+@pytest.mark.parametrize("shape", [(256, 512), (255, 509)])
+def test_unwrap_residue_free_scan(lib, shape):
+    """The residue-free scan (k_colk + k_rowscan) against the oracle, on a 64-multiple
+    shape and on an odd one (scanned unpadded, 64-pixel chunks with a partial last one)."""
     from oracle import fcd_oracle as O
-    y, x = np.mgrid[0:256, 0:512]
+    y, x = np.mgrid[0:shape[0], 0:shape[1]]
     phi = 0.05 * x + 0.03 * y + 2.0 * np.sin(x / 40.0) * np.cos(y / 55.0)
     w = np.angle(np.exp(1j * phi)).astype(np.float32)
     assert O.count_residues(w) == 0
@@ -276,24 +267,23 @@ def test_unwrap_residue_free_scan(lib):
 
 
 @pytest.mark.parametrize("n,count", [(1024, 7), (2048, 3)])
-def test_band_phase_resident_equals_classic(lib, monkeypatch, n, count):
+def test_band_phase_resident_matches_oracle(lib, n, count):
     """The theta-resident band kernel (k_band_phase_res: reference angles kept in
-    registers across the frames of an item, one wave (1024^2) or wave pair (2048^2)
-    per tile row) and k_band_phase (FCD_BAND_RES=0) run the same transform and phase
-    step: bit-identical wrapped phases, over odd frame counts (uneven frame slices)."""
+    registers across the frames of an item, one wave (1024^2) or wave pair (2048^2) per
+    tile row) over odd frame counts (uneven frame slices): wrapped phases of the last
+    frame against the oracle within 2e-4 rad, and every frame equal to its single-frame
+    call bit for bit."""
     from bench_data import make_frames_numpy
     from oracle import fcd_oracle as O
     ref, frames = make_frames_numpy(n, count, seed=21, rotate_deg=5.0)
     eng = lib.Engine(ref.shape)
     eng.set_reference(ref, 0.001)
     _, w_res, _ = eng.process(frames, 1.0, unwrap=False)
-    monkeypatch.setenv("FCD_BAND_RES", "0")
-    _, w_cls, _ = eng.process(frames, 1.0, unwrap=False)
-    assert np.array_equal(w_res, w_cls)
-    if n == 1024:
-        _, _, _, ex = O.compute_height_map(ref, frames[3], 0.001, height=1.0, unwrap_phases=False)
-        for q in range(2):
-            assert wrap_diff(w_res[3][q], ex["wrapped"][q]).max() < 2e-4
+    _, w_one, _ = eng.process(frames[count - 1:], 1.0, unwrap=False)
+    assert np.array_equal(w_res[count - 1], w_one[0])
+    _, _, _, ex = O.compute_height_map(ref, frames[count - 1], 0.001, height=1.0, unwrap_phases=False)
+    for q in range(2):
+        assert wrap_diff(w_res[count - 1][q], ex["wrapped"][q]).max() < 2e-4
 
 
 # ---------------------------------------------------------------- end to end
@@ -617,16 +607,16 @@ def test_census_flags_residues_on_tile_seams(lib, monkeypatch, n, count):
 
 # (y0, x0) of dislocation pairs whose residues fall on plaquette rows 128k - 1 in both
 # carrier maps at 1024^2: the edges between the fused kernel's dynamic chunks of 16
-# eight-row tiles (FCD_PR_CHUNK), found with the oracle as SEAM_PAIRS were
+# eight-row tiles, found with the oracle as SEAM_PAIRS were
 CHUNK_EDGE_PAIRS = [(512.0, 307.2), (512.0, 512.0), (639.5, 358.4), (639.75, 358.4)]
 
 
 @pytest.mark.parametrize("count", [6, 40])
-def test_fused_dynamic_schedule_matches_static(lib, monkeypatch, count):
-    """k_phase_rows at 1024^2 takes its tiles in chunks from a counter (FCD_PR_DYNAMIC=1,
-    the default) or as one contiguous range per block (=0): residue pairs on chunk
-    edges (checked by the deferred k_seam_check) and inside chunks are flagged by both
-    schedules, and every height is bit-identical; 6 frames = fewer chunks than CUs."""
+def test_fused_range_edges_flag_residues(lib, count):
+    """k_phase_rows at 1024^2 gives each block a contiguous range of eight-row tiles: residue
+    pairs on range edges (checked by the deferred k_seam_check) and inside ranges are all
+    flagged, and the batch's heights equal the single-frame calls bit for bit; 6 frames =
+    fewer ranges than CUs."""
     from pyfcd import _lib
     from bench_data import make_frames_numpy
     n = 1024
@@ -635,21 +625,18 @@ def test_fused_dynamic_schedule_matches_static(lib, monkeypatch, count):
     _, smooth = make_frames_numpy(n, count - len(dis), seed=5)
     frames = np.concatenate([dis, smooth.astype(np.float32)])
     _lib._engines.clear()
-    heights = {}
-    for dyn in ("0", "1"):
-        monkeypatch.setenv("FCD_PR_DYNAMIC", dyn)
-        eng = lib.Engine(ref.shape)
-        eng.set_reference(ref, 0.001)
-        eng.profile(True)
-        h, _, _ = eng.process(frames, 1.0, unwrap=True, want_phases=False)
-        st, _ = eng.stage_times()
-        eng.profile(False)
-        assert int(st["fixup_frames"]) == len(dis), (dyn, st)
-        heights[dyn] = h
-        del eng
-    monkeypatch.delenv("FCD_PR_DYNAMIC")
+    eng = lib.Engine(ref.shape)
+    eng.set_reference(ref, 0.001)
+    eng.profile(True)
+    h, _, _ = eng.process(frames, 1.0, unwrap=True, want_phases=False)
+    st, _ = eng.stage_times()
+    eng.profile(False)
+    assert int(st["fixup_frames"]) == len(dis), st
+    for i in (0, len(dis) - 1, len(dis), count - 1):
+        hs, _, _ = eng.process(frames[i:i + 1], 1.0, unwrap=True, want_phases=False)
+        assert np.array_equal(h[i], hs[0]), i
+    del eng
     _lib._engines.clear()
-    assert np.array_equal(heights["0"], heights["1"])
 
 
 def test_full_size_2048_vs_oracle(lib):

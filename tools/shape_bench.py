@@ -18,9 +18,9 @@ for p in (ROOT, os.path.join(ROOT, "trapped-modes-ltg_amd")):
 import numpy as np  # noqa: E402
 
 
-def frames_for(rows, cols, count):
+def frames_for(rows, cols, count, rotate):
     from bench_data import checkerboard, displacement_numpy, warp_numpy
-    ref = checkerboard(rows, 5.0, cols=cols)
+    ref = checkerboard(rows, rotate, cols=cols)
     base = [warp_numpy(ref, *displacement_numpy(rows, s, cols=cols)) for s in range(4)]
     return ref, np.stack([base[i % 4] for i in range(count)])
 
@@ -30,13 +30,14 @@ def main():
     ap.add_argument("shapes", nargs="*", default=["1024x1280", "1536x2048", "960x1024"])
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--rotate", type=float, default=5.0, help="board rotation (deg); 0 gives residue-free frames")
     args = ap.parse_args()
     import torch
     from pyfcd import _lib
     dev = torch.device("cuda", 0)
     for sh in args.shapes:
         rows, cols = (int(v) for v in sh.split("x"))
-        ref, frames = frames_for(rows, cols, args.batch)
+        ref, frames = frames_for(rows, cols, args.batch, args.rotate)
         fr = torch.from_numpy(frames).to(dev)
         h = torch.empty_like(fr)
         eng = _lib.Engine(ref.shape)
@@ -55,9 +56,17 @@ def main():
         torch.cuda.synchronize(dev)
         dt = (time.perf_counter() - t0) / args.steps
         mp = rows * cols / 1e6
-        print(json.dumps({"shape": [rows, cols], "frames_per_step": len(frames), "frames_per_s": round(len(frames) / dt, 1),
-                          "us_per_frame": round(dt / len(frames) * 1e6, 2),
-                          "us_per_megapixel": round(dt / len(frames) * 1e6 / mp, 2)}), flush=True)
+        eng.profile(True)  # one profiled step: stage split and the frames with residues
+        step()
+        torch.cuda.synchronize(dev)
+        st, nf = eng.stage_times()
+        eng.profile(False)
+        print(json.dumps({"shape": [rows, cols], "rotate_deg": args.rotate, "frames_per_step": len(frames),
+                          "frames_per_s": round(len(frames) / dt, 1), "us_per_frame": round(dt / len(frames) * 1e6, 2),
+                          "us_per_megapixel": round(dt / len(frames) * 1e6 / mp, 2),
+                          "residue_frames": int(st["fixup_frames"]),
+                          "profiled_ms": {k: round(st[k], 3) for k in ("demod", "unwrap", "integrate", "total", "fixup")}}),
+              flush=True)
         eng.close()
 
 

@@ -194,7 +194,8 @@ struct fcd_ctx {
     DevBuf mr_scratch;  // the mixed-radix column transforms' transposed copy (chunk frames)
     DevBuf gb_tables;   // generic chain's band columns (build_demod_tables)
     DevBuf mst_slot;    // map -> MST slot (-1: not in it) for k_int_rows2 kmode 3
-    DevBuf pad_w, pad_k;  // maps padded to multiples of 64 for the unwrap (unwrap_maps) and their k
+    DevBuf pad_w, pad_k;  // maps with residues padded to multiples of 64 for the MST (unwrap_maps) and their k
+    DevBuf pad_ids;       // their map indices
     int gb_NU = 0;      // columns in either carrier's disk
     hipStream_t own = nullptr;
     DevBuf tw_row, tw_col;        // plain tables exp(-2 pi i m / n) (generic LDS FFT kernels)
@@ -223,16 +224,12 @@ struct fcd_ctx {
     bool fused_ok = false;           // k_phase_rows applies (height-only calls)
     bool force_unfused = false;      // FCD_UNFUSED=1: take the unfused chain (A/B measurement)
     int nstreams = 2;                // FCD_STREAMS: device-path chunks split over 1 or 2 streams
-    bool defer_seam = true;          // FCD_DEFER_SEAM: the fused chain's seam census after the integration
     bool early_census = true;        // FCD_EARLY_CENSUS: device calls read the census back before the integration
     hipStream_t cstream = nullptr;   // its copy stream and the two halves' "census complete" events
     hipEvent_t ev_cen[2] = {nullptr, nullptr};
     hipEvent_t ev_done = nullptr;    // end of the last device call's work on its (caller's) stream
     hipStream_t done_stream = nullptr;  // that stream, while the work may still be running
     bool done_pending = false;
-    bool pr_dynamic = false;         // FCD_PR_DYNAMIC=1: the 1024 fused kernel takes tile chunks from a counter
-                                     // (r03t: 80.1-81.0k vs 80.0-81.6k frames/s static, no gain; kept as an option)
-    DevBuf pr_ctr;                   // its counter pairs, one per concurrent half (each launch leaves them 0)
     hipStream_t aux = nullptr;       // the second stream and its fork / join events
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     DevBuf ir_seam;                  // k_int_rows2's seam rows (tile-range edges), one region per stream
@@ -457,7 +454,11 @@ void unwrap_core(fcd_ctx* c, const float* w, int nmaps, int H, int W, int Hr, in
         HIPCHK(hipMemsetAsync(m.nhooks + 1, 0, (1 + fcdk::kCgRounds) * sizeof(int), s));
         fcdk::mst_tile_level0(w, c->mst_ids.as<int>(), nact, H, W, m, s, true);
         bool fits = true;
-        static const bool cg_dbg = std::getenv("FCD_MST_DEBUG") != nullptr;
+#ifdef FCD_DIAGNOSTIC
+        static const bool cg_dbg = std::getenv("FCD_MST_DEBUG") != nullptr;  // (diagnostic builds only)
+#else
+        constexpr bool cg_dbg = false;
+#endif
         auto cg_dump = [&](int r) {  // diagnostic: components and contracted edges entering round r
             const size_t nt = (size_t)nact * (H / tile_h) * (W / tile_w);
             std::vector<int> nc(nt), ne(nt);
@@ -478,7 +479,7 @@ void unwrap_core(fcd_ctx* c, const float* w, int nmaps, int H, int W, int Hr, in
         // the first check after FCD_CG_FIRST rounds (camera frames converge in 7-9, and a
         // round of finished tiles costs one load per tile), then every third: each check
         // is a host round trip with the GPU idle
-        static const int first = std::min(std::max(1, fcd_env_int("FCD_CG_FIRST", 9)), 64);  // (rounds < kCgRounds)
+        constexpr int first = 9;  // (rounds < kCgRounds; 6 / 7 / 12 measured no better, r04k)
         for (int step = first; rounds < max_rounds; rounds += step, step = 3) {
             for (int g = 0; g < step; ++g) {
                 if (cg_dbg) cg_dump(rounds + g);
@@ -522,7 +523,11 @@ void unwrap_core(fcd_ctx* c, const float* w, int nmaps, int H, int W, int Hr, in
         }
         // then rounds over the boundary / root lists only
         fcdk::mst_level_setup(nact, H, W, m, s);
+#ifdef FCD_DIAGNOSTIC
         static const bool dbg = std::getenv("FCD_MST_DEBUG") != nullptr;
+#else
+        constexpr bool dbg = false;
+#endif
         auto dump = [&](int r) {  // diagnostic: list sizes (B, R) entering round r
             std::vector<int> cnt((size_t)fcdk::mst_level_counts());
             HIPCHK(hipMemcpyAsync(cnt.data(), m.cnt, cnt.size() * 4, hipMemcpyDeviceToHost, s));
@@ -561,9 +566,11 @@ void unwrap_core(fcd_ctx* c, const float* w, int nmaps, int H, int W, int Hr, in
     fcdk::mst_finalize(c->mst_ids.as<int>(), nact, H, W, m, k, s);
 }
 
-// k-fields of nmaps wrapped maps of the context's frame size (unwrap_core); a frame whose
-// sides are not multiples of 64 is unwrapped in a copy padded by replicating its last row
-// and column (kernels_unwrap.hip pad_maps: same residues, same k on the frame's pixels).
+// k-fields of nmaps wrapped maps of the context's frame size (unwrap_core).  A frame whose
+// sides are not multiples of 64: the residue census and the scan of the residue-free maps
+// run on the maps themselves; the maps with residues go to the MST tiles in copies padded
+// by replicating their last row and column (kernels_unwrap.hip pad_maps: same residues,
+// same k on the frame's pixels).
 void unwrap_maps(fcd_ctx* c, const float* w, int nmaps, int32_t* k, int* res_host, hipStream_t s,
                  bool all_mst = false, fcdk::MstK* mk = nullptr, bool any_res = false) {
     const int H = c->H, W = c->W;
@@ -572,15 +579,35 @@ void unwrap_maps(fcd_ctx* c, const float* w, int nmaps, int32_t* k, int* res_hos
         return;
     }
     if (mk) mk->map_slot = nullptr;
+    std::vector<int> active;
+    if (all_mst) {
+        for (int i = 0; i < nmaps; ++i) active.push_back(i);
+    } else {
+        int* res = c->rescnt.as<int>();
+        fcdk::residues(w, nmaps, H, W, res, s, any_res);
+        std::vector<int> counts(nmaps);
+        HIPCHK(hipMemcpyAsync(counts.data(), res, sizeof(int) * nmaps, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        if (res_host) std::copy(counts.begin(), counts.end(), res_host);
+        for (int i = 0; i < nmaps; ++i)
+            if (counts[i] > 0) active.push_back(i);
+        if ((int)active.size() < nmaps) {
+            c->colk.ensure((size_t)nmaps * H * sizeof(int));
+            fcdk::unwrap_scan(w, nmaps, H, W, c->colk.as<int>(), k, s);
+        }
+    }
+    if (active.empty()) return;
+    const int nact = (int)active.size();
     const int Hp = (H + 63) / 64 * 64, Wp = (W + 63) / 64 * 64;
-    const size_t np = (size_t)nmaps * Hp * Wp;
+    const size_t np = (size_t)nact * Hp * Wp;
     c->pad_w.ensure(np * sizeof(float));
     c->pad_k.ensure(np * sizeof(int32_t));
-    c->colk.ensure((size_t)nmaps * Hp * sizeof(int));
-    fcdk::pad_maps(w, nmaps, H, W, Hp, Wp, c->pad_w.as<float>(), s);
-    unwrap_core(c, c->pad_w.as<float>(), nmaps, Hp, Wp, H, W, c->pad_k.as<int32_t>(), res_host, s, all_mst, nullptr,
-                any_res);
-    fcdk::unpad_k(c->pad_k.as<int32_t>(), nmaps, Hp, Wp, H, W, k, s);
+    c->pad_ids.ensure((size_t)nact * sizeof(int));
+    upload(c->pad_ids.p, active.data(), (size_t)nact * sizeof(int), s);
+    fcdk::pad_maps(w, nact, H, W, Hp, Wp, c->pad_w.as<float>(), s, c->pad_ids.as<int>());
+    unwrap_core(c, c->pad_w.as<float>(), nact, Hp, Wp, H, W, c->pad_k.as<int32_t>(), nullptr, s, true, nullptr, false);
+    fcdk::unpad_k(c->pad_k.as<int32_t>(), nact, Hp, Wp, H, W, k, s, c->pad_ids.as<int>());
+    HIPCHK(hipStreamSynchronize(s));  // (active, the ids' host copy, dies here)
 }
 
 // Integration tables for calibration factor cf (fourier.py:128-131, 75-92).
@@ -635,9 +662,13 @@ fcdk::IntegCoef integ_coef(fcd_ctx* c, double a0, double b0, double a1, double b
 // transforms: specT [nb][NU][H].  The demodulation reads no other column of the spectrum.
 void generic_fft2_t(fcd_ctx* c, const float* in, int nb, float2* specT, hipStream_t s) {
     float2* tmp = c->spec.as<float2>();
-    const int* ucols = c->gb_tables.as<int>();
-    rows_fft(c, false, fcdk::ROW_IN_REAL, fcdk::ROW_OUT_COMPLEX, in, tmp, (long)nb * c->H, 0.f, nullptr, s);
-    fcdk::mr_gather_cols(tmp, specT, nb, c->H, c->W, ucols, c->gb_NU, s);
+    const int NU = c->gb_NU;
+    fcdk::PhaseOut bo{};  // two rows per transform, their band columns only stored: [nb][H][NU]
+    bo.bslot = c->gb_tables.as<int>() + NU + 2 * (c->NCc[0] + c->NCc[1]) + 2 * (size_t)c->W;
+    bo.bnc = NU;
+    fcdk::mr_rows(c->mr_row, false, fcdk::ROW_IN_REAL2, fcdk::ROW_OUT_BAND2, in, tmp, (long)nb * c->H, c->H, 0.f,
+                  c->tw_row.as<float2>(), &bo, s);
+    fcdk::mr_transpose(tmp, specT, nb, c->H, NU, s);
     fcdk::mr_rows(c->mr_col, false, fcdk::ROW_IN_COMPLEX, fcdk::ROW_OUT_COMPLEX, specT, specT, (long)nb * c->gb_NU, c->gb_NU,
                   0.f, c->tw_col.as<float2>(), nullptr, s);
 }
@@ -673,21 +704,27 @@ void generic_demod_t(fcd_ctx* c, const float2* specT, int nb, float* wrapped, hi
 void generic_integrate_t(fcd_ctx* c, int nb, const float* w, const int32_t* kf, const fcdk::IntegCoef& k, float* h_out,
                          hipStream_t s) {
     float2* Z = c->spec.as<float2>();
-    float2* ZT = c->mr_scratch.as<float2>();
-    float2* HT = c->work.as<float2>();
     const float2* twc = c->tw_col.as<float2>();
     fcdk::PhaseOut zin{};
     zin.kin = kf;
     fcdk::mr_rows(c->mr_row, false, fcdk::ROW_IN_Z, fcdk::ROW_OUT_COMPLEX, w, Z, (long)nb * c->H, c->H, 0.f,
                   c->tw_row.as<float2>(), &zin, s);
-    fcdk::mr_transpose(Z, ZT, nb, c->H, c->W, s);
-    fcdk::mr_rows(c->mr_col, false, fcdk::ROW_IN_COMPLEX, fcdk::ROW_OUT_COMPLEX, ZT, ZT, (long)nb * c->W, c->W, 0.f, twc,
-                  nullptr, s);
-    fcdk::integ_multiply(ZT, HT, nb, c->H, c->W, k, s, true);
-    fcdk::mr_rows(c->mr_col, true, fcdk::ROW_IN_COMPLEX, fcdk::ROW_OUT_COMPLEX, HT, HT, (long)nb * c->W, c->W, 0.f, twc,
-                  nullptr, s);
-    fcdk::mr_transpose(HT, Z, nb, c->W, c->H, s);
-    rows_fft(c, true, fcdk::ROW_IN_COMPLEX, fcdk::ROW_OUT_REAL, Z, h_out, (long)nb * c->H, 0.f, nullptr, s);
+    if (fcdk::mr_int_cols_supported(c->mr_col)) {  // the column pairs in place
+        fcdk::mr_int_cols(c->mr_col, Z, nb, c->W, twc, k, s);
+    } else {  // (a prime factor of H above 7 but <= 61) transposed, the spectrum kept transposed between the passes
+        float2* ZT = c->mr_scratch.as<float2>();
+        float2* HT = c->work.as<float2>();
+        fcdk::mr_transpose(Z, ZT, nb, c->H, c->W, s);
+        fcdk::mr_rows(c->mr_col, false, fcdk::ROW_IN_COMPLEX, fcdk::ROW_OUT_COMPLEX, ZT, ZT, (long)nb * c->W, c->W, 0.f,
+                      twc, nullptr, s);
+        fcdk::integ_multiply(ZT, HT, nb, c->H, c->W, k, s, true);
+        fcdk::mr_rows(c->mr_col, true, fcdk::ROW_IN_COMPLEX, fcdk::ROW_OUT_COMPLEX, HT, HT, (long)nb * c->W, c->W, 0.f,
+                      twc, nullptr, s);
+        fcdk::mr_transpose(HT, Z, nb, c->W, c->H, s);
+    }
+    // two Hermitian rows per inverse transform
+    fcdk::mr_rows(c->mr_row, true, fcdk::ROW_IN_COMPLEX2, fcdk::ROW_OUT_REAL2, Z, h_out, (long)nb * c->H, c->H, 0.f,
+                  c->tw_row.as<float2>(), nullptr, s);
 }
 
 // h = real(ifft2(multiplier * fft2(z)))  for nb fields z (in c->spec).
@@ -695,6 +732,11 @@ void integrate_z(fcd_ctx* c, int nb, const fcdk::IntegCoef& k, float* h_out, hip
     float2* Z = c->spec.as<float2>();
     float2* Hh = c->work.as<float2>();
     rows_fft(c, false, fcdk::ROW_IN_COMPLEX, fcdk::ROW_OUT_COMPLEX, Z, Z, (long)nb * c->H, 0.f, nullptr, s);
+    if (c->generic && fcdk::mr_int_cols_supported(c->mr_col)) {  // the column pairs in place (kernels_mr.hip)
+        fcdk::mr_int_cols(c->mr_col, Z, nb, c->W, c->tw_col.as<float2>(), k, s);
+        rows_fft(c, true, fcdk::ROW_IN_COMPLEX, fcdk::ROW_OUT_REAL, Z, h_out, (long)nb * c->H, 0.f, nullptr, s);
+        return;
+    }
     cols_fft(c, false, Z, nb, s);
     fcdk::integ_multiply(Z, Hh, nb, c->H, c->W, k, s);
     cols_fft(c, true, Hh, nb, s);
@@ -782,7 +824,7 @@ void build_demod_tables(fcd_ctx* c, hipStream_t s) {
         c->band_B = c->fused_B = 0;
         c->fused_ok = false;
         // [NU union columns][carrier 0 columns][carrier 1 columns][their union slots (2)]
-        // [colslot: 2 x W] (generic_demod_t)
+        // [colslot: 2 x W] (generic_demod_t) [union slot of each column: W] (generic_fft2_t)
         std::vector<int> uslot_of(W, -1), ucols, cols[2], uslot[2];
         for (int uc = 0; uc < W; ++uc)
             if (colslot[uc] >= 0 || colslot[(size_t)W + uc] >= 0) {
@@ -804,6 +846,7 @@ void build_demod_tables(fcd_ctx* c, hipStream_t s) {
         for (int q = 0; q < 2; ++q) gb.insert(gb.end(), cols[q].begin(), cols[q].end());
         for (int q = 0; q < 2; ++q) gb.insert(gb.end(), uslot[q].begin(), uslot[q].end());
         gb.insert(gb.end(), colslot.begin(), colslot.end());
+        gb.insert(gb.end(), uslot_of.begin(), uslot_of.end());
         c->gb_tables.ensure(gb.size() * sizeof(int));
         upload(c->gb_tables.p, gb.data(), gb.size() * sizeof(int), s);
         return;
@@ -1133,9 +1176,7 @@ FCD_API int fcd_create(int device, int rows, int cols, fcd_ctx** out) {
         c->device = device;
         c->force_unfused = fcd_env_int("FCD_UNFUSED", 0) != 0;
         c->nstreams = fcd_env_int("FCD_STREAMS", 2) >= 2 ? 2 : 1;
-        c->defer_seam = fcd_env_int("FCD_DEFER_SEAM", 1) != 0;
         c->early_census = fcd_env_int("FCD_EARLY_CENSUS", 1) != 0;
-        c->pr_dynamic = fcd_env_int("FCD_PR_DYNAMIC", 0) != 0;
         c->H = rows;
         c->W = cols;
         c->generic = !pow2;
@@ -1144,8 +1185,6 @@ FCD_API int fcd_create(int device, int rows, int cols, fcd_ctx** out) {
             c->mr_col = fcdk::mr_plan(rows);
         }
         HIPCHK(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking));
-        c->pr_ctr.ensure(4 * sizeof(unsigned));
-        HIPCHK(hipMemset(c->pr_ctr.p, 0, 4 * sizeof(unsigned)));
         // plain tables exp(-2 pi i m / n) (power-of-two LDS kernels), or the mixed-radix plans'
         // tables (with Bluestein's chirp and convolution spectra)
         const std::vector<float2> tr = c->generic ? fcdk::mr_tables(c->mr_row) : twiddles(cols),
@@ -1385,12 +1424,10 @@ void first_pass_chunk(fcd_ctx* c, const float* fr, int nb, bool unwrap, bool fus
         fcdk::demod_rows(c->W, fr, c->H, nb, T, Xb, c->twp_row.as<float2>(), s);
         fcdk::demod_cols(c->H, Xb, nb, T, Ab, c->NCA, dc_tw(c), s);
         if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
-        // dynamic chunk schedule: each concurrent half (fo) has its own counter pair
-        unsigned* ctr = c->pr_dynamic ? c->pr_ctr.as<unsigned>() + (fo ? 2 : 0) : nullptr;
-        const bool defer = c->defer_seam && !census_ev;
+        const bool defer = !census_ev;
         fcdk::phase_rows(c->W, unwrap, Ab, c->H, nb, c->NCA, c->NCc[0], c->NCc[1], c->theta_p.as<float>(),
                          c->band_pre.as<float2>(), c->band_ptw.as<float2>(), c->ztw.as<float2>(), col0, res, Zt, seam,
-                         s, defer, ctr);
+                         s, defer);
         if (census_ev) HIPCHK(hipEventRecord(census_ev, s));
         if (unwrap) fcdk::unwrap_colk_compact(col0, 2 * nb, c->H, colk, s);
         if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
@@ -1399,7 +1436,7 @@ void first_pass_chunk(fcd_ctx* c, const float* fr, int nb, bool unwrap, bool fus
         // the census of the tile-range edges: its flags are read only when the call ends,
         // so it runs last instead of holding the integration kernels behind it (a small
         // grid waiting for CUs the other stream's fused kernel holds)
-        if (unwrap && defer) fcdk::phase_rows_seam(c->W, c->H, nb, seam, res, s, ctr != nullptr);
+        if (unwrap && defer) fcdk::phase_rows_seam(c->W, c->H, nb, seam, res, s);
     } else {
         const long H = c->H, W = c->W;
         float* wrapped = c->wrapped.as<float>() + fo * 2 * H * W;
@@ -1848,13 +1885,9 @@ int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int f
     // ---- pass 2: frames whose maps have residues are redone with the Boruvka (MST) unwrap
     // into page-locked memory: a pageable destination went through the runtime's staging
     // copy (a blit kernel, then a host memcpy before the stream reports completion)
-    static const int pinned_env = fcd_env_int("FCD_CENSUS_PINNED", 1);
     std::vector<int> counts((size_t)n_frames * 2);
-    int* cdst = counts.data();
-    if (pinned_env) {
-        c->census.ensure(counts.size() * sizeof(int));
-        cdst = static_cast<int*>(c->census.p);
-    }
+    c->census.ensure(counts.size() * sizeof(int));
+    int* cdst = static_cast<int*>(c->census.p);
     hipStream_t qs = s;  // the stream the readback runs on (and the poll below queries)
     if (cen_halves > 0) {
         qs = c->cstream;
@@ -1864,18 +1897,18 @@ int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int f
     // polled rather than a blocking wait: the caller's next batch is enqueued as soon
     // as this one's census is back (a blocking wait's wake-up sat in every bench step,
     // ~17 us per 256-frame step at 1024^2).  The poll yields the core between queries
-    // and gives up after FCD_SPIN_US (default 20 ms: a 1024^2 chunk's first pass takes
-    // ~3 ms, a 4096^2 one ~6 ms), then blocks; FCD_SPIN_US=0 always blocks.
-    static const long spin_us = fcd_env_int("FCD_SPIN_US", 20000);
+    // and gives up after 20 ms (a 1024^2 chunk's first pass takes ~3 ms, a 4096^2 one
+    // ~6 ms), then blocks.
+    constexpr long spin_us = 20000;
     hipError_t qe = hipErrorNotReady;
-    if (spin_us > 0) {
+    {
         const auto t_end = std::chrono::steady_clock::now() + std::chrono::microseconds(spin_us);
         while ((qe = hipStreamQuery(qs)) == hipErrorNotReady && std::chrono::steady_clock::now() < t_end)
             std::this_thread::yield();
     }
     if (qe == hipErrorNotReady) qe = hipStreamSynchronize(qs);
     HIPCHK(qe);
-    if (cdst != counts.data()) std::memcpy(counts.data(), cdst, counts.size() * sizeof(int));
+    std::memcpy(counts.data(), cdst, counts.size() * sizeof(int));
     std::vector<int> redo;
     for (int f = 0; f < n_frames; ++f)
         if (counts[2 * (size_t)f] || counts[2 * (size_t)f + 1]) redo.push_back(f);

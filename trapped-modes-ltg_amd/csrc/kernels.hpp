@@ -16,15 +16,22 @@ namespace fcdk {
 // wrapped [nb][2][H][W], PhaseOut::kin the k-fields (null: none), as make_z
 // ROW_IN_BAND (mr_rows only): row (b, i) of the band columns held transposed, in = [nb][bnc][H]
 // complex, column j = in[b][bslot[j]][i] (bslot[j] < 0: zero)
-enum RowIn { ROW_IN_COMPLEX = 0, ROW_IN_REAL = 1, ROW_IN_Z = 2, ROW_IN_BAND = 3 };
-enum RowOut { ROW_OUT_COMPLEX = 0, ROW_OUT_REAL = 1, ROW_OUT_PHASE = 2 };
+// ROW_IN_REAL2 / ROW_IN_COMPLEX2 (mr_rows only, with ROW_OUT_BAND2 / ROW_OUT_REAL2): rows 2p and
+// 2p + 1 of a frame (nrows a multiple of H; an odd H's last row alone) in one complex
+// transform -- two real rows as re + i im (their spectra split by Hermitian symmetry), or
+// the real parts of two rows' inverses as those of ifft(Herm(A) + i Herm(B)),
+// Herm(Y)(k) = (Y(k) + conj Y(-k)) / 2
+enum RowIn { ROW_IN_COMPLEX = 0, ROW_IN_REAL = 1, ROW_IN_Z = 2, ROW_IN_BAND = 3, ROW_IN_REAL2 = 4, ROW_IN_COMPLEX2 = 5 };
+// ROW_OUT_BAND2 (mr_rows only): the band columns of each row, out = [nrows][bnc] complex,
+// column j to slot bslot[j] (bslot[j] < 0: not stored)
+enum RowOut { ROW_OUT_COMPLEX = 0, ROW_OUT_REAL = 1, ROW_OUT_PHASE = 2, ROW_OUT_BAND2 = 4, ROW_OUT_REAL2 = 5 };
 
 struct PhaseOut {          // ROW_OUT_PHASE: w = wrap(theta - atan2(A))
     const float* theta;    // [H][W] reference angle of this carrier
     float* wrapped;        // output base; row r of batch b -> wrapped + ((b*2 + carrier)*H + r)*W
     int carrier;
     const int32_t* kin = nullptr;  // ROW_IN_Z's k-fields
-    const int* bslot = nullptr;    // ROW_IN_BAND's column slots [W] and their count
+    const int* bslot = nullptr;    // ROW_IN_BAND's / ROW_OUT_BAND2's column slots [W] and their count
     int bnc = 0;
 };
 
@@ -118,8 +125,7 @@ void unwrap_colk(const float* w, int nmaps, int H, int W, int* colk, hipStream_t
 // the same over compact column-0 values col0[map][H] (the fused path's side output)
 void unwrap_colk_compact(const float* col0, int nmaps, int H, int* colk, hipStream_t s);
 // fused band transform + phase + unwrap + z-row FFT (kernels_phase_rows.hip)
-// W = 1024 (B = 128), 2048 (B = 256) and 4096 (B = 512; kernels_phase_rows_wide.hip;
-// FCD_FUSED_2048 / FCD_FUSED_4096 = 0 keep the unfused chain there).  ztw:
+// W = 1024 (B = 128), 2048 (B = 256) and 4096 (B = 512; kernels_phase_rows_wide.hip).  ztw:
 // group_twiddles(W) at 1024; wider: the 1024-point table followed by the join twiddles
 // exp(-2 pi i h k / W), h = 1 .. W/1024 - 1, k < 1024.
 bool phase_rows_supported(int W, int B, int H);
@@ -127,14 +133,10 @@ int phase_rows_tile(int W);  // rows per fused tile (seam buffer: nb * H / tile 
 // defer_seam: the census of the edges between the blocks' tile ranges is left to a
 // later phase_rows_seam on the same stream (its flags are read only at the end of the
 // call, so the headline chain launches it after the integration kernels).
-// ctr (1024-point rows only): two zeroed device counters, private to the stream, the
-// blocks take chunks of tiles from (dynamic schedule, FCD_PR_CHUNK tiles each; the
-// launch leaves them zeroed).  phase_rows_seam's dyn must match the launch's schedule
-// (ctr != null).
 void phase_rows(int W, bool unwrap, const float2* Ab, int H, int nb, int NCA, int ncc0, int ncc1, const float* theta,
                 const float2* pre, const float2* ptw, const float2* ztw, float* col0, int* flags, float2* Zt,
-                float2* seam, hipStream_t s, bool defer_seam = false, unsigned* ctr = nullptr);
-void phase_rows_seam(int W, int H, int nb, const float2* seam, int* flags, hipStream_t s, bool dyn = false);
+                float2* seam, hipStream_t s, bool defer_seam = false);
+void phase_rows_seam(int W, int H, int nb, const float2* seam, int* flags, hipStream_t s);
 
 // In-place or out-of-place batched row FFT over nrows rows of length W.
 void row_fft(int W, bool inverse, RowIn in_mode, RowOut out_mode, const void* in, void* out, long nrows,
@@ -164,6 +166,14 @@ void mr_rows(const MrPlan& p, bool inverse, RowIn in_mode, RowOut out_mode, cons
 void mr_transpose(const float2* in, float2* out, int nb, int R, int C, hipStream_t s);
 // column subset: [nb][R][C] -> [nb][NS][R] (columns cols[])
 void mr_gather_cols(const float2* in, float2* out, int nb, int R, int C, const int* cols, int NS, hipStream_t s);
+// The spectral integration's column stage of the generic chain, in place on Z [nb][p.n][W]
+// (the row spectra of phi0 + i phi1): per workgroup a run of columns in LDS, forward column
+// transforms, the multiplier (m1 + i m0) Z -- integ_multiply's h_hat up to its real part
+// after the inverse, which ROW_IN_COMPLEX2 takes --, inverse column transforms: no
+// transposes, one read and one write of Z.
+// (column lengths whose plan has radices <= 8 only, mr_int_cols_supported)
+bool mr_int_cols_supported(const MrPlan& p);
+void mr_int_cols(const MrPlan& p, float2* Z, int nb, int W, const float2* tw, const IntegCoef& c, hipStream_t s);
 // in-place column transforms of [nb][p.n][W] (through scratch: nb * p.n * W complex)
 void mr_cols(const MrPlan& p, int W, bool inverse, float2* data, int nb, const float2* tw, float2* scratch,
              hipStream_t s);
@@ -205,10 +215,6 @@ void phase_rows_wide(int W, bool unwrap, const float2* Ab, int H, int nb, int NC
 void phase_rows_wide_seam(int W, int H, int nb, const float2* seam, int* flags, hipStream_t s);
 void phase_rows_wide_ref(int W, const float2* Ab, int H, int NCA, int ncc0, int ncc1, const float2* pre,
                          const float2* ptw, float* theta_b, hipStream_t s);
-inline bool fcd_fused_env(const char* name) {  // FCD_FUSED_2048 / FCD_FUSED_4096 = 0: the unfused chain
-    const char* e = std::getenv(name);
-    return !(e && e[0] == '0');
-}
 
 // ---- unwrap ----
 // counts[m] = residues of map m; any_only: counts[m] > 0 iff map m has residues (blocks of
@@ -217,8 +223,11 @@ void residues(const float* w, int nmaps, int H, int W, int* counts, hipStream_t 
 void unwrap_scan(const float* w, int nmaps, int H, int W, int* colk, int32_t* k, hipStream_t s);
 // frames whose sides are not multiples of 64: unwrapped in a copy padded to Hp x Wp by
 // replicating the last row / column (kernels_unwrap.hip), k copied back
-void pad_maps(const float* w, int nmaps, int H, int W, int Hp, int Wp, float* out, hipStream_t s);
-void unpad_k(const int32_t* kp, int nmaps, int Hp, int Wp, int H, int W, int32_t* k, hipStream_t s);
+// ids (nullable): padded map m is map ids[m] of w / k
+void pad_maps(const float* w, int nmaps, int H, int W, int Hp, int Wp, float* out, hipStream_t s,
+              const int* ids = nullptr);
+void unpad_k(const int32_t* kp, int nmaps, int Hp, int Wp, int H, int W, int32_t* k, hipStream_t s,
+             const int* ids = nullptr);
 
 // The component-graph path's tile geometry: level-0 component of pixel v (vertex id slot *
 // H * W + pixel) = tile_of(v) * ccap + crank[v]

@@ -493,9 +493,7 @@ static void launch_band(bool ref, const float2* Ab, int H, int nb, int NCA, int 
     } else {
         if constexpr ((W == 1024 || W == 2048) && B <= W / 8 && FCD_BAND_RESIDENT && FCD_ATAN_N > 0 && !FCD_BAND_ABL &&
                       !FCD_BAND_NOSTORE && !FCD_BAND_NOTHETA) {
-            // FCD_BAND_RES=0 in the environment selects k_band_phase (equality tests)
-            const char* env = std::getenv("FCD_BAND_RES");
-            if (!(env && env[0] == '0')) {
+            {
                 // rows per item: 1024 threads at most (2048-point rows take two waves)
                 constexpr int ROWS = FCD_BAND_RES_ROWS * (W / 16) <= 1024 ? FCD_BAND_RES_ROWS : 1024 / (W / 16);
                 using R = BRCfg<W, B, ROWS>;

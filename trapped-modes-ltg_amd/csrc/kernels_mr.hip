@@ -24,6 +24,7 @@
 // buffers fill at most 128 KB of the 160 KB LDS.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <complex>
 #include <stdexcept>
 #include <string>
@@ -204,12 +205,25 @@ __global__ __launch_bounds__(MR_THREADS) void k_mr_rows(const void* __restrict__
                                                         PhaseOut ph) {
     extern __shared__ __attribute__((aligned(16))) float2 mr_lds[];
     const int n = p.n, len = p.blue ? p.M : n;
-    const long row = blockIdx.x;
+    constexpr bool PAIR = IN == ROW_IN_REAL2 || IN == ROW_IN_COMPLEX2;
+    // pairs never straddle two frames (a batch gives every frame the single-frame call's
+    // bits): with H odd each frame's last row transforms alone
+    const long hp = (H + 1) / 2;
+    const long row = PAIR ? (long)(blockIdx.x / hp) * H + 2 * (long)(blockIdx.x % hp) : (long)blockIdx.x;
+    const bool second = PAIR && 2 * (long)(blockIdx.x % hp) + 1 < H;
     float2* b0 = mr_lds;
     float2* b1 = mr_lds + len;
     for (int i = threadIdx.x; i < n; i += MR_THREADS) {
         float2 v;
-        if constexpr (IN == ROW_IN_REAL) {
+        if constexpr (IN == ROW_IN_REAL2) {
+            const float* x = static_cast<const float*>(in) + row * n + i;
+            v = make_float2(x[0] - sub, second ? x[n] - sub : 0.f);
+        } else if constexpr (IN == ROW_IN_COMPLEX2) {  // raw rows a, b -> b0, b1 (combined below)
+            const float2* x = static_cast<const float2*>(in) + row * n + i;
+            b1[i] = second ? x[n] : make_float2(0.f, 0.f);
+            b0[i] = x[0];
+            continue;
+        } else if constexpr (IN == ROW_IN_REAL) {
             v = make_float2(static_cast<const float*>(in)[row * n + i] - sub, 0.f);
         } else if constexpr (IN == ROW_IN_Z) {  // k_make_z's arithmetic
             const long b = row / H, r = row % H;
@@ -230,6 +244,25 @@ __global__ __launch_bounds__(MR_THREADS) void k_mr_rows(const void* __restrict__
         if (p.blue) v = cmul_dir<INV>(v, tw[p.tc + i]);  // Bluestein: the chirp premultiply
         b0[i] = v;
     }
+    if constexpr (IN == ROW_IN_COMPLEX2) {
+        // Re(ifft(A)) + i Re(ifft(B)) = ifft(Herm(A) + i Herm(B)), Herm(Y)(k) = (Y(k) + conj Y(-k)) / 2:
+        // the thread of the pair (k, n - k) reads all four values before writing both
+        __syncthreads();
+        for (int i = threadIdx.x; i <= n / 2; i += MR_THREADS) {
+            const int im = i ? n - i : 0;
+            const float2 a = b0[i], am = b0[im], bb = b1[i], bm = b1[im];
+            const float2 ha = make_float2(0.5f * (a.x + am.x), 0.5f * (a.y - am.y));
+            const float2 hb = make_float2(0.5f * (bb.x + bm.x), 0.5f * (bb.y - bm.y));
+            float2 v = make_float2(ha.x - hb.y, ha.y + hb.x);        // Herm(A)(k) + i Herm(B)(k)
+            float2 vm = make_float2(ha.x + hb.y, -ha.y + hb.x);      // at -k: conj(Herm(A)(k)) + i conj(Herm(B)(k))
+            if (p.blue) {
+                v = cmul_dir<INV>(v, tw[p.tc + i]);
+                vm = cmul_dir<INV>(vm, tw[p.tc + im]);
+            }
+            b0[i] = v;
+            if (im != i) b0[im] = vm;
+        }
+    }
     for (int i = n + threadIdx.x; i < len; i += MR_THREADS) b0[i] = make_float2(0.f, 0.f);  // (Bluestein) zero padding
     __syncthreads();
     float2* r;
@@ -248,6 +281,22 @@ __global__ __launch_bounds__(MR_THREADS) void k_mr_rows(const void* __restrict__
     b0 = r;
     if constexpr (OUT == ROW_OUT_COMPLEX) {
         for (int i = threadIdx.x; i < n; i += MR_THREADS) static_cast<float2*>(out)[row * n + i] = b0[i];
+    } else if constexpr (OUT == ROW_OUT_BAND2) {  // X_a = (Z(k) + conj Z(-k)) / 2, X_b = (Z(k) - conj Z(-k)) / 2i
+        float2* o = static_cast<float2*>(out) + row * (long)ph.bnc;
+        for (int i = threadIdx.x; i < n; i += MR_THREADS) {
+            const int sl = ph.bslot[i];
+            if (sl < 0) continue;
+            const float2 z = b0[i], zm = b0[i ? n - i : 0];
+            o[sl] = make_float2(0.5f * (z.x + zm.x), 0.5f * (z.y - zm.y));
+            if (second) o[ph.bnc + sl] = make_float2(0.5f * (z.y + zm.y), -0.5f * (z.x - zm.x));
+        }
+    } else if constexpr (OUT == ROW_OUT_REAL2) {
+        float* o = static_cast<float*>(out) + row * n;
+        for (int i = threadIdx.x; i < n; i += MR_THREADS) {
+            const float2 v = b0[i];
+            o[i] = v.x;
+            if (second) o[n + i] = v.y;
+        }
     } else if constexpr (OUT == ROW_OUT_REAL) {
         for (int i = threadIdx.x; i < n; i += MR_THREADS) static_cast<float*>(out)[row * n + i] = b0[i].x;
     } else {
@@ -281,6 +330,181 @@ __global__ __launch_bounds__(256) void k_mr_transpose(const float2* __restrict__
         if (c0 + y < C && r0 + tx < R) dst[(long)(c0 + y) * R + r0 + tx] = tile[tx][y];
 }
 
+// ------------------------------------------------------------------ integration columns
+// Column transforms of several columns at once (radices 8 / 4 / 2 / 3 / 5 / 7; a column
+// length with a larger prime factor takes the transpose route), in place in one LDS buffer (column c at
+// buf + c * pitch, a team of `team` threads per column, team a power of two): each pass
+// first loads every butterfly input of the thread into registers (at most MC_EPL values
+// per thread: len <= MC_EPL * team), then, after a barrier, writes the outputs.  One
+// buffer instead of the rows' two: twice the columns per workgroup.
+constexpr int MC_EPL = 16;
+
+template <int R>
+constexpr int mc_nbf() { return (MC_EPL + R - 1) / R; }  // butterflies per thread (n / R <= nbf * team)
+
+template <int R, bool INV>
+__device__ __forceinline__ void mc_pass(float2* buf, int pitch, int team, int n, int L, const float2* __restrict__ tw) {
+    constexpr int NBF = mc_nbf<R>();
+    const int nbt = n / R, step = n / (L * R);
+    const int col = threadIdx.x / team, t = threadIdx.x & (team - 1);
+    float2* const cb = buf + col * pitch;
+    float2 a[NBF][R];
+#pragma unroll
+    for (int m = 0; m < NBF; ++m) {
+        const int j = t + m * team;
+        if (j < nbt) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) a[m][r] = cb[j + r * nbt];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < NBF; ++m) {
+        const int j = t + m * team;
+        if (j < nbt) {
+            const int k = j % L;
+            if (L > 1) {
+#pragma unroll
+                for (int r = 1; r < R; ++r) a[m][r] = cmul_dir<INV>(a[m][r], tw[r * k * step]);
+            }
+            dft_any<R, INV>(a[m]);
+            float2* dst = cb + (j - k) * R + k;
+#pragma unroll
+            for (int r = 0; r < R; ++r) dst[r * L] = a[m][r];
+        }
+    }
+    __syncthreads();
+}
+
+template <bool INV>
+__device__ __forceinline__ void mc_run(float2* buf, int pitch, int team, int len, const int* fct, int nf,
+                                       const float2* __restrict__ tw) {
+    int L = 1;
+    for (int f = 0; f < nf; ++f) {
+        const int R = fct[f];
+        switch (R) {
+            case 8: mc_pass<8, INV>(buf, pitch, team, len, L, tw); break;
+            case 4: mc_pass<4, INV>(buf, pitch, team, len, L, tw); break;
+            case 2: mc_pass<2, INV>(buf, pitch, team, len, L, tw); break;
+            case 3: mc_pass<3, INV>(buf, pitch, team, len, L, tw); break;
+            case 5: mc_pass<5, INV>(buf, pitch, team, len, L, tw); break;
+            default: mc_pass<7, INV>(buf, pitch, team, len, L, tw);  // (mr_int_cols_supported: no larger primes)
+        }
+        L *= R;
+    }
+}
+
+// The length-H DFT of the workgroup's columns (Bluestein: the columns' first H values hold
+// the chirp-premultiplied input, the rest zeros, on entry; the transform's H values on exit).
+// tws: the passes' twiddles (LDS), tw: the plan's table (chirp, G).
+template <bool INV, int NT>
+__device__ __forceinline__ void mc_dft(float2* buf, int ncol, int pitch, int team, const MrPlan& p,
+                                       const float2* tws, const float2* __restrict__ tw) {
+    if (!p.blue) {
+        mc_run<INV>(buf, pitch, team, p.n, p.fct, p.nf, tws);
+        return;
+    }
+    const int M = p.M, H = p.n;
+    mc_run<false>(buf, pitch, team, M, p.fct, p.nf, tws);
+    const float2* G = tw + (INV ? p.tgi : p.tgf);
+    for (int u = threadIdx.x; u < ncol * M; u += NT) {
+        const int col = u / M, i = u - col * M;
+        buf[col * pitch + i] = cmul(buf[col * pitch + i], G[i]);
+    }
+    __syncthreads();
+    mc_run<true>(buf, pitch, team, M, p.fct, p.nf, tws);
+    for (int u = threadIdx.x; u < ncol * H; u += NT) {
+        const int col = u / H, i = u - col * H;
+        buf[col * pitch + i] = cmul_dir<INV>(buf[col * pitch + i], tw[p.tc + i]);
+    }
+    __syncthreads();
+}
+
+// The spectral integration without the Z(k) / Z(-k) pairing: with m0, m1 the real, odd
+// multipliers of integ_multiply (h_hat = i (m0 Phi0 + m1 Phi1), Phi0 / Phi1 the Hermitian
+// / anti-Hermitian parts of Z), h = Re(ifft2(h_hat)) = Re(ifft2((m1 + i m0) Z)) exactly
+// (the conjugate-mirrored term's real part equals its unmirrored image's); the row
+// inverse takes the real part (ROW_IN_COMPLEX2: each row's Hermitian part).
+__device__ __forceinline__ float2 mc_mult(float2 z, int q, int r, const IntegCoef& c) {
+    const float kx = c.kxe[q], ky = c.kye[r];
+    float k2 = c.kx2[q] + c.ky2[r];
+    if (r == 0 && q == 0) k2 = 1.f;
+    const float s = c.norm / k2;
+    const float m0 = (kx * c.a0 + ky * c.b0) * s;
+    const float m1 = (kx * c.a1 + ky * c.b1) * s;
+    return make_float2(m1 * z.x - m0 * z.y, m1 * z.y + m0 * z.x);
+}
+
+// Columns q0 .. q0 + cnt - 1 (q0 = g C) of a frame in LDS slots 0 .. cnt - 1, a team of
+// NT / C threads per column, the transform's twiddles copied to LDS after the columns; reads
+// and writes run over the slots fastest (C consecutive columns per row), each thread's
+// loads issued together (at most MC_EPL: cnt H <= C len <= MC_EPL NT).
+template <int NT>
+__global__ __launch_bounds__(NT, 4) void k_mr_int_cols(float2* __restrict__ Z, int nblk, int W, int C, int ngroups,
+                                                       MrPlan p, const float2* __restrict__ tw, IntegCoef ic) {
+    extern __shared__ __attribute__((aligned(16))) float2 mc_lds[];
+    const int H = p.n, len = p.blue ? p.M : H, pitch = len + 1;
+    // XCD-aware numbering (the grid a multiple of 8; block b runs on XCD b % 8): consecutive
+    // column groups on one XCD at once, so their row runs share the XCD's L2 lines
+    const long wk = (long)(blockIdx.x % 8) * (gridDim.x / 8) + blockIdx.x / 8;
+    if (wk >= nblk) return;
+    const long b = wk / ngroups;
+    const int g = (int)(wk % ngroups);
+    float2* const Zb = Z + b * (long)H * W;
+    const int q0 = g * C, cnt = min(C, W - q0);
+    const int team = NT / C, total = cnt * H;
+    float2* const tws = mc_lds + C * pitch;  // len twiddles (Bluestein: the M-point table)
+    const float2* const twsrc = p.blue ? tw + p.tM : tw;
+    for (int i = threadIdx.x; i < len; i += NT) tws[i] = twsrc[i];
+    {
+        float2 v[MC_EPL];
+#pragma unroll
+        for (int m = 0; m < MC_EPL; ++m) {
+            const int u = threadIdx.x + m * NT;
+            if (u < total) {
+                const int i = u / cnt, sl = u - i * cnt;
+                v[m] = Zb[(long)i * W + q0 + sl];
+            }
+        }
+#pragma unroll
+        for (int m = 0; m < MC_EPL; ++m) {
+            const int u = threadIdx.x + m * NT;
+            if (u < total) {
+                const int i = u / cnt, sl = u - i * cnt;
+                mc_lds[sl * pitch + i] = p.blue ? cmul_dir<false>(v[m], tw[p.tc + i]) : v[m];
+            }
+        }
+    }
+    if (p.blue)
+        for (int u = threadIdx.x; u < cnt * (len - H); u += NT) {
+            const int sl = u / (len - H), i = H + u - sl * (len - H);
+            mc_lds[sl * pitch + i] = make_float2(0.f, 0.f);
+        }
+    __syncthreads();
+    mc_dft<false, NT>(mc_lds, cnt, pitch, team, p, tws, tw);
+#pragma unroll
+    for (int m = 0; m < MC_EPL; ++m) {
+        const int u = threadIdx.x + m * NT;
+        if (u < total) {
+            const int sl = u / H, r = u - sl * H;
+            float2 v = mc_mult(mc_lds[sl * pitch + r], q0 + sl, r, ic);
+            if (p.blue) v = cmul_dir<true>(v, tw[p.tc + r]);  // the inverse's chirp premultiply
+            mc_lds[sl * pitch + r] = v;
+        }
+    }
+    if (p.blue)
+        for (int u = threadIdx.x; u < cnt * (len - H); u += NT) {
+            const int sl = u / (len - H), i = H + u - sl * (len - H);
+            mc_lds[sl * pitch + i] = make_float2(0.f, 0.f);
+        }
+    __syncthreads();
+    mc_dft<true, NT>(mc_lds, cnt, pitch, team, p, tws, tw);
+    for (int u = threadIdx.x; u < total; u += NT) {
+        const int i = u / cnt, sl = u - i * cnt;
+        Zb[(long)i * W + q0 + sl] = mc_lds[sl * pitch + i];
+    }
+}
+
 template <bool INV, int IN, int OUT>
 void launch_mr(const MrPlan& p, const void* in, void* out, long nrows, int H, float sub, const float2* tw,
                const PhaseOut* ph, hipStream_t s) {
@@ -293,7 +517,8 @@ void launch_mr(const MrPlan& p, const void* in, void* out, long nrows, int H, fl
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         attr = true;
     }
-    hipLaunchKernelGGL((k_mr_rows<INV, IN, OUT>), dim3((unsigned)nrows), dim3(MR_THREADS), lds, s, in, out, nrows, H,
+    const long grid = (IN == ROW_IN_REAL2 || IN == ROW_IN_COMPLEX2) ? nrows / H * ((H + 1) / 2) : nrows;
+    hipLaunchKernelGGL((k_mr_rows<INV, IN, OUT>), dim3((unsigned)grid), dim3(MR_THREADS), lds, s, in, out, nrows, H,
                        sub, p, tw, q);
     FCD_CHECK_LAUNCH();
 }
@@ -419,6 +644,10 @@ void mr_rows(const MrPlan& p, bool inverse, RowIn im, RowOut om, const void* in,
     if (nrows <= 0) return;
     if (!inverse && im == ROW_IN_REAL && om == ROW_OUT_COMPLEX)
         launch_mr<false, ROW_IN_REAL, ROW_OUT_COMPLEX>(p, in, out, nrows, H, sub, tw, ph, s);
+    else if (!inverse && im == ROW_IN_REAL2 && om == ROW_OUT_BAND2)
+        launch_mr<false, ROW_IN_REAL2, ROW_OUT_BAND2>(p, in, out, nrows, H, sub, tw, ph, s);
+    else if (inverse && im == ROW_IN_COMPLEX2 && om == ROW_OUT_REAL2)
+        launch_mr<true, ROW_IN_COMPLEX2, ROW_OUT_REAL2>(p, in, out, nrows, H, sub, tw, ph, s);
     else if (!inverse && im == ROW_IN_COMPLEX && om == ROW_OUT_COMPLEX)
         launch_mr<false, ROW_IN_COMPLEX, ROW_OUT_COMPLEX>(p, in, out, nrows, H, sub, tw, ph, s);
     else if (!inverse && im == ROW_IN_Z && om == ROW_OUT_COMPLEX)
@@ -433,6 +662,48 @@ void mr_rows(const MrPlan& p, bool inverse, RowIn im, RowOut om, const void* in,
         launch_mr<true, ROW_IN_BAND, ROW_OUT_PHASE>(p, in, out, nrows, H, sub, tw, ph, s);
     else
         throw std::runtime_error("mr_rows: unsupported mode combination");
+}
+
+bool mr_int_cols_supported(const MrPlan& p) {  // (also Bluestein: M is a power of two)
+    for (int f = 0; f < p.nf; ++f)
+        if (p.fct[f] > 8 || p.fct[f] == 6) return false;  // the generic odd-prime passes: the transpose route
+    return true;
+}
+
+// Columns per group C (a power of two <= 16: up to 128-byte row runs), 512 threads with a team
+// of 512 / C per column (len <= MC_EPL * team), or 1024 when the 512 would leave C = 1;
+// LDS: the C columns and the len twiddles, at most 80 KB (two 512-thread workgroups per CU).
+void mr_int_cols(const MrPlan& p, float2* Z, int nb, int W, const float2* tw, const IntegCoef& c, hipStream_t s) {
+    if (nb <= 0) return;
+    if (!mr_int_cols_supported(p)) throw std::runtime_error("mr_int_cols: a radix above 8");
+    const int len = p.blue ? p.M : p.n;
+    auto lds_of = [&](int C) { return (size_t)(C * (len + 1) + len) * sizeof(float2); };
+    auto fits = [&](int C, int nt) { return len <= MC_EPL * (nt / C) && lds_of(C) <= (nt == 512 ? 80 : 160) * 1024; };
+    int nt = 512, C = 1;
+    while (C < 16 && fits(2 * C, 512)) C *= 2;
+    if (!fits(C, 512)) {  // (1024 threads with twice the columns measured 2-3 % slower at 1080 x 1920, r05)
+        nt = 1024;
+        C = 1;
+        while (C < 16 && fits(2 * C, 1024)) C *= 2;
+        if (!fits(C, 1024)) throw std::runtime_error("mr_int_cols: column length " + std::to_string(len) + " exceeds the workgroup");
+    }
+    const int ngroups = (W + C - 1) / C;
+    const size_t lds = lds_of(C);
+    const long blocks = (long)nb * ngroups;
+    static bool attr = false;
+    if (!attr) {
+        FCD_HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mr_int_cols<512>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        FCD_HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mr_int_cols<1024>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        attr = true;
+    }
+    const unsigned grid = (unsigned)((blocks + 7) / 8 * 8);
+    if (nt == 512)
+        hipLaunchKernelGGL(k_mr_int_cols<512>, dim3(grid), dim3(512), lds, s, Z, (int)blocks, W, C, ngroups, p, tw, c);
+    else
+        hipLaunchKernelGGL(k_mr_int_cols<1024>, dim3(grid), dim3(1024), lds, s, Z, (int)blocks, W, C, ngroups, p, tw, c);
+    FCD_CHECK_LAUNCH();
 }
 
 void mr_transpose(const float2* in, float2* out, int nb, int R, int C, hipStream_t s) {

@@ -111,8 +111,7 @@ template <bool UNWRAP>
 __global__ __launch_bounds__(PR_THREADS, FCD_PR_MINB) void k_phase_rows(
     const float2* __restrict__ Ab, int H, int nb, int NCA, int ncc0, int ncc1, const float* __restrict__ theta,
     const float2* __restrict__ pre, const float2* __restrict__ ptw, const float2* __restrict__ ztw,
-    float* __restrict__ col0, int* __restrict__ flags, float2* __restrict__ Zt, float2* __restrict__ seam, int per,
-    unsigned* __restrict__ ctr) {
+    float* __restrict__ col0, int* __restrict__ flags, float2* __restrict__ Zt, float2* __restrict__ seam, int per) {
     extern __shared__ __attribute__((aligned(16))) float2 lds_p[];
     float2* const stage = lds_p + OFF_STAGE;
     float2* const ptl = lds_p + OFF_PRE;
@@ -132,20 +131,12 @@ __global__ __launch_bounds__(PR_THREADS, FCD_PR_MINB) void k_phase_rows(
     const int rbs = H / PR_ROWS;
     const int items = nb * rbs;
     const int tiles16 = H / 16;
-    // Work comes in chunks of `per` consecutive tiles: consecutive tiles of a frame are
-    // checked against each other here, only the chunk edges go to k_seam_check.  Static
-    // (ctr null): chunk = block.  Dynamic: the blocks take chunks from the counter
-    // ctr[0], so a block that started late, behind the other stream's kernels, takes
-    // fewer of them instead of ending the launch late; the last block to leave (ctr[1]
-    // counts them) sets both back to 0 for the next launch on the stream.
+    // Each block takes a contiguous range of `per` consecutive tiles: consecutive tiles of a
+    // frame are checked against each other here, only the range edges go to k_seam_check.
+    // (A dynamic schedule -- chunks of tiles from a counter -- measured 80.0-81.6 k vs
+    // 80.1-81.0 k frames/s static, r03t, and was removed.)
     const int nch = (items + per - 1) / per;
-    __shared__ int s_next;
-    int ch = blockIdx.x;
-    if (ctr) {
-        if (threadIdx.x == 0) s_next = (int)atomicAdd(ctr, 1u);
-        __syncthreads();
-        ch = s_next;
-    }
+    const int ch = blockIdx.x;
     // staged band values of the next item, prefetched into registers: entry
     // e = (c, j, row) with row fastest, 8 rows = one 64-byte run of Ab's 16-row tile
     constexpr int NST = 2 * PR_B * PR_ROWS;
@@ -168,13 +159,8 @@ __global__ __launch_bounds__(PR_THREADS, FCD_PR_MINB) void k_phase_rows(
 #ifdef FCD_STAMPS
     unsigned long long ph[16] = {}, tprev = __builtin_readcyclecounter();
 #endif
-    while (ch < nch) {
+    if (ch < nch) {
     const int it0 = ch * per, it1 = min(it0 + per, items);
-    // the next chunk, taken now so the chunk's last tile can prefetch its first band
-    // tile; read by every thread after the first staging barrier below, rewritten only
-    // at the next chunk's start (after this chunk's closing barriers)
-    if (ctr && threadIdx.x == 0) s_next = (int)atomicAdd(ctr, 1u);
-    int nxt = nch;
     for (int blk = it0; blk < it1; ++blk) {
         const int f = blk / rbs, rb = blk % rbs;
         const int r = rb * PR_ROWS + wave;           // this wave's row
@@ -188,11 +174,7 @@ __global__ __launch_bounds__(PR_THREADS, FCD_PR_MINB) void k_phase_rows(
         }
         __syncthreads();
         PR_STAMP(1);
-        if (ctr && blk == it0) nxt = s_next;
-        if (blk + 1 < it1)
-            fetch(blk + 1);
-        else if (nxt < nch)
-            fetch(nxt * per);
+        if (blk + 1 < it1) fetch(blk + 1);
         PR_STAMP(2);
         // ---- band transforms of both carriers -> wrapped phases (natural strided)
         float w0[16], w1[16];
@@ -391,13 +373,6 @@ __global__ __launch_bounds__(PR_THREADS, FCD_PR_MINB) void k_phase_rows(
         __syncthreads();
         PR_STAMP(12);
     }
-    ch = nxt;
-    }
-    // every grab of this block precedes its exit count (each atomic returns before the
-    // next is issued), so the last block out resets the counters with no grab pending
-    if (ctr && threadIdx.x == 0 && atomicAdd(ctr + 1, 1u) == gridDim.x - 1) {
-        atomicExch(ctr, 0u);
-        atomicExch(ctr + 1, 0u);
     }
 #ifdef FCD_STAMPS
     if (blockIdx.x == 0 && lane == 0)
@@ -446,26 +421,16 @@ extern "C" __attribute__((visibility("default"))) int fcd_debug_pr_stamps(unsign
 
 bool phase_rows_supported(int W, int B, int H) {
     if (H % 16 != 0 || H < 16) return false;
-    if (W == 2048 && B == 256) return fcd_fused_env("FCD_FUSED_2048");
-    if (W == 4096 && B == 512) return fcd_fused_env("FCD_FUSED_4096");
+    if (W == 2048 && B == 256) return true;
+    if (W == 4096 && B == 512) return true;
     return W == PR_W && B == PR_B;
 }
 
 int phase_rows_tile(int W) { return W == 2048 ? 4 : (W == 4096 ? 2 : PR_ROWS); }
 
-// Blocks of k_phase_rows at 1024-point rows and their chunks of `per` consecutive
-// 8-row tiles.  Static: one chunk per block, the tiles split evenly over one block per
-// CU.  Dynamic (FCD_PR_CHUNK tiles per chunk, default 16): one block per CU, chunks
-// from a counter.
-static int pr_chunk_tiles() {
-    static const int v = [] {
-        const char* e = std::getenv("FCD_PR_CHUNK");
-        return std::max(1, (e && *e) ? std::atoi(e) : 16);
-    }();
-    return v;
-}
-
-static void pr_layout(int H, int nb, bool dyn, int& grid, int& per) {
+// Blocks of k_phase_rows at 1024-point rows: the tiles split evenly over the blocks (one
+// block per CU), each a contiguous range of `per` consecutive 8-row tiles.
+static void pr_layout(int H, int nb, int& grid, int& per) {
     static int ncu = 0;
     if (!ncu) {
         int dev = 0;
@@ -478,18 +443,13 @@ static void pr_layout(int H, int nb, bool dyn, int& grid, int& per) {
     const int slots = (int)std::min<long>(items, (long)ncu * per_cu);
     grid = per = 0;
     if (slots <= 0) return;
-    if (dyn) {
-        per = pr_chunk_tiles();
-        grid = (int)std::min<long>((items + per - 1) / per, slots);
-        return;
-    }
     per = (int)((items + slots - 1) / slots);  // tiles per block, a contiguous range
     grid = (int)((items + per - 1) / per);
 }
 
 void phase_rows(int W, bool unwrap, const float2* Ab, int H, int nb, int NCA, int ncc0, int ncc1, const float* theta,
                 const float2* pre, const float2* ptw, const float2* ztw, float* col0, int* flags, float2* Zt,
-                float2* seam, hipStream_t s, bool defer_seam, unsigned* ctr) {
+                float2* seam, hipStream_t s, bool defer_seam) {
     if (W == 2048 || W == 4096) {
         phase_rows_wide(W, unwrap, Ab, H, nb, NCA, ncc0, ncc1, theta, pre, ptw, ztw, col0, flags, Zt, seam, s,
                         defer_seam);
@@ -497,34 +457,34 @@ void phase_rows(int W, bool unwrap, const float2* Ab, int H, int nb, int NCA, in
     }
     if (W != PR_W) throw std::runtime_error("phase_rows: unsupported row length");
     int grid, per;
-    pr_layout(H, nb, ctr != nullptr, grid, per);
+    pr_layout(H, nb, grid, per);
     if (grid <= 0) return;
     if (unwrap) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_phase_rows<true>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)PR_LDS);
         hipLaunchKernelGGL(k_phase_rows<true>, dim3(grid), dim3(PR_THREADS), PR_LDS, s, Ab, H, nb, NCA, ncc0, ncc1,
-                           theta, pre, ptw, ztw, col0, flags, Zt, seam, per, ctr);
-        if (!defer_seam) phase_rows_seam(W, H, nb, seam, flags, s, ctr != nullptr);
+                           theta, pre, ptw, ztw, col0, flags, Zt, seam, per);
+        if (!defer_seam) phase_rows_seam(W, H, nb, seam, flags, s);
     } else {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_phase_rows<false>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)PR_LDS);
         hipLaunchKernelGGL(k_phase_rows<false>, dim3(grid), dim3(PR_THREADS), PR_LDS, s, Ab, H, nb, NCA, ncc0, ncc1,
-                           theta, pre, ptw, ztw, col0, flags, Zt, seam, per, ctr);
+                           theta, pre, ptw, ztw, col0, flags, Zt, seam, per);
     }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) throw std::runtime_error(std::string("phase_rows launch: ") + hipGetErrorString(e));
 }
 
-void phase_rows_seam(int W, int H, int nb, const float2* seam, int* flags, hipStream_t s, bool dyn) {
+void phase_rows_seam(int W, int H, int nb, const float2* seam, int* flags, hipStream_t s) {
     if (W == 2048 || W == 4096) {
         phase_rows_wide_seam(W, H, nb, seam, flags, s);
         return;
     }
     int grid, per;
-    pr_layout(H, nb, dyn, grid, per);
+    pr_layout(H, nb, grid, per);
     if (grid <= 0) return;
     const long items = (long)nb * (H / PR_ROWS);
-    const long edges = (items + per - 1) / per - 1;  // chunk edges (those at frame starts return at once)
+    const long edges = (items + per - 1) / per - 1;  // range edges (those at frame starts return at once)
     if (edges > 0)
         hipLaunchKernelGGL(k_seam_check, dim3((unsigned)((edges + 3) / 4)), dim3(256), 0, s, seam, H, nb, per, flags);
     const hipError_t e = hipGetLastError();

@@ -44,9 +44,6 @@ namespace fcdk {
 constexpr double kPi = 3.141592653589793;      // skimage unwrap's PI (probed: double M_PI)
 constexpr double kTwoPi = 6.283185307179586;
 constexpr double kBorderRel = 9999999.0;
-#ifndef FCD_MST_TILE_DEFAULT
-#define FCD_MST_TILE_DEFAULT 64  // tile pass shape code (mst_tile_shape)
-#endif
 #ifndef FCD_T0_REL_UNROLL
 #define FCD_T0_REL_UNROLL 2  // reliability loop trips unrolled (A/B r04t: 1 8.46-8.50k, 2 8.56k, 5 8.39-8.44k frames/s)
 #endif
@@ -116,19 +113,23 @@ __global__ __launch_bounds__(256) void k_residues(const float* __restrict__ w, i
                                                   bool any_only) {
     const int map = (int)(blockIdx.x % (unsigned)nmaps);
     if (any_only && __hip_atomic_load(counts + map, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > 0) return;
-    const int q = W / 4;  // column quads per row (W % 4 == 0)
+    const int q = (W + 3) / 4;  // column quads per row
     const long idx = (long)(blockIdx.x / (unsigned)nmaps) * 256 + threadIdx.x;
     const int strip = (int)(idx / q), j = (int)(idx % q) * 4;
     const int i0 = strip * kResRows, i1 = min(i0 + kResRows, H - 1);  // plaquette rows [i0, i1)
     int r = 0;
     if (i0 < i1) {
         const float* m = w + (long)map * H * W + (long)i0 * W + j;
-        const bool last = j + 4 >= W;  // the row's last plaquette column is j + 2
-        const int nk = last ? 3 : 4;
+        const int nk = min(4, W - 1 - j);  // plaquettes j .. j + nk - 1 (the row's last one is W - 2)
         auto load = [&](const float* p, float (&v)[5]) {
-            const float4 a = *reinterpret_cast<const float4*>(p);
-            v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
-            v[4] = last ? 0.f : p[4];
+            if ((W & 3) == 0) {  // 16-byte aligned quads
+                const float4 a = *reinterpret_cast<const float4*>(p);
+                v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) v[k] = j + k < W ? p[k] : 0.f;
+            }
+            v[4] = j + 4 < W ? p[4] : 0.f;
         };
         float ra[5], rc[5], rn[5] = {};
         load(m, ra);
@@ -159,8 +160,7 @@ __global__ __launch_bounds__(256) void k_residues(const float* __restrict__ w, i
 
 void residues(const float* w, int nmaps, int H, int W, int* counts, hipStream_t s, bool any_only) {
     FCD_HIPCHK(hipMemsetAsync(counts, 0, sizeof(int) * nmaps, s));
-    if (W % 4 != 0) throw std::runtime_error("residues: W must be a multiple of 4");
-    const long threads = (long)(H - 1 + kResRows - 1) / kResRows * (W / 4);
+    const long threads = (long)(H - 1 + kResRows - 1) / kResRows * ((W + 3) / 4);
     const long blocks = (threads + 255) / 256 * nmaps;
     if (blocks > 0x7fffffffL) throw std::runtime_error("residues: too many maps in one launch");
     hipLaunchKernelGGL(k_residues, dim3((unsigned)blocks), dim3(256), 0, s, w, H, W, nmaps, counts, any_only);
@@ -174,12 +174,12 @@ __global__ __launch_bounds__(256) void k_colk(const float* __restrict__ w, int H
     __shared__ int part[256];
     const int map = blockIdx.x;
     const float* m = w + (long)map * map_stride;
-    const int per = (H + 255) / 256;
+    const int per = (H + 255) / 256;  // <= 32
     const int i0 = threadIdx.x * per;
-    int loc[16];
+    int loc[32];
     int sum = 0;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
+    for (int q = 0; q < 32; ++q) {
         const int i = i0 + q;
         loc[q] = 0;
         if (q < per && i + 1 < H) {
@@ -199,7 +199,7 @@ __global__ __launch_bounds__(256) void k_colk(const float* __restrict__ w, int H
     const int base = threadIdx.x ? part[threadIdx.x - 1] : 0;
     int* out = colk + (long)map * H;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
+    for (int q = 0; q < 32; ++q) {
         const int i = i0 + q;
         if (q < per && i < H) out[i] = base + (q ? loc[q - 1] : 0);
     }
@@ -218,9 +218,9 @@ __global__ __launch_bounds__(256) void k_rowscan(const float* __restrict__ w, lo
     const float* r = w + row * W;
     int32_t* ko = k + row * W;
     int acc = colk[row];  // row index == map * H + i == colk layout
-    float cur = r[lane];  // W % 64 == 0
+    float cur = lane < W ? r[lane] : 0.f;
     for (int c0 = 0; c0 < W; c0 += 64) {
-        const float nxt = c0 + 64 < W ? r[c0 + 64 + lane] : 0.f;
+        const float nxt = c0 + 64 + lane < W ? r[c0 + 64 + lane] : 0.f;
         float right = __shfl_down(cur, 1, 64);
         const float n0 = __shfl(nxt, 0, 64);
         if (lane == 63) right = n0;
@@ -234,7 +234,7 @@ __global__ __launch_bounds__(256) void k_rowscan(const float* __restrict__ w, lo
             const int v = __shfl_up(incl, off, 64);
             if (lane >= off) incl += v;
         }
-        ko[c0 + lane] = acc + incl - d;
+        if (c0 + lane < W) ko[c0 + lane] = acc + incl - d;
         acc += __shfl(incl, 63, 64);
         cur = nxt;
     }
@@ -251,11 +251,10 @@ void unwrap_colk_compact(const float* col0, int nmaps, int H, int* colk, hipStre
 }
 
 void unwrap_scan(const float* w, int nmaps, int H, int W, int* colk, int32_t* k, hipStream_t s) {
-    if (H > 4096) throw std::runtime_error("unwrap_scan: H too large");
+    if (H > 8192) throw std::runtime_error("unwrap_scan: H too large");
     hipLaunchKernelGGL(k_colk, dim3(nmaps), dim3(256), 0, s, w, H, (long)H * W, (long)W, colk);
     FCD_CHECK_LAUNCH();
     const long nrows = (long)nmaps * H;
-    if (W % 64 != 0) throw std::runtime_error("unwrap_scan: W must be a multiple of 64");
     hipLaunchKernelGGL(k_rowscan, dim3((unsigned)((nrows + 3) / 4)), dim3(256), 0, s, w, nrows, H, W, colk, k);
     FCD_CHECK_LAUNCH();
 }
@@ -267,34 +266,36 @@ void unwrap_scan(const float* w, int nmaps, int H, int W, int* colk, int32_t* k,
 // residue-free scan integrates the frame's pixels from their own left / upper neighbours
 // only, and the MST pass gives pad pixels the reliability kPadRel (MstWork::Hr / Wr).
 __global__ __launch_bounds__(256) void k_pad_maps(const float* __restrict__ w, long n, int H, int W, int Hp, int Wp,
-                                                  float* __restrict__ out) {
+                                                  const int* __restrict__ ids, float* __restrict__ out) {
     for (long g = (long)blockIdx.x * 256 + threadIdx.x; g < n; g += (long)gridDim.x * 256) {
         const long m = g / ((long)Hp * Wp), p = g - m * Hp * Wp;
         const int i = (int)(p / Wp), j = (int)(p % Wp);
-        out[g] = w[(m * H + min(i, H - 1)) * W + min(j, W - 1)];
+        const long src = ids ? ids[m] : m;
+        out[g] = w[(src * H + min(i, H - 1)) * W + min(j, W - 1)];
     }
 }
 
 __global__ __launch_bounds__(256) void k_unpad_k(const int32_t* __restrict__ kp, long n, int H, int W, int Hp, int Wp,
-                                                 int32_t* __restrict__ k) {
+                                                 const int* __restrict__ ids, int32_t* __restrict__ k) {
     for (long g = (long)blockIdx.x * 256 + threadIdx.x; g < n; g += (long)gridDim.x * 256) {
         const long m = g / ((long)H * W), p = g - m * H * W;
         const int i = (int)(p / W), j = (int)(p % W);
-        k[g] = kp[(m * Hp + i) * Wp + j];
+        const long dst = ids ? ids[m] : m;
+        k[dst * H * W + p] = kp[(m * Hp + i) * Wp + j];
     }
 }
 
 static unsigned grid_of(long n) { return (unsigned)std::min<long>(std::max<long>((n + 255) / 256, 1), 16384); }
 
-void pad_maps(const float* w, int nmaps, int H, int W, int Hp, int Wp, float* out, hipStream_t s) {
+void pad_maps(const float* w, int nmaps, int H, int W, int Hp, int Wp, float* out, hipStream_t s, const int* ids) {
     const long n = (long)nmaps * Hp * Wp;
-    hipLaunchKernelGGL(k_pad_maps, dim3(grid_of(n)), dim3(256), 0, s, w, n, H, W, Hp, Wp, out);
+    hipLaunchKernelGGL(k_pad_maps, dim3(grid_of(n)), dim3(256), 0, s, w, n, H, W, Hp, Wp, ids, out);
     FCD_CHECK_LAUNCH();
 }
 
-void unpad_k(const int32_t* kp, int nmaps, int Hp, int Wp, int H, int W, int32_t* k, hipStream_t s) {
+void unpad_k(const int32_t* kp, int nmaps, int Hp, int Wp, int H, int W, int32_t* k, hipStream_t s, const int* ids) {
     const long n = (long)nmaps * H * W;
-    hipLaunchKernelGGL(k_unpad_k, dim3(grid_of(n)), dim3(256), 0, s, kp, n, H, W, Hp, Wp, k);
+    hipLaunchKernelGGL(k_unpad_k, dim3(grid_of(n)), dim3(256), 0, s, kp, n, H, W, Hp, Wp, ids, k);
     FCD_CHECK_LAUNCH();
 }
 
@@ -1716,13 +1717,9 @@ void mst_cg_finalize(const int* map_ids, int nact, int H, int W, MstWork m, int3
 }
 
 int mst_tile_shape(int H, int W, int* th) {
-    // FCD_MST_TILE (diagnostic override, read per call): 64 (64 x 64), 6432 (64 wide, 32
-    // tall) or 32 (32 x 32); the default, and the fallbacks when H, W are not multiples
-    const char* e = std::getenv("FCD_MST_TILE");
-    const int want = e ? std::atoi(e) : FCD_MST_TILE_DEFAULT;
-    if (want == 64 && H % 64 == 0 && W % 64 == 0) return *th = 64, 64;
-    if (want == 6432 && H % 32 == 0 && W % 64 == 0) return *th = 32, 64;
-    if (H % 32 == 0 && W % 32 == 0) return *th = 32, 32;
+    // 64 x 64 tiles (a frame of another size reaches the unwrap padded to multiples of 64,
+    // unwrap_maps; 32 x 32 and 64 x 32 tiles measured slower and were removed, r04x)
+    if (H % 64 == 0 && W % 64 == 0) return *th = 64, 64;
     return *th = 0, 0;
 }
 
@@ -1732,21 +1729,14 @@ void mst_tile_level0(const float* w, const int* map_ids, int nact, int H, int W,
     if (!tw) throw std::runtime_error("mst_tile_level0: frame not a multiple of the tile");
     const dim3 g((unsigned)((long)nact * (H / th) * (W / tw)));
     const dim3 b((unsigned)(tw * th / 4));
-    // FCD_T0_ROUNDS (A/B override, read per call): the tile rounds before the cap applies
+    // FCD_T0_ROUNDS (read per call; tests/test_gpu_parity.py runs 0 / 1 / 2 / 99 against the
+    // default): the tile rounds before the cap applies
     const char* e = std::getenv("FCD_T0_ROUNDS");
     const int cap = e ? std::atoi(e) : FCD_T0_ROUNDS_DEFAULT;
-#define FCD_T0_LAUNCH(TW, TH, CG) hipLaunchKernelGGL((k_mst_tile0<TW, TH, CG>), g, b, 0, s, w, map_ids, nact, H, W, m, cap)
-    if (tw == 64 && th == 64) {
-        if (graph) FCD_T0_LAUNCH(64, 64, true);
-        else FCD_T0_LAUNCH(64, 64, false);
-    } else if (tw == 64) {
-        if (graph) FCD_T0_LAUNCH(64, 32, true);
-        else FCD_T0_LAUNCH(64, 32, false);
-    } else {
-        if (graph) FCD_T0_LAUNCH(32, 32, true);
-        else FCD_T0_LAUNCH(32, 32, false);
-    }
-#undef FCD_T0_LAUNCH
+    if (graph)
+        hipLaunchKernelGGL((k_mst_tile0<64, 64, true>), g, b, 0, s, w, map_ids, nact, H, W, m, cap);
+    else
+        hipLaunchKernelGGL((k_mst_tile0<64, 64, false>), g, b, 0, s, w, map_ids, nact, H, W, m, cap);
     FCD_CHECK_LAUNCH();
 }
 
