@@ -17,6 +17,7 @@
 #include <numeric>
 #include <stdexcept>
 #include <string>
+#include <exception>
 #include <thread>
 #include <vector>
 
@@ -183,6 +184,20 @@ struct PinBuf {
     }
 };
 
+// The exact (MST) unwrap's workspace: Boruvka arrays, component-graph edge records, the
+// residue counts and scan offsets of the maps it is handed, the MST slot of each map, the
+// copies of maps padded to multiples of 64.  The context holds two, so the two halves of
+// an exact-first chunk unwrap side by side (process_impl).
+struct MstSpace {
+    DevBuf comp, off, rel, cw, ce, bw, be, link, hooks, ids;
+    DevBuf rootof, offk, lb0, lb1, lr0, lr1, ll0, cnt, mb0, mb1;  // two-level rounds
+    DevBuf cg_ncomp, cg_ecnt, cg_ea, cg_eb, cg_ew, cg_ec, cg_ed, cg_lcol;  // component-graph rounds
+    DevBuf slot;                // map -> MST slot (-1: not in it) for k_int_rows2 kmode 3
+    DevBuf rescnt, colk;        // residue counts, the scan's column-0 offsets
+    DevBuf pad_w, pad_k, pad_ids;  // maps with residues padded to multiples of 64, their k and indices
+    size_t cap = 0;
+};
+
 }  // namespace
 
 struct fcd_ctx {
@@ -193,9 +208,6 @@ struct fcd_ctx {
     fcdk::MrPlan mr_row{}, mr_col{};
     DevBuf mr_scratch;  // the mixed-radix column transforms' transposed copy (chunk frames)
     DevBuf gb_tables;   // generic chain's band columns (build_demod_tables)
-    DevBuf mst_slot;    // map -> MST slot (-1: not in it) for k_int_rows2 kmode 3
-    DevBuf pad_w, pad_k;  // maps with residues padded to multiples of 64 for the MST (unwrap_maps) and their k
-    DevBuf pad_ids;       // their map indices
     int gb_NU = 0;      // columns in either carrier's disk
     hipStream_t own = nullptr;
     DevBuf tw_row, tw_col;        // plain tables exp(-2 pi i m / n) (generic LDS FFT kernels)
@@ -254,11 +266,7 @@ struct fcd_ctx {
     DevBuf t_stage, t_tab, t_bins, t_part, t_out, t_win, t_wsum, t_slices;
     DevBuf t_chirp, t_bhat, t_work, t_gpart, t_zo, t_bad;  // the FFT path of the mean spectrum
     HostPipe pipe;
-    // MST workspace
-    DevBuf mst_comp, mst_off, mst_rel, mst_cw, mst_ce, mst_bw, mst_be, mst_link, mst_hooks, mst_ids;
-    DevBuf mst_rootof, mst_offk, mst_lb0, mst_lb1, mst_lr0, mst_lr1, mst_ll0, mst_cnt, mst_mb0, mst_mb1;  // two-level rounds
-    DevBuf cg_ncomp, cg_ecnt, cg_ea, cg_eb, cg_ew, cg_ec, cg_ed, cg_lcol;  // component-graph rounds
-    size_t mst_cap = 0;
+    MstSpace ms[2];  // MST workspaces (the second: the other half of an exact-first chunk)
 
     // stage timing: 4 events per chunk (start, after demod, after unwrap, after integrate)
     bool profiling = false;
@@ -294,66 +302,64 @@ void ensure_chunk_buffers(fcd_ctx* c) {
     c->rescnt.ensure(n * 2 * sizeof(int));
 }
 
-void ensure_mst(fcd_ctx* c, int nact, long hw) {
+void ensure_mst(fcd_ctx* c, MstSpace& S, int nact, long hw) {
     const size_t nv = (size_t)nact * hw;
-    if (nv <= c->mst_cap) return;
-    c->mst_comp.ensure(nv * 4);
-    c->mst_off.ensure(nv * 4);
-    c->mst_rel.ensure(nv * 8);
-    c->mst_cw.ensure(nv * 8);
-    c->mst_ce.ensure(nv * 4);
-    c->mst_bw.ensure(nv * 8);
-    c->mst_be.ensure(nv * 4);
-    c->mst_link.ensure(nv * 8);
-    c->mst_hooks.ensure((2 + fcdk::kCgRounds) * sizeof(int));  // hooks this round; graph overflow; graph rounds' hooks
-    // edge records for any tile side (FCD_MST_TILE may change between calls on the same buffers)
+    S.ids.ensure(sizeof(int) * 2 * (size_t)std::max(c->chunk, c->fchunk) + 64);
+    if (nv <= S.cap) return;
+    S.comp.ensure(nv * 4);
+    S.off.ensure(nv * 4);
+    S.rel.ensure(nv * 8);
+    S.cw.ensure(nv * 8);
+    S.ce.ensure(nv * 4);
+    S.bw.ensure(nv * 8);
+    S.be.ensure(nv * 4);
+    S.link.ensure(nv * 8);
+    S.hooks.ensure((2 + fcdk::kCgRounds) * sizeof(int));  // hooks this round; graph overflow; graph rounds' hooks
     const size_t ne = (size_t)fcdk::mst_cg_edge_capacity((long)nv);
-    const size_t nt = (size_t)nact * hw / 1024 + 1;  // tiles (32 x 32 at the smallest)
-    c->cg_ncomp.ensure(nt * 4);
-    c->cg_lcol.ensure(nt * 64 * 4);  // tile height <= 64
-    c->cg_ecnt.ensure(nt * 4);
-    for (DevBuf* b : {&c->cg_ea, &c->cg_eb, &c->cg_ec, &c->cg_ed}) b->ensure(ne * 4);
-    c->cg_ew.ensure(ne * 8);
-    for (DevBuf* b : {&c->mst_rootof, &c->mst_offk, &c->mst_lb0, &c->mst_lb1, &c->mst_lr0, &c->mst_lr1, &c->mst_ll0})
-        b->ensure(nv * 4);
-    c->mst_cnt.ensure((size_t)fcdk::mst_level_counts() * sizeof(int));
-    c->mst_mb0.ensure(nv);
-    c->mst_mb1.ensure(nv);
-    c->mst_ids.ensure(sizeof(int) * 2 * (size_t)std::max(c->chunk, c->fchunk) + 64);
-    c->mst_cap = nv;
+    const size_t nt = (size_t)nact * hw / 1024 + 1;  // tiles (at most one per 1024 pixels)
+    S.cg_ncomp.ensure(nt * 4);
+    S.cg_lcol.ensure(nt * 64 * 4);  // tile height <= 64
+    S.cg_ecnt.ensure(nt * 4);
+    for (DevBuf* b : {&S.cg_ea, &S.cg_eb, &S.cg_ec, &S.cg_ed}) b->ensure(ne * 4);
+    S.cg_ew.ensure(ne * 8);
+    for (DevBuf* b : {&S.rootof, &S.offk, &S.lb0, &S.lb1, &S.lr0, &S.lr1, &S.ll0}) b->ensure(nv * 4);
+    S.cnt.ensure((size_t)fcdk::mst_level_counts() * sizeof(int));
+    S.mb0.ensure(nv);
+    S.mb1.ensure(nv);
+    S.cap = nv;
 }
 
-fcdk::MstWork mst_work(fcd_ctx* c) {
+fcdk::MstWork mst_work(fcd_ctx* c, MstSpace& S) {
     fcdk::MstWork m;
-    m.comp = c->mst_comp.as<int>();
-    m.off = c->mst_off.as<int>();
-    m.crank = c->mst_comp.as<unsigned char>();
-    m.coff = c->mst_off.as<short>();
-    m.rel = c->mst_rel.as<double>();
-    m.cand_w = c->mst_cw.as<double>();
-    m.cand_e = c->mst_ce.as<int>();
-    m.best_w = c->mst_bw.as<unsigned long long>();
-    m.best_e = c->mst_be.as<int>();
-    m.link = c->mst_link.as<unsigned long long>();
-    m.nhooks = c->mst_hooks.as<int>();
-    m.rootof = c->mst_rootof.as<int>();
-    m.offk = c->mst_offk.as<int>();
-    m.listB[0] = c->mst_lb0.as<int>();
-    m.listB[1] = c->mst_lb1.as<int>();
-    m.listR[0] = c->mst_lr0.as<int>();
-    m.listR[1] = c->mst_lr1.as<int>();
-    m.listL0 = c->mst_ll0.as<int>();
-    m.cnt = c->mst_cnt.as<int>();
-    m.maskB[0] = c->mst_mb0.as<unsigned char>();
-    m.maskB[1] = c->mst_mb1.as<unsigned char>();
-    m.cg_ncomp = c->cg_ncomp.as<int>();
-    m.cg_lcol = c->cg_lcol.as<unsigned>();
-    m.cg_ecnt = c->cg_ecnt.as<int>();
-    m.cg_ea = c->cg_ea.as<int>();
-    m.cg_eb = c->cg_eb.as<int>();
-    m.cg_ew = c->cg_ew.as<unsigned long long>();
-    m.cg_ec = c->cg_ec.as<int>();
-    m.cg_ed = c->cg_ed.as<int>();
+    m.comp = S.comp.as<int>();
+    m.off = S.off.as<int>();
+    m.crank = S.comp.as<unsigned char>();
+    m.coff = S.off.as<short>();
+    m.rel = S.rel.as<double>();
+    m.cand_w = S.cw.as<double>();
+    m.cand_e = S.ce.as<int>();
+    m.best_w = S.bw.as<unsigned long long>();
+    m.best_e = S.be.as<int>();
+    m.link = S.link.as<unsigned long long>();
+    m.nhooks = S.hooks.as<int>();
+    m.rootof = S.rootof.as<int>();
+    m.offk = S.offk.as<int>();
+    m.listB[0] = S.lb0.as<int>();
+    m.listB[1] = S.lb1.as<int>();
+    m.listR[0] = S.lr0.as<int>();
+    m.listR[1] = S.lr1.as<int>();
+    m.listL0 = S.ll0.as<int>();
+    m.cnt = S.cnt.as<int>();
+    m.maskB[0] = S.mb0.as<unsigned char>();
+    m.maskB[1] = S.mb1.as<unsigned char>();
+    m.cg_ncomp = S.cg_ncomp.as<int>();
+    m.cg_lcol = S.cg_lcol.as<unsigned>();
+    m.cg_ecnt = S.cg_ecnt.as<int>();
+    m.cg_ea = S.cg_ea.as<int>();
+    m.cg_eb = S.cg_eb.as<int>();
+    m.cg_ew = S.cg_ew.as<unsigned long long>();
+    m.cg_ec = S.cg_ec.as<int>();
+    m.cg_ed = S.cg_ed.as<int>();
     m.Hr = c->H;
     m.Wr = c->W;
     return m;
@@ -416,15 +422,16 @@ int mst_level() {
 // the rest of a map once it has found one
 // H x W: the maps' (padded) size, multiples of 64 for the tile passes; Hr x Wr: the
 // frame's own size (the reliabilities' border, MstWork::Hr / Wr).
-void unwrap_core(fcd_ctx* c, const float* w, int nmaps, int H, int W, int Hr, int Wr, int32_t* k, int* res_host,
-                 hipStream_t s, bool all_mst, fcdk::MstK* mk, bool any_res) {
+void unwrap_core(fcd_ctx* c, MstSpace& S, const float* w, int nmaps, int H, int W, int Hr, int Wr, int32_t* k,
+                 int* res_host, hipStream_t s, bool all_mst, fcdk::MstK* mk, bool any_res) {
     if (mk) mk->map_slot = nullptr;
     const long hw = (long)H * W;
     std::vector<int> active;
     if (all_mst) {
         for (int i = 0; i < nmaps; ++i) active.push_back(i);
     } else {
-        int* res = c->rescnt.as<int>();
+        S.rescnt.ensure((size_t)nmaps * sizeof(int));
+        int* res = S.rescnt.as<int>();
         fcdk::residues(w, nmaps, H, W, res, s, any_res);
         std::vector<int> counts(nmaps);
         HIPCHK(hipMemcpyAsync(counts.data(), res, sizeof(int) * nmaps, hipMemcpyDeviceToHost, s));
@@ -435,14 +442,17 @@ void unwrap_core(fcd_ctx* c, const float* w, int nmaps, int H, int W, int Hr, in
     }
     // the scan unwrap for the residue-free maps (the MST pass overwrites the others);
     // skipped when every map has residues (the fix-up groups of camera frames)
-    if ((int)active.size() < nmaps) fcdk::unwrap_scan(w, nmaps, H, W, c->colk.as<int>(), k, s);
+    if ((int)active.size() < nmaps) {
+        S.colk.ensure((size_t)nmaps * H * sizeof(int));
+        fcdk::unwrap_scan(w, nmaps, H, W, S.colk.as<int>(), k, s);
+    }
     if (active.empty()) return;
-    ensure_mst(c, (int)active.size(), hw);
-    fcdk::MstWork m = mst_work(c);
+    ensure_mst(c, S, (int)active.size(), hw);
+    fcdk::MstWork m = mst_work(c, S);
     m.Hr = Hr;
     m.Wr = Wr;
     const int nact = (int)active.size();
-    upload(c->mst_ids.p, active.data(), sizeof(int) * nact, s);
+    upload(S.ids.p, active.data(), sizeof(int) * nact, s);
     const int max_rounds = 64;
     int rounds = 0;
     // Boruvka halves the component count every round; check convergence every
@@ -452,7 +462,7 @@ void unwrap_core(fcd_ctx* c, const float* w, int nmaps, int H, int W, int Hr, in
     const int tile_w = fcdk::mst_tile_shape(H, W, &tile_h);
     if (level == 3 && tile_w > 0) {
         HIPCHK(hipMemsetAsync(m.nhooks + 1, 0, (1 + fcdk::kCgRounds) * sizeof(int), s));
-        fcdk::mst_tile_level0(w, c->mst_ids.as<int>(), nact, H, W, m, s, true);
+        fcdk::mst_tile_level0(w, S.ids.as<int>(), nact, H, W, m, s, true);
         bool fits = true;
 #ifdef FCD_DIAGNOSTIC
         static const bool cg_dbg = std::getenv("FCD_MST_DEBUG") != nullptr;  // (diagnostic builds only)
@@ -501,12 +511,12 @@ void unwrap_core(fcd_ctx* c, const float* w, int nmaps, int H, int W, int Hr, in
             if (mk) {
                 std::vector<int> slot(nmaps, -1);
                 for (int i = 0; i < nact; ++i) slot[active[i]] = i;
-                c->mst_slot.ensure(slot.size() * sizeof(int));
-                upload(c->mst_slot.p, slot.data(), slot.size() * sizeof(int), s);
-                *mk = fcdk::MstK{m.crank, m.coff, m.offk, c->mst_slot.as<int>(), fcdk::mst_cg_geom(H, W)};
+                S.slot.ensure(slot.size() * sizeof(int));
+                upload(S.slot.p, slot.data(), slot.size() * sizeof(int), s);
+                *mk = fcdk::MstK{m.crank, m.coff, m.offk, S.slot.as<int>(), fcdk::mst_cg_geom(H, W)};
                 return;
             }
-            fcdk::mst_cg_finalize(c->mst_ids.as<int>(), nact, H, W, m, k, s);
+            fcdk::mst_cg_finalize(S.ids.as<int>(), nact, H, W, m, k, s);
             return;
         }
         level = 2;  // the boundary-list rounds need no capacity bound
@@ -515,11 +525,11 @@ void unwrap_core(fcd_ctx* c, const float* w, int nmaps, int H, int W, int Hr, in
     if (level >= 1) {
         if (level >= 2 && tile_w > 0) {
             // level-0 components from Boruvka inside 32 x 32 tiles (LDS)
-            fcdk::mst_tile_level0(w, c->mst_ids.as<int>(), nact, H, W, m, s);
+            fcdk::mst_tile_level0(w, S.ids.as<int>(), nact, H, W, m, s);
         } else {
             // one pixel round
-            fcdk::mst_init(w, c->mst_ids.as<int>(), nact, H, W, m, s);
-            fcdk::mst_round(w, c->mst_ids.as<int>(), nact, H, W, m, s, true);
+            fcdk::mst_init(w, S.ids.as<int>(), nact, H, W, m, s);
+            fcdk::mst_round(w, S.ids.as<int>(), nact, H, W, m, s, true);
         }
         // then rounds over the boundary / root lists only
         fcdk::mst_level_setup(nact, H, W, m, s);
@@ -542,7 +552,7 @@ void unwrap_core(fcd_ctx* c, const float* w, int nmaps, int H, int W, int Hr, in
         for (; rounds < max_rounds; rounds += 3) {
             for (int g = 0; g < 3; ++g) {
                 if (dbg) dump(rounds + g);
-                fcdk::mst_level_round(w, c->mst_ids.as<int>(), nact, H, W, m, rounds + g, s);
+                fcdk::mst_level_round(w, S.ids.as<int>(), nact, H, W, m, rounds + g, s);
             }
             int hooks = 0;
             HIPCHK(hipMemcpyAsync(&hooks, m.nhooks, sizeof(int), hipMemcpyDeviceToHost, s));
@@ -550,20 +560,20 @@ void unwrap_core(fcd_ctx* c, const float* w, int nmaps, int H, int W, int Hr, in
             if (hooks == 0) break;
         }
         if (rounds >= max_rounds) throw FcdError(FCD_E_INTERNAL, "unwrap: Boruvka did not converge");
-        fcdk::mst_level_finalize(c->mst_ids.as<int>(), nact, H, W, m, k, s);
+        fcdk::mst_level_finalize(S.ids.as<int>(), nact, H, W, m, k, s);
         return;
     }
-    fcdk::mst_init(w, c->mst_ids.as<int>(), nact, H, W, m, s);
+    fcdk::mst_init(w, S.ids.as<int>(), nact, H, W, m, s);
     for (; rounds < max_rounds; rounds += 3) {
         for (int g = 0; g < 3; ++g)
-            fcdk::mst_round(w, c->mst_ids.as<int>(), nact, H, W, m, s, rounds + g == 0);
+            fcdk::mst_round(w, S.ids.as<int>(), nact, H, W, m, s, rounds + g == 0);
         int hooks = 0;
         HIPCHK(hipMemcpyAsync(&hooks, m.nhooks, sizeof(int), hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
         if (hooks == 0) break;
     }
     if (rounds == max_rounds) throw FcdError(FCD_E_INTERNAL, "unwrap: Boruvka did not converge");
-    fcdk::mst_finalize(c->mst_ids.as<int>(), nact, H, W, m, k, s);
+    fcdk::mst_finalize(S.ids.as<int>(), nact, H, W, m, k, s);
 }
 
 // k-fields of nmaps wrapped maps of the context's frame size (unwrap_core).  A frame whose
@@ -572,10 +582,11 @@ void unwrap_core(fcd_ctx* c, const float* w, int nmaps, int H, int W, int Hr, in
 // by replicating their last row and column (kernels_unwrap.hip pad_maps: same residues,
 // same k on the frame's pixels).
 void unwrap_maps(fcd_ctx* c, const float* w, int nmaps, int32_t* k, int* res_host, hipStream_t s,
-                 bool all_mst = false, fcdk::MstK* mk = nullptr, bool any_res = false) {
+                 bool all_mst = false, fcdk::MstK* mk = nullptr, bool any_res = false, int space = 0) {
     const int H = c->H, W = c->W;
+    MstSpace& S = c->ms[space];
     if (H % 64 == 0 && W % 64 == 0) {
-        unwrap_core(c, w, nmaps, H, W, H, W, k, res_host, s, all_mst, mk, any_res);
+        unwrap_core(c, S, w, nmaps, H, W, H, W, k, res_host, s, all_mst, mk, any_res);
         return;
     }
     if (mk) mk->map_slot = nullptr;
@@ -583,7 +594,8 @@ void unwrap_maps(fcd_ctx* c, const float* w, int nmaps, int32_t* k, int* res_hos
     if (all_mst) {
         for (int i = 0; i < nmaps; ++i) active.push_back(i);
     } else {
-        int* res = c->rescnt.as<int>();
+        S.rescnt.ensure((size_t)nmaps * sizeof(int));
+        int* res = S.rescnt.as<int>();
         fcdk::residues(w, nmaps, H, W, res, s, any_res);
         std::vector<int> counts(nmaps);
         HIPCHK(hipMemcpyAsync(counts.data(), res, sizeof(int) * nmaps, hipMemcpyDeviceToHost, s));
@@ -592,21 +604,21 @@ void unwrap_maps(fcd_ctx* c, const float* w, int nmaps, int32_t* k, int* res_hos
         for (int i = 0; i < nmaps; ++i)
             if (counts[i] > 0) active.push_back(i);
         if ((int)active.size() < nmaps) {
-            c->colk.ensure((size_t)nmaps * H * sizeof(int));
-            fcdk::unwrap_scan(w, nmaps, H, W, c->colk.as<int>(), k, s);
+            S.colk.ensure((size_t)nmaps * H * sizeof(int));
+            fcdk::unwrap_scan(w, nmaps, H, W, S.colk.as<int>(), k, s);
         }
     }
     if (active.empty()) return;
     const int nact = (int)active.size();
     const int Hp = (H + 63) / 64 * 64, Wp = (W + 63) / 64 * 64;
     const size_t np = (size_t)nact * Hp * Wp;
-    c->pad_w.ensure(np * sizeof(float));
-    c->pad_k.ensure(np * sizeof(int32_t));
-    c->pad_ids.ensure((size_t)nact * sizeof(int));
-    upload(c->pad_ids.p, active.data(), (size_t)nact * sizeof(int), s);
-    fcdk::pad_maps(w, nact, H, W, Hp, Wp, c->pad_w.as<float>(), s, c->pad_ids.as<int>());
-    unwrap_core(c, c->pad_w.as<float>(), nact, Hp, Wp, H, W, c->pad_k.as<int32_t>(), nullptr, s, true, nullptr, false);
-    fcdk::unpad_k(c->pad_k.as<int32_t>(), nact, Hp, Wp, H, W, k, s, c->pad_ids.as<int>());
+    S.pad_w.ensure(np * sizeof(float));
+    S.pad_k.ensure(np * sizeof(int32_t));
+    S.pad_ids.ensure((size_t)nact * sizeof(int));
+    upload(S.pad_ids.p, active.data(), (size_t)nact * sizeof(int), s);
+    fcdk::pad_maps(w, nact, H, W, Hp, Wp, S.pad_w.as<float>(), s, S.pad_ids.as<int>());
+    unwrap_core(c, S, S.pad_w.as<float>(), nact, Hp, Wp, H, W, S.pad_k.as<int32_t>(), nullptr, s, true, nullptr, false);
+    fcdk::unpad_k(S.pad_k.as<int32_t>(), nact, Hp, Wp, H, W, k, s, S.pad_ids.as<int>());
     HIPCHK(hipStreamSynchronize(s));  // (active, the ids' host copy, dies here)
 }
 
@@ -915,7 +927,7 @@ void build_demod_tables(fcd_ctx* c, hipStream_t s) {
     if (c->fused_ok) c->seam.ensure(nb * (size_t)(H / fcdk::phase_rows_tile(W)) * 2 * W * sizeof(float2));
     c->ir_seam.ensure(2 * fcdk::int_rows_seam_bytes(W, H, (int)nb));
     c->rescnt.ensure(std::max(nb, (size_t)c->chunk) * 2 * sizeof(int));
-    c->mst_cap = 0;  // re-size the MST workspace for the new chunk on next use
+    c->ms[0].cap = c->ms[1].cap = 0;  // re-size the MST workspaces for the new chunk on next use
 }
 
 fcdk::DemodTables demod_tables(fcd_ctx* c) {
@@ -1758,16 +1770,60 @@ int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int f
                 stage_frames(c, frames, format, dev, idx.data(), nb, s);
                 fr = c->frames_in.as<float>();
             }
-            fast_demod(c, fr, nb, s);
             int32_t* kf = dev && k_out ? k_out + (size_t)f0 * 2 * hw : c->fk.as<int32_t>();
             counts.assign((size_t)2 * nb, 0);
-            fcdk::MstK mk{};
-            unwrap_maps(c, c->wrapped.as<float>(), 2 * nb, kf, counts.data(), s, false, k_out ? nullptr : &mk, true);
-            fcdk::int_rows(c->W, mk.map_slot ? 3 : 2, c->wrapped.as<float>(), nullptr, kf, nullptr, nullptr, c->H, nb,
-                           c->Zt.as<float2>(), c->twp_row.as<float2>(), nullptr, s, mk.map_slot ? &mk : nullptr);
-            fcdk::int_cols(c->H, c->Zt.as<float2>(), c->W, nb, coef, c->Ht.as<float2>(), ic_tw(c), s);
             float* hdst = dev && height_out ? height_out + (size_t)f0 * hw : c->out_h.as<float>();
-            fcdk::int_c2r(c->W, c->Ht.as<float2>(), c->H, nb, hdst, c->twp_row.as<float2>(), s);
+            // frames fo .. fo + n - 1 of the chunk: demod, unwrap (census, scan / MST in MST
+            // workspace h), integration, all on stream hs
+            auto half = [&](int h, int fo, int n, hipStream_t hs) {
+                float* wr = c->wrapped.as<float>() + (size_t)fo * 2 * hw;
+                int32_t* kh = kf + (size_t)fo * 2 * hw;
+                float2* Zt = c->Zt.as<float2>() + (size_t)fo * hw;
+                float2* Ht = c->Ht.as<float2>() + (size_t)fo * c->H * (c->W / 2 + 1);
+                fast_demod(c, fr + (size_t)fo * hw, n, hs, fo);
+                fcdk::MstK mk{};
+                unwrap_maps(c, wr, 2 * n, kh, counts.data() + 2 * (size_t)fo, hs, false, k_out ? nullptr : &mk, true, h);
+                fcdk::int_rows(c->W, mk.map_slot ? 3 : 2, wr, nullptr, kh, nullptr, nullptr, c->H, n, Zt,
+                               c->twp_row.as<float2>(), nullptr, hs, mk.map_slot ? &mk : nullptr);
+                fcdk::int_cols(c->H, Zt, c->W, n, coef, Ht, ic_tw(c), hs);
+                fcdk::int_c2r(c->W, Ht, c->H, n, hdst + (size_t)fo * hw, c->twp_row.as<float2>(), hs);
+            };
+            if (c->nstreams < 2 || nb < 8) {
+                half(0, 0, nb, s);
+            } else {
+                // Two halves side by side, each driven by its own host thread on its own stream
+                // and MST workspace: one half's census read-back, graph-round convergence checks
+                // and small graph-round kernels overlap the other half's kernels, instead of
+                // leaving the chip idle (the camera frames' exact chain, r04ap trace).
+                const int nb0 = (nb + 1) / 2;
+                if (!c->aux) {
+                    HIPCHK(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
+                    HIPCHK(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+                    HIPCHK(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
+                }
+                HIPCHK(hipEventRecord(c->ev_fork, s));
+                HIPCHK(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
+                std::exception_ptr err1;
+                std::thread t1([&] {
+                    try {
+                        HIPCHK(hipSetDevice(c->device));
+                        half(1, nb0, nb - nb0, c->aux);
+                    } catch (...) {
+                        err1 = std::current_exception();
+                    }
+                });
+                std::exception_ptr err0;
+                try {
+                    half(0, 0, nb0, s);
+                } catch (...) {
+                    err0 = std::current_exception();
+                }
+                t1.join();
+                HIPCHK(hipEventRecord(c->ev_join, c->aux));
+                HIPCHK(hipStreamWaitEvent(s, c->ev_join, 0));
+                if (err0) std::rethrow_exception(err0);
+                if (err1) std::rethrow_exception(err1);
+            }
             // The chunk's residue-free frames get the first pass's heights, as when this call
             // had not followed a residue-heavy one: a frame's heights never depend on what
             // earlier calls held (the reference is a pure function of its inputs, fcd.py:13-35).
