@@ -142,11 +142,45 @@ def test_anyshape_raw_formats(anyshape, golden):
     eng.close()
 
 
-def test_unsupported_shapes_raise():
-    """Sides below 16 or above 8192, and sides above 4096 with a prime factor above 61
-    (Bluestein's convolution would exceed the row's LDS), stay refused (FCD_E_UNSUPPORTED)."""
+@pytest.mark.parametrize("shape", [(4099, 96), (96, 8200), (64, 16384)])
+def test_long_sides_match_oracle(shape):
+    """Sides the rows' LDS cannot hold (kernels_mr.hip global-scratch rows): 4099 (prime:
+    Bluestein with M = 16384, the columns through the transpose route), 8200 (2^3 5^2 41:
+    a generic radix-41 pass over 8200-point rows), 16384 (2^14).  Setup bit-exact against
+    the oracle's restatement of the reference's spectrum, heights rel-L2 1e-5 against the
+    oracle (fcd.compute_height_map with the unwrap), the k-fields of the maps equal to the
+    oracle's on the engine's phases (up to the constant)."""
+    from bench_data import make_residue_frame
+    from oracle import fcd_oracle as O
     from pyfcd import _lib
-    for shape in ((8, 64), (64, 8200), (4099, 64)):
+    rows, cols = shape
+    pairs = [(rows // 2 + 0.5, min(cols // 3, 40) + 0.25)]
+    ref, frame = make_residue_frame(rows, pairs, seed=3, rotate_deg=5.0, quantum=4096, cols=cols)
+    eng = _lib.Engine(shape)
+    info = eng.set_reference(ref, 0.001)
+    (cars, cf) = O.compute_carriers(ref, 0.001)
+    assert info.calibration_factor == cf
+    got = sorted(tuple(info.peaks[i]) for i in range(2))
+    want = sorted(tuple(int(v) for v in c.pixels) for c in cars)
+    assert got == want, (got, want)
+    h, w, k = eng.process(frame[None], 1.0, unwrap=True, want_phases=True)
+    hf, _, _ = eng.process(frame[None], 1.0, unwrap=True, want_phases=False)
+    assert np.array_equal(h, hf)
+    ho, _, _, ex = O.compute_height_map(ref, frame, 0.001, height=1.0)
+    assert rel_l2(h[0], ho) < 1e-5, rel_l2(h[0], ho)
+    for m in range(2):
+        assert wrap_diff(w[0][m], ex["wrapped"][m]).max() < 2e-4
+        _, ko = O.unwrap(w[0][m])
+        d = k[0][m].astype(np.int64) - ko
+        assert np.all(d == d.flat[0]), m
+    eng.close()
+
+
+def test_unsupported_shapes_raise():
+    """Sides below 16 or above 16384 stay refused (FCD_E_UNSUPPORTED): the MST's 32-bit
+    vertex ids bound a batch's pixels."""
+    from pyfcd import _lib
+    for shape in ((8, 64), (64, 16400), (16385, 64)):
         with pytest.raises(_lib.FcdError) as e:
             _lib.Engine(shape)
         assert e.value.code == _lib.FCD_E_UNSUPPORTED

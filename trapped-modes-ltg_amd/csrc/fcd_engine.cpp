@@ -208,6 +208,7 @@ struct fcd_ctx {
     fcdk::MrPlan mr_row{}, mr_col{};
     DevBuf mr_scratch;  // the mixed-radix column transforms' transposed copy (chunk frames)
     DevBuf gb_tables;   // generic chain's band columns (build_demod_tables)
+    DevBuf gk_flag;     // generic chain: per map of a chunk, 1 if its k-field came from the MST
     int gb_NU = 0;      // columns in either carrier's disk
     hipStream_t own = nullptr;
     DevBuf tw_row, tw_col;        // plain tables exp(-2 pi i m / n) (generic LDS FFT kernels)
@@ -423,7 +424,7 @@ int mst_level() {
 // H x W: the maps' (padded) size, multiples of 64 for the tile passes; Hr x Wr: the
 // frame's own size (the reliabilities' border, MstWork::Hr / Wr).
 void unwrap_core(fcd_ctx* c, MstSpace& S, const float* w, int nmaps, int H, int W, int Hr, int Wr, int32_t* k,
-                 int* res_host, hipStream_t s, bool all_mst, fcdk::MstK* mk, bool any_res) {
+                 int* res_host, hipStream_t s, bool all_mst, fcdk::MstK* mk, bool any_res, bool colk_only = false) {
     if (mk) mk->map_slot = nullptr;
     const long hw = (long)H * W;
     std::vector<int> active;
@@ -444,7 +445,8 @@ void unwrap_core(fcd_ctx* c, MstSpace& S, const float* w, int nmaps, int H, int 
     // skipped when every map has residues (the fix-up groups of camera frames)
     if ((int)active.size() < nmaps) {
         S.colk.ensure((size_t)nmaps * H * sizeof(int));
-        fcdk::unwrap_scan(w, nmaps, H, W, S.colk.as<int>(), k, s);
+        if (colk_only) fcdk::unwrap_colk(w, nmaps, H, W, S.colk.as<int>(), s);
+        else fcdk::unwrap_scan(w, nmaps, H, W, S.colk.as<int>(), k, s);
     }
     if (active.empty()) return;
     ensure_mst(c, S, (int)active.size(), hw);
@@ -581,12 +583,15 @@ void unwrap_core(fcd_ctx* c, MstSpace& S, const float* w, int nmaps, int H, int 
 // run on the maps themselves; the maps with residues go to the MST tiles in copies padded
 // by replicating their last row and column (kernels_unwrap.hip pad_maps: same residues,
 // same k on the frame's pixels).
+// colk_only: the residue-free maps get only their column-0 offsets (ms[space].colk), no
+// k-field: the generic chain's z rows scan them themselves (PhaseOut::kflag).
 void unwrap_maps(fcd_ctx* c, const float* w, int nmaps, int32_t* k, int* res_host, hipStream_t s,
-                 bool all_mst = false, fcdk::MstK* mk = nullptr, bool any_res = false, int space = 0) {
+                 bool all_mst = false, fcdk::MstK* mk = nullptr, bool any_res = false, int space = 0,
+                 bool colk_only = false) {
     const int H = c->H, W = c->W;
     MstSpace& S = c->ms[space];
     if (H % 64 == 0 && W % 64 == 0) {
-        unwrap_core(c, S, w, nmaps, H, W, H, W, k, res_host, s, all_mst, mk, any_res);
+        unwrap_core(c, S, w, nmaps, H, W, H, W, k, res_host, s, all_mst, mk, any_res, colk_only);
         return;
     }
     if (mk) mk->map_slot = nullptr;
@@ -605,7 +610,8 @@ void unwrap_maps(fcd_ctx* c, const float* w, int nmaps, int32_t* k, int* res_hos
             if (counts[i] > 0) active.push_back(i);
         if ((int)active.size() < nmaps) {
             S.colk.ensure((size_t)nmaps * H * sizeof(int));
-            fcdk::unwrap_scan(w, nmaps, H, W, S.colk.as<int>(), k, s);
+            if (colk_only) fcdk::unwrap_colk(w, nmaps, H, W, S.colk.as<int>(), s);
+            else fcdk::unwrap_scan(w, nmaps, H, W, S.colk.as<int>(), k, s);
         }
     }
     if (active.empty()) return;
@@ -713,12 +719,15 @@ void generic_demod_t(fcd_ctx* c, const float2* specT, int nb, float* wrapped, hi
 }
 
 // z of the maps (w + 2 pi k, make_z's arithmetic) built in the row transform's load
+// kflag / colk (nullable, device): per map, its k-field in kf (MST) or its scan in the z rows
 void generic_integrate_t(fcd_ctx* c, int nb, const float* w, const int32_t* kf, const fcdk::IntegCoef& k, float* h_out,
-                         hipStream_t s) {
+                         hipStream_t s, const int* kflag = nullptr, const int* colk = nullptr) {
     float2* Z = c->spec.as<float2>();
     const float2* twc = c->tw_col.as<float2>();
     fcdk::PhaseOut zin{};
     zin.kin = kf;
+    zin.kflag = kflag;
+    zin.colk = colk;
     fcdk::mr_rows(c->mr_row, false, fcdk::ROW_IN_Z, fcdk::ROW_OUT_COMPLEX, w, Z, (long)nb * c->H, c->H, 0.f,
                   c->tw_row.as<float2>(), &zin, s);
     if (fcdk::mr_int_cols_supported(c->mr_col)) {  // the column pairs in place
@@ -1176,9 +1185,8 @@ FCD_API int fcd_create(int device, int rows, int cols, fcd_ctx** out) {
         *out = nullptr;
         const bool pow2 = fcdk::fft_size_supported(rows) && fcdk::fft_size_supported(cols);
         if (!pow2 && !(rows >= kMinSide && cols >= kMinSide && fcdk::mr_supported(rows) && fcdk::mr_supported(cols)))
-            throw FcdError(FCD_E_UNSUPPORTED, "frame sides must be in [" + std::to_string(kMinSide) +
-                                                  ", 8192] (at most 4096 for a side with a prime factor above " +
-                                                  std::to_string(fcdk::kMrMaxRadix) + "), got " + std::to_string(rows) +
+            throw FcdError(FCD_E_UNSUPPORTED, "frame sides must be in [" + std::to_string(kMinSide) + ", " +
+                                                  std::to_string(fcdk::kMrMaxLen) + "], got " + std::to_string(rows) +
                                                   "x" + std::to_string(cols));
         int ndev = 0;
         HIPCHK(hipGetDeviceCount(&ndev));
@@ -1645,11 +1653,26 @@ int process_generic(fcd_ctx* c, const void* frames, int format, int n_frames, bo
         generic_demod_t(c, specT, nb, w, s);
         if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
         int32_t* k = nullptr;
+        const int* kflag = nullptr;
+        std::vector<int> flags;
         if (unwrap) {
             std::vector<int> counts(2 * (size_t)nb);
             k = c->kbuf.as<int32_t>();
             const auto tu = std::chrono::steady_clock::now();
-            unwrap_maps(c, w, 2 * nb, k, counts.data(), s, false, nullptr, true);
+            // heights only: the residue-free maps' scan runs in the z rows (no k-field pass)
+            const bool zscan = k_out == nullptr;
+            unwrap_maps(c, w, 2 * nb, k, counts.data(), s, false, nullptr, true, 0, zscan);
+            if (zscan) {
+                flags.resize(2 * (size_t)nb);
+                for (size_t m = 0; m < flags.size(); ++m) flags[m] = counts[m] > 0;
+                // (the scanned maps' column-0 offsets were computed iff some map is residue-free)
+                bool any_scan = false;
+                for (int f : flags) any_scan |= f == 0;
+                if (any_scan && !c->ms[0].colk.p) throw FcdError(FCD_E_INTERNAL, "column offsets missing");
+                c->gk_flag.ensure(flags.size() * sizeof(int));
+                upload(c->gk_flag.p, flags.data(), flags.size() * sizeof(int), s);
+                kflag = c->gk_flag.as<int>();
+            }
             if (c->profiling) {  // the unwrap span (it synchronises), counted as the exact pass's time
                 HIPCHK(hipStreamSynchronize(s));
                 unwrap_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tu).count();
@@ -1658,7 +1681,7 @@ int process_generic(fcd_ctx* c, const void* frames, int format, int n_frames, bo
         }
         if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
         float* hdst = dev && height_out ? height_out + (size_t)f0 * hw : c->out_h.as<float>();
-        generic_integrate_t(c, nb, w, k, coef, hdst, s);
+        generic_integrate_t(c, nb, w, k, coef, hdst, s, kflag, kflag ? c->ms[0].colk.as<int>() : nullptr);
         if (c->profiling) {
             HIPCHK(hipEventRecord(c->next_event(), s));
             c->prof_frames += nb;

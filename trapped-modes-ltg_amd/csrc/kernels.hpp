@@ -33,6 +33,11 @@ struct PhaseOut {          // ROW_OUT_PHASE: w = wrap(theta - atan2(A))
     const int32_t* kin = nullptr;  // ROW_IN_Z's k-fields
     const int* bslot = nullptr;    // ROW_IN_BAND's / ROW_OUT_BAND2's column slots [W] and their count
     int bnc = 0;
+    // ROW_IN_Z with kflag: map m takes kin where kflag[m] != 0 (its MST k-field), else its
+    // residue-free scan k(i, j) = colk[m][i] - sum_{j' < j} find_wrap(w(i, j'), w(i, j' + 1)),
+    // computed in the row's load (k_rowscan's integers)
+    const int* kflag = nullptr;
+    const int* colk = nullptr;
 };
 
 // Disk band-pass of one carrier (skimage.draw.disk raster in fftshifted
@@ -75,7 +80,11 @@ struct DemodTables {
 // (1.37x -> 1.00x the compulsory reads, int_cols + c2r 123.6 -> 107.7 us/frame), but the
 // fused wide kernel then writes 16-byte pieces of 8-tile runs: plain stores read every
 // line back (152.9 -> 202.7 us/frame), streaming ones crawl (396.9); c5 3.14k -> 2.83k /
-// 1.78k frames/s (r04q / r04r).  So 4.
+// 1.78k frames/s (r04q / r04r).  With 4 the fused kernel's 2-row tiles write half runs
+// (PMC: 2.08x the Zt bytes written).  2 (the fused tile writes whole layout tiles, one
+// contiguous 64 KB region; k_int_cols reads 16-byte runs in groups of 8 blocks on one XCD
+// taking a line's 8 columns together): fused 152.8 -> 144.6 us/frame but int_cols + c2r
+// 124.2 -> 147.3, c5 3.13k -> 2.98k frames/s (r05).  So 4.
 #ifndef FCD_ZT_4096
 #define FCD_ZT_4096 4
 #endif
@@ -145,9 +154,10 @@ void row_fft(int W, bool inverse, RowIn in_mode, RowOut out_mode, const void* in
 void col_fft(int H, int W, bool inverse, float2* data, int nbatch, const float2* tw, hipStream_t s);
 // Mixed-radix row / column transforms (kernels_mr.hip) of the generic chain for sides that
 // are not powers of two: radix 8 / 4 / 2 / 3 / 5 / 7 codelets, a generic pass for odd
-// primes <= kMrMaxRadix, Bluestein (power-of-two M) otherwise.  Sides up to 8192 (4096
-// with Bluestein).
+// primes <= kMrMaxRadix, Bluestein (power-of-two M) otherwise.  Any side in [2, kMrMaxLen]
+// (rows beyond 8192 complex in global scratch).
 constexpr int kMrMaxRadix = 61;
+constexpr int kMrMaxLen = 16384;  // longest side of the generic chain
 struct MrPlan {
     int n, nf;
     int fct[24];  // radices in pass order (of n; of M with Bluestein)

@@ -458,19 +458,21 @@ __global__ __launch_bounds__(IntColsCfg<H>::THREADS, IntColsCfg<H>::V) void k_in
     // (3.9x the compulsory Zt reads, PMC r03t4096).  There the blocks work in QUADS:
     // the 4 blocks of a group sit on one XCD (dispatch deals block b to XCD b % 8)
     // and take columns 4k, 4k + 1, 4k + 2, 4k + 3 of the same quad at the same time.
-    const bool quad = zts == 2 && TEAMS == 1 && gridDim.x % 32 == 0 && FCD_INTCOLS_QUADS;
+    // (2-row Zt tiles: a line holds 8 columns x 2 rows, groups of 8 blocks)
+    const int G = zts == 2 ? 4 : (zts == 1 ? 8 : 0);  // columns per 128-byte line
+    const bool quad = G && TEAMS == 1 && gridDim.x % (8 * G) == 0 && FCD_INTCOLS_QUADS;
     const bool xcd = !quad && gridDim.x % 8 == 0;
-    const int NQ = (NCH + 3) / 4;
-    const int CW = quad ? 4 * NQ : NCH;
+    const int NQ = G ? (NCH + G - 1) / G : 0;
+    const int CW = quad ? G * NQ : NCH;
     int c0, cstep, cend, bstride;  // first item, item step between teams, end, step between iterations
     if (quad) {
-        const int q = blockIdx.x / 8, j = q % 4;
-        const int grp = blockIdx.x % 8 + 8 * (q / 4), ngrp = gridDim.x / 4;
+        const int q = blockIdx.x / 8, j = q % G;
+        const int grp = blockIdx.x % 8 + 8 * (q / G), ngrp = gridDim.x / G;
         const int nquads = nb * NQ, perq = (nquads + ngrp - 1) / ngrp;
         const int Q0 = min(grp * perq, nquads), Q1 = min(Q0 + perq, nquads);
-        c0 = 4 * Q0 + j;
-        cstep = 4;
-        cend = 4 * Q1;
+        c0 = G * Q0 + j;
+        cstep = G;
+        cend = G * Q1;
         bstride = TEAMS * cstep;
     } else if (xcd) {
         const int bpx = gridDim.x / 8;                      // blocks per XCD
@@ -795,7 +797,7 @@ static void launch_int_cols(const float2* Zt, int W, int nb, const IntegCoef& c,
     set_lds(k_int_cols<H>, lds);
     const int grid = grid_for(((long)nb * (W / 2 + 1) + C::TEAMS - 1) / C::TEAMS, 4);
     const int zt = zt_layout(W);
-    const int zts = zt == 16 ? 4 : (zt == 8 ? 3 : 2);
+    const int zts = zt == 16 ? 4 : (zt == 8 ? 3 : (zt == 4 ? 2 : 1));
     hipLaunchKernelGGL(k_int_cols<H>, dim3(grid), dim3(C::THREADS), lds, s, Zt, W, nb, c, Ht, tw, zts, colk);
     FCD_CHECK_LAUNCH();
 }

@@ -13,24 +13,32 @@
 //    terms), each pass reading one LDS buffer and writing the other; twiddles exp(-+2 pi
 //    i m / n) from the context's table (computed in f64 on the host);
 //  * n with a prime factor above 61 (1021, 2039, 4093 ...): Bluestein's identity, the
-//    length-n DFT as a circular convolution of length M = 2^ceil(log2(2n - 1)) <= 8192:
-//    a chirp c[m] = exp(-i pi (m^2 mod 2n) / n) premultiply, a radix-8/4/2 FFT of length
-//    M, a multiply by the precomputed FFT of the conjugate chirp (1/M folded in), the
-//    inverse FFT, the chirp postmultiply, all in the row's LDS (2 M complex).
+//    length-n DFT as a circular convolution of length M = 2^ceil(log2(2n - 1)): a chirp
+//    c[m] = exp(-i pi (m^2 mod 2n) / n) premultiply, a radix-8/4/2 FFT of length M, a
+//    multiply by the precomputed FFT of the conjugate chirp (1/M folded in), the inverse
+//    FFT, the chirp postmultiply.
 //
-// Columns go through a tiled transpose, the row transform of length H, and the transpose
-// back.  These are the generic-chain transforms, not the band-pruned register FFTs of
-// the power-of-two fast path.  Sides up to 8192 (4096 with Bluestein): a row's two
-// buffers fill at most 128 KB of the 160 KB LDS.
+// A row's two buffers sit in LDS up to 8192 complex (128 KB); longer rows (sides above
+// 8192, Bluestein's M above 8192) run the same passes in global scratch (L2 / MALL
+// resident, a launch of at most kMrLongRows rows).  Sides up to kMrMaxLen = 16384.
+//
+// Columns: the spectral integration's column stage in place in LDS (k_mr_int_cols, no
+// transposes), the demodulation's band columns and long columns through a tiled
+// transpose, the row transform of length H and the transpose back.  These are the
+// generic-chain transforms, not the band-pruned register FFTs of the power-of-two fast
+// path.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <complex>
+#include <map>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
 
 #include "fft_lds.hpp"
+#include "gfft.hpp"
 #include "kernels.hpp"
 
 namespace fcdk {
@@ -199,20 +207,83 @@ __device__ __forceinline__ float2* mr_run(float2* b0, float2* b1, int len, const
     return b0;
 }
 
+// find_wrap of the reference unwrapper (exact in f64, kernels_unwrap.hip)
+__device__ __forceinline__ int mr_find_wrap(float a, float b) {
+    const double d = (double)a - (double)b;
+    return d > 3.141592653589793 ? -1 : (d < -3.141592653589793 ? 1 : 0);
+}
+
+// ROW_IN_Z with per-map k sources (PhaseOut::kflag): the row pair staged in b1, each
+// thread's contiguous run of edges summed, a block-wide exclusive scan of the two maps'
+// run sums, then each run walked again: k(j) = colk(i) + sum_{j' < j} -find_wrap(w(j'),
+// w(j' + 1)) -- the integers of k_colk / k_rowscan -- for a residue-free map, kin for a map
+// the MST unwrapped; z(j) = (w0 + 2 pi k0) + i (w1 + 2 pi k1) (k_make_z) into b0.
+template <bool INV>
+__device__ __noinline__ void mr_load_z_scan(const float* in, long row, int H, int n, const MrPlan& p,
+                                            const float2* __restrict__ tw, const PhaseOut& ph, float2* b0, float2* b1) {
+    __shared__ int scn[2][MR_THREADS];
+    const long b = row / H, r = row % H;
+    const long o0 = ((2 * b) * H + r) * n, o1 = ((2 * b + 1) * H + r) * n;
+    const bool mst0 = ph.kflag[2 * b] != 0, mst1 = ph.kflag[2 * b + 1] != 0;
+    for (int i = threadIdx.x; i < n; i += MR_THREADS) b1[i] = make_float2(in[o0 + i], in[o1 + i]);
+    __syncthreads();
+    const int per = (n + MR_THREADS - 1) / MR_THREADS;
+    const int j0 = min((int)threadIdx.x * per, n), j1 = min(j0 + per, n);
+    int s0 = 0, s1 = 0;
+    for (int j = j0; j < j1 && j + 1 < n; ++j) {
+        const float2 a = b1[j], c = b1[j + 1];
+        s0 -= mr_find_wrap(a.x, c.x);
+        s1 -= mr_find_wrap(a.y, c.y);
+    }
+    scn[0][threadIdx.x] = s0;
+    scn[1][threadIdx.x] = s1;
+    __syncthreads();
+    for (int off = 1; off < MR_THREADS; off <<= 1) {  // inclusive Hillis-Steele scan
+        const int t0 = threadIdx.x >= off ? scn[0][threadIdx.x - off] : 0;
+        const int t1 = threadIdx.x >= off ? scn[1][threadIdx.x - off] : 0;
+        __syncthreads();
+        scn[0][threadIdx.x] += t0;
+        scn[1][threadIdx.x] += t1;
+        __syncthreads();
+    }
+    // (colk is read for the scanned maps only: with every map of a chunk unwrapped by the
+    // MST the caller computes no column offsets)
+    int k0 = (mst0 ? 0 : ph.colk[2 * b * H + r]) + scn[0][threadIdx.x] - s0;
+    int k1 = (mst1 ? 0 : ph.colk[(2 * b + 1) * H + r]) + scn[1][threadIdx.x] - s1;
+    for (int j = j0; j < j1; ++j) {
+        const float2 a = b1[j];
+        const int kk0 = mst0 ? ph.kin[o0 + j] : k0, kk1 = mst1 ? ph.kin[o1 + j] : k1;
+        float2 v = make_float2((float)((double)a.x + 6.283185307179586 * (double)kk0),
+                               (float)((double)a.y + 6.283185307179586 * (double)kk1));
+        if (p.blue) v = cmul_dir<INV>(v, tw[p.tc + j]);
+        b0[j] = v;
+        if (j + 1 < n) {
+            const float2 c = b1[j + 1];
+            k0 -= mr_find_wrap(a.x, c.x);
+            k1 -= mr_find_wrap(a.y, c.y);
+        }
+    }
+    // (the caller's barrier after the zero padding orders these writes before the passes)
+}
+
+// gs (null: LDS): rows longer than the LDS holds run their passes in global scratch, the
+// block's 2 len complex at gs + blockIdx.x * 2 len (the L2 / MALL-resident working set of a
+// launch of at most kMrLongRows rows); blk0: the launch's first block (row batches).
 template <bool INV, int IN, int OUT>
 __global__ __launch_bounds__(MR_THREADS) void k_mr_rows(const void* __restrict__ in, void* __restrict__ out, long nrows,
                                                         int H, float sub, MrPlan p, const float2* __restrict__ tw,
-                                                        PhaseOut ph) {
+                                                        PhaseOut ph, float2* __restrict__ gs, long blk0) {
     extern __shared__ __attribute__((aligned(16))) float2 mr_lds[];
     const int n = p.n, len = p.blue ? p.M : n;
     constexpr bool PAIR = IN == ROW_IN_REAL2 || IN == ROW_IN_COMPLEX2;
     // pairs never straddle two frames (a batch gives every frame the single-frame call's
     // bits): with H odd each frame's last row transforms alone
     const long hp = (H + 1) / 2;
-    const long row = PAIR ? (long)(blockIdx.x / hp) * H + 2 * (long)(blockIdx.x % hp) : (long)blockIdx.x;
-    const bool second = PAIR && 2 * (long)(blockIdx.x % hp) + 1 < H;
-    float2* b0 = mr_lds;
-    float2* b1 = mr_lds + len;
+    const long blk = blk0 + blockIdx.x;
+    const long row = PAIR ? (blk / hp) * H + 2 * (blk % hp) : blk;
+    const bool second = PAIR && 2 * (blk % hp) + 1 < H;
+    float2* b0 = gs ? gs + (size_t)blockIdx.x * 2 * len : mr_lds;
+    float2* b1 = b0 + len;
     for (int i = threadIdx.x; i < n; i += MR_THREADS) {
         float2 v;
         if constexpr (IN == ROW_IN_REAL2) {
@@ -226,6 +297,7 @@ __global__ __launch_bounds__(MR_THREADS) void k_mr_rows(const void* __restrict__
         } else if constexpr (IN == ROW_IN_REAL) {
             v = make_float2(static_cast<const float*>(in)[row * n + i] - sub, 0.f);
         } else if constexpr (IN == ROW_IN_Z) {  // k_make_z's arithmetic
+            if (ph.kflag) break;  // (the scan form below)
             const long b = row / H, r = row % H;
             const long i0 = ((2 * b) * H + r) * n + i, i1 = ((2 * b + 1) * H + r) * n + i;
             float p0 = static_cast<const float*>(in)[i0], p1 = static_cast<const float*>(in)[i1];
@@ -243,6 +315,9 @@ __global__ __launch_bounds__(MR_THREADS) void k_mr_rows(const void* __restrict__
         }
         if (p.blue) v = cmul_dir<INV>(v, tw[p.tc + i]);  // Bluestein: the chirp premultiply
         b0[i] = v;
+    }
+    if constexpr (IN == ROW_IN_Z) {
+        if (ph.kflag) mr_load_z_scan<INV>(static_cast<const float*>(in), row, H, n, p, tw, ph, b0, b1);
     }
     if constexpr (IN == ROW_IN_COMPLEX2) {
         // Re(ifft(A)) + i Re(ifft(B)) = ifft(Herm(A) + i Herm(B)), Herm(Y)(k) = (Y(k) + conj Y(-k)) / 2:
@@ -306,7 +381,7 @@ __global__ __launch_bounds__(MR_THREADS) void k_mr_rows(const void* __restrict__
         float* wo = ph.wrapped + ((b * 2 + ph.carrier) * H + r) * (long)n;
         for (int i = threadIdx.x; i < n; i += MR_THREADS) {
             const float2 a = b0[i];
-            float d = th[i] - atan2f(a.y, a.x);
+            float d = th[i] - fast_atan2(a.y, a.x);  // (gfft.hpp: 3.3e-7 rad, as the fast path's phase kernels)
             if (d > kPiF) d -= kTwoPiF;
             else if (d < -kPiF) d += kTwoPiF;
             wo[i] = d;
@@ -505,22 +580,57 @@ __global__ __launch_bounds__(NT, 4) void k_mr_int_cols(float2* __restrict__ Z, i
     }
 }
 
+// Rows whose two buffers exceed 128 KB of LDS (len > kMrLdsLen) take global scratch,
+// kMrLongRows blocks per launch.
+constexpr int kMrLdsLen = 8192;
+constexpr long kMrLongRows = 1024;
+
+// the long rows' scratch, per device (grown on demand; the generic chain's sides above 8192)
+static float2* long_scratch(size_t bytes) {
+    static std::mutex mu;
+    static std::map<int, std::pair<void*, size_t>> bufs;
+    int dev = 0;
+    FCD_HIPCHK(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lock(mu);
+    auto& b = bufs[dev];
+    if (b.second < bytes) {
+        if (b.first) FCD_HIPCHK(hipFree(b.first));
+        b.first = nullptr;
+        b.second = 0;
+        FCD_HIPCHK(hipMalloc(&b.first, bytes));
+        b.second = bytes;
+    }
+    return static_cast<float2*>(b.first);
+}
+
 template <bool INV, int IN, int OUT>
 void launch_mr(const MrPlan& p, const void* in, void* out, long nrows, int H, float sub, const float2* tw,
                const PhaseOut* ph, hipStream_t s) {
     PhaseOut q{};
     if (ph) q = *ph;
-    const size_t lds = 2 * (size_t)(p.blue ? p.M : p.n) * sizeof(float2);
+    const int len = p.blue ? p.M : p.n;
     static bool attr = false;
     if (!attr) {
+        // (the rows need at most 2 x 8192 complex; ROW_IN_Z's scan adds 2 KB of static LDS)
         FCD_HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mr_rows<INV, IN, OUT>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024));
         attr = true;
     }
     const long grid = (IN == ROW_IN_REAL2 || IN == ROW_IN_COMPLEX2) ? nrows / H * ((H + 1) / 2) : nrows;
-    hipLaunchKernelGGL((k_mr_rows<INV, IN, OUT>), dim3((unsigned)grid), dim3(MR_THREADS), lds, s, in, out, nrows, H,
-                       sub, p, tw, q);
-    FCD_CHECK_LAUNCH();
+    if (len <= kMrLdsLen) {
+        const size_t lds = 2 * (size_t)len * sizeof(float2);
+        hipLaunchKernelGGL((k_mr_rows<INV, IN, OUT>), dim3((unsigned)grid), dim3(MR_THREADS), lds, s, in, out, nrows,
+                           H, sub, p, tw, q, nullptr, 0L);
+        FCD_CHECK_LAUNCH();
+        return;
+    }
+    float2* gs = long_scratch((size_t)kMrLongRows * 2 * len * sizeof(float2));
+    for (long b0 = 0; b0 < grid; b0 += kMrLongRows) {  // (in order on the stream: the scratch is reused)
+        const long nblk = std::min(kMrLongRows, grid - b0);
+        hipLaunchKernelGGL((k_mr_rows<INV, IN, OUT>), dim3((unsigned)nblk), dim3(MR_THREADS), 0, s, in, out, nrows, H,
+                           sub, p, tw, q, gs, b0);
+        FCD_CHECK_LAUNCH();
+    }
 }
 
 }  // namespace
@@ -536,11 +646,9 @@ static int mr_lpf(int n) {
     return n > 1 ? n : res;
 }
 
-bool mr_supported(int n) {
-    if (n < 2) return false;
-    if (mr_lpf(n) <= kMrMaxRadix) return n <= 8192;
-    return n <= 4096;  // Bluestein: M <= 8192
-}
+// Sides up to kMrMaxLen (the MST's 32-bit vertex ids bound a frame's pixels); rows longer
+// than the LDS holds (kMrLdsLen complex, Bluestein's M included) run in global scratch.
+bool mr_supported(int n) { return n >= 2 && n <= kMrMaxLen; }
 
 MrPlan mr_plan(int n) {
     if (!mr_supported(n)) throw std::runtime_error("mixed-radix plan: unsupported length " + std::to_string(n));
@@ -665,6 +773,7 @@ void mr_rows(const MrPlan& p, bool inverse, RowIn im, RowOut om, const void* in,
 }
 
 bool mr_int_cols_supported(const MrPlan& p) {  // (also Bluestein: M is a power of two)
+    if ((p.blue ? p.M : p.n) > kMrLdsLen) return false;  // long columns: the transpose route (global-scratch rows)
     for (int f = 0; f < p.nf; ++f)
         if (p.fct[f] > 8 || p.fct[f] == 6) return false;  // the generic odd-prime passes: the transpose route
     return true;

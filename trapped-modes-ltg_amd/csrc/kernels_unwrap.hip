@@ -174,12 +174,12 @@ __global__ __launch_bounds__(256) void k_colk(const float* __restrict__ w, int H
     __shared__ int part[256];
     const int map = blockIdx.x;
     const float* m = w + (long)map * map_stride;
-    const int per = (H + 255) / 256;  // <= 32
+    const int per = (H + 255) / 256;  // <= 64
     const int i0 = threadIdx.x * per;
-    int loc[32];
+    int loc[64];
     int sum = 0;
 #pragma unroll
-    for (int q = 0; q < 32; ++q) {
+    for (int q = 0; q < 64; ++q) {
         const int i = i0 + q;
         loc[q] = 0;
         if (q < per && i + 1 < H) {
@@ -199,7 +199,7 @@ __global__ __launch_bounds__(256) void k_colk(const float* __restrict__ w, int H
     const int base = threadIdx.x ? part[threadIdx.x - 1] : 0;
     int* out = colk + (long)map * H;
 #pragma unroll
-    for (int q = 0; q < 32; ++q) {
+    for (int q = 0; q < 64; ++q) {
         const int i = i0 + q;
         if (q < per && i < H) out[i] = base + (q ? loc[q - 1] : 0);
     }
@@ -251,7 +251,7 @@ void unwrap_colk_compact(const float* col0, int nmaps, int H, int* colk, hipStre
 }
 
 void unwrap_scan(const float* w, int nmaps, int H, int W, int* colk, int32_t* k, hipStream_t s) {
-    if (H > 8192) throw std::runtime_error("unwrap_scan: H too large");
+    if (H > 16384) throw std::runtime_error("unwrap_scan: H too large");
     hipLaunchKernelGGL(k_colk, dim3(nmaps), dim3(256), 0, s, w, H, (long)H * W, (long)W, colk);
     FCD_CHECK_LAUNCH();
     const long nrows = (long)nmaps * H;
