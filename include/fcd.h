@@ -16,13 +16,14 @@
  *     all array arguments are device pointers on the context's device and the
  *     call is asynchronous on `stream` (NULL = the context's own stream),
  *     except where a function says it synchronises.
- *   - Images are row-major float32 [rows][cols]; complex arrays are
- *     interleaved complex64.  rows and cols are multiples of 64 in [64, 4096]
- *     of the form 2^a 3^b 5^c (camera formats such as 1280 x 1024 or
- *     2048 x 1536 included).  Powers of two take the band-pruned fast path;
- *     other sides take the generic chain (the reference's own sequence of
- *     2-D FFTs on mixed-radix transforms), with the same results and
- *     tolerances.
+ *   - Images are row-major float32 [rows][cols] (float64 where FCD_IMG_F64
+ *     says so); complex arrays are interleaved complex64 (complex128).  rows and
+ *     cols are any sides in [16, 16384] (the reference's scipy FFTs take any
+ *     length): powers of two in [64, 4096] take the band-pruned fast path, every
+ *     other shape (1920 x 1080, 1000 x 1000, 1023 x 1021, 4099 x 96 ...) the
+ *     generic chain (the reference's own sequence of 2-D FFTs on mixed-radix /
+ *     Bluestein transforms), with the same results and tolerances.  Larger
+ *     sides return FCD_E_UNSUPPORTED (the exact unwrap's 32-bit vertex ids).
  *   - A context belongs to one device and one host thread at a time.
  */
 #ifndef FCD_H
@@ -39,7 +40,7 @@ extern "C" {
 enum {
     FCD_OK = 0,
     FCD_E_INVALID = -1,      /* bad argument (null pointer, size mismatch, ...) */
-    FCD_E_UNSUPPORTED = -2,  /* shape not supported (side not a 5-smooth multiple of 64 in [64, 4096]) */
+    FCD_E_UNSUPPORTED = -2,  /* shape not supported (a side outside [16, 16384]) */
     FCD_E_HIP = -3,          /* HIP runtime / launch failure */
     FCD_E_STATE = -4,        /* no reference set */
     FCD_E_NOPEAKS = -5,      /* < 2 carrier peaks: the reference raises ValueError/IndexError */

@@ -219,7 +219,7 @@ __device__ __forceinline__ int mr_find_wrap(float a, float b) {
 // w(j' + 1)) -- the integers of k_colk / k_rowscan -- for a residue-free map, kin for a map
 // the MST unwrapped; z(j) = (w0 + 2 pi k0) + i (w1 + 2 pi k1) (k_make_z) into b0.
 template <bool INV>
-__device__ __noinline__ void mr_load_z_scan(const float* in, long row, int H, int n, const MrPlan& p,
+__device__ __forceinline__ void mr_load_z_scan(const float* in, long row, int H, int n, const MrPlan& p,
                                             const float2* __restrict__ tw, const PhaseOut& ph, float2* b0, float2* b1) {
     __shared__ int scn[2][MR_THREADS];
     const long b = row / H, r = row % H;
@@ -269,7 +269,9 @@ __device__ __noinline__ void mr_load_z_scan(const float* in, long row, int H, in
 // gs (null: LDS): rows longer than the LDS holds run their passes in global scratch, the
 // block's 2 len complex at gs + blockIdx.x * 2 len (the L2 / MALL-resident working set of a
 // launch of at most kMrLongRows rows); blk0: the launch's first block (row batches).
-template <bool INV, int IN, int OUT>
+// (GS a template parameter: with a runtime choice the compiler cannot tell the buffers are
+// LDS and every access of the LDS rows becomes a flat one, 1.5x slower, r05)
+template <bool INV, int IN, int OUT, bool GS>
 __global__ __launch_bounds__(MR_THREADS) void k_mr_rows(const void* __restrict__ in, void* __restrict__ out, long nrows,
                                                         int H, float sub, MrPlan p, const float2* __restrict__ tw,
                                                         PhaseOut ph, float2* __restrict__ gs, long blk0) {
@@ -282,7 +284,7 @@ __global__ __launch_bounds__(MR_THREADS) void k_mr_rows(const void* __restrict__
     const long blk = blk0 + blockIdx.x;
     const long row = PAIR ? (blk / hp) * H + 2 * (blk % hp) : blk;
     const bool second = PAIR && 2 * (blk % hp) + 1 < H;
-    float2* b0 = gs ? gs + (size_t)blockIdx.x * 2 * len : mr_lds;
+    float2* b0 = GS ? gs + (size_t)blockIdx.x * 2 * len : mr_lds;
     float2* b1 = b0 + len;
     for (int i = threadIdx.x; i < n; i += MR_THREADS) {
         float2 v;
@@ -612,23 +614,23 @@ void launch_mr(const MrPlan& p, const void* in, void* out, long nrows, int H, fl
     static bool attr = false;
     if (!attr) {
         // (the rows need at most 2 x 8192 complex; ROW_IN_Z's scan adds 2 KB of static LDS)
-        FCD_HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mr_rows<INV, IN, OUT>),
+        FCD_HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mr_rows<INV, IN, OUT, false>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024));
         attr = true;
     }
     const long grid = (IN == ROW_IN_REAL2 || IN == ROW_IN_COMPLEX2) ? nrows / H * ((H + 1) / 2) : nrows;
     if (len <= kMrLdsLen) {
         const size_t lds = 2 * (size_t)len * sizeof(float2);
-        hipLaunchKernelGGL((k_mr_rows<INV, IN, OUT>), dim3((unsigned)grid), dim3(MR_THREADS), lds, s, in, out, nrows,
-                           H, sub, p, tw, q, nullptr, 0L);
+        hipLaunchKernelGGL((k_mr_rows<INV, IN, OUT, false>), dim3((unsigned)grid), dim3(MR_THREADS), lds, s, in, out,
+                           nrows, H, sub, p, tw, q, nullptr, 0L);
         FCD_CHECK_LAUNCH();
         return;
     }
     float2* gs = long_scratch((size_t)kMrLongRows * 2 * len * sizeof(float2));
     for (long b0 = 0; b0 < grid; b0 += kMrLongRows) {  // (in order on the stream: the scratch is reused)
         const long nblk = std::min(kMrLongRows, grid - b0);
-        hipLaunchKernelGGL((k_mr_rows<INV, IN, OUT>), dim3((unsigned)nblk), dim3(MR_THREADS), 0, s, in, out, nrows, H,
-                           sub, p, tw, q, gs, b0);
+        hipLaunchKernelGGL((k_mr_rows<INV, IN, OUT, true>), dim3((unsigned)nblk), dim3(MR_THREADS), 0, s, in, out,
+                           nrows, H, sub, p, tw, q, gs, b0);
         FCD_CHECK_LAUNCH();
     }
 }
