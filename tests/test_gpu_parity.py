@@ -12,6 +12,8 @@ Tolerances (SURVEY.md §8a "Parity facts"):
   * height: rel-L2 <= 1e-5 synthetic (1e-4 on the real pair whose golden has one
     randomly-seeded border pixel), max-abs <= 1e-4 * max|h| synthetic.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -372,6 +374,39 @@ def test_batch_equals_single(lib, golden, monkeypatch, exact_first):
     for i in range(3):
         h1, _, _ = fcd.compute_height_map(ref, frames[i], float(s["sine256_sq"]), height=1.0)
         assert np.array_equal(hb[i], h1.astype(np.float32))
+
+
+@pytest.mark.parametrize("streams", ["2", "1"])
+def test_exact_chain_halves_equal_single_frames(lib, golden, monkeypatch, streams):
+    """The exact-first chain runs a chunk of 8 or more frames as two halves on two streams,
+    each driven by its own host thread and MST workspace (FCD_STREAMS=2), or in one piece
+    (=1): 11 frames -- the three real camera frames (7..1611 residues per map) tiled, with
+    two residue-free frames among them -- give heights bit-identical to single-frame calls
+    either way, and the halves equal the one-piece chain."""
+    from bench_data import make_frames_numpy
+    from pyfcd import _lib
+    d = golden("real_df")
+    ref = d["ref_u16"].astype(np.float32)
+    real = d["frames_u16"].astype(np.float32)
+    monkeypatch.setenv("FCD_EXACT_FIRST", "1")
+    monkeypatch.setenv("FCD_STREAMS", streams)
+    _lib._engines.clear()
+    eng = lib.Engine(ref.shape)
+    eng.set_reference(ref, float(d["square_size"]))
+    clean = eng.process(ref[None], 1.0, unwrap=True, want_phases=False)[0]  # (the reference: a zero map)
+    frames = np.stack([real[i % 3] for i in range(9)] + [ref, ref * np.float32(0.5)])
+    hb, _, _ = eng.process(frames, 1.0, unwrap=True, want_phases=False)
+    for i in (0, 1, 2, 8, 9, 10):
+        hs, _, _ = eng.process(frames[i:i + 1], 1.0, unwrap=True, want_phases=False)
+        assert np.array_equal(hb[i], hs[0]), i
+    assert np.array_equal(hb[9], clean[0])
+    for i in range(3, 9):
+        assert np.array_equal(hb[i], hb[i % 3]), i
+    np.save(f"/tmp/halves_{streams}.npy", hb)
+    if streams == "1" and os.path.exists("/tmp/halves_2.npy"):
+        assert np.array_equal(np.load("/tmp/halves_2.npy"), hb)
+    del eng
+    _lib._engines.clear()
 
 
 def test_full_size_1024_vs_oracle(lib):
