@@ -142,6 +142,29 @@ def test_anyshape_raw_formats(anyshape, golden):
     eng.close()
 
 
+@pytest.mark.parametrize("tag", ["r1000x1000", "s1023x1021"])
+def test_mst_levels_agree_on_odd_shapes(anyshape, golden, monkeypatch, tag):
+    """The exact unwrap's other round structures (FCD_MST_LEVEL=2: tiles then boundary
+    lists; 1: one pixel round then lists; 0: all-pixel rounds) on maps of odd shapes,
+    padded to multiples of 64 for them: the same k-fields as the default tiles +
+    component-graph rounds (the level-2 / 1 fallback of a tile graph over its capacity
+    decodes pixels with the padded, not power-of-two, sides: ADVICE r04)."""
+    from pyfcd import _lib
+    g = anyshape
+    ref, frame, sq = case_frames(g, golden, tag)
+    eng = _lib.Engine(ref.shape)
+    eng.set_reference(ref, sq)
+    _, w, _ = eng.process(frame[None], 1.0, unwrap=True, want_phases=True)
+    k3, res = eng.unwrap(w[0])
+    assert (res > 0).any()
+    for level in ("2", "1", "0"):
+        monkeypatch.setenv("FCD_MST_LEVEL", level)
+        k, _ = eng.unwrap(w[0])
+        assert np.array_equal(k, k3), level
+    monkeypatch.delenv("FCD_MST_LEVEL")
+    eng.close()
+
+
 @pytest.mark.parametrize("shape", [(4099, 96), (96, 8200), (64, 16384)])
 def test_long_sides_match_oracle(shape):
     """Sides the rows' LDS cannot hold (kernels_mr.hip global-scratch rows): 4099 (prime:
