@@ -57,6 +57,17 @@ namespace fcdk {
 namespace {
 
 constexpr int MR_THREADS = 256;
+constexpr int MR_LU = 8;  // row loads in flight per thread
+
+// a / d for 0 <= a < 2^24 and the runtime divisor d (inv = 1 / d in f32): the f32 quotient
+// is off by at most one, fixed by the remainder (an integer division is a ~40-instruction
+// sequence on the GPU, and the passes took one per butterfly)
+__device__ __forceinline__ int mr_div(int a, int d, float inv) {
+    int q = (int)((float)a * inv);
+    const int r = a - q * d;
+    q += r >= d ? 1 : (r < 0 ? -1 : 0);
+    return q;
+}
 constexpr float kPiF = 3.14159265358979f;
 constexpr float kTwoPiF = 6.28318530717959f;
 // radix-3 / radix-5 DFT constants
@@ -137,8 +148,9 @@ __device__ __forceinline__ void dft_any(float2* a) {
 template <int R, bool INV>
 __device__ __forceinline__ void mr_pass(const float2* src, float2* dst, int n, int L, const float2* __restrict__ tw) {
     const int nb = n / R, step = n / (L * R);
+    const float invL = 1.f / (float)L;
     for (int j = threadIdx.x; j < nb; j += MR_THREADS) {
-        const int k = j % L;
+        const int k = j - L * mr_div(j, L, invL);
         float2 a[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) a[r] = src[j + r * nb];
@@ -159,15 +171,16 @@ __device__ __forceinline__ void mr_pass(const float2* src, float2* dst, int n, i
 template <bool INV>
 __device__ __forceinline__ void mr_pass_gen(float2* src, float2* dst, int n, int L, int R, const float2* __restrict__ tw) {
     const int nb = n / R, step = n / (L * R), wstep = n / R;
+    const float invL = 1.f / (float)L, invnb = 1.f / (float)nb;
     if (L > 1) {
         for (int idx = threadIdx.x; idx < n; idx += MR_THREADS) {
-            const int r = idx / nb, j = idx - r * nb;
-            if (r > 0) src[idx] = cmul_dir<INV>(src[idx], tw[r * (j % L) * step]);
+            const int r = mr_div(idx, nb, invnb), j = idx - r * nb;
+            if (r > 0) src[idx] = cmul_dir<INV>(src[idx], tw[r * (j - L * mr_div(j, L, invL)) * step]);
         }
         __syncthreads();
     }
     for (int idx = threadIdx.x; idx < n; idx += MR_THREADS) {
-        const int q = idx / nb, j = idx - q * nb, k = j % L;
+        const int q = mr_div(idx, nb, invnb), j = idx - q * nb, k = j - L * mr_div(j, L, invL);
         float2 acc = src[j];
         int m = 0;
         for (int r = 1; r < R; ++r) {
@@ -286,20 +299,15 @@ __global__ __launch_bounds__(MR_THREADS) void k_mr_rows(const void* __restrict__
     const bool second = PAIR && 2 * (blk % hp) + 1 < H;
     float2* b0 = GS ? gs + (size_t)blockIdx.x * 2 * len : mr_lds;
     float2* b1 = b0 + len;
-    for (int i = threadIdx.x; i < n; i += MR_THREADS) {
-        float2 v;
+    // the row's loads in groups of MR_LU per thread, all issued before their LDS stores
+    // (a load-store pair per trip left each trip waiting for its load)
+    auto load_elem = [&](int i) -> float2 {
         if constexpr (IN == ROW_IN_REAL2) {
             const float* x = static_cast<const float*>(in) + row * n + i;
-            v = make_float2(x[0] - sub, second ? x[n] - sub : 0.f);
-        } else if constexpr (IN == ROW_IN_COMPLEX2) {  // raw rows a, b -> b0, b1 (combined below)
-            const float2* x = static_cast<const float2*>(in) + row * n + i;
-            b1[i] = second ? x[n] : make_float2(0.f, 0.f);
-            b0[i] = x[0];
-            continue;
+            return make_float2(x[0] - sub, second ? x[n] - sub : 0.f);
         } else if constexpr (IN == ROW_IN_REAL) {
-            v = make_float2(static_cast<const float*>(in)[row * n + i] - sub, 0.f);
+            return make_float2(static_cast<const float*>(in)[row * n + i] - sub, 0.f);
         } else if constexpr (IN == ROW_IN_Z) {  // k_make_z's arithmetic
-            if (ph.kflag) break;  // (the scan form below)
             const long b = row / H, r = row % H;
             const long i0 = ((2 * b) * H + r) * n + i, i1 = ((2 * b + 1) * H + r) * n + i;
             float p0 = static_cast<const float*>(in)[i0], p1 = static_cast<const float*>(in)[i1];
@@ -307,16 +315,50 @@ __global__ __launch_bounds__(MR_THREADS) void k_mr_rows(const void* __restrict__
                 p0 = (float)((double)p0 + 6.283185307179586 * (double)ph.kin[i0]);
                 p1 = (float)((double)p1 + 6.283185307179586 * (double)ph.kin[i1]);
             }
-            v = make_float2(p0, p1);
+            return make_float2(p0, p1);
         } else if constexpr (IN == ROW_IN_BAND) {
             const long b = row / H, r = row % H;
             const int sl = ph.bslot[i];
-            v = sl >= 0 ? static_cast<const float2*>(in)[(b * ph.bnc + sl) * H + r] : make_float2(0.f, 0.f);
+            return sl >= 0 ? static_cast<const float2*>(in)[(b * ph.bnc + sl) * H + r] : make_float2(0.f, 0.f);
         } else {
-            v = static_cast<const float2*>(in)[row * n + i];
+            return static_cast<const float2*>(in)[row * n + i];
         }
-        if (p.blue) v = cmul_dir<INV>(v, tw[p.tc + i]);  // Bluestein: the chirp premultiply
-        b0[i] = v;
+    };
+    if constexpr (IN == ROW_IN_COMPLEX2) {  // raw rows a, b -> b0, b1 (combined below)
+        for (int i0 = threadIdx.x; i0 < n; i0 += MR_LU * MR_THREADS) {
+            float2 va[MR_LU], vb[MR_LU];
+#pragma unroll
+            for (int u = 0; u < MR_LU; ++u) {
+                const int i = i0 + u * MR_THREADS;
+                if (i < n) {
+                    const float2* x = static_cast<const float2*>(in) + row * n + i;
+                    va[u] = x[0];
+                    vb[u] = second ? x[n] : make_float2(0.f, 0.f);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < MR_LU; ++u) {
+                const int i = i0 + u * MR_THREADS;
+                if (i < n) {
+                    b0[i] = va[u];
+                    b1[i] = vb[u];
+                }
+            }
+        }
+    } else if (IN != ROW_IN_Z || !ph.kflag) {  // (ROW_IN_Z with kflag: the scan form below)
+        for (int i0 = threadIdx.x; i0 < n; i0 += MR_LU * MR_THREADS) {
+            float2 v[MR_LU];
+#pragma unroll
+            for (int u = 0; u < MR_LU; ++u) {
+                const int i = i0 + u * MR_THREADS;
+                if (i < n) v[u] = load_elem(i);
+            }
+#pragma unroll
+            for (int u = 0; u < MR_LU; ++u) {
+                const int i = i0 + u * MR_THREADS;
+                if (i < n) b0[i] = p.blue ? cmul_dir<INV>(v[u], tw[p.tc + i]) : v[u];  // Bluestein: the chirp premultiply
+            }
+        }
     }
     if constexpr (IN == ROW_IN_Z) {
         if (ph.kflag) mr_load_z_scan<INV>(static_cast<const float*>(in), row, H, n, p, tw, ph, b0, b1);
@@ -381,12 +423,23 @@ __global__ __launch_bounds__(MR_THREADS) void k_mr_rows(const void* __restrict__
         const long b = row / H, r = row % H;
         const float* th = ph.theta + r * n;
         float* wo = ph.wrapped + ((b * 2 + ph.carrier) * H + r) * (long)n;
-        for (int i = threadIdx.x; i < n; i += MR_THREADS) {
-            const float2 a = b0[i];
-            float d = th[i] - fast_atan2(a.y, a.x);  // (gfft.hpp: 3.3e-7 rad, as the fast path's phase kernels)
-            if (d > kPiF) d -= kTwoPiF;
-            else if (d < -kPiF) d += kTwoPiF;
-            wo[i] = d;
+        for (int i0 = threadIdx.x; i0 < n; i0 += MR_LU * MR_THREADS) {
+            float t[MR_LU];  // the reference angles of the group, loaded together
+#pragma unroll
+            for (int u = 0; u < MR_LU; ++u) {
+                const int i = i0 + u * MR_THREADS;
+                if (i < n) t[u] = th[i];
+            }
+#pragma unroll
+            for (int u = 0; u < MR_LU; ++u) {
+                const int i = i0 + u * MR_THREADS;
+                if (i >= n) continue;
+                const float2 a = b0[i];
+                float d = t[u] - fast_atan2(a.y, a.x);  // (gfft.hpp: 3.3e-7 rad, as the fast path's phase kernels)
+                if (d > kPiF) d -= kTwoPiF;
+                else if (d < -kPiF) d += kTwoPiF;
+                wo[i] = d;
+            }
         }
     }
 }
@@ -423,6 +476,7 @@ template <int R, bool INV>
 __device__ __forceinline__ void mc_pass(float2* buf, int pitch, int team, int n, int L, const float2* __restrict__ tw) {
     constexpr int NBF = mc_nbf<R>();
     const int nbt = n / R, step = n / (L * R);
+    const float invL = 1.f / (float)L;
     const int col = threadIdx.x / team, t = threadIdx.x & (team - 1);
     float2* const cb = buf + col * pitch;
     float2 a[NBF][R];
@@ -439,7 +493,7 @@ __device__ __forceinline__ void mc_pass(float2* buf, int pitch, int team, int n,
     for (int m = 0; m < NBF; ++m) {
         const int j = t + m * team;
         if (j < nbt) {
-            const int k = j % L;
+            const int k = j - L * mr_div(j, L, invL);
             if (L > 1) {
 #pragma unroll
                 for (int r = 1; r < R; ++r) a[m][r] = cmul_dir<INV>(a[m][r], tw[r * k * step]);
@@ -530,6 +584,7 @@ __global__ __launch_bounds__(NT, 4) void k_mr_int_cols(float2* __restrict__ Z, i
     float2* const Zb = Z + b * (long)H * W;
     const int q0 = g * C, cnt = min(C, W - q0);
     const int team = NT / C, total = cnt * H;
+    const float invcnt = 1.f / (float)cnt, invH = 1.f / (float)H;
     float2* const tws = mc_lds + C * pitch;  // len twiddles (Bluestein: the M-point table)
     const float2* const twsrc = p.blue ? tw + p.tM : tw;
     for (int i = threadIdx.x; i < len; i += NT) tws[i] = twsrc[i];
@@ -539,7 +594,7 @@ __global__ __launch_bounds__(NT, 4) void k_mr_int_cols(float2* __restrict__ Z, i
         for (int m = 0; m < MC_EPL; ++m) {
             const int u = threadIdx.x + m * NT;
             if (u < total) {
-                const int i = u / cnt, sl = u - i * cnt;
+                const int i = mr_div(u, cnt, invcnt), sl = u - i * cnt;
                 v[m] = Zb[(long)i * W + q0 + sl];
             }
         }
@@ -547,7 +602,7 @@ __global__ __launch_bounds__(NT, 4) void k_mr_int_cols(float2* __restrict__ Z, i
         for (int m = 0; m < MC_EPL; ++m) {
             const int u = threadIdx.x + m * NT;
             if (u < total) {
-                const int i = u / cnt, sl = u - i * cnt;
+                const int i = mr_div(u, cnt, invcnt), sl = u - i * cnt;
                 mc_lds[sl * pitch + i] = p.blue ? cmul_dir<false>(v[m], tw[p.tc + i]) : v[m];
             }
         }
@@ -563,7 +618,7 @@ __global__ __launch_bounds__(NT, 4) void k_mr_int_cols(float2* __restrict__ Z, i
     for (int m = 0; m < MC_EPL; ++m) {
         const int u = threadIdx.x + m * NT;
         if (u < total) {
-            const int sl = u / H, r = u - sl * H;
+            const int sl = mr_div(u, H, invH), r = u - sl * H;
             float2 v = mc_mult(mc_lds[sl * pitch + r], q0 + sl, r, ic);
             if (p.blue) v = cmul_dir<true>(v, tw[p.tc + r]);  // the inverse's chirp premultiply
             mc_lds[sl * pitch + r] = v;
@@ -577,7 +632,7 @@ __global__ __launch_bounds__(NT, 4) void k_mr_int_cols(float2* __restrict__ Z, i
     __syncthreads();
     mc_dft<true, NT>(mc_lds, cnt, pitch, team, p, tws, tw);
     for (int u = threadIdx.x; u < total; u += NT) {
-        const int i = u / cnt, sl = u - i * cnt;
+        const int i = mr_div(u, cnt, invcnt), sl = u - i * cnt;
         Zb[(long)i * W + q0 + sl] = mc_lds[sl * pitch + i];
     }
 }
