@@ -141,6 +141,35 @@ def real_frames_rate(dev, stream, batch=96, reps=3):
             "ms_per_frame": round(dt / len(frames) * 1e3, 4)}
 
 
+def generic_shape_rate(dev, stream, rows=1080, cols=1920, batch=64, reps=3):
+    """Side measurement, never `value`: the generic chain (kernels_mr.hip, frame sides that
+    are not powers of two) at the HD camera format, residue-free synthetic boards (the
+    pattern.py board warped by the bump field of bench_data.py, generated on the host),
+    `batch` device-resident frames per call, frames/s over `reps` calls after a warm-up."""
+    import numpy as np
+    import torch
+    from bench_data import checkerboard, displacement_numpy, warp_numpy
+    from pyfcd import _lib
+    ref = checkerboard(rows, cols=cols)
+    base = [warp_numpy(ref, *displacement_numpy(rows, s, cols=cols)) for s in range(4)]
+    fr = torch.from_numpy(np.stack([base[i % 4] for i in range(batch)])).to(dev)
+    h = torch.empty_like(fr)
+    eng = _lib.Engine((rows, cols), device=dev.index)
+    eng.set_reference(ref, 0.001)
+    eng.process_device(fr.data_ptr(), batch, 1.0, True, h.data_ptr(), stream=stream)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        eng.process_device(fr.data_ptr(), batch, 1.0, True, h.data_ptr(), stream=stream)
+    torch.cuda.synchronize(dev)
+    dt = (time.perf_counter() - t0) / reps
+    eng.close()
+    return {"value": round(batch / dt, 1), "unit": "frames/s", "shape": [rows, cols],
+            "us_per_megapixel": round(dt / batch * 1e6 / (rows * cols / 1e6), 2),
+            "sample": f"{batch} synthetic {rows}x{cols} boards per call (residue-free), device-resident, "
+                      "the generic mixed-radix chain"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -350,6 +379,7 @@ def main():
                                 "not inside the frames/s"}
     if world == 1 and n == 1024 and not args.no_real_frames:
         out["residue_frames"] = real_frames_rate(dev, stream)
+        out["generic_hd_frames"] = generic_shape_rate(dev, stream)
     if world == 1 and not args.no_cpu_baseline:
         log("CPU baseline (oracle, 1 core, then all cores)")
         single = cpu_baseline(n, args.cpu_frames)
