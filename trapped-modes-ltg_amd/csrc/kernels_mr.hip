@@ -467,17 +467,27 @@ __global__ __launch_bounds__(256) void k_mr_transpose(const float2* __restrict__
 // first loads every butterfly input of the thread into registers (at most MC_EPL values
 // per thread: len <= MC_EPL * team), then, after a barrier, writes the outputs.  One
 // buffer instead of the rows' two: twice the columns per workgroup.
-constexpr int MC_EPL = 16;
+constexpr int MC_EPL = 16;   // values per thread, block-synchronised teams
+constexpr int MC_EPL_W = 20; // values per thread, one wave per column (len <= 1280; 18 and 24 spill)
 
-template <int R>
-constexpr int mc_nbf() { return (MC_EPL + R - 1) / R; }  // butterflies per thread (n / R <= nbf * team)
+template <int R, int EPL>
+constexpr int mc_nbf() { return (EPL + R - 1) / R; }  // butterflies per thread (n / R <= nbf * team)
 
-template <int R, bool INV>
+// WAVE: the team is one wave (64 threads per column), so a pass synchronises the wave
+// only; otherwise the workgroup
+template <bool WAVE>
+__device__ __forceinline__ void mc_sync() {
+    if constexpr (WAVE) wave_sync();
+    else __syncthreads();
+}
+
+template <int R, bool INV, int EPL, bool WAVE>
 __device__ __forceinline__ void mc_pass(float2* buf, int pitch, int team, int n, int L, const float2* __restrict__ tw) {
-    constexpr int NBF = mc_nbf<R>();
+    constexpr int NBF = mc_nbf<R, EPL>();
     const int nbt = n / R, step = n / (L * R);
     const float invL = 1.f / (float)L;
-    const int col = threadIdx.x / team, t = threadIdx.x & (team - 1);
+    const int col = WAVE ? (int)(threadIdx.x >> 6) : (int)(threadIdx.x / team);
+    const int t = threadIdx.x & (team - 1);
     float2* const cb = buf + col * pitch;
     float2 a[NBF][R];
 #pragma unroll
@@ -488,7 +498,7 @@ __device__ __forceinline__ void mc_pass(float2* buf, int pitch, int team, int n,
             for (int r = 0; r < R; ++r) a[m][r] = cb[j + r * nbt];
         }
     }
-    __syncthreads();
+    mc_sync<WAVE>();
 #pragma unroll
     for (int m = 0; m < NBF; ++m) {
         const int j = t + m * team;
@@ -504,46 +514,48 @@ __device__ __forceinline__ void mc_pass(float2* buf, int pitch, int team, int n,
             for (int r = 0; r < R; ++r) dst[r * L] = a[m][r];
         }
     }
-    __syncthreads();
+    mc_sync<WAVE>();
 }
 
-template <bool INV>
+// every pass of the plan; ends with a workgroup barrier (the callers' next steps cross columns)
+template <bool INV, int EPL, bool WAVE>
 __device__ __forceinline__ void mc_run(float2* buf, int pitch, int team, int len, const int* fct, int nf,
                                        const float2* __restrict__ tw) {
     int L = 1;
     for (int f = 0; f < nf; ++f) {
         const int R = fct[f];
         switch (R) {
-            case 8: mc_pass<8, INV>(buf, pitch, team, len, L, tw); break;
-            case 4: mc_pass<4, INV>(buf, pitch, team, len, L, tw); break;
-            case 2: mc_pass<2, INV>(buf, pitch, team, len, L, tw); break;
-            case 3: mc_pass<3, INV>(buf, pitch, team, len, L, tw); break;
-            case 5: mc_pass<5, INV>(buf, pitch, team, len, L, tw); break;
-            default: mc_pass<7, INV>(buf, pitch, team, len, L, tw);  // (mr_int_cols_supported: no larger primes)
+            case 8: mc_pass<8, INV, EPL, WAVE>(buf, pitch, team, len, L, tw); break;
+            case 4: mc_pass<4, INV, EPL, WAVE>(buf, pitch, team, len, L, tw); break;
+            case 2: mc_pass<2, INV, EPL, WAVE>(buf, pitch, team, len, L, tw); break;
+            case 3: mc_pass<3, INV, EPL, WAVE>(buf, pitch, team, len, L, tw); break;
+            case 5: mc_pass<5, INV, EPL, WAVE>(buf, pitch, team, len, L, tw); break;
+            default: mc_pass<7, INV, EPL, WAVE>(buf, pitch, team, len, L, tw);  // (mr_int_cols_supported: no larger primes)
         }
         L *= R;
     }
+    if constexpr (WAVE) __syncthreads();
 }
 
 // The length-H DFT of the workgroup's columns (Bluestein: the columns' first H values hold
 // the chirp-premultiplied input, the rest zeros, on entry; the transform's H values on exit).
 // tws: the passes' twiddles (LDS), tw: the plan's table (chirp, G).
-template <bool INV, int NT>
+template <bool INV, int NT, int EPL, bool WAVE>
 __device__ __forceinline__ void mc_dft(float2* buf, int ncol, int pitch, int team, const MrPlan& p,
                                        const float2* tws, const float2* __restrict__ tw) {
     if (!p.blue) {
-        mc_run<INV>(buf, pitch, team, p.n, p.fct, p.nf, tws);
+        mc_run<INV, EPL, WAVE>(buf, pitch, team, p.n, p.fct, p.nf, tws);
         return;
     }
     const int M = p.M, H = p.n;
-    mc_run<false>(buf, pitch, team, M, p.fct, p.nf, tws);
+    mc_run<false, EPL, WAVE>(buf, pitch, team, M, p.fct, p.nf, tws);
     const float2* G = tw + (INV ? p.tgi : p.tgf);
     for (int u = threadIdx.x; u < ncol * M; u += NT) {
         const int col = u / M, i = u - col * M;
         buf[col * pitch + i] = cmul(buf[col * pitch + i], G[i]);
     }
     __syncthreads();
-    mc_run<true>(buf, pitch, team, M, p.fct, p.nf, tws);
+    mc_run<true, EPL, WAVE>(buf, pitch, team, M, p.fct, p.nf, tws);
     for (int u = threadIdx.x; u < ncol * H; u += NT) {
         const int col = u / H, i = u - col * H;
         buf[col * pitch + i] = cmul_dir<INV>(buf[col * pitch + i], tw[p.tc + i]);
@@ -570,7 +582,7 @@ __device__ __forceinline__ float2 mc_mult(float2 z, int q, int r, const IntegCoe
 // NT / C threads per column, the transform's twiddles copied to LDS after the columns; reads
 // and writes run over the slots fastest (C consecutive columns per row), each thread's
 // loads issued together (at most MC_EPL: cnt H <= C len <= MC_EPL NT).
-template <int NT>
+template <int NT, int EPL, bool WAVE>
 __global__ __launch_bounds__(NT, 4) void k_mr_int_cols(float2* __restrict__ Z, int nblk, int W, int C, int ngroups,
                                                        MrPlan p, const float2* __restrict__ tw, IntegCoef ic) {
     extern __shared__ __attribute__((aligned(16))) float2 mc_lds[];
@@ -588,19 +600,19 @@ __global__ __launch_bounds__(NT, 4) void k_mr_int_cols(float2* __restrict__ Z, i
     float2* const tws = mc_lds + C * pitch;  // len twiddles (Bluestein: the M-point table)
     const float2* const twsrc = p.blue ? tw + p.tM : tw;
     for (int i = threadIdx.x; i < len; i += NT) tws[i] = twsrc[i];
-    {
-        float2 v[MC_EPL];
+    for (int m0 = 0; m0 < EPL; m0 += 8) {  // loads in groups of 8 (registers)
+        float2 v[8];
 #pragma unroll
-        for (int m = 0; m < MC_EPL; ++m) {
-            const int u = threadIdx.x + m * NT;
+        for (int m = 0; m < 8; ++m) {
+            const int u = threadIdx.x + (m0 + m) * NT;
             if (u < total) {
                 const int i = mr_div(u, cnt, invcnt), sl = u - i * cnt;
                 v[m] = Zb[(long)i * W + q0 + sl];
             }
         }
 #pragma unroll
-        for (int m = 0; m < MC_EPL; ++m) {
-            const int u = threadIdx.x + m * NT;
+        for (int m = 0; m < 8; ++m) {
+            const int u = threadIdx.x + (m0 + m) * NT;
             if (u < total) {
                 const int i = mr_div(u, cnt, invcnt), sl = u - i * cnt;
                 mc_lds[sl * pitch + i] = p.blue ? cmul_dir<false>(v[m], tw[p.tc + i]) : v[m];
@@ -613,9 +625,9 @@ __global__ __launch_bounds__(NT, 4) void k_mr_int_cols(float2* __restrict__ Z, i
             mc_lds[sl * pitch + i] = make_float2(0.f, 0.f);
         }
     __syncthreads();
-    mc_dft<false, NT>(mc_lds, cnt, pitch, team, p, tws, tw);
-#pragma unroll
-    for (int m = 0; m < MC_EPL; ++m) {
+    mc_dft<false, NT, EPL, WAVE>(mc_lds, cnt, pitch, team, p, tws, tw);
+#pragma unroll 4
+    for (int m = 0; m < EPL; ++m) {
         const int u = threadIdx.x + m * NT;
         if (u < total) {
             const int sl = mr_div(u, H, invH), r = u - sl * H;
@@ -630,7 +642,7 @@ __global__ __launch_bounds__(NT, 4) void k_mr_int_cols(float2* __restrict__ Z, i
             mc_lds[sl * pitch + i] = make_float2(0.f, 0.f);
         }
     __syncthreads();
-    mc_dft<true, NT>(mc_lds, cnt, pitch, team, p, tws, tw);
+    mc_dft<true, NT, EPL, WAVE>(mc_lds, cnt, pitch, team, p, tws, tw);
     for (int u = threadIdx.x; u < total; u += NT) {
         const int i = mr_div(u, cnt, invcnt), sl = u - i * cnt;
         Zb[(long)i * W + q0 + sl] = mc_lds[sl * pitch + i];
@@ -836,14 +848,45 @@ bool mr_int_cols_supported(const MrPlan& p) {  // (also Bluestein: M is a power 
     return true;
 }
 
-// Columns per group C (a power of two <= 16: up to 128-byte row runs), 512 threads with a team
-// of 512 / C per column (len <= MC_EPL * team), or 1024 when the 512 would leave C = 1;
-// LDS: the C columns and the len twiddles, at most 80 KB (two 512-thread workgroups per CU).
+// Columns per group C (a power of two <= 16: up to 128-byte row runs).  Columns up to 1280
+// points: one wave per column (EPL 20 values per thread, passes synchronised per wave, the
+// workgroup 64 C threads); longer ones: a team of 512 / C threads per column (EPL 16;
+// 1024 threads for the 8192-point columns).  LDS: the C columns and the len twiddles, at
+// most 80 KB (two workgroups per CU).
+template <int NT, int EPL, bool WAVE>
+static void launch_int_cols(const MrPlan& p, float2* Z, long blocks, int W, int C, int ngroups, size_t lds,
+                            const float2* tw, const IntegCoef& c, hipStream_t s) {
+    static bool attr = false;
+    if (!attr) {
+        FCD_HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mr_int_cols<NT, EPL, WAVE>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        attr = true;
+    }
+    const unsigned grid = (unsigned)((blocks + 7) / 8 * 8);
+    hipLaunchKernelGGL((k_mr_int_cols<NT, EPL, WAVE>), dim3(grid), dim3(NT), lds, s, Z, (int)blocks, W, C, ngroups, p,
+                       tw, c);
+    FCD_CHECK_LAUNCH();
+}
+
 void mr_int_cols(const MrPlan& p, float2* Z, int nb, int W, const float2* tw, const IntegCoef& c, hipStream_t s) {
     if (nb <= 0) return;
     if (!mr_int_cols_supported(p)) throw std::runtime_error("mr_int_cols: a radix above 8");
     const int len = p.blue ? p.M : p.n;
     auto lds_of = [&](int C) { return (size_t)(C * (len + 1) + len) * sizeof(float2); };
+    if (len <= MC_EPL_W * 64) {  // wave teams
+        int C = 16;
+        while (C > 1 && lds_of(C) > 80 * 1024) C /= 2;
+        const int ngroups = (W + C - 1) / C;
+        const long blocks = (long)nb * ngroups;
+        switch (C) {
+            case 16: launch_int_cols<1024, MC_EPL_W, true>(p, Z, blocks, W, C, ngroups, lds_of(C), tw, c, s); break;
+            case 8: launch_int_cols<512, MC_EPL_W, true>(p, Z, blocks, W, C, ngroups, lds_of(C), tw, c, s); break;
+            case 4: launch_int_cols<256, MC_EPL_W, true>(p, Z, blocks, W, C, ngroups, lds_of(C), tw, c, s); break;
+            case 2: launch_int_cols<128, MC_EPL_W, true>(p, Z, blocks, W, C, ngroups, lds_of(C), tw, c, s); break;
+            default: launch_int_cols<64, MC_EPL_W, true>(p, Z, blocks, W, C, ngroups, lds_of(C), tw, c, s);
+        }
+        return;
+    }
     auto fits = [&](int C, int nt) { return len <= MC_EPL * (nt / C) && lds_of(C) <= (nt == 512 ? 80 : 160) * 1024; };
     int nt = 512, C = 1;
     while (C < 16 && fits(2 * C, 512)) C *= 2;
@@ -854,22 +897,9 @@ void mr_int_cols(const MrPlan& p, float2* Z, int nb, int W, const float2* tw, co
         if (!fits(C, 1024)) throw std::runtime_error("mr_int_cols: column length " + std::to_string(len) + " exceeds the workgroup");
     }
     const int ngroups = (W + C - 1) / C;
-    const size_t lds = lds_of(C);
     const long blocks = (long)nb * ngroups;
-    static bool attr = false;
-    if (!attr) {
-        FCD_HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mr_int_cols<512>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        FCD_HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mr_int_cols<1024>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        attr = true;
-    }
-    const unsigned grid = (unsigned)((blocks + 7) / 8 * 8);
-    if (nt == 512)
-        hipLaunchKernelGGL(k_mr_int_cols<512>, dim3(grid), dim3(512), lds, s, Z, (int)blocks, W, C, ngroups, p, tw, c);
-    else
-        hipLaunchKernelGGL(k_mr_int_cols<1024>, dim3(grid), dim3(1024), lds, s, Z, (int)blocks, W, C, ngroups, p, tw, c);
-    FCD_CHECK_LAUNCH();
+    if (nt == 512) launch_int_cols<512, MC_EPL, false>(p, Z, blocks, W, C, ngroups, lds_of(C), tw, c, s);
+    else launch_int_cols<1024, MC_EPL, false>(p, Z, blocks, W, C, ngroups, lds_of(C), tw, c, s);
 }
 
 void mr_transpose(const float2* in, float2* out, int nb, int R, int C, hipStream_t s) {
