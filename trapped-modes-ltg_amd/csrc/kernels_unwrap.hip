@@ -1195,7 +1195,9 @@ __global__ __launch_bounds__(TW * TH / 4, 4) void k_mst_tile0(const float* __res
     __shared__ __attribute__((aligned(16))) unsigned char pool[16 * T0N];
     unsigned long long* const bw = reinterpret_cast<unsigned long long*>(pool);  // component minima (f64 bits)
     int* const be = reinterpret_cast<int*>(pool + 8 * T0N);                      // their edge codes
-    unsigned* const lnk = reinterpret_cast<unsigned*>(pool + 8 * T0N);           // then the roots' links
+    // the roots' links (their own array, so the hooks write them directly and the minima's
+    // reset needs no barrier of its own; 1 workgroup per CU by registers, LDS to spare)
+    __shared__ unsigned lnk[T0N];
     short* const lc = reinterpret_cast<short*>(pool + 12 * T0N);                 // component of each pixel
     short* const lo = reinterpret_cast<short*>(pool + 14 * T0N);                 // K(pixel) - K(component)
     float* const ws = reinterpret_cast<float*>(pool);
@@ -1289,6 +1291,7 @@ __global__ __launch_bounds__(TW * TH / 4, 4) void k_mst_tile0(const float* __res
         lo[i] = 0;
         bw[i] = 0x7ff0000000000000ull;
         be[i] = 0x7fffffff;
+        lnk[i] = t0_link(i, 0);  // (a root's link stays its own: only hooked roots' links change)
     }
     __shared__ int t0roots[2];  // the capped rounds' component counts (by round parity)
     if (threadIdx.x == 0) t0roots[0] = t0roots[1] = 0;
@@ -1353,9 +1356,8 @@ __global__ __launch_bounds__(TW * TH / 4, 4) void k_mst_tile0(const float* __res
         // (the minima are final: with few enough components they are round 0 of the graph)
         if (capped && t0roots[nrounds & 1] <= cg_ccap(TW, TH)) break;
         // (c) hooks: the pixel holding its component's lightest edge (unique: weight,
-        // then edge code) decides, if that edge ends inside the tile, and leaves the link
-        // in the component's (no longer needed) minimum slot, marked by bit 63 (a weight's
-        // bits never have it); the roots then move the links over their edge codes
+        // then edge code) decides, if that edge ends inside the tile, and writes the
+        // component's link (every current root's link is its own until then)
         int hooked = 0;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -1371,25 +1373,24 @@ __global__ __launch_bounds__(TW * TH / 4, 4) void k_mst_tile0(const float* __res
             const int delta = (d == 0 || d == 2) ? -inc : inc;  // k(y) - k(i) across the edge
             const int dr = lc[y];
             if (be[dr] == ke[k] && c < dr) continue;  // mutual pair: the smaller root stays
-            bw[c] = (1ull << 63) | t0_link(dr, lo[y] - lor[k] - delta);  // K_c - K_dr
+            lnk[c] = t0_link(dr, lo[y] - lor[k] - delta);  // K_c - K_dr
             hooked = 1;
         }
         const int any = __syncthreads_or(hooked);
         if (!any) break;
-        // (this thread's pixels' labels are still cs[]: lc changes only in the relabel step)
+        T0_STAMP(4);
+        // the minima's reset for the next round (nothing reads them after the hooks)
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const int c = threadIdx.x + NT * k;
-            if (cs[k] != c) continue;
-            const unsigned long long v = bw[c];
-            lnk[c] = (v >> 63) ? (unsigned)v : t0_link(c, 0);
+            const int i = threadIdx.x + NT * k;
+            bw[i] = 0x7ff0000000000000ull;
+            be[i] = 0x7fffffff;
         }
-        __syncthreads();
-        T0_STAMP(4);
         // (d) every hooked root to its final root (a root's link is one 32-bit word, so
         // parent and offset are read together)
         // each root walks to its final root, publishing the shortcuts as it goes (lockstep
-        // pointer jumping with a barrier per pass measured 9.0 k vs 9.9 k frames/s, r04aj)
+        // pointer jumping with a barrier per pass measured 9.0 k vs 9.9 k frames/s, r04aj;
+        // every pixel walking, no barrier before the relabel: 10.45 k -> 10.12 k, r05t)
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int c = threadIdx.x + NT * k;
@@ -1408,22 +1409,14 @@ __global__ __launch_bounds__(TW * TH / 4, 4) void k_mst_tile0(const float* __res
         }
         __syncthreads();
         T0_STAMP(5);
-        int nc[4], no[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const unsigned l = lnk[cs[k]];
-            nc[k] = t0_parent(l);
-            no[k] = lor[k] + t0_off(l);
-        }
-        __syncthreads();
+        // labels and offsets (this phase reads only links)
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int i = threadIdx.x + NT * k;
-            lc[i] = (short)nc[k];
-            lo[i] = (short)no[k];
-            lor[k] = (short)no[k];
-            bw[i] = 0x7ff0000000000000ull;
-            be[i] = 0x7fffffff;
+            const unsigned l = lnk[cs[k]];
+            lc[i] = (short)t0_parent(l);
+            lo[i] = (short)(lor[k] + t0_off(l));
+            lor[k] = (short)(lor[k] + t0_off(l));
         }
         __syncthreads();
         T0_STAMP(6);
