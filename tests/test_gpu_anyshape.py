@@ -171,8 +171,25 @@ def test_long_sides_match_oracle(shape):
     Bluestein with M = 16384, the columns through the transpose route), 8200 (2^3 5^2 41:
     a generic radix-41 pass over 8200-point rows), 16384 (2^14).  Setup bit-exact against
     the oracle's restatement of the reference's spectrum, heights rel-L2 1e-5 against the
-    oracle (fcd.compute_height_map with the unwrap), the k-fields of the maps equal to the
-    oracle's on the engine's phases (up to the constant)."""
+    oracle (fcd.compute_height_map with the unwrap, and the oracle's unwrap and integration on
+    the engine's phases), the k-fields of the maps equal to the oracle's on the engine's phases (up to the
+    constant)."""
+    check_shape_against_oracle(shape)
+
+
+@pytest.mark.parametrize("shape", [(509, 384), (97, 1000), (1200, 250), (1536, 160)])
+def test_integration_column_paths_match_oracle(shape):
+    """The generic integration's column kernel (kernels_mr.hip k_mr_int_cols) in each of its
+    forms: one wave per column with Bluestein columns (509: M = 1024 with 4 columns per
+    group; 97: M = 256 with 16), one wave per 1200-point mixed-radix column, and a
+    multi-wave team per 1536-point column.  Same checks as test_long_sides_match_oracle (at
+    509 x 384 one pixel next to a branch cut takes another k in the oracle's own chain -- its
+    f32 phases' last bits on the other side of pi -- so there the heights are checked
+    against the oracle's unwrap and integration of the engine's phases only)."""
+    check_shape_against_oracle(shape)
+
+
+def check_shape_against_oracle(shape):
     from bench_data import make_residue_frame
     from oracle import fcd_oracle as O
     from pyfcd import _lib
@@ -190,12 +207,24 @@ def test_long_sides_match_oracle(shape):
     hf, _, _ = eng.process(frame[None], 1.0, unwrap=True, want_phases=False)
     assert np.array_equal(h, hf)
     ho, _, _, ex = O.compute_height_map(ref, frame, 0.001, height=1.0)
-    assert rel_l2(h[0], ho) < 1e-5, rel_l2(h[0], ho)
+    flips = 0
+    phases = np.zeros((2, rows, cols))
     for m in range(2):
         assert wrap_diff(w[0][m], ex["wrapped"][m]).max() < 2e-4
-        _, ko = O.unwrap(w[0][m])
+        phases[m], ko = O.unwrap(w[0][m])
         d = k[0][m].astype(np.int64) - ko
         assert np.all(d == d.flat[0]), m
+        # the oracle's own k-field: it may differ at a pixel next to a branch cut, where the
+        # two f32 phase chains' last bits fall on either side of +-pi (test_gpu_large)
+        dk = ex["k"][m].astype(np.int64) - ko
+        flips += int(np.count_nonzero(dk != dk.flat[0]))
+    assert flips <= 2, flips
+    if flips == 0:
+        assert rel_l2(h[0], ho) < 1e-5, rel_l2(h[0], ho)
+    # heights against the oracle's chain (its unwrap and integration) on the engine's phases
+    disp = O.displacement_field(phases, ex["carriers"])
+    he = O.integrate_in_fourier(-disp[0], -disp[1], info.calibration_factor)
+    assert rel_l2(h[0], he) < 1e-5, rel_l2(h[0], he)
     eng.close()
 
 

@@ -873,7 +873,7 @@ void mr_int_cols(const MrPlan& p, float2* Z, int nb, int W, const float2* tw, co
     if (!mr_int_cols_supported(p)) throw std::runtime_error("mr_int_cols: a radix above 8");
     const int len = p.blue ? p.M : p.n;
     auto lds_of = [&](int C) { return (size_t)(C * (len + 1) + len) * sizeof(float2); };
-    if (len <= MC_EPL_W * 64) {  // wave teams
+    if (len <= MC_EPL_W * 64) {  // wave teams (bit-identical to the block teams: same passes and order)
         int C = 16;
         while (C > 1 && lds_of(C) > 80 * 1024) C /= 2;
         const int ngroups = (W + C - 1) / C;
