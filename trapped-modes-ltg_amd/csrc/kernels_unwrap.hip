@@ -169,39 +169,44 @@ void residues(const float* w, int nmaps, int H, int W, int* counts, hipStream_t 
 
 // ------------------------------------------------------------------ residue-free scan path
 // colk[map][i] = k(i, 0) = -sum_{i' < i} find_wrap(w[i'][0], w[i'+1][0])
-__global__ __launch_bounds__(256) void k_colk(const float* __restrict__ w, int H, long map_stride, long W,
-                                              int* __restrict__ colk) {
-    __shared__ int part[256];
-    const int map = blockIdx.x;
+// One wave per map (a 64-thread block), 8 rows per lane and chunk, a wave scan of the
+// lanes' sums, the running total carried over chunks.  At most 32 VGPRs and no LDS, so its
+// blocks fit beside the other stream's fused kernel (2 waves / SIMD at 235 VGPRs) instead
+// of waiting for that kernel's CUs: the 256-thread form (loc[64], ~80 VGPRs) ran 6-188 us
+// per launch in the two-stream headline chain, ahead of the integration (r05c).
+// CONTIG: the compact column-0 copy (row stride 1: immediate load offsets, ~30 VGPRs).
+constexpr int COLK_R = 8;
+template <bool CONTIG>
+__global__ __launch_bounds__(64) void k_colk(const float* __restrict__ w, int H, long map_stride, long W_,
+                                             int* __restrict__ colk) {
+    const long W = CONTIG ? 1 : W_;
+    const int map = blockIdx.x, lane = threadIdx.x;
     const float* m = w + (long)map * map_stride;
-    const int per = (H + 255) / 256;  // <= 64
-    const int i0 = threadIdx.x * per;
-    int loc[64];
-    int sum = 0;
-#pragma unroll
-    for (int q = 0; q < 64; ++q) {
-        const int i = i0 + q;
-        loc[q] = 0;
-        if (q < per && i + 1 < H) {
-            sum -= find_wrap(m[(long)i * W], m[(long)(i + 1) * W]);  // W: row stride
-        }
-        loc[q] = sum;  // inclusive within the thread: k(i+1,0) - base
-    }
-    part[threadIdx.x] = sum;
-    __syncthreads();
-    // exclusive scan of part (256 entries)
-    for (int off = 1; off < 256; off <<= 1) {
-        const int v = (int)threadIdx.x >= off ? part[threadIdx.x - off] : 0;
-        __syncthreads();
-        part[threadIdx.x] += v;
-        __syncthreads();
-    }
-    const int base = threadIdx.x ? part[threadIdx.x - 1] : 0;
     int* out = colk + (long)map * H;
+    int carry = 0;
+    for (int i0 = 0; i0 < H; i0 += 64 * COLK_R) {
+        const int r0 = i0 + lane * COLK_R;
+        float v[COLK_R + 1];
 #pragma unroll
-    for (int q = 0; q < 64; ++q) {
-        const int i = i0 + q;
-        if (q < per && i < H) out[i] = base + (q ? loc[q - 1] : 0);
+        for (int q = 0; q <= COLK_R; ++q) v[q] = r0 + q < H ? m[(long)(r0 + q) * W] : 0.f;
+        int loc[COLK_R];  // exclusive: sum of d over rows r0 .. r0 + q - 1
+        int sum = 0;
+#pragma unroll
+        for (int q = 0; q < COLK_R; ++q) {
+            loc[q] = sum;
+            if (r0 + q + 1 < H) sum -= find_wrap(v[q], v[q + 1]);
+        }
+        int incl = sum;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int t = __shfl_up(incl, off, 64);
+            if (lane >= off) incl += t;
+        }
+        const int base = carry + incl - sum;
+#pragma unroll
+        for (int q = 0; q < COLK_R; ++q)
+            if (r0 + q < H) out[r0 + q] = base + loc[q];
+        carry += __shfl(incl, 63, 64);
     }
 }
 
@@ -241,18 +246,18 @@ __global__ __launch_bounds__(256) void k_rowscan(const float* __restrict__ w, lo
 }
 
 void unwrap_colk(const float* w, int nmaps, int H, int W, int* colk, hipStream_t s) {
-    hipLaunchKernelGGL(k_colk, dim3(nmaps), dim3(256), 0, s, w, H, (long)H * W, (long)W, colk);
+    hipLaunchKernelGGL(k_colk<false>, dim3(nmaps), dim3(64), 0, s, w, H, (long)H * W, (long)W, colk);
     FCD_CHECK_LAUNCH();
 }
 
 void unwrap_colk_compact(const float* col0, int nmaps, int H, int* colk, hipStream_t s) {
-    hipLaunchKernelGGL(k_colk, dim3(nmaps), dim3(256), 0, s, col0, H, (long)H, 1L, colk);
+    hipLaunchKernelGGL(k_colk<true>, dim3(nmaps), dim3(64), 0, s, col0, H, (long)H, 1L, colk);
     FCD_CHECK_LAUNCH();
 }
 
 void unwrap_scan(const float* w, int nmaps, int H, int W, int* colk, int32_t* k, hipStream_t s) {
     if (H > 16384) throw std::runtime_error("unwrap_scan: H too large");
-    hipLaunchKernelGGL(k_colk, dim3(nmaps), dim3(256), 0, s, w, H, (long)H * W, (long)W, colk);
+    hipLaunchKernelGGL(k_colk<false>, dim3(nmaps), dim3(64), 0, s, w, H, (long)H * W, (long)W, colk);
     FCD_CHECK_LAUNCH();
     const long nrows = (long)nmaps * H;
     hipLaunchKernelGGL(k_rowscan, dim3((unsigned)((nrows + 3) / 4)), dim3(256), 0, s, w, nrows, H, W, colk, k);
