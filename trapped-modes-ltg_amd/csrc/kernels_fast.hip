@@ -90,9 +90,8 @@ struct KCfg {
 #ifndef FCD_INTCOLS_WAVES_E16
 #define FCD_INTCOLS_WAVES_E16 2  // at 16 elements per lane (3: 168 VGPRs, 22 spilled, 2.81 -> 3.71 us/frame, kbench r03w3)
 #endif
-// k_int_cols prefetches the next item's column (PREF_X) always and its mirror column
-// (PREF_Y) at 4096 points (2 waves / SIMD either way there); it reads ky_eff / ky^2 from
-// LDS copies.
+// k_int_cols prefetches the next item's column; its mirror column is loaded at the top of
+// the item (16 fewer VGPRs live across the transforms; IntColsCfg).
 #ifndef FCD_INTCOLS_QUADS
 #define FCD_INTCOLS_QUADS 1  // 4-row Zt tiles: sibling blocks on one XCD share each line's 4 columns
 #endif
@@ -124,7 +123,14 @@ template <int N>
 struct IntColsCfg : KCfg<N, FCD_INTCOLS_BLOCK, int_cols_elems(N)> {
     // 16 elements per lane at 1024: 186 VGPRs, 2 waves / SIMD
     static constexpr int V = N <= 1024 ? (int_cols_elems(N) == 16 ? FCD_INTCOLS_WAVES_E16 : FCD_INTCOLS_WAVES) : ColWaves<N>::V;
-    static constexpr bool PREF_Y = N >= 4096;
+    // The row wavenumber tables as LDS copies below 4096 points.  At 4096 they are read
+    // from global memory (L1 / L2) and the next item's mirror column is no longer
+    // prefetched (248 VGPRs, no spills): the 99 KB of LDS with the copies held the 4-wave
+    // workgroup (room for two by registers) at one per CU; the twiddle table and the
+    // team's exchange row (67 KB) let two run.  c5 3.13 k -> 3.36-3.38 k frames/s,
+    // int_cols + c2r 124.9 -> 107.8 us/frame (r05y / r05z; the ky loads from global memory
+    // WITH the mirror prefetch spill 59 VGPRs, the twiddles from global memory 62).
+    static constexpr bool LKY = N < 4096;
 };
 
 // find_wrap(a, b) of the reference unwrapper with an f32 fast path:
@@ -409,11 +415,18 @@ __global__ __launch_bounds__(IntColsCfg<H>::THREADS, IntColsCfg<H>::V) void k_in
     RegFFT<H, false, C::E> fft;
     fft.init(tw, lds_raw, threadIdx.x, C::THREADS);
     // the row wavenumber tables (ky_eff, ky^2) of every element, read per item: LDS copies
-    float* const lky = reinterpret_cast<float*>(lds + TEAMS * C::ROW);
-    float* const lky2 = lky + H;
-    for (int i = threadIdx.x; i < H; i += C::THREADS) {
-        lky[i] = c.kye[i];
-        lky2[i] = c.ky2[i];
+    // (LKY) or the tables themselves
+    const float* lky = c.kye;
+    const float* lky2 = c.ky2;
+    if constexpr (C::LKY) {
+        float* const k1 = reinterpret_cast<float*>(lds + TEAMS * C::ROW);
+        float* const k2 = k1 + H;
+        for (int i = threadIdx.x; i < H; i += C::THREADS) {
+            k1[i] = c.kye[i];
+            k2[i] = c.ky2[i];
+        }
+        lky = k1;
+        lky2 = k2;
     }
     __syncthreads();
     const int NCH = W / 2 + 1;
@@ -494,7 +507,6 @@ __global__ __launch_bounds__(IntColsCfg<H>::THREADS, IntColsCfg<H>::V) void k_in
         fetch_fc(valid ? code / CW : 0, valid ? code % CW : 0, mirror, v);
     };
     auto fetch = [&](int code) {
-        if constexpr (C::PREF_Y) fetch_col(code, true, py);
         fetch_col(code, false, px);
     };
     fetch(c0 + team * cstep);
@@ -507,7 +519,7 @@ __global__ __launch_bounds__(IntColsCfg<H>::THREADS, IntColsCfg<H>::V) void k_in
         // column -c: sum_y z(y, -c) e^{+2 pi i ky y / H} at index ky, so both operands
         // of the Hermitian split sit in the same lane and slot (no mirror exchange).
         float2 x[E], y[E];
-        if constexpr (!C::PREF_Y) fetch_col(item, true, py);
+        fetch_col(item, true, py);
 #pragma unroll
         for (int q = 0; q < E; ++q) {
             y[q] = py[q];
@@ -793,7 +805,7 @@ template <int H>
 static void launch_int_cols(const float2* Zt, int W, int nb, const IntegCoef& c, float2* Ht, const float2* tw,
                             hipStream_t s, const int* colk) {
     using C = IntColsCfg<H>;
-    const size_t lds = (size_t)C::NLEN * 8 + (size_t)C::TEAMS * C::ROW * 8 + (size_t)H * 8;
+    const size_t lds = (size_t)C::NLEN * 8 + (size_t)C::TEAMS * C::ROW * 8 + (C::LKY ? (size_t)H * 8 : 0);
     set_lds(k_int_cols<H>, lds);
     const int grid = grid_for(((long)nb * (W / 2 + 1) + C::TEAMS - 1) / C::TEAMS, 4);
     const int zt = zt_layout(W);
