@@ -158,11 +158,11 @@ constexpr int DR_HCR = FCD_DR_HCREG;
 // values straight to Xb instead, 16 bytes per column, measured 25.9 vs 26.0 us/frame at
 // 4096 and 5.94 vs 5.66 at 2048 but k_demod_cols +0.24 behind it, kbench r03v.)
 
-template <int W>
-__global__ __launch_bounds__(KCfg<W>::THREADS, FCD_MIN_WAVES) void k_demod_rows(const float* __restrict__ frames, int H, int nb,
+template <int W, int B = BLOCK>
+__global__ __launch_bounds__((KCfg<W, B>::THREADS), FCD_MIN_WAVES) void k_demod_rows(const float* __restrict__ frames, int H, int nb,
                                                       DemodTables T, float2* __restrict__ Xb,
                                                       const float2* __restrict__ tw) {
-    using C = KCfg<W>;
+    using C = KCfg<W, B>;
     constexpr int TT = C::TT, E = C::E, TEAMS = C::TEAMS;
     extern __shared__ __attribute__((aligned(16))) float2 lds_raw[];
     float2* const lds = lds_raw + C::NLEN;  // lds_raw[0, NLEN): the twiddle table
@@ -720,6 +720,19 @@ static void set_lds(K kernel, size_t bytes) {
 template <int W>
 static void launch_demod_rows(const float* frames, int H, int nb, const DemodTables& T, float2* Xb, const float2* tw,
                               hipStream_t s) {
+    // 4096-point rows: 1024-thread workgroups (two 8-wave teams share the twiddle table and
+    // the staged band block: 16 waves per CU instead of 8) when the band block leaves room
+    // for the second exchange row (c5 demod 33.6 -> 32.0 us/frame; at 2048 four 4-wave
+    // teams measured 7.64 -> 7.96, r05za / r05zb)
+    using C2 = KCfg<W, 1024>;
+    const size_t lds2 = (size_t)C2::NLEN * 8 + (size_t)C2::TEAMS * C2::ROW * 8 + (size_t)T.NC * (TILE + 1) * 8;
+    if (W >= 4096 && C2::TEAMS >= 2 && lds2 <= 160 * 1024) {
+        set_lds(k_demod_rows<W, 1024>, lds2);
+        const int grid = grid_for((long)nb * (H / TILE), 1);
+        hipLaunchKernelGGL((k_demod_rows<W, 1024>), dim3(grid), dim3(C2::THREADS), lds2, s, frames, H, nb, T, Xb, tw);
+        FCD_CHECK_LAUNCH();
+        return;
+    }
     using C = KCfg<W>;
     const size_t lds = (size_t)C::NLEN * 8 + (size_t)C::TEAMS * C::ROW * 8 + (size_t)T.NC * (TILE + 1) * 8;
     set_lds(k_demod_rows<W>, lds);
