@@ -48,7 +48,7 @@ groups, in_group = [], set()
 for i, k in enumerate(names):
     if k in BAND and len(groups) < n_roof:
         j_cols = max(j for j in range(i) if names[j] == "fcdk::k_demod_cols<1024>")
-        j_rows = max(j for j in range(j_cols) if names[j] == "fcdk::k_demod_rows<1024>")
+        j_rows = max(j for j in range(j_cols) if names[j] in ("fcdk::k_demod_rows<1024>", "fcdk::k_demod_rows<1024, 256>"))
         groups.append((dur[j_rows], dur[j_cols], dur[i]))
         in_group.update((j_rows, j_cols, i))
 streams = int(sys.argv[3]) if len(sys.argv) > 3 else prof_bench["config"].get("streams_per_chunk", 1)
