@@ -363,6 +363,8 @@ fcdk::MstWork mst_work(fcd_ctx* c, MstSpace& S) {
     m.cg_ed = S.cg_ed.as<int>();
     m.Hr = c->H;
     m.Wr = c->W;
+    m.Hs = c->H;
+    m.Ws = c->W;
     return m;
 }
 
@@ -423,12 +425,21 @@ int mst_level() {
 // the rest of a map once it has found one
 // H x W: the maps' (padded) size, multiples of 64 for the tile passes; Hr x Wr: the
 // frame's own size (the reliabilities' border, MstWork::Hr / Wr).
-void unwrap_core(fcd_ctx* c, MstSpace& S, const float* w, int nmaps, int H, int W, int Hr, int Wr, int32_t* k,
-                 int* res_host, hipStream_t s, bool all_mst, fcdk::MstK* mk, bool any_res, bool colk_only = false) {
+// frame_ids (the generic chain's copy-free pass, H x W the padded size, Hr x Wr the
+// frame's): the maps listed (indices into w and k, both in the frame's own layout) go
+// through the tile pass and the component-graph rounds with no padded copies -- the tiles'
+// clamped loads replicate the last row / column as the copy would, the k-field is written
+// in the frame's layout; returns false, with nothing written, if a tile graph exceeds its
+// capacity (the caller then takes the padded copy and the list rounds).
+bool unwrap_core(fcd_ctx* c, MstSpace& S, const float* w, int nmaps, int H, int W, int Hr, int Wr, int32_t* k,
+                 int* res_host, hipStream_t s, bool all_mst, fcdk::MstK* mk, bool any_res, bool colk_only = false,
+                 const std::vector<int>* frame_ids = nullptr) {
     if (mk) mk->map_slot = nullptr;
     const long hw = (long)H * W;
     std::vector<int> active;
-    if (all_mst) {
+    if (frame_ids) {
+        active = *frame_ids;
+    } else if (all_mst) {
         for (int i = 0; i < nmaps; ++i) active.push_back(i);
     } else {
         S.rescnt.ensure((size_t)nmaps * sizeof(int));
@@ -443,16 +454,18 @@ void unwrap_core(fcd_ctx* c, MstSpace& S, const float* w, int nmaps, int H, int 
     }
     // the scan unwrap for the residue-free maps (the MST pass overwrites the others);
     // skipped when every map has residues (the fix-up groups of camera frames)
-    if ((int)active.size() < nmaps) {
+    if (!frame_ids && (int)active.size() < nmaps) {
         S.colk.ensure((size_t)nmaps * H * sizeof(int));
         if (colk_only) fcdk::unwrap_colk(w, nmaps, H, W, S.colk.as<int>(), s);
         else fcdk::unwrap_scan(w, nmaps, H, W, S.colk.as<int>(), k, s);
     }
-    if (active.empty()) return;
+    if (active.empty()) return true;
     ensure_mst(c, S, (int)active.size(), hw);
     fcdk::MstWork m = mst_work(c, S);
     m.Hr = Hr;
     m.Wr = Wr;
+    m.Hs = frame_ids ? Hr : H;
+    m.Ws = frame_ids ? Wr : W;
     const int nact = (int)active.size();
     upload(S.ids.p, active.data(), sizeof(int) * nact, s);
     const int max_rounds = 64;
@@ -462,6 +475,7 @@ void unwrap_core(fcd_ctx* c, MstSpace& S, const float* w, int nmaps, int H, int 
     int level = mst_level();
     int tile_h = 0;
     const int tile_w = fcdk::mst_tile_shape(H, W, &tile_h);
+    if (frame_ids && !(level == 3 && tile_w > 0)) return false;
     if (level == 3 && tile_w > 0) {
         HIPCHK(hipMemsetAsync(m.nhooks + 1, 0, (1 + fcdk::kCgRounds) * sizeof(int), s));
         fcdk::mst_tile_level0(w, S.ids.as<int>(), nact, H, W, m, s, true);
@@ -516,11 +530,12 @@ void unwrap_core(fcd_ctx* c, MstSpace& S, const float* w, int nmaps, int H, int 
                 S.slot.ensure(slot.size() * sizeof(int));
                 upload(S.slot.p, slot.data(), slot.size() * sizeof(int), s);
                 *mk = fcdk::MstK{m.crank, m.coff, m.offk, S.slot.as<int>(), fcdk::mst_cg_geom(H, W)};
-                return;
+                return true;
             }
-            fcdk::mst_cg_finalize(S.ids.as<int>(), nact, H, W, m, k, s);
-            return;
+            fcdk::mst_cg_finalize(S.ids.as<int>(), nact, H, W, m, k, s, frame_ids != nullptr);
+            return true;
         }
+        if (frame_ids) return false;
         level = 2;  // the boundary-list rounds need no capacity bound
         rounds = 0;
     }
@@ -563,7 +578,7 @@ void unwrap_core(fcd_ctx* c, MstSpace& S, const float* w, int nmaps, int H, int 
         }
         if (rounds >= max_rounds) throw FcdError(FCD_E_INTERNAL, "unwrap: Boruvka did not converge");
         fcdk::mst_level_finalize(S.ids.as<int>(), nact, H, W, m, k, s);
-        return;
+        return true;
     }
     fcdk::mst_init(w, S.ids.as<int>(), nact, H, W, m, s);
     for (; rounds < max_rounds; rounds += 3) {
@@ -576,6 +591,7 @@ void unwrap_core(fcd_ctx* c, MstSpace& S, const float* w, int nmaps, int H, int 
     }
     if (rounds == max_rounds) throw FcdError(FCD_E_INTERNAL, "unwrap: Boruvka did not converge");
     fcdk::mst_finalize(S.ids.as<int>(), nact, H, W, m, k, s);
+    return true;
 }
 
 // k-fields of nmaps wrapped maps of the context's frame size (unwrap_core).  A frame whose
@@ -617,6 +633,14 @@ void unwrap_maps(fcd_ctx* c, const float* w, int nmaps, int32_t* k, int* res_hos
     if (active.empty()) return;
     const int nact = (int)active.size();
     const int Hp = (H + 63) / 64 * 64, Wp = (W + 63) / 64 * 64;
+    // the tile pass and the component-graph rounds straight on the maps (no padded copy of
+    // the phases, the k-field written in the frame's layout: 1080 x 1920 with residues,
+    // pad_maps + unpad_k were ~0.53 ms of a 32-frame chunk's ~7 ms); the padded copy below
+    // only for the other MST levels or a tile graph over its capacity
+    if (unwrap_core(c, S, w, nmaps, Hp, Wp, H, W, k, nullptr, s, true, nullptr, false, false, &active)) {
+        HIPCHK(hipStreamSynchronize(s));  // (active, the ids' host copy, dies here)
+        return;
+    }
     const size_t np = (size_t)nact * Hp * Wp;
     S.pad_w.ensure(np * sizeof(float));
     S.pad_k.ensure(np * sizeof(int32_t));

@@ -286,6 +286,11 @@ struct MstWork {
     // heavier than every edge of the frame and the frame's MST is the padded graph's
     // restricted to the frame (the k-field of the frame's pixels is unchanged)
     int Hr, Wr;
+    // the layout the tile pass loads the wrapped phases from: the maps as given (Hs x Ws =
+    // the unwrap's H x W), or (the generic chain's level-3 pass) the frame's own maps,
+    // Hr x Wr, whose clamped loads replicate the last row / column exactly as the padded
+    // copy does
+    int Hs, Ws;
 };
 constexpr double kPadRel = 1e300;
 // Maps listed in map_ids (device int[nact]) of the wrapped stack w.
@@ -311,7 +316,10 @@ long mst_cg_edge_capacity(long nv);  // edge records for nv vertices (any tile s
 constexpr int kCgRounds = 72;
 void mst_cg_round(int nact, int H, int W, MstWork m, int r, hipStream_t s);
 // k of the component-graph path (every level-0 component's offk final)
-void mst_cg_finalize(const int* map_ids, int nact, int H, int W, MstWork m, int32_t* k, hipStream_t s);
+// frame_layout: k is the frame's own layout (maps of m.Hr x m.Wr, map_ids index it), the
+// pad pixels dropped; else the unwrap's H x W layout
+void mst_cg_finalize(const int* map_ids, int nact, int H, int W, MstWork m, int32_t* k, hipStream_t s,
+                     bool frame_layout = false);
 CgGeom mst_cg_geom(int H, int W);
 void mst_level_setup(int nact, int H, int W, MstWork m, hipStream_t s);
 void mst_level_round(const float* w, const int* map_ids, int nact, int H, int W, MstWork m, int r, hipStream_t s);

@@ -1214,7 +1214,7 @@ __global__ __launch_bounds__(TW * TH / 4, 4) void k_mst_tile0(const float* __res
     const int tiles_x = W / TW, tiles = (H / TH) * tiles_x;
     const int slot = blockIdx.x / tiles, tile = blockIdx.x % tiles;
     const int gi0 = (tile / tiles_x) * TH, gj0 = (tile % tiles_x) * TW;
-    const float* mw = w + (long)map_ids[slot] * hw;
+    const float* mw = w + (long)map_ids[slot] * ((long)m.Hs * m.Ws);
     const long vbase = (long)slot * hw;
     // wrapped phases, 2-pixel halo (outside the map: never read for an existing edge).
     // All of a thread's loads are issued before the first LDS store (clamped addresses,
@@ -1226,8 +1226,8 @@ __global__ __launch_bounds__(TW * TH / 4, 4) void k_mst_tile0(const float* __res
     for (int u = 0; u < NL; ++u) {
         const int i = threadIdx.x + u * NT;
         const int gi = gi0 - 2 + i / T0W, gj = gj0 - 2 + i % T0W;
-        const int ci = min(max(gi, 0), H - 1), cj = min(max(gj, 0), W - 1);
-        v[u] = mw[(long)ci * W + cj];
+        const int ci = min(max(gi, 0), m.Hs - 1), cj = min(max(gj, 0), m.Ws - 1);
+        v[u] = mw[(long)ci * m.Ws + cj];
     }
 #pragma unroll
     for (int u = 0; u < NL; ++u) asm volatile("" ::"v"(v[u]));  // (keeps the last load up here)
@@ -1692,6 +1692,7 @@ void mst_cg_round(int nact, int H, int W, MstWork m, int r, hipStream_t s) {
 }
 
 // k(v) = K[component] + off(v) - (the same at the map's pixel 0): 4 pixels per thread.
+template <bool FRAME>
 __global__ __launch_bounds__(256) void k_cg_finalize(const int* __restrict__ map_ids, int nact, MstWork m, CgGeom geo,
                                                      int32_t* __restrict__ k) {
     const long v = 4 * ((long)blockIdx.x * blockDim.x + threadIdx.x);
@@ -1704,13 +1705,27 @@ __global__ __launch_bounds__(256) void k_cg_finalize(const int* __restrict__ map
     const short4 o = *reinterpret_cast<const short4*>(m.coff + v);
     const int4 kv = make_int4(m.offk[cb + r.x] + o.x - kb, m.offk[cb + r.y] + o.y - kb, m.offk[cb + r.z] + o.z - kb,
                               m.offk[cb + r.w] + o.w - kb);
-    *reinterpret_cast<int4*>(k + (long)map_ids[slot] * geo.hw + (v - base)) = kv;
+    if constexpr (FRAME) {  // the frame's own layout: pixels past Hr x Wr are pad
+        const long p = v - base;
+        const int i = (int)(p / geo.W), j = (int)(p % geo.W);
+        if (i >= m.Hr) return;
+        int32_t* kr = k + (long)map_ids[slot] * ((long)m.Hr * m.Wr) + (long)i * m.Wr;
+        const int kk[4] = {kv.x, kv.y, kv.z, kv.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (j + q < m.Wr) kr[j + q] = kk[q];
+    } else {
+        *reinterpret_cast<int4*>(k + (long)map_ids[slot] * geo.hw + (v - base)) = kv;
+    }
 }
 
-void mst_cg_finalize(const int* map_ids, int nact, int H, int W, MstWork m, int32_t* k, hipStream_t s) {
+void mst_cg_finalize(const int* map_ids, int nact, int H, int W, MstWork m, int32_t* k, hipStream_t s,
+                     bool frame_layout) {
     const CgGeom geo = mst_cg_geom(H, W);
     const long n4 = (long)nact * H * W / 4;
-    hipLaunchKernelGGL(k_cg_finalize, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, map_ids, nact, m, geo, k);
+    const dim3 g((unsigned)((n4 + 255) / 256));
+    if (frame_layout) hipLaunchKernelGGL(k_cg_finalize<true>, g, dim3(256), 0, s, map_ids, nact, m, geo, k);
+    else hipLaunchKernelGGL(k_cg_finalize<false>, g, dim3(256), 0, s, map_ids, nact, m, geo, k);
     FCD_CHECK_LAUNCH();
 }
 
