@@ -345,8 +345,10 @@ def main():
                                f"(demod + unwrap + integration), reference state cached",
                    "frame": n, "batch_per_gpu": B, "global_batch": B * world,
                    "parallelism": f"frame-sharded x{world}, no collective in the compute",
-                   # each step's chunk runs as this many concurrent halves (engine FCD_STREAMS)
-                   "streams_per_chunk": 2 if int(os.environ.get("FCD_STREAMS", "2")) >= 2 else 1},
+                   # each step's chunk runs as this many concurrent parts (engine FCD_STREAMS;
+                   # default two up to 1024-wide rows, one above)
+                   "streams_per_chunk": (2 if int(os.environ["FCD_STREAMS"]) >= 2 else 1) if os.environ.get("FCD_STREAMS")
+                   else (2 if n <= 1024 else 1)},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic_launch,

@@ -237,6 +237,7 @@ struct fcd_ctx {
     bool fused_ok = false;           // k_phase_rows applies (height-only calls)
     bool force_unfused = false;      // FCD_UNFUSED=1: take the unfused chain (A/B measurement)
     int nstreams = 2;                // FCD_STREAMS: device-path chunks split over 1 or 2 streams
+    int fused_split = 2;             // ... for the fused chain (default: 2 up to 1024-wide rows, 1 above)
     bool early_census = true;        // FCD_EARLY_CENSUS: device calls read the census back before the integration
     hipStream_t cstream = nullptr;   // its copy stream and the two halves' "census complete" events
     hipEvent_t ev_cen[2] = {nullptr, nullptr};
@@ -944,9 +945,10 @@ void build_demod_tables(fcd_ctx* c, hipStream_t s) {
     const long per_frame = 8L * H * c->NC + 16L * H * c->NCA + 8L * hw + 8L * hw + 8L * H * (W / 2 + 1) + 8L * hw;
     // frames per launch: large launches amortise every kernel's tail wave; at
     // 1024^2 (bench.py, 256 frames) 8 / 32 / 128 / 256 frames per launch gave
-    // 50.5k / 63.5k / 68.1k / 68.9k frames/s.  8 GiB of workspace by default
-    // (of 288 GB HBM): 256 frames at 1024^2, 16 at 4096^2.
-    const long budget = (long)fcd_env_int("FCD_CHUNK_MB", 8192) << 20;
+    // 50.5k / 63.5k / 68.1k / 68.9k frames/s.  16 GiB of workspace by default
+    // (of 288 GB HBM): 256 frames at 1024^2, 128 at 2048^2, 32 at 4096^2 (8 GiB, 16 frames
+    // at 4096^2: c5 3.40 k -> 3.49 k; 24 GiB measured 3.43 k, r05zd / r05ze).
+    const long budget = (long)fcd_env_int("FCD_CHUNK_MB", 16384) << 20;
     c->fchunk = (int)std::max(1L, std::min((long)fcd_env_int("FCD_CHUNK_MAX", 256), budget / per_frame));
     const size_t nb = (size_t)c->fchunk;
     c->Xb.ensure(nb * H * c->NC * sizeof(float2));
@@ -1220,6 +1222,9 @@ FCD_API int fcd_create(int device, int rows, int cols, fcd_ctx** out) {
         c->device = device;
         c->force_unfused = fcd_env_int("FCD_UNFUSED", 0) != 0;
         c->nstreams = fcd_env_int("FCD_STREAMS", 2) >= 2 ? 2 : 1;
+        // the fused chain at 2048- / 4096-wide rows: one stream (its kernels fill the chip
+        // alone; with 32-frame chunks c5 3.48 k -> 3.52 k, c3 18.29 k -> 18.35 k, r05ze/zf)
+        c->fused_split = fcd_env_int("FCD_STREAMS", 0) ? c->nstreams : (cols <= 1024 ? 2 : 1);
         c->early_census = fcd_env_int("FCD_EARLY_CENSUS", 1) != 0;
         c->H = rows;
         c->W = cols;
@@ -1924,9 +1929,9 @@ int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int f
             float* hdst = (dev && height_out) ? height_out + (size_t)f0 * hw : c->out_h.as<float>();
             int32_t* kdst = k_out && unwrap ? (dev ? k_out + (size_t)f0 * 2 * hw : c->fk.as<int32_t>()) : nullptr;
             int* rs = res ? res + (size_t)f0 * 2 : nullptr;
-            // the fused (1024-wide) chain only: split, the unfused chain at 2048^2 / 4096^2
-            // measured 1-2 % slower (r01br), though its workspace offsets allow it
-            const int nsplit = fused && !c->profiling && nb >= 2 ? c->nstreams : 1;
+            // the fused chain only: split (the unfused chain at 2048^2 / 4096^2 measured 1-2 %
+            // slower split, r01br, though its workspace offsets allow it)
+            const int nsplit = fused && !c->profiling && nb >= 2 ? c->fused_split : 1;
             // early census: the last chunk's halves mark when their census flags are final,
             // and the readback below waits for those marks only, not for the integration
             const bool last = f0 + nb >= n_frames;
