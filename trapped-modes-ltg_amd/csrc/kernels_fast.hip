@@ -580,7 +580,10 @@ __global__ __launch_bounds__(IntColsCfg<H>::THREADS, IntColsCfg<H>::V) void k_in
 #ifndef FCD_C2R_RPW_2048
 #define FCD_C2R_RPW_2048 8  // 16 waves per CU in 156 KB of LDS: 8.97 -> 7.17 us/frame (kbench r03c8; 4 before)
 #endif
-__host__ __device__ constexpr int c2r_rpw(int W) { return W <= 1024 ? 16 : (W == 2048 ? FCD_C2R_RPW_2048 : 2); }
+// 4096-point rows: 4-row blocks (two 8-wave teams, 16 waves per CU) with the twiddles
+// read from the global table (C2RCfg::GTW): 152 KB of LDS instead of 116 KB for a 2-row,
+// one-team block (int_cols + c2r 104.7 -> 103.1 us/frame, c5 +0.6 %, r05zh)
+__host__ __device__ constexpr int c2r_rpw(int W) { return W <= 1024 ? 16 : (W == 2048 ? FCD_C2R_RPW_2048 : 4); }
 
 template <int W>
 struct C2RCfg {
@@ -594,7 +597,8 @@ struct C2RCfg {
     static constexpr int THREADS = (RPW / 2) * TT < 1024 ? ((RPW / 2) * TT > TT ? (RPW / 2) * TT : TT) : 1024;
     static constexpr int TEAMS = THREADS / TT;
     static constexpr int ROW = padded_len(W);
-    static constexpr int NLEN = W;
+    static constexpr bool GTW = W >= 4096;
+    static constexpr int NLEN = GTW ? 0 : W;
 };
 
 template <int W>
@@ -607,7 +611,7 @@ __global__ __launch_bounds__(C2RCfg<W>::THREADS) void k_int_c2r(const float2* __
     const int team = threadIdx.x / TT, t = threadIdx.x % TT;
     float2* s = lds + team * C::ROW;
     float2* stage = lds + TEAMS * C::ROW;  // [NCH][rpw + 1]
-    RegFFT<W> fft;
+    RegFFT<W, C::GTW> fft;
     fft.init(tw, lds_raw, threadIdx.x, C::THREADS);
     __syncthreads();
     const int NCH = W / 2 + 1;
