@@ -846,10 +846,23 @@ def rfft_rows(x, dtype=None):
     return re, im
 
 
+def spectrum_dtype(dtype):
+    """The real type scipy 1.7.1's fft2 computes an image of this dtype in
+    (`scipy/fft/_pocketfft/helper.py:91-92`, `_asfarray`): float32 and float16 -> float32
+    (pocketfft has no half precision), float64 stays float64, and every non-float dtype
+    (bool, int, uint) -> float64.  fourier.py:18's `image - np.mean(image)` gives the same
+    types (an integer image minus its float64 mean is float64)."""
+    dt = np.dtype(dtype)
+    if dt in (np.float32, np.float16):
+        return np.float32
+    return np.float64
+
+
 def fft2(x):
-    """scipy.fft.fft2 of a real float32 / float64 image (c2c_sym_internal): complex [H, W]."""
+    """scipy.fft.fft2 of a real image (c2c_sym_internal): complex [H, W], complex64 for
+    float32 / float16 images, complex128 for everything else (spectrum_dtype)."""
     x = np.ascontiguousarray(x)
-    T = np.float64 if x.dtype == np.float64 else np.float32
+    T = spectrum_dtype(x.dtype)
     x = x.astype(T)
     H, W = x.shape
     hr, hi = rfft_rows(x, T)                            # [H, W/2+1]
@@ -954,7 +967,18 @@ def abs_c(z):
 
 
 def find_peaks_spectrum(image):
-    """|fftshift(fft2(image - mean(image)))| of a float32 / float64 image, as fourier.py:18."""
-    T = np.float64 if np.asarray(image).dtype == np.float64 else np.float32
+    """|fftshift(fft2(image - mean(image)))| as fourier.py:18, in spectrum_dtype's precision:
+    an integer image's mean is float64 and exact (every partial sum is an integer below
+    2^53 for images up to 16384^2 of 16-bit samples), so converting first changes nothing."""
+    T = spectrum_dtype(np.asarray(image).dtype)
     img = np.ascontiguousarray(image, T)
     return np.fft.fftshift(abs_c(fft2((img - mean_T(img, T)).astype(T))))
+
+
+# ---- float32 names (fourier.py:18 for a float32 image), used by tests and tools
+def mean_f32(x):
+    return mean_T(x, np.float32)
+
+
+def abs_c64(z):
+    return abs_c(np.asarray(z, np.complex64))

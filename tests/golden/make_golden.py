@@ -24,7 +24,7 @@ Fixtures (all under tests/golden/):
                      analyze.folder loop body's height maps with and without the mask
   spectrum.npz       sha256 digests of scipy.fft.fft2, np.mean and the find_peaks spectrum
                      |fftshift(fft2(image - mean))| (fourier.py:18) for float32 images of
-                     several shapes (the bit-exact restatement in oracle/pocketfft32.py and
+                     several shapes (the bit-exact restatement in oracle/pocketfft.py and
                      the engine's fcd_fft2 are checked against them)
   bench_board.npz    the benchmarked c2 board (bench_data.py: pattern.py geometry, 1024^2,
                      unrotated and rotated 5 degrees): the reference's find_peaks picks,
@@ -41,6 +41,9 @@ Fixtures (all under tests/golden/):
                      hashed integer images (bench_data.hash_image) at odd, prime, Bluestein
                      and camera shapes in float32 and float64, and the reference's carrier
                      picks for float64 references (pyval's tie-prone sine board I0 among them)
+  intref.npz         integer-typed references (pattern.py's uint16 board, raw uint8 / uint16
+                     example pictures): the reference's complex128 picks, blobs, threshold,
+                     cf and fft2 digests, and heights with the uint16 board as reference
   analyze_ref.npz    pydata/analyze.py ITSELF (imported with a placeholder `cv2` module
                      whose every attribute access raises: cv2 is only used on the polar
                      paths, analyze.py:237-241, 674-676, which are not run): analyze.mask /
@@ -647,6 +650,69 @@ def make_shapes():
     np.savez_compressed(os.path.join(OUT, "shapes.npz"), **out)
 
 
+# Integer-typed references: scipy's fft2 promotes every non-float
+# image to float64 (scipy/fft/_pocketfft/helper.py:91-92) and `image - np.mean(image)` of
+# an integer image is float64, so the reference picks carriers from a complex128 spectrum
+# for them (fourier.py:18).  pattern.py:17-36 writes its board as uint16; the example
+# pictures decode to uint8 / uint16 before analyze.load_image's float32 cast.
+INT_REFS = {
+    "board_u16": dict(kind="board", rows=1024, rot=0.0, dtype="uint16"),
+    "board_rot5_u16": dict(kind="board", rows=1024, rot=5.0, dtype="uint16"),
+    "board_i32": dict(kind="board", rows=512, rot=0.0, dtype="int32"),
+    "ref2_u8": dict(kind="picture", name="reference_2.png"),
+    "refdf_u16": dict(kind="picture", name="reference_df.tif"),
+}
+
+
+def int_reference(spec):
+    sys.path.insert(0, os.path.dirname(os.path.dirname(OUT)))
+    from bench_data import checkerboard
+    if spec["kind"] == "picture":
+        return load_raw(spec["name"])
+    return checkerboard(spec["rows"], spec["rot"], dtype=np.dtype(spec["dtype"]))
+
+
+def make_intref():
+    """intref.npz: find_peaks / compute_calibration_factor of integer-typed references as
+    the reference computes them (complex128 spectrum), the picks of the same images as
+    float32 (what a float32 engine would pick), scipy's fft2 digest of each integer image,
+    and compute_height_map heights with the uint16 board as the reference."""
+    import hashlib
+    sys.path.insert(0, os.path.dirname(os.path.dirname(OUT)))
+    from bench_data import make_frames_numpy
+    out = {"versions": VERSIONS, "tags": np.array(list(INT_REFS))}
+    for tag, spec in INT_REFS.items():
+        img = int_reference(spec)
+        assert img.dtype.kind in "iu", (tag, img.dtype)
+        sq = 0.001
+        cf, (p0, p1) = fcd.compute_calibration_factor(sq, img)
+        locs, thr = peak_locations(img)
+        F = fft2(img)
+        assert F.dtype == np.complex128
+        out[f"{tag}_dtype"] = str(img.dtype)
+        out[f"{tag}_sha"] = hashlib.sha256(img.tobytes()).hexdigest()
+        out[f"{tag}_fft2_sha"] = hashlib.sha256(F.tobytes()).hexdigest()
+        out[f"{tag}_peaks"] = np.array([np.asarray(p0), np.asarray(p1)], np.int64)
+        out[f"{tag}_cf"] = cf
+        out[f"{tag}_blob_peaks"] = locs
+        out[f"{tag}_threshold"] = thr
+        c32, (q0, q1) = fcd.compute_calibration_factor(sq, img.astype(np.float32))
+        out[f"{tag}_peaks_f32"] = np.array([np.asarray(q0), np.asarray(q1)], np.int64)
+        print("intref", tag, img.dtype, img.shape, out[f"{tag}_peaks"].tolist(), "f32 picks",
+              out[f"{tag}_peaks_f32"].tolist(), locs.tolist(), thr, cf, flush=True)
+    # the uint16 board as the reference of compute_height_map (fcd.py:13-35): carriers from
+    # the complex128 spectrum, displaced frames as float32 (analyze.load_image's type)
+    ref = int_reference(INT_REFS["board_u16"])
+    _, frames = make_frames_numpy(1024, 2, seed=0, rotate_deg=0.0)
+    out["board_u16_frames_sha"] = hashlib.sha256(frames.tobytes()).hexdigest()
+    for f in range(2):
+        hmap, phases, cf = fcd.compute_height_map(ref, frames[f], 0.001, height=1.0)
+        out[f"board_u16_height_sub{f}"] = hmap[::4, ::4].astype(np.float32)
+        out[f"board_u16_height_stats{f}"] = stats(hmap)
+        out[f"board_u16_hcf{f}"] = cf
+    np.savez_compressed(os.path.join(OUT, "intref.npz"), **out)
+
+
 def import_reference_analyze():
     """/root/reference/pydata/analyze.py, imported as the reference ships it.  Its module
     top level does `import cv2` (analyze.py:21), absent here; cv2 is used only by the
@@ -776,7 +842,7 @@ def make_analyze_ref():
 
 if __name__ == "__main__":
     which = sys.argv[1:] or ["real_pair", "real_df", "unwrap", "synthetic", "integrate", "val", "ingest",
-                             "bench_board", "analyze_ref", "spectrum", "large", "mixed", "shapes", "anyshape"]
+                             "bench_board", "analyze_ref", "spectrum", "large", "mixed", "shapes", "anyshape", "intref"]
     if "real_pair" in which:
         make_real_pair()
     if "real_df" in which:
@@ -805,3 +871,5 @@ if __name__ == "__main__":
         make_shapes()
     if "anyshape" in which:
         make_mixed(ANY_CASES, "anyshape")
+    if "intref" in which:
+        make_intref()

@@ -235,3 +235,38 @@ def test_large_unwrap_equals_oracle_on_engine_phases(large, fresh, n):
         d = k[0][m].astype(np.int64) - ko
         assert np.all(d == d.flat[0]), (m, int((d != d.flat[0]).sum()))
     eng.close()
+
+
+def test_single_call_device_memory_is_bounded(fresh):
+    """A stateless drop-in call (fcd.py:13-35) sizes its workspace to the call: one 4096^2
+    fcd.compute_height_map raises the device's memory use (hipMemGetInfo, through torch)
+    by at most 2 GiB -- not the 16 GiB chunk budget a 32-frame batch uses --, a second
+    call with the same reference adds nothing, and the engine cache stays bounded per
+    thread and device."""
+    import gc
+
+    import torch
+    from bench_data import checkerboard
+    from pyfcd import _lib
+    from pyfcd.fcd import fcd
+    torch.cuda.init()
+    gc.collect()
+    free0, _ = torch.cuda.mem_get_info(0)
+    ref = checkerboard(4096, 5.0)
+    frame = np.roll(ref, 1, axis=1)
+    h, ph, cf = fcd.compute_height_map(ref, frame, 0.001, height=1.0)
+    assert np.isfinite(h).all()
+    free1, _ = torch.cuda.mem_get_info(0)
+    used = free0 - free1
+    assert used <= 2 << 30, f"one 4096^2 call pinned {used / 2**30:.2f} GiB"
+    fcd.compute_height_map(ref, frame, 0.001, height=1.0)
+    free2, _ = torch.cuda.mem_get_info(0)
+    assert free2 >= free1 - (64 << 20), "a repeated call grew the workspace"
+    # the cache: at most FCD_ENGINE_CACHE shapes per thread and device, LRU closed
+    for n in (64, 128, 256, 512, 1024):
+        _lib.engine_for((n, n))
+    mine = [k for k in _lib._engines if k[2] == __import__("threading").get_ident()]
+    assert len(mine) <= _lib._engine_cache_size()
+    assert (4096, 4096) not in [k[0] for k in mine]
+    _lib._engines.clear()
+    gc.collect()

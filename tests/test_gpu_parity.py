@@ -376,37 +376,38 @@ def test_batch_equals_single(lib, golden, monkeypatch, exact_first):
         assert np.array_equal(hb[i], h1.astype(np.float32))
 
 
-@pytest.mark.parametrize("streams", ["2", "1"])
-def test_exact_chain_halves_equal_single_frames(lib, golden, monkeypatch, streams):
+def test_exact_chain_halves_equal_single_frames(lib, golden, monkeypatch):
     """The exact-first chain runs a chunk of 8 or more frames as two halves on two streams,
     each driven by its own host thread and MST workspace (FCD_STREAMS=2), or in one piece
     (=1): 11 frames -- the three real camera frames (7..1611 residues per map) tiled, with
     two residue-free frames among them -- give heights bit-identical to single-frame calls
-    either way, and the halves equal the one-piece chain."""
-    from bench_data import make_frames_numpy
+    either way, and the halves equal the one-piece chain (both modes in this one test, on
+    fresh engines, compared in memory)."""
     from pyfcd import _lib
     d = golden("real_df")
     ref = d["ref_u16"].astype(np.float32)
     real = d["frames_u16"].astype(np.float32)
     monkeypatch.setenv("FCD_EXACT_FIRST", "1")
-    monkeypatch.setenv("FCD_STREAMS", streams)
-    _lib._engines.clear()
-    eng = lib.Engine(ref.shape)
-    eng.set_reference(ref, float(d["square_size"]))
-    clean = eng.process(ref[None], 1.0, unwrap=True, want_phases=False)[0]  # (the reference: a zero map)
     frames = np.stack([real[i % 3] for i in range(9)] + [ref, ref * np.float32(0.5)])
-    hb, _, _ = eng.process(frames, 1.0, unwrap=True, want_phases=False)
-    for i in (0, 1, 2, 8, 9, 10):
-        hs, _, _ = eng.process(frames[i:i + 1], 1.0, unwrap=True, want_phases=False)
-        assert np.array_equal(hb[i], hs[0]), i
-    assert np.array_equal(hb[9], clean[0])
-    for i in range(3, 9):
-        assert np.array_equal(hb[i], hb[i % 3]), i
-    np.save(f"/tmp/halves_{streams}.npy", hb)
-    if streams == "1" and os.path.exists("/tmp/halves_2.npy"):
-        assert np.array_equal(np.load("/tmp/halves_2.npy"), hb)
-    del eng
+    out = {}
+    for streams in ("2", "1"):
+        monkeypatch.setenv("FCD_STREAMS", streams)
+        _lib._engines.clear()
+        eng = lib.Engine(ref.shape)
+        eng.set_reference(ref, float(d["square_size"]))
+        clean = eng.process(ref[None], 1.0, unwrap=True, want_phases=False)[0]  # (the reference: a zero map)
+        hb, _, _ = eng.process(frames, 1.0, unwrap=True, want_phases=False)
+        for i in (0, 1, 2, 8, 9, 10):
+            hs, _, _ = eng.process(frames[i:i + 1], 1.0, unwrap=True, want_phases=False)
+            assert np.array_equal(hb[i], hs[0]), (streams, i)
+        assert np.array_equal(hb[9], clean[0])
+        for i in range(3, 9):
+            assert np.array_equal(hb[i], hb[i % 3]), (streams, i)
+        out[streams] = hb
+        eng.close()
+        del eng
     _lib._engines.clear()
+    assert np.array_equal(out["2"], out["1"])
 
 
 def test_full_size_1024_vs_oracle(lib):
@@ -442,7 +443,7 @@ def test_bench_board_matches_reference_run(lib, golden, tag, rot):
     is itself an exact tie (|atan2| = pi/4 for (461, 563) and (563, 563)): the reference's
     choice is made by the float32 rounding of scipy's FFT, numpy's mean and np.abs
     (SURVEY.md §8a parity fact 2), which the engine's reference setup reproduces
-    operation for operation (kernels_pocketfft.hip, oracle/pocketfft32.py)."""
+    operation for operation (kernels_pocketfft.hip, oracle/pocketfft.py)."""
     import hashlib
     from bench_data import make_frames_numpy
     from pyfcd.fcd import fcd

@@ -79,3 +79,52 @@ def test_float64_reference_high_level(shapes):
     cf, (p0, p1) = fcd.compute_calibration_factor(0.001, img)
     assert cf == float(g["val1024_cf"])
     assert np.array_equal(np.array([p0, p1]), g["val1024_peaks"])
+
+
+@pytest.mark.parametrize("tag", ["board_u16", "board_rot5_u16", "board_i32", "ref2_u8", "refdf_u16"])
+def test_integer_reference_picks(golden, tag):
+    """Integer-typed references (pattern.py:17-36 writes its board as uint16; raw uint8 /
+    uint16 camera pictures) reach the engine as float64, the type scipy's fft2 promotes
+    them to (scipy/fft/_pocketfft/helper.py:91-92, fourier.py:18), so set_reference,
+    find_peaks and fft2 reproduce the reference's complex128 picks, blob order, threshold,
+    cf and spectrum bits -- including the unrotated board's [[563, 563], [461, 563]], which
+    the float32 rounding of the same board would not pick."""
+    from test_oracle_golden import int_reference_image
+    from pyfcd import _lib
+    from pyfcd.fcd import fcd
+    g = golden("intref")
+    img = int_reference_image(golden, tag)
+    eng = _lib.Engine(img.shape)
+    info = eng.set_reference(img, 0.001)
+    peaks = np.array([[info.peaks[i][0], info.peaks[i][1]] for i in range(2)])
+    assert np.array_equal(peaks, g[f"{tag}_peaks"]), (tag, peaks.tolist())
+    assert info.calibration_factor == float(g[f"{tag}_cf"]), tag
+    blobs = np.array([[info.blob_peaks[i][0], info.blob_peaks[i][1]] for i in range(info.n_blobs)])
+    assert np.array_equal(blobs, g[f"{tag}_blob_peaks"]), tag
+    assert info.threshold == float(g[f"{tag}_threshold"]), tag
+    (i2,) = eng.find_peaks(img, 0.001)
+    assert [tuple(i2.peaks[i]) for i in range(2)] == [tuple(p) for p in peaks.tolist()], tag
+    F = eng.fft2(img)
+    assert F.dtype == np.complex128
+    assert hashlib.sha256(F.tobytes()).hexdigest() == str(g[f"{tag}_fft2_sha"]), tag
+    eng.close()
+    # the drop-in classmethods with the integer image itself
+    cf, (p0, p1) = fcd.compute_calibration_factor(0.001, img)
+    assert cf == float(g[f"{tag}_cf"]) and np.array_equal(np.array([p0, p1]), g[f"{tag}_peaks"]), tag
+
+
+def test_integer_reference_heights(golden):
+    """fcd.compute_height_map with pattern.py's uint16 board as the reference (fcd.py:13-35):
+    the reference's carriers, and heights within the float32 tolerance of its run."""
+    from bench_data import make_frames_numpy
+    from test_oracle_golden import int_reference_image
+    from pyfcd.fcd import fcd
+    g = golden("intref")
+    ref = int_reference_image(golden, "board_u16")
+    _, frames = make_frames_numpy(1024, 2, seed=0, rotate_deg=0.0)
+    assert hashlib.sha256(frames.tobytes()).hexdigest() == str(g["board_u16_frames_sha"])
+    for f in range(2):
+        h, ph, cf = fcd.compute_height_map(ref, frames[f], 0.001, height=1.0)
+        assert cf == float(g[f"board_u16_hcf{f}"])
+        sub = g[f"board_u16_height_sub{f}"]
+        assert np.linalg.norm(h[::4, ::4] - sub) / np.linalg.norm(sub) < 1e-5, f

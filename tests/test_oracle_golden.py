@@ -138,13 +138,13 @@ def test_residue_counter_matches_definition():
     assert O.count_residues(w) == int(((fw(a, b) + fw(b, c) + fw(c, d) + fw(d, a)) != 0).sum())
 
 
-def test_pocketfft32_matches_scipy_digests(golden):
-    """oracle/pocketfft32.py restates scipy 1.7.1's float32 fft2, numpy 1.26.4's float32
+def test_pocketfft_f32_matches_scipy_digests(golden):
+    """oracle/pocketfft.py restates scipy 1.7.1's float32 fft2, numpy 1.26.4's float32
     mean and complex64 abs bit for bit: sha256 of every output equals the reference
     interpreter's (fourier.py:18's spectrum included)."""
     import hashlib
     from conftest import spectrum_images
-    from oracle import pocketfft32 as P
+    from oracle import pocketfft as P
     g, imgs = spectrum_images(golden)
     assert sorted(imgs) == sorted(str(n) for n in g["names"])
     for name, img in imgs.items():
@@ -181,11 +181,11 @@ def test_oracle_large_frames_vs_reference_run(golden, tag):
     assert np.linalg.norm(hs - g[f"{tag}_height_sub"]) / np.linalg.norm(g[f"{tag}_height_sub"]) < 1e-5
 
 
-def test_pocketfft32_mixed_radix_digests(golden):
-    """oracle/pocketfft32.py's radf3 / radf5 / pass3 / pass5 (5-smooth shapes) against
+def test_pocketfft_f32_mixed_radix_digests(golden):
+    """oracle/pocketfft.py's radf3 / radf5 / pass3 / pass5 (5-smooth shapes) against
     scipy 1.7.1's float32 fft2, numpy's mean and the find_peaks spectrum, by digest."""
     import hashlib
-    from oracle import pocketfft32 as P
+    from oracle import pocketfft as P
     g = golden("mixed")
     for h, w in g["rand_shapes"]:
         img = g[f"rand_{h}x{w}_u16"].astype(np.float32) * np.float32(0.37)
@@ -270,3 +270,62 @@ def test_oracle_float64_reference_picks(golden):
         assert cf == float(g[f"{tag}_cf"]), tag
         _, p32 = O.calibration_factor(0.001, img.astype(np.float32), exact=True)
         assert np.array_equal(np.array(p32), g[f"{tag}_peaks_f32"]), tag
+
+
+def int_reference_image(golden, tag):
+    """The integer-typed references of intref.npz, rebuilt exactly (make_golden.py INT_REFS):
+    pattern.py's board as uint16 / int32 (bench_data.checkerboard) and the raw example
+    pictures (real_pair.npz / real_df.npz)."""
+    import hashlib
+    from bench_data import checkerboard
+    g = golden("intref")
+    if tag == "ref2_u8":
+        img = golden("real_pair")["ref_u8"]
+    elif tag == "refdf_u16":
+        img = golden("real_df")["ref_u16"]
+    else:
+        rows, rot, dt = {"board_u16": (1024, 0.0, np.uint16), "board_rot5_u16": (1024, 5.0, np.uint16),
+                         "board_i32": (512, 0.0, np.int32)}[tag]
+        img = checkerboard(rows, rot, dtype=dt)
+    assert str(img.dtype) == str(g[f"{tag}_dtype"]), tag
+    assert hashlib.sha256(img.tobytes()).hexdigest() == str(g[f"{tag}_sha"]), tag
+    return img
+
+
+INT_TAGS = ["board_u16", "board_rot5_u16", "board_i32", "ref2_u8", "refdf_u16"]
+
+
+@pytest.mark.parametrize("tag", INT_TAGS)
+def test_oracle_integer_reference_picks(golden, tag):
+    """Integer-typed references take the complex128 spectrum (scipy's `_asfarray`,
+    scipy/fft/_pocketfft/helper.py:91-92; fourier.py:18): the oracle's exact spectrum gives
+    the reference's picks, cf, fft2 bits -- and on the unrotated board (uint16 as pattern.py
+    writes it, and int32) picks that differ from the float32 rounding's."""
+    import hashlib
+    from oracle import fcd_oracle as O
+    from oracle import pocketfft as P
+    g = golden("intref")
+    img = int_reference_image(golden, tag)
+    if img.size <= 512 * 512:
+        F = P.fft2(img)
+        assert F.dtype == np.complex128
+        assert hashlib.sha256(F.tobytes()).hexdigest() == str(g[f"{tag}_fft2_sha"])
+    cf, peaks = O.calibration_factor(0.001, img, exact=True)
+    assert np.array_equal(np.array(peaks), g[f"{tag}_peaks"]), tag
+    assert cf == float(g[f"{tag}_cf"]), tag
+    if tag in ("board_u16", "board_i32"):
+        assert not np.array_equal(g[f"{tag}_peaks"], g[f"{tag}_peaks_f32"])
+
+
+def test_image_precision_follows_scipy():
+    """pyfcd._lib._img: the dtype an image reaches the engine in is scipy's fft2 type
+    (float32 / float16 -> float32, float64 and every integer / bool type -> float64)."""
+    from pyfcd import _lib
+    from oracle import pocketfft as P
+    for dt in (np.float32, np.float16, np.float64, np.uint8, np.uint16, np.int16, np.int32, np.int64, np.uint64,
+               np.bool_):
+        a = np.ones((4, 4), dt)
+        assert _lib._img(a).dtype == P.spectrum_dtype(dt), dt
+        assert _lib._img_flag(_lib._img(a)) == (_lib.FCD_IMG_F64 if P.spectrum_dtype(dt) == np.float64 else 0)
+    with pytest.raises(TypeError):
+        _lib._img(np.ones((4, 4), np.complex64))

@@ -1,12 +1,12 @@
 """Diagnostic: which stage of the engine's exact reference spectrum differs from the
-oracle (oracle/pocketfft32.py) on a golden reference image.  GPU box only."""
+oracle (oracle/pocketfft.py) on a golden reference image.  GPU box only."""
 import os
 import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "trapped-modes-ltg_amd"), os.path.join(ROOT, "tests")]
 import numpy as np  # noqa: E402
 import torch  # noqa: E402,F401
-from oracle import pocketfft32 as P, fcd_oracle as O  # noqa: E402
+from oracle import pocketfft as P, fcd_oracle as O  # noqa: E402
 from pyfcd import _lib  # noqa: E402
 
 for name, key in (("real_pair", "ref_u8"), ("real_df", "ref_u16")):

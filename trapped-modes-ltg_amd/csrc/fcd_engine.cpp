@@ -138,7 +138,7 @@ std::vector<float2> band_pretwiddles(int W, int B) {
     return t;
 }
 
-// the smallest frame side fcd_create accepts (any larger one up to 8192, see mr_supported)
+// the smallest frame side fcd_create accepts (any larger one up to kMrMaxLen = 16384, see mr_supported)
 constexpr int kMinSide = 16;
 
 int fcd_env_int(const char* name, int dflt) {
@@ -212,6 +212,7 @@ struct fcd_ctx {
     int gb_NU = 0;      // columns in either carrier's disk
     hipStream_t own = nullptr;
     DevBuf tw_row, tw_col;        // plain tables exp(-2 pi i m / n) (generic LDS FFT kernels)
+    DevBuf mr_gs;                 // the generic chain's global-scratch rows (sides / Bluestein M above 8192)
     DevBuf twp_row, twp_col;      // pass-major tables (register FFT kernels)
     DevBuf twp_col16;             // the column table for 16 elements per lane (k_int_cols / k_demod_cols at 1024)
 
@@ -228,7 +229,8 @@ struct fcd_ctx {
     // band-pruned demodulation tables (DemodTables) and the fast path's workspace
     DevBuf dt_hc, dt_outs, dt_outrows, dt_nouts, dt_colslot;
     int NC = 0, NCc[2] = {0, 0}, NCA = 0;
-    int fchunk = 1;                  // frames per fast-path chunk
+    int fchunk = 1;                  // frames per fast-path chunk (the workspace budget's capacity)
+    int ws_nb = 0;                   // frames the fast-path chunk workspace is allocated for (<= fchunk)
     DevBuf Xb, Ab, Zt, Ht, fk, fres; // per-chunk intermediates; fk: k-fields for the fix-up pass
     int band_B = 0;                  // band window of the pruned inverse (0: full-length k_demod_phase)
     int fused_B = 0;                 // band window of the fused kernel (= band_B, or 512 at 4096-point rows)
@@ -297,11 +299,19 @@ void ensure_chunk_buffers(fcd_ctx* c) {
     const long hw = c->hw();
     const size_t n = (size_t)c->chunk;
     c->spec.ensure(n * hw * sizeof(float2));
-    c->work.ensure(n * hw * sizeof(float2));
     c->wrapped.ensure(n * 2 * hw * sizeof(float));
-    c->kbuf.ensure(n * 2 * hw * sizeof(int32_t));
     c->colk.ensure(n * 2 * c->H * sizeof(int));
     c->rescnt.ensure(n * 2 * sizeof(int));
+}
+
+// The full-transform chain's second plane and k-field staging (the generic chain, and the
+// fcd_phases_from_spectrum / fcd_unwrap / fcd_integrate entry points): allocated on first
+// use, so the power-of-two fast path never holds them.
+void ensure_aux_buffers(fcd_ctx* c) {
+    const long hw = c->hw();
+    const size_t n = (size_t)c->chunk;
+    c->work.ensure(n * hw * sizeof(float2));
+    c->kbuf.ensure(n * 2 * hw * sizeof(int32_t));
 }
 
 void ensure_mst(fcd_ctx* c, MstSpace& S, int nact, long hw) {
@@ -374,7 +384,7 @@ fcdk::MstWork mst_work(fcd_ctx* c, MstSpace& S) {
 void rows_fft(fcd_ctx* c, bool inv, fcdk::RowIn im, fcdk::RowOut om, const void* in, void* out, long nrows, float sub,
               const fcdk::PhaseOut* ph, hipStream_t s) {
     if (c->generic)
-        fcdk::mr_rows(c->mr_row, inv, im, om, in, out, nrows, c->H, sub, c->tw_row.as<float2>(), ph, s);
+        fcdk::mr_rows(c->mr_row, inv, im, om, in, out, nrows, c->H, sub, c->tw_row.as<float2>(), ph, s, c->mr_gs.as<float2>());
     else
         fcdk::row_fft(c->W, inv, im, om, in, out, nrows, c->H, sub, c->tw_row.as<float2>(), ph, s);
 }
@@ -383,7 +393,8 @@ void cols_fft(fcd_ctx* c, bool inv, float2* data, int nb, hipStream_t s) {
     if (c->generic) {
         if ((size_t)nb * c->hw() * sizeof(float2) > c->mr_scratch.bytes)
             throw FcdError(FCD_E_INTERNAL, "mixed-radix scratch too small");
-        fcdk::mr_cols(c->mr_col, c->W, inv, data, nb, c->tw_col.as<float2>(), c->mr_scratch.as<float2>(), s);
+        fcdk::mr_cols(c->mr_col, c->W, inv, data, nb, c->tw_col.as<float2>(), c->mr_scratch.as<float2>(), s,
+                      c->mr_gs.as<float2>());
     } else {
         fcdk::col_fft(c->H, c->W, inv, data, nb, c->tw_col.as<float2>(), s);
     }
@@ -710,10 +721,10 @@ void generic_fft2_t(fcd_ctx* c, const float* in, int nb, float2* specT, hipStrea
     bo.bslot = c->gb_tables.as<int>() + NU + 2 * (c->NCc[0] + c->NCc[1]) + 2 * (size_t)c->W;
     bo.bnc = NU;
     fcdk::mr_rows(c->mr_row, false, fcdk::ROW_IN_REAL2, fcdk::ROW_OUT_BAND2, in, tmp, (long)nb * c->H, c->H, 0.f,
-                  c->tw_row.as<float2>(), &bo, s);
+                  c->tw_row.as<float2>(), &bo, s, c->mr_gs.as<float2>());
     fcdk::mr_transpose(tmp, specT, nb, c->H, NU, s);
     fcdk::mr_rows(c->mr_col, false, fcdk::ROW_IN_COMPLEX, fcdk::ROW_OUT_COMPLEX, specT, specT, (long)nb * c->gb_NU, c->gb_NU,
-                  0.f, c->tw_col.as<float2>(), nullptr, s);
+                  0.f, c->tw_col.as<float2>(), nullptr, s, c->mr_gs.as<float2>());
 }
 
 // Per carrier: the disk-masked band columns [nb][NCc][H], their inverse column
@@ -732,14 +743,14 @@ void generic_demod_t(fcd_ctx* c, const float2* specT, int nb, float* wrapped, hi
         fcdk::disk_band_t(specT, AT, nb, c->H, c->W, NU, cols[car], uslot[car], nc, t, s);
         if (nc > 0)
             fcdk::mr_rows(c->mr_col, true, fcdk::ROW_IN_COMPLEX, fcdk::ROW_OUT_COMPLEX, AT, AT, (long)nb * nc, nc, 0.f,
-                          c->tw_col.as<float2>(), nullptr, s);
+                          c->tw_col.as<float2>(), nullptr, s, c->mr_gs.as<float2>());
         fcdk::PhaseOut ph{c->theta.as<float>() + (size_t)car * c->hw(), wrapped, car};
         // the inverse rows gather their band columns themselves (scattering the band into
         // zero-filled rows first measured 7.68 k vs 8.18 k frames/s at 1024 x 1280, r04w)
         ph.bslot = colslot + (size_t)car * c->W;
         ph.bnc = nc;
         fcdk::mr_rows(c->mr_row, true, fcdk::ROW_IN_BAND, fcdk::ROW_OUT_PHASE, AT, nullptr, (long)nb * c->H, c->H, 0.f,
-                      c->tw_row.as<float2>(), &ph, s);
+                      c->tw_row.as<float2>(), &ph, s, c->mr_gs.as<float2>());
     }
 }
 
@@ -754,7 +765,7 @@ void generic_integrate_t(fcd_ctx* c, int nb, const float* w, const int32_t* kf, 
     zin.kflag = kflag;
     zin.colk = colk;
     fcdk::mr_rows(c->mr_row, false, fcdk::ROW_IN_Z, fcdk::ROW_OUT_COMPLEX, w, Z, (long)nb * c->H, c->H, 0.f,
-                  c->tw_row.as<float2>(), &zin, s);
+                  c->tw_row.as<float2>(), &zin, s, c->mr_gs.as<float2>());
     if (fcdk::mr_int_cols_supported(c->mr_col)) {  // the column pairs in place
         fcdk::mr_int_cols(c->mr_col, Z, nb, c->W, twc, k, s);
     } else {  // (a prime factor of H above 7 but <= 61) transposed, the spectrum kept transposed between the passes
@@ -762,15 +773,15 @@ void generic_integrate_t(fcd_ctx* c, int nb, const float* w, const int32_t* kf, 
         float2* HT = c->work.as<float2>();
         fcdk::mr_transpose(Z, ZT, nb, c->H, c->W, s);
         fcdk::mr_rows(c->mr_col, false, fcdk::ROW_IN_COMPLEX, fcdk::ROW_OUT_COMPLEX, ZT, ZT, (long)nb * c->W, c->W, 0.f,
-                      twc, nullptr, s);
+                      twc, nullptr, s, c->mr_gs.as<float2>());
         fcdk::integ_multiply(ZT, HT, nb, c->H, c->W, k, s, true);
         fcdk::mr_rows(c->mr_col, true, fcdk::ROW_IN_COMPLEX, fcdk::ROW_OUT_COMPLEX, HT, HT, (long)nb * c->W, c->W, 0.f,
-                      twc, nullptr, s);
+                      twc, nullptr, s, c->mr_gs.as<float2>());
         fcdk::mr_transpose(HT, Z, nb, c->W, c->H, s);
     }
     // two Hermitian rows per inverse transform
     fcdk::mr_rows(c->mr_row, true, fcdk::ROW_IN_COMPLEX2, fcdk::ROW_OUT_REAL2, Z, h_out, (long)nb * c->H, c->H, 0.f,
-                  c->tw_row.as<float2>(), nullptr, s);
+                  c->tw_row.as<float2>(), nullptr, s, c->mr_gs.as<float2>());
 }
 
 // h = real(ifft2(multiplier * fft2(z)))  for nb fields z (in c->spec).
@@ -819,6 +830,35 @@ void check_ctx(fcd_ctx* c, bool settle_pending = true) {
     if (!c) throw FcdError(FCD_E_INVALID, "null context");
     HIPCHK(hipSetDevice(c->device));
     if (settle_pending) settle(c);
+}
+
+// The fast path's chunk workspace (Xb, Ab, Zt, Ht, the k-field, seams, staging) for nb
+// frames, nb <= fchunk, grown on demand: a one-frame compute_height_map pins one frame's
+// workspace (tens of MB at 1024^2), not the 16 GiB throughput budget a 256-frame batch
+// uses.  Sizes follow the current reference's band tables.
+void ensure_fast_ws(fcd_ctx* c, int nb) {
+    nb = std::max(1, std::min(nb, c->fchunk));
+    if (nb <= c->ws_nb) return;
+    // growing frees buffers the integration of an earlier asynchronous device call may
+    // still be reading on the caller's stream (early census, settle())
+    if (c->done_pending) {
+        HIPCHK(hipEventSynchronize(c->ev_done));
+        c->done_pending = false;
+    }
+    const long H = c->H, W = c->W, hw = c->hw();
+    const size_t n = (size_t)nb, nw = std::max(n, (size_t)c->chunk);
+    c->Xb.ensure(n * H * c->NC * sizeof(float2));
+    c->Ab.ensure(n * 2 * H * c->NCA * sizeof(float2));
+    c->Zt.ensure(n * hw * sizeof(float2));
+    c->Ht.ensure(n * H * (W / 2 + 1) * sizeof(float2));
+    c->wrapped.ensure(nw * 2 * hw * sizeof(float));
+    c->colk.ensure(nw * 2 * H * sizeof(int));
+    c->fk.ensure(n * 2 * hw * sizeof(int32_t));
+    c->col0.ensure(n * 2 * (size_t)H * sizeof(float));
+    if (c->fused_ok) c->seam.ensure(n * (size_t)(H / fcdk::phase_rows_tile(W)) * 2 * W * sizeof(float2));
+    c->ir_seam.ensure(2 * fcdk::int_rows_seam_bytes(W, H, nb));
+    c->rescnt.ensure(nw * 2 * sizeof(int));
+    c->ws_nb = nb;
 }
 
 // Band-pruned demodulation tables: which unshifted columns each carrier disk
@@ -950,19 +990,11 @@ void build_demod_tables(fcd_ctx* c, hipStream_t s) {
     // at 4096^2: c5 3.40 k -> 3.49 k; 24 GiB measured 3.43 k, r05zd / r05ze).
     const long budget = (long)fcd_env_int("FCD_CHUNK_MB", 16384) << 20;
     c->fchunk = (int)std::max(1L, std::min((long)fcd_env_int("FCD_CHUNK_MAX", 256), budget / per_frame));
-    const size_t nb = (size_t)c->fchunk;
-    c->Xb.ensure(nb * H * c->NC * sizeof(float2));
-    c->Ab.ensure(nb * 2 * H * c->NCA * sizeof(float2));
-    c->Zt.ensure(nb * hw * sizeof(float2));
-    c->Ht.ensure(nb * H * (W / 2 + 1) * sizeof(float2));
-    c->wrapped.ensure(std::max(nb, (size_t)c->chunk) * 2 * hw * sizeof(float));
-    c->colk.ensure(std::max(nb, (size_t)c->chunk) * 2 * H * sizeof(int));
-    c->fk.ensure(nb * 2 * hw * sizeof(int32_t));
-    c->col0.ensure(nb * 2 * (size_t)H * sizeof(float));
-    if (c->fused_ok) c->seam.ensure(nb * (size_t)(H / fcdk::phase_rows_tile(W)) * 2 * W * sizeof(float2));
-    c->ir_seam.ensure(2 * fcdk::int_rows_seam_bytes(W, H, (int)nb));
-    c->rescnt.ensure(std::max(nb, (size_t)c->chunk) * 2 * sizeof(int));
+    // the workspace itself is allocated per call, for the frames the call launches at once
+    // (ensure_fast_ws): the reference's own setup below needs one frame's
+    c->ws_nb = 0;
     c->ms[0].cap = c->ms[1].cap = 0;  // re-size the MST workspaces for the new chunk on next use
+    ensure_fast_ws(c, 1);
 }
 
 fcdk::DemodTables demod_tables(fcd_ctx* c) {
@@ -1232,6 +1264,8 @@ FCD_API int fcd_create(int device, int rows, int cols, fcd_ctx** out) {
         if (c->generic) {
             c->mr_row = fcdk::mr_plan(cols);
             c->mr_col = fcdk::mr_plan(rows);
+            const size_t gsb = std::max(fcdk::mr_long_scratch_bytes(c->mr_row), fcdk::mr_long_scratch_bytes(c->mr_col));
+            if (gsb) c->mr_gs.ensure(gsb);
         }
         HIPCHK(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking));
         // plain tables exp(-2 pi i m / n) (power-of-two LDS kernels), or the mixed-radix plans'
@@ -1329,6 +1363,7 @@ FCD_API int fcd_set_reference(fcd_ctx* c, const float* reference, int flags, dou
         }
         // the carrier picks from the reference's own precision (fourier.py:18)
         find_peaks_batch(c, dref, f64, 1, square_size, nullptr, s);
+        c->pk_F.release();  // (the exact spectrum: a one-off per reference, not kept)
         const float* dref32 = static_cast<const float*>(dref);
         if (f64) {  // the per-frame demodulation's carrier signals from its float32 rounding
             c->ref32.ensure(hw * sizeof(float));
@@ -1499,7 +1534,7 @@ void first_pass_chunk(fcd_ctx* c, const float* fr, int nb, bool unwrap, bool fus
         if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
         // the second concurrent half (fo > 0) has its own seam region
         float2* seam = c->ir_seam.as<float2>() +
-                       (fo ? fcdk::int_rows_seam_bytes(c->W, c->H, c->fchunk) / sizeof(float2) : 0);
+                       (fo ? fcdk::int_rows_seam_bytes(c->W, c->H, c->ws_nb) / sizeof(float2) : 0);
         fcdk::int_rows(c->W, unwrap ? 1 : 0, wrapped, colk, nullptr, kdst, res, c->H, nb, Zt, c->twp_row.as<float2>(),
                        seam, s);
         fcdk::int_cols(c->H, Zt, c->W, nb, coef, Ht, ic_tw(c), s);
@@ -1589,6 +1624,7 @@ void host_pipeline(fcd_ctx* c, const void* frames, int format, int n_frames, boo
     } drain{P, s};
     const size_t rb = fcdk::raw_frame_bytes(format, c->H, c->W);
     const bool pin_src = host_pinned(frames), pin_dst = host_pinned(height_out);
+    ensure_fast_ws(c, std::min(P.nb, n_frames));
     const int nchunks = (n_frames + P.nb - 1) / P.nb;
     auto chunk_frames = [&](int i) { return std::min(P.nb, n_frames - i * P.nb); };
     auto retire = [&](int i) {  // chunk i's heights: pinned slot -> caller memory
@@ -1658,6 +1694,7 @@ void stage_frames(fcd_ctx* c, const void* frames, int format, bool dev, const in
 // transforms.  Synchronous on `s`.
 int process_generic(fcd_ctx* c, const void* frames, int format, int n_frames, bool dev, bool unwrap,
                     const fcdk::IntegCoef& coef, float* height_out, float* wrapped_out, int32_t* k_out, hipStream_t s) {
+    ensure_aux_buffers(c);
     const long hw = c->hw();
     const hipMemcpyKind kind = dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
     c->frames_in.ensure((size_t)c->chunk * hw * sizeof(float));
@@ -1790,7 +1827,9 @@ int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int f
                                             -in.frequencies[0][0] * sc, in.frequencies[0][1] * sc);
     if (c->generic)
         return process_generic(c, frames, format, n_frames, dev, unwrap != 0, coef, height_out, wrapped_out, k_out, s);
-    const int nbmax = c->fchunk;
+    // frames launched at once: the call's own, up to the workspace budget's fchunk
+    const int nbmax = std::max(1, std::min(c->fchunk, n_frames));
+    ensure_fast_ws(c, nbmax);
     c->frames_in.ensure((size_t)nbmax * hw * sizeof(float));
     c->out_h.ensure((size_t)nbmax * hw * sizeof(float));
     const hipMemcpyKind out_kind = dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
@@ -2127,6 +2166,7 @@ FCD_API int fcd_phases_from_spectrum(fcd_ctx* c, const float* spectrum, int n, i
                                      float* wrapped_out, int32_t* k_out, void* stream) {
     FCD_TRY({
         check_ctx(c);
+        ensure_aux_buffers(c);
         if (!c->has_ref) throw FcdError(FCD_E_STATE, "no reference set");
         if (!spectrum || n < 0) throw FcdError(FCD_E_INVALID, "bad spectrum");
         hipStream_t s = c->pick(stream);
@@ -2164,6 +2204,7 @@ FCD_API int fcd_unwrap(fcd_ctx* c, const float* wrapped, int n_maps, int flags, 
                        int32_t* residues_out, void* stream) {
     FCD_TRY({
         check_ctx(c);
+        ensure_aux_buffers(c);
         if (!wrapped || !k_out || n_maps < 0) throw FcdError(FCD_E_INVALID, "bad arguments");
         hipStream_t s = c->pick(stream);
         const long hw = c->hw();
@@ -2193,6 +2234,7 @@ FCD_API int fcd_integrate(fcd_ctx* c, const float* gx, const float* gy, int n, d
                           void* stream) {
     FCD_TRY({
         check_ctx(c);
+        ensure_aux_buffers(c);
         if (!gx || !gy || !h_out || n < 0) throw FcdError(FCD_E_INVALID, "bad arguments");
         hipStream_t s = c->pick(stream);
         const long hw = c->hw();
@@ -2253,6 +2295,13 @@ FCD_API int fcd_fft2(fcd_ctx* c, const float* in, int n, int flags, float* out, 
                                       (size_t)nb * hw * 2 * es, hipMemcpyDeviceToHost, s));
                 HIPCHK(hipStreamSynchronize(s));
             }
+        }
+        if (dev && n > 0) {  // the pocketfft scratch stays in use on the caller's stream: any
+            // other entry point (find_peaks / set_reference on c->own reuse it) settles first
+            if (!c->ev_done) HIPCHK(hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming));
+            HIPCHK(hipEventRecord(c->ev_done, s));
+            c->done_stream = s;
+            c->done_pending = true;
         }
     })
 }

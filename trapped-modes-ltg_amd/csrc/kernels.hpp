@@ -170,8 +170,11 @@ MrPlan mr_plan(int n);
 // and the convolution kernels' spectra
 std::vector<float2> mr_tables(const MrPlan& p);
 // as row_fft (same modes; tw: mr_tables(p) on the device)
+// gs: the caller's global scratch of mr_long_scratch_bytes(p) bytes (rows longer than the
+// LDS holds; null when that is 0) -- per context, so contexts on one device never share it
 void mr_rows(const MrPlan& p, bool inverse, RowIn in_mode, RowOut out_mode, const void* in, void* out, long nrows,
-             int H, float sub, const float2* tw, const PhaseOut* ph, hipStream_t s);
+             int H, float sub, const float2* tw, const PhaseOut* ph, hipStream_t s, float2* gs);
+size_t mr_long_scratch_bytes(const MrPlan& p);
 // [nb][R][C] -> [nb][C][R]
 void mr_transpose(const float2* in, float2* out, int nb, int R, int C, hipStream_t s);
 // column subset: [nb][R][C] -> [nb][NS][R] (columns cols[])
@@ -186,7 +189,7 @@ bool mr_int_cols_supported(const MrPlan& p);
 void mr_int_cols(const MrPlan& p, float2* Z, int nb, int W, const float2* tw, const IntegCoef& c, hipStream_t s);
 // in-place column transforms of [nb][p.n][W] (through scratch: nb * p.n * W complex)
 void mr_cols(const MrPlan& p, int W, bool inverse, float2* data, int nb, const float2* tw, float2* scratch,
-             hipStream_t s);
+             hipStream_t s, float2* gs);
 
 // out[b] = in[b] * disk (unshifted spectrum index)
 // the generic chain's band columns: out[b][k][i] = spec_t[b][uslot[k]][i] inside carrier's disk

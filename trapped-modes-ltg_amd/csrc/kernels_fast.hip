@@ -17,6 +17,7 @@
 // a column kernel reads/writes whole 128-byte lines (16 rows of one column),
 // a row-block workgroup covers whole tiles.  All FFT data stays in registers
 // (regfft.hpp); LDS carries only pass exchanges and small staging blocks.
+#include <atomic>
 #include <hip/hip_runtime.h>
 
 #include <stdexcept>
@@ -689,16 +690,19 @@ __global__ __launch_bounds__(C2RCfg<W>::THREADS) void k_int_c2r(const float2* __
 #include "int_rows.inc"
 
 // ------------------------------------------------------------------ launchers
-static int g_num_cu = 0;
+// (atomic: the exact-first chain's two halves launch from two host threads)
+static std::atomic<int> g_num_cu{0};
 static int grid_for(long work_items, int per_cu) {
-    if (!g_num_cu) {
+    int ncu = g_num_cu.load(std::memory_order_relaxed);
+    if (!ncu) {
         int dev = 0;
         hipDeviceProp_t p;
         if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&p, dev) == hipSuccess)
-            g_num_cu = p.multiProcessorCount;
-        if (!g_num_cu) g_num_cu = 256;
+            ncu = p.multiProcessorCount;
+        if (!ncu) ncu = 256;
+        g_num_cu.store(ncu, std::memory_order_relaxed);
     }
-    const long cap = (long)g_num_cu * per_cu;
+    const long cap = (long)ncu * per_cu;
     return (int)(work_items < cap ? (work_items > 0 ? work_items : 1) : cap);
 }
 

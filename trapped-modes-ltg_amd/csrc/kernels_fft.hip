@@ -6,6 +6,7 @@
 //   fft2(reference), ifft2(... * mask)    /root/reference/pyfcd/carriers.py:22-24
 //   fft2(image - mean) for peak finding   /root/reference/pyfcd/fourier.py:18
 // and the disk band-pass of carriers.py:17-20 (skimage.draw.disk raster).
+#include <atomic>
 #include <hip/hip_runtime.h>
 
 #include <stdexcept>
@@ -184,7 +185,7 @@ static void launch_col(int W, bool inv, float2* data, int nbatch, const float2* 
     const int g_used = W < C::G ? W : C::G;
     const size_t lds = (size_t)C::G * C::STRIDE * sizeof(float2);
     const unsigned blocks = (unsigned)((long)nbatch * (W / g_used));
-    static bool attr_set = false;  // per instantiation: allow > 64 KiB dynamic LDS (gfx950 has 160 KiB)
+    static std::atomic<bool> attr_set{false};  // per instantiation: allow > 64 KiB dynamic LDS (gfx950 has 160 KiB)
     if (!attr_set) {
         FCD_HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_col_fft<N, true>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));

@@ -27,12 +27,11 @@
 // transpose, the row transform of length H and the transpose back.  These are the
 // generic-chain transforms, not the band-pruned register FFTs of the power-of-two fast
 // path.
+#include <atomic>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <complex>
-#include <map>
-#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -654,31 +653,13 @@ __global__ __launch_bounds__(NT, 4) void k_mr_int_cols(float2* __restrict__ Z, i
 constexpr int kMrLdsLen = 8192;
 constexpr long kMrLongRows = 1024;
 
-// the long rows' scratch, per device (grown on demand; the generic chain's sides above 8192)
-static float2* long_scratch(size_t bytes) {
-    static std::mutex mu;
-    static std::map<int, std::pair<void*, size_t>> bufs;
-    int dev = 0;
-    FCD_HIPCHK(hipGetDevice(&dev));
-    std::lock_guard<std::mutex> lock(mu);
-    auto& b = bufs[dev];
-    if (b.second < bytes) {
-        if (b.first) FCD_HIPCHK(hipFree(b.first));
-        b.first = nullptr;
-        b.second = 0;
-        FCD_HIPCHK(hipMalloc(&b.first, bytes));
-        b.second = bytes;
-    }
-    return static_cast<float2*>(b.first);
-}
-
 template <bool INV, int IN, int OUT>
 void launch_mr(const MrPlan& p, const void* in, void* out, long nrows, int H, float sub, const float2* tw,
-               const PhaseOut* ph, hipStream_t s) {
+               const PhaseOut* ph, hipStream_t s, float2* gs) {
     PhaseOut q{};
     if (ph) q = *ph;
     const int len = p.blue ? p.M : p.n;
-    static bool attr = false;
+    static std::atomic<bool> attr{false};
     if (!attr) {
         // (the rows need at most 2 x 8192 complex; ROW_IN_Z's scan adds 2 KB of static LDS)
         FCD_HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mr_rows<INV, IN, OUT, false>),
@@ -693,7 +674,7 @@ void launch_mr(const MrPlan& p, const void* in, void* out, long nrows, int H, fl
         FCD_CHECK_LAUNCH();
         return;
     }
-    float2* gs = long_scratch((size_t)kMrLongRows * 2 * len * sizeof(float2));
+    if (!gs) throw std::runtime_error("mr_rows: rows above 8192 points need the context's global scratch");
     for (long b0 = 0; b0 < grid; b0 += kMrLongRows) {  // (in order on the stream: the scratch is reused)
         const long nblk = std::min(kMrLongRows, grid - b0);
         hipLaunchKernelGGL((k_mr_rows<INV, IN, OUT, true>), dim3((unsigned)nblk), dim3(MR_THREADS), 0, s, in, out,
@@ -718,6 +699,11 @@ static int mr_lpf(int n) {
 // Sides up to kMrMaxLen (the MST's 32-bit vertex ids bound a frame's pixels); rows longer
 // than the LDS holds (kMrLdsLen complex, Bluestein's M included) run in global scratch.
 bool mr_supported(int n) { return n >= 2 && n <= kMrMaxLen; }
+
+size_t mr_long_scratch_bytes(const MrPlan& p) {
+    const int len = p.blue ? p.M : p.n;
+    return len <= kMrLdsLen ? 0 : (size_t)kMrLongRows * 2 * len * sizeof(float2);
+}
 
 MrPlan mr_plan(int n) {
     if (!mr_supported(n)) throw std::runtime_error("mixed-radix plan: unsupported length " + std::to_string(n));
@@ -817,26 +803,26 @@ std::vector<float2> mr_tables(const MrPlan& p) {
 }
 
 void mr_rows(const MrPlan& p, bool inverse, RowIn im, RowOut om, const void* in, void* out, long nrows, int H,
-             float sub, const float2* tw, const PhaseOut* ph, hipStream_t s) {
+             float sub, const float2* tw, const PhaseOut* ph, hipStream_t s, float2* gs) {
     if (nrows <= 0) return;
     if (!inverse && im == ROW_IN_REAL && om == ROW_OUT_COMPLEX)
-        launch_mr<false, ROW_IN_REAL, ROW_OUT_COMPLEX>(p, in, out, nrows, H, sub, tw, ph, s);
+        launch_mr<false, ROW_IN_REAL, ROW_OUT_COMPLEX>(p, in, out, nrows, H, sub, tw, ph, s, gs);
     else if (!inverse && im == ROW_IN_REAL2 && om == ROW_OUT_BAND2)
-        launch_mr<false, ROW_IN_REAL2, ROW_OUT_BAND2>(p, in, out, nrows, H, sub, tw, ph, s);
+        launch_mr<false, ROW_IN_REAL2, ROW_OUT_BAND2>(p, in, out, nrows, H, sub, tw, ph, s, gs);
     else if (inverse && im == ROW_IN_COMPLEX2 && om == ROW_OUT_REAL2)
-        launch_mr<true, ROW_IN_COMPLEX2, ROW_OUT_REAL2>(p, in, out, nrows, H, sub, tw, ph, s);
+        launch_mr<true, ROW_IN_COMPLEX2, ROW_OUT_REAL2>(p, in, out, nrows, H, sub, tw, ph, s, gs);
     else if (!inverse && im == ROW_IN_COMPLEX && om == ROW_OUT_COMPLEX)
-        launch_mr<false, ROW_IN_COMPLEX, ROW_OUT_COMPLEX>(p, in, out, nrows, H, sub, tw, ph, s);
+        launch_mr<false, ROW_IN_COMPLEX, ROW_OUT_COMPLEX>(p, in, out, nrows, H, sub, tw, ph, s, gs);
     else if (!inverse && im == ROW_IN_Z && om == ROW_OUT_COMPLEX)
-        launch_mr<false, ROW_IN_Z, ROW_OUT_COMPLEX>(p, in, out, nrows, H, sub, tw, ph, s);
+        launch_mr<false, ROW_IN_Z, ROW_OUT_COMPLEX>(p, in, out, nrows, H, sub, tw, ph, s, gs);
     else if (inverse && im == ROW_IN_COMPLEX && om == ROW_OUT_COMPLEX)
-        launch_mr<true, ROW_IN_COMPLEX, ROW_OUT_COMPLEX>(p, in, out, nrows, H, sub, tw, ph, s);
+        launch_mr<true, ROW_IN_COMPLEX, ROW_OUT_COMPLEX>(p, in, out, nrows, H, sub, tw, ph, s, gs);
     else if (inverse && im == ROW_IN_COMPLEX && om == ROW_OUT_REAL)
-        launch_mr<true, ROW_IN_COMPLEX, ROW_OUT_REAL>(p, in, out, nrows, H, sub, tw, ph, s);
+        launch_mr<true, ROW_IN_COMPLEX, ROW_OUT_REAL>(p, in, out, nrows, H, sub, tw, ph, s, gs);
     else if (inverse && im == ROW_IN_COMPLEX && om == ROW_OUT_PHASE)
-        launch_mr<true, ROW_IN_COMPLEX, ROW_OUT_PHASE>(p, in, out, nrows, H, sub, tw, ph, s);
+        launch_mr<true, ROW_IN_COMPLEX, ROW_OUT_PHASE>(p, in, out, nrows, H, sub, tw, ph, s, gs);
     else if (inverse && im == ROW_IN_BAND && om == ROW_OUT_PHASE)
-        launch_mr<true, ROW_IN_BAND, ROW_OUT_PHASE>(p, in, out, nrows, H, sub, tw, ph, s);
+        launch_mr<true, ROW_IN_BAND, ROW_OUT_PHASE>(p, in, out, nrows, H, sub, tw, ph, s, gs);
     else
         throw std::runtime_error("mr_rows: unsupported mode combination");
 }
@@ -856,7 +842,7 @@ bool mr_int_cols_supported(const MrPlan& p) {  // (also Bluestein: M is a power 
 template <int NT, int EPL, bool WAVE>
 static void launch_int_cols(const MrPlan& p, float2* Z, long blocks, int W, int C, int ngroups, size_t lds,
                             const float2* tw, const IntegCoef& c, hipStream_t s) {
-    static bool attr = false;
+    static std::atomic<bool> attr{false};
     if (!attr) {
         FCD_HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mr_int_cols<NT, EPL, WAVE>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
@@ -935,10 +921,10 @@ void mr_gather_cols(const float2* in, float2* out, int nb, int R, int C, const i
 }
 
 void mr_cols(const MrPlan& p, int W, bool inverse, float2* data, int nb, const float2* tw, float2* scratch,
-             hipStream_t s) {
+             hipStream_t s, float2* gs) {
     const int H = p.n;
     mr_transpose(data, scratch, nb, H, W, s);
-    mr_rows(p, inverse, ROW_IN_COMPLEX, ROW_OUT_COMPLEX, scratch, scratch, (long)nb * W, W, 0.f, tw, nullptr, s);
+    mr_rows(p, inverse, ROW_IN_COMPLEX, ROW_OUT_COMPLEX, scratch, scratch, (long)nb * W, W, 0.f, tw, nullptr, s, gs);
     mr_transpose(scratch, data, nb, W, H, s);
 }
 

@@ -4,6 +4,7 @@ The engine is the in-tree shared library lib/libfcd_mi355x.so built from
 csrc/ (HIP kernels for gfx950).  There is no fallback: if the library or a
 HIP device is missing every entry point raises.
 """
+import collections
 import ctypes
 import os
 import threading
@@ -125,11 +126,23 @@ def _f32(a):
     return np.ascontiguousarray(a, dtype=np.float32)
 
 
+def _spectrum_dtype(dtype):
+    """The precision the reference computes an image's spectrum in (fourier.py:18, fcd.py:28):
+    scipy's fft2 keeps float32 (and computes float16 in float32) and promotes everything
+    else -- float64, bool, int, uint -- to float64 (scipy/fft/_pocketfft/helper.py:91-92,
+    `_asfarray`); `image - np.mean(image)` of an integer image is float64 as well."""
+    dt = np.dtype(dtype)
+    return np.float32 if dt in (np.float32, np.float16) else np.float64
+
+
 def _img(a):
-    """An image in the precision the reference computes its spectrum in (fourier.py:18):
-    float64 stays float64, everything else becomes float32."""
+    """An image in the precision the reference computes its spectrum in (_spectrum_dtype):
+    a uint8 / uint16 reference (pattern.py's board, a raw camera frame) goes to the engine
+    as float64 (FCD_IMG_F64) exactly as scipy promotes it, not rounded to float32."""
     a = np.asarray(a)
-    return np.ascontiguousarray(a, dtype=np.float64 if a.dtype == np.float64 else np.float32)
+    if a.dtype.kind not in "biuf":
+        raise TypeError(f"image dtype {a.dtype} is not real")
+    return np.ascontiguousarray(a, dtype=_spectrum_dtype(a.dtype))
 
 
 def _img_flag(a):
@@ -418,19 +431,38 @@ class Engine:
         return out
 
 
-_engines = {}
+_engines = collections.OrderedDict()  # (shape, device, thread) -> Engine, least recently used first
 _engines_lock = threading.Lock()
 
 
+def _engine_cache_size():
+    return max(1, int(os.environ.get("FCD_ENGINE_CACHE", "4")))
+
+
 def engine_for(shape, device=None):
-    """Process-wide engine cache, one per (shape, device, thread)."""
-    key = (tuple(int(s) for s in shape), device, threading.get_ident())
+    """Process-wide engine cache: one engine per (shape, device, host thread) -- a context
+    is driven by one host thread at a time (fcd.h) -- and at most FCD_ENGINE_CACHE (4)
+    shapes per thread and device, the least recently used closed first; the engines of
+    threads that have ended are closed on the next miss.  A stateless drop-in call
+    (fcd.py:13-35) therefore never accumulates device memory beyond that bound; each
+    engine's chunk workspace is itself sized to the calls it has served (fcd_process)."""
+    tid = threading.get_ident()
+    key = (tuple(int(s) for s in shape), device, tid)
+    stale = []
     with _engines_lock:
-        e = _engines.get(key)
+        e = _engines.pop(key, None)
         if e is None:
+            alive = {t.ident for t in threading.enumerate()}
+            for k in [k for k in _engines if k[2] not in alive]:
+                stale.append(_engines.pop(k))
+            mine = [k for k in _engines if k[1] == device and k[2] == tid]
+            while len(mine) >= _engine_cache_size():
+                stale.append(_engines.pop(mine.pop(0)))
             e = Engine(shape, device)
-            _engines[key] = e
-        return e
+        _engines[key] = e  # most recently used last
+    for old in stale:
+        old.close()
+    return e
 
 
 def temporal_engine(device=None):
