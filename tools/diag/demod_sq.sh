@@ -7,7 +7,7 @@ out=gpurun_out/${TAG:-r06sq}
 mkdir -p $out
 export TMPDIR=/tmp
 args=${*:---steps 2 --warmup 1 --no-cpu-baseline --no-real-frames}
-re='band_phase_res|k_phase_rows|demod_rows|demod_cols|int_cols|int_c2r'
+re='band_phase_res|k_phase_rows|demod_rows|demod_cols|demod_phase|int_cols|int_c2r'
 i=0
 for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT" \
            "SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_SALU" \

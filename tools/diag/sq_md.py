@@ -22,14 +22,19 @@ def short(n):
     return n[:p] if p > 0 else n
 
 
+FPL = None  # frames per launch of the roofline pass (the chunk), from the command line
+
+
 def frames_of(name, grid_rank):
-    # k_band_phase_res only runs in the roofline pass (256 frames per launch); the other
-    # kernels' largest launches: 256 frames in the roofline pass, 128 in the headline halves
-    if "band_phase_res" in name:
-        return 256
+    # k_band_phase_res / k_demod_phase only run in the roofline pass (FPL frames per launch,
+    # 256 at 1024^2); the other kernels' largest launches: FPL in the roofline pass, FPL / 2
+    # in the headline's two halves (1024^2: 256 / 128)
+    fpl = FPL or 256
+    if "band_phase_res" in name or "demod_phase" in name:
+        return fpl
     if "k_phase_rows" in name or "int_c" in name:
-        return 128
-    return 256 if grid_rank == 0 else 128
+        return fpl // 2 if fpl == 256 else fpl
+    return fpl if grid_rank == 0 else fpl // 2
 
 
 def main(d):
@@ -75,4 +80,6 @@ def main(d):
 
 
 if __name__ == "__main__":
+    if len(sys.argv) > 2:
+        FPL = int(sys.argv[2])
     main(sys.argv[1])

@@ -68,6 +68,49 @@ __device__ __forceinline__ float2 cmulmi(float2 a) {
 }
 // Streaming store: the line is not kept in L2 / the Infinity Cache, so a large
 // output stream does not evict the small inputs every frame re-reads.
+// A load the compiler cannot move: issued where it stands (ahead of later stores, which
+// a plain load's use after them would let the compiler sink it behind), NOT tracked by
+// the compiler's wait insertion -- the caller waits with wait_vmcnt<N> before the first
+// use, N = the vector-memory operations it issued after the load (vmcnt retires in issue
+// order on gfx950, stores included).
+__device__ __forceinline__ float2 load_async(const float2* p) {
+    fv2 v;
+    asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+    return make_float2(v.x, v.y);
+}
+__device__ __forceinline__ float4 load_async4(const float4* p) {
+    float4 v;
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+    return v;
+}
+// s_waitcnt vmcnt(N), then the registers of v passed through empty volatile asm: the
+// values' uses depend on those statements, and volatile asm keeps its order, so no use of
+// a load_async result can be scheduled ahead of the wait (a wait with no data link to the
+// registers let the compiler hoist a use above it).  N <= 63.
+template <int N, int K>
+__device__ __forceinline__ void wait_vmcnt_for(float2 (&v)[K]) {
+    static_assert(N >= 0 && N <= 63, "vmcnt 0..63");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        fv2 t = pv(v[i]);
+        asm volatile("" : "+v"(t));
+        v[i] = vp(t);
+    }
+}
+template <int N, int K>
+__device__ __forceinline__ void wait_vmcnt_for(float4 (&v)[K]) {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    static_assert(N >= 0 && N <= 63, "vmcnt 0..63");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        f4 t = {v[i].x, v[i].y, v[i].z, v[i].w};
+        asm volatile("" : "+v"(t));
+        v[i] = make_float4(t.x, t.y, t.z, t.w);
+    }
+}
+
 __device__ __forceinline__ void st_stream(float* p, float v) {
     __builtin_nontemporal_store(v, p);
 }

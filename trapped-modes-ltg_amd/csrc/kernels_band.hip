@@ -277,6 +277,13 @@ __global__ __launch_bounds__((BPCfg<W, B>::THREADS), FCD_BAND_WAVES) void k_band
 #ifndef FCD_BAND_RES_ITEMS
 #define FCD_BAND_RES_ITEMS 4  // target items per CU (frame slices = items * CUs / (2 * row tiles))
 #endif
+// Phase stores of the theta-resident kernel: streaming (nt) or plain.  With two waves per
+// row (2048) a wave's store covers 16-byte pieces of every 32-byte sector (groups 0-3 of
+// each 8, the other wave groups 4-7), so streaming stores leave the HBM partial sectors;
+// plain ones merge both halves in the L2 first.
+#ifndef FCD_BAND_RES_STORE
+#define FCD_BAND_RES_STORE 0  // 0: plain where two waves share a row, streaming otherwise; 1: always streaming; 2: always plain
+#endif
 #ifndef FCD_BAND_RES_ROWS
 #define FCD_BAND_RES_ROWS 16  // rows per item (waves per workgroup): 16 = one Ab tile; 8 = half a tile, two workgroups per CU (same speed, kbench r02ap)
 #endif
@@ -348,7 +355,9 @@ __global__ __launch_bounds__((BRCfg<W, B, ROWS>::THREADS), 1) void k_band_phase_
 #pragma unroll
         for (int i = 0; i < SPT; ++i) {
             const int idx = min((int)threadIdx.x + i * C::THREADS, TN - 1);
-            pf[i] = src[min(idx / ROWS, NCA - 1) * BTILE + idx % ROWS];  // past the band: zeroed at staging
+            // issued here, ahead of the frame's phase stores (the compiler would sink a plain
+            // load to its use after them); awaited by the explicit wait in front of stage_in
+            pf[i] = load_async(src + min(idx / ROWS, NCA - 1) * BTILE + idx % ROWS);  // past the band: zeroed at staging
         }
     };
     // one row of one (item, frame): this wave's transform, phase step and stores
@@ -373,8 +382,14 @@ __global__ __launch_bounds__((BRCfg<W, B, ROWS>::THREADS), 1) void k_band_phase_
 #pragma unroll
             for (int k = 0; k < FCD_ATAN_N; ++k) {
                 const int n = g + L * t + RL * (q0 + 2 * k);
-                st_stream(o + n, wq[k].x);
-                st_stream(o + n + RL, wq[k].y);
+                constexpr bool NT = FCD_BAND_RES_STORE == 1 || (FCD_BAND_RES_STORE == 0 && RL == 64);
+                if constexpr (NT) {
+                    st_stream(o + n, wq[k].x);
+                    st_stream(o + n + RL, wq[k].y);
+                } else {
+                    o[n] = wq[k].x;
+                    o[n + RL] = wq[k].y;
+                }
             }
         }
     };
@@ -401,27 +416,46 @@ __global__ __launch_bounds__((BRCfg<W, B, ROWS>::THREADS), 1) void k_band_phase_
     int f = cur.f0;
     fetch(cur, f);
     float th[E];
+    load_theta(th, cur.c, cur.rt * ROWS + rl);  // kept for the item's frames (the compiler waits for them)
+    wait_vmcnt_for<0>(pf);                       // the tile
     int buf = 0;
-    bool fresh = true;
-    while (cur.it < items) {
-        const int c = cur.c, row = cur.rt * ROWS + rl;
-        const int ncc = c ? ncc1 : ncc0;
-        if (fresh) load_theta(th, c, row);  // kept for the item's frames
-        // Buffer `buf` was last read two frames ago, before the previous barrier.
-        float2* const st = stage0 + buf * C::STAGE;
-        stage_in(st, ncc);
-        __syncthreads();
+    stage_in(stage0, cur.c ? ncc1 : ncc0);
+    // Steady state (FCD_BAND_RES_ROTATED): the next frame's tile is loaded BEFORE this
+    // frame's phase stores and staged AFTER them, on a path with no other order of memory
+    // operations, so the wait for the tile (vmcnt counts stores too, in issue order) leaves
+    // the stores in flight.  The loop entered at its top with the first tile staged above
+    // otherwise merges the first iteration's state (only the tile outstanding) into the
+    // wait: vmcnt(0), every wave waiting for its previous row's store acknowledgements
+    // before each frame's barrier.  The next item's reference angles are loaded after the
+    // stores (waited for at their first use, once per item).
+    while (true) {
+        __syncthreads();  // stage(buf) complete; stage(buf ^ 1) last read before the previous barrier
+        const Item itc = cur;
         const int fcur = f;
-        fresh = f + 1 >= cur.f1;
+        const bool fresh = f + 1 >= cur.f1;
         if (fresh) {
             cur = seek(cur.it + gridDim.x);
             f = cur.f0;
         } else {
             ++f;
         }
-        if (cur.it < items) fetch(cur, f);
-        row_step(st, th, c, row, fcur);
+        const bool more = cur.it < items;
+        // (unconditional: a conditional load would merge a path without it into the
+        // compiler's count, and the waits would fall back to vmcnt(0))
+        fetch(more ? cur : itc, more ? f : fcur);
+        row_step(stage0 + buf * C::STAGE, th, itc.c, itc.rt * ROWS + rl, fcur);
+        if (!more) break;
+        if (fresh) {
+            load_theta(th, cur.c, cur.rt * ROWS + rl);
+            // waited for here, once per item (with the stores before it), so that no
+            // per-frame wait on the non-fresh path counts a pending angle load
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         buf ^= 1;
+        // the tile's SPT loads were followed by this row's E phase stores: vmcnt(E) (the
+        // counter retires in issue order) leaves the stores in flight
+        wait_vmcnt_for<E>(pf);
+        stage_in(stage0 + buf * C::STAGE, cur.c ? ncc1 : ncc0);
     }
 }
 

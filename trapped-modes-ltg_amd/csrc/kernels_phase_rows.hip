@@ -104,6 +104,9 @@ __device__ unsigned long long g_pr_stamps[PR_WAVES * 16];
     } while (0)
 #endif
 
+#ifndef FCD_PR_ASYNC
+#define FCD_PR_ASYNC 1  // counted waits for the tile / angle loads (fetch); 0: the compiler's waits
+#endif
 #ifndef FCD_PR_MINB
 #define FCD_PR_MINB 1  // workgroups per CU the register allocation must allow (launch-bounds)
 #endif
@@ -142,6 +145,12 @@ __global__ __launch_bounds__(PR_THREADS, FCD_PR_MINB) void k_phase_rows(
     constexpr int NST = 2 * PR_B * PR_ROWS;
     constexpr int SPT = (NST + PR_THREADS - 1) / PR_THREADS;
     float2 pf[SPT];
+    // (FCD_PR_ASYNC) the loads issue where they stand and are awaited by explicit counted
+    // waits (fft_lds.hpp load_async): the tile of the next item before this item's Zt
+    // stores, so its wait at the bottom of the loop leaves those stores in flight -- the
+    // compiler's own waits merged the loop's entry path into vmcnt(0) there, and counted the
+    // next tile's loads into the wait for the reference angles.  Band slots past the
+    // carrier's columns load a valid in-band value and are zeroed at staging.
     auto fetch = [&](int blk) {
         const int f = blk / rbs, rb = blk % rbs;
         const int r = rb * PR_ROWS + (threadIdx.x % PR_ROWS);
@@ -149,10 +158,26 @@ __global__ __launch_bounds__(PR_THREADS, FCD_PR_MINB) void k_phase_rows(
         for (int i = 0; i < SPT; ++i) {
             const int e = threadIdx.x + i * PR_THREADS;
             const int c = e / (PR_B * PR_ROWS), j = (e / PR_ROWS) % PR_B;
-            float2 v = make_float2(0.f, 0.f);
-            if ((NST % PR_THREADS == 0 || e < NST) && j < (c ? ncc1 : ncc0))
-                v = Ab[((((long)f * 2 + c) * tiles16 + (r >> 4)) * NCA + j) * 16 + (r & 15)];
-            pf[i] = v;
+            if constexpr (FCD_PR_ASYNC) {
+                const int cc = (NST % PR_THREADS == 0 || e < NST) ? c : 0;
+                const int jj = min(j, (cc ? ncc1 : ncc0) - 1);
+                pf[i] = load_async(Ab + ((((long)f * 2 + cc) * tiles16 + (r >> 4)) * NCA + max(jj, 0)) * 16 + (r & 15));
+            } else {
+                float2 v = make_float2(0.f, 0.f);
+                if ((NST % PR_THREADS == 0 || e < NST) && j < (c ? ncc1 : ncc0))
+                    v = Ab[((((long)f * 2 + c) * tiles16 + (r >> 4)) * NCA + j) * 16 + (r & 15)];
+                pf[i] = v;
+            }
+        }
+    };
+    // the staged tile: slots past a carrier's band as zeros (FCD_PR_ASYNC loads them)
+    auto stage_tile = [&]() {
+#pragma unroll
+        for (int i = 0; i < SPT; ++i) {
+            const int e = threadIdx.x + i * PR_THREADS;
+            const int c = e / (PR_B * PR_ROWS), j = (e / PR_ROWS) % PR_B;
+            const bool live = !FCD_PR_ASYNC || j < (c ? ncc1 : ncc0);
+            if (NST % PR_THREADS == 0 || e < NST) stage[(e / PR_ROWS) * PR_SROW + e % PR_ROWS] = live ? pf[i] : make_float2(0.f, 0.f);
         }
     };
     if (ch < nch) fetch(ch * per);
@@ -161,20 +186,22 @@ __global__ __launch_bounds__(PR_THREADS, FCD_PR_MINB) void k_phase_rows(
 #endif
     if (ch < nch) {
     const int it0 = ch * per, it1 = min(it0 + per, items);
+    if constexpr (FCD_PR_ASYNC) {  // the first tile, staged ahead of the loop
+        wait_vmcnt_for<0>(pf);
+        stage_tile();
+    }
     for (int blk = it0; blk < it1; ++blk) {
         const int f = blk / rbs, rb = blk % rbs;
         const int r = rb * PR_ROWS + wave;           // this wave's row
         const int par = (blk - it0) & 1;
         float2* const slot = row_slot(wave, par);    // band exchange, unwrapped row
         PR_STAMP(0);
-#pragma unroll
-        for (int i = 0; i < SPT; ++i) {
-            const int e = threadIdx.x + i * PR_THREADS;
-            if (NST % PR_THREADS == 0 || e < NST) stage[(e / PR_ROWS) * PR_SROW + e % PR_ROWS] = pf[i];
-        }
+        if constexpr (!FCD_PR_ASYNC) stage_tile();
         __syncthreads();
         PR_STAMP(1);
-        if (blk + 1 < it1) fetch(blk + 1);
+        if constexpr (!FCD_PR_ASYNC) {
+            if (blk + 1 < it1) fetch(blk + 1);
+        }
         PR_STAMP(2);
         // ---- band transforms of both carriers -> wrapped phases (natural strided)
         float w0[16], w1[16];
@@ -194,7 +221,7 @@ __global__ __launch_bounds__(PR_THREADS, FCD_PR_MINB) void k_phase_rows(
                 for (int c = 0; c < 2; ++c) {
                     const float4* tp = reinterpret_cast<const float4*>(theta + ((long)c * H + r) * PR_W) + lane * 4;
 #pragma unroll
-                    for (int k = 0; k < 4; ++k) th4[c][k] = tp[k];
+                    for (int k = 0; k < 4; ++k) th4[c][k] = FCD_PR_ASYNC ? load_async4(tp + k) : tp[k];
                 }
             };
             // both carriers' transforms in lockstep (GroupFFTTab2): float-half
@@ -212,6 +239,12 @@ __global__ __launch_bounds__(PR_THREADS, FCD_PR_MINB) void k_phase_rows(
                                                        sx + (PR_L + g) * GSched<PR_B>::REGION, t, btab);
             PR_STAMP(3);
             load_theta();  // after the transforms: register pressure
+            if constexpr (FCD_PR_ASYNC) {
+                // the next item's tile behind the angles: the angles' wait leaves it in flight
+                fetch(blk + 1 < it1 ? blk + 1 : blk);
+                wait_vmcnt_for<SPT>(th4[0]);
+                wait_vmcnt_for<SPT>(th4[1]);
+            }
             // FCD_PR_ATAN_N pixel pairs of each carrier per interleaved group
             // (wrapped_phase_pkn: 2 * FCD_PR_ATAN_N independent chains)
 #pragma unroll
@@ -372,6 +405,13 @@ __global__ __launch_bounds__(PR_THREADS, FCD_PR_MINB) void k_phase_rows(
         PR_STAMP(11);
         __syncthreads();
         PR_STAMP(12);
+        if constexpr (FCD_PR_ASYNC) {
+            // the next tile: its loads were followed by at least this item's PR_W / 64 Zt
+            // stores, so vmcnt(PR_W / 64) has retired them and leaves the stores in flight
+            static_assert(!(FCD_PR_ABL & 2), "the counted wait needs the Zt stores");
+            wait_vmcnt_for<PR_W / 64>(pf);
+            stage_tile();
+        }
     }
     }
 #ifdef FCD_STAMPS
