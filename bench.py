@@ -268,7 +268,7 @@ def main():
     #      FFT, kernels_phase_rows.hip), for the stage breakdown;
     #  (2) the demodulation unit of SURVEY.md §8d as its own launch group: the same
     #      frames with the wrapped phases written to HBM (k_demod_rows + k_demod_cols
-    #      + k_band_phase), for the roofline.
+    #      + k_band_phase_res), for the roofline.
     prof_steps = max(2, min(args.steps, 4))
     eng.profile(True)
     for _ in range(prof_steps):
@@ -309,7 +309,7 @@ def main():
 
     # Roofline of the demodulation launch group (SURVEY.md §8d unit: frame f32 in ->
     # two wrapped phase planes f32 out, B_demod = 12 N^2 bytes per frame): one group =
-    # k_demod_rows + k_demod_cols + k_band_phase over one chunk of `chunk` frames,
+    # k_demod_rows + k_demod_cols + k_band_phase_res over one chunk of `chunk` frames,
     # timed by HIP events the engine records on the launch stream around the group.
     chunk = int(stages.pop("chunk"))
     launches = int(stages.pop("launches"))
@@ -352,7 +352,8 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic_launch,
-                     "kernel": "demod launch group k_demod_rows + k_demod_cols + k_band_phase "
+                     "kernel": "demod launch group k_demod_rows + k_demod_cols + k_band_phase_res "
+                               "(theta-resident band-pruned inverse + phase; 512-bin window at 4096) "
                                "(frame f32 in -> 2 wrapped phases f32 out), 12*N^2 B/frame",
                      "frames_per_launch": round(demod_frames_per_launch, 2),
                      "us_per_launch": round(demod_us_per_launch, 2),

@@ -19,8 +19,8 @@ import statistics
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-# the demod launch group of bench.py's roofline pass: the band kernel up to 2048-point
-# rows, the full-length inverse k_demod_phase at 4096 (512-bin carrier windows)
+# the demod launch group of bench.py's roofline pass: the band kernel (k_band_phase_res;
+# at 4096 its 512-bin form since round 6; k_demod_phase before, and where no band fits)
 DEMOD = ("k_demod_rows", "k_demod_cols", "k_band_phase", "k_demod_phase")
 # the heights-only headline path (fused band transform + unwrap + row FFT)
 HEADLINE = ("k_demod_rows", "k_demod_cols", "k_phase_rows", "k_colk", "k_seam_check", "k_int_cols", "k_int_c2r")

@@ -1020,9 +1020,12 @@ void fast_demod(fcd_ctx* c, const float* frames, int nb, hipStream_t s, int fo =
     float* wrapped = c->wrapped.as<float>() + fo * 2 * c->hw();
     fcdk::demod_rows(c->W, frames, c->H, nb, T, Xb, c->twp_row.as<float2>(), s);
     fcdk::demod_cols(c->H, Xb, nb, T, Ab, c->NCA, dc_tw(c), s);
-    if (c->band_B)
-        fcdk::band_phase(c->W, c->band_B, false, Ab, c->H, nb, c->NCA, c->NCc[0], c->NCc[1], c->theta_p.as<float>(),
-                         wrapped, c->band_pre.as<float2>(), c->band_ptw.as<float2>(), s);
+    // band-pruned inverse: band_B up to 2048-point rows; at 4096-point rows the fused
+    // kernel's 512-bin window (its REF mode made theta_b in the same decomposition)
+    const int bB = c->band_B ? c->band_B : (c->W == 4096 && fcd_env_int("FCD_WIDE_BAND", 1) ? c->fused_B : 0);
+    if (bB)
+        fcdk::band_phase(c->W, bB, false, Ab, c->H, nb, c->NCA, c->NCc[0], c->NCc[1], c->theta_p.as<float>(), wrapped,
+                         c->band_pre.as<float2>(), c->band_ptw.as<float2>(), s);
     else
         fcdk::demod_phase(c->W, Ab, c->H, nb, c->NCA, T, c->theta.as<float>(), wrapped, c->twp_row.as<float2>(), s);
 }

@@ -245,6 +245,58 @@ struct GroupFFTTab {
             pass<P + 1, INV>(x, s, t, tab);
         }
     }
+
+    // float-half exchange (GroupFFT::run_half) with the table twiddles: the 512-point
+    // band transform of the theta-resident band kernel, whose register twiddles
+    // (23 complex per lane) would spill at four waves per SIMD
+    template <bool INV>
+    __device__ __forceinline__ static void run_half(float2 (&x)[E], float* s, int t, const float2* tab) {
+        pass_half<0, INV>(x, s, t, tab);
+    }
+
+    template <int P, bool INV>
+    __device__ __forceinline__ static void pass_half(float2 (&x)[E], float* s, int t, const float2* tab) {
+        constexpr int R = S::radix(P), L = S::ell(P), BPT = E / R;
+        float2 a[BPT][R];
+#pragma unroll
+        for (int b = 0; b < BPT; ++b) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) a[b][r] = x[b + BPT * r];
+            if constexpr (P > 0) {
+                const int k = (t + b * G) & (L - 1);
+                const float2* tk = tab + S::passoff(P) + k * (R - 1) - 1;
+#pragma unroll
+                for (int r = 1; r < R; ++r) a[b][r] = cmul_dir<INV>(a[b][r], tk[r]);
+            }
+            dft_reg<R, INV>(a[b]);
+        }
+        if constexpr (P + 1 == NP) {
+#pragma unroll
+            for (int b = 0; b < BPT; ++b)
+#pragma unroll
+                for (int r = 0; r < R; ++r) x[b + BPT * r] = a[b][r];
+        } else {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                wave_sync();
+#pragma unroll
+                for (int b = 0; b < BPT; ++b) {
+                    const int j = t + b * G;
+                    const int k = j & (L - 1);
+                    const int base = (j - k) * R + k;
+#pragma unroll
+                    for (int r = 0; r < R; ++r) s[pad(base + r * L)] = h ? a[b][r].y : a[b][r].x;
+                }
+                wave_sync();
+#pragma unroll
+                for (int q = 0; q < E; ++q) {
+                    const float v = s[pad(t + G * q)];
+                    if (h) x[q].y = v; else x[q].x = v;
+                }
+            }
+            pass_half<P + 1, INV>(x, s, t, tab);
+        }
+    }
 };
 
 // Two independent transforms of the same length advanced in lockstep (the two
