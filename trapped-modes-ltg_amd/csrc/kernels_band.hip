@@ -297,6 +297,9 @@ __global__ __launch_bounds__((BPCfg<W, B>::THREADS), FCD_BAND_WAVES) void k_band
 #ifndef FCD_BAND_RES_PAIR
 #define FCD_BAND_RES_PAIR 1  // 512-bin window: the half-wave groups' neighbouring pixels paired into float2 stores
 #endif
+#ifndef FCD_BAND_QUAD
+#define FCD_BAND_QUAD 1  // 256-bin window: the quarter-wave groups' neighbouring pixels transposed into float4 stores
+#endif
 #ifndef FCD_BAND_RES_TAB512
 #define FCD_BAND_RES_TAB512 1  // 512-bin window: pass twiddles from LDS (register twiddles spill at 4 waves per SIMD)
 #endif
@@ -416,6 +419,31 @@ __global__ __launch_bounds__((BRCfg<W, B, ROWS>::THREADS), 1) void k_band_phase_
                 uq[2 * k + 1] = x[q0 + 2 * k + 1];
             }
             wrapped_phase_pkn<FCD_ATAN_N>(tq, uq, wq);
+            if constexpr (G == 16 && FCD_ATAN_N == 2 && FCD_BAND_QUAD) {
+                // 256-bin groups are quarter waves: groups g0 .. g0 + 3 (lane rows 0-3) hold
+                // the four neighbouring pixels g0 + j + L t.  A 4 x 4 transpose of slots
+                // q0 .. q0 + 3 across the lane rows (permlane32 then permlane16 half
+                // exchanges) gives lane row j the four pixels of slot q0 + j: float4 stores
+                unsigned a0 = __float_as_uint(wq[0].x), a1 = __float_as_uint(wq[0].y);
+                unsigned a2 = __float_as_uint(wq[1].x), a3 = __float_as_uint(wq[1].y);
+                auto r = __builtin_amdgcn_permlane32_swap(a0, a2, false, false);
+                a0 = r[0];
+                a2 = r[1];
+                r = __builtin_amdgcn_permlane32_swap(a1, a3, false, false);
+                a1 = r[0];
+                a3 = r[1];
+                r = __builtin_amdgcn_permlane16_swap(a0, a1, false, false);
+                a0 = r[0];
+                a1 = r[1];
+                r = __builtin_amdgcn_permlane16_swap(a2, a3, false, false);
+                a2 = r[0];
+                a3 = r[1];
+                const float4 v = make_float4(__uint_as_float(a0), __uint_as_float(a1), __uint_as_float(a2), __uint_as_float(a3));
+                const int j = g & 3;
+                if (!FCD_BAND_NOSTORE || v.x == 1234.5f)
+                    *reinterpret_cast<float4*>(o + (g - j) + L * t + RL * (q0 + j)) = v;
+                continue;
+            }
 #pragma unroll
             for (int k = 0; k < FCD_ATAN_N; ++k) {
                 const int n = g + L * t + RL * (q0 + 2 * k);
