@@ -127,6 +127,8 @@ int c2r_rows_per_block(int W);
 // band_phase (REF = false) and phase_rows read as their `theta`
 void band_theta_lanes(int W, int B, const float* theta, int rows, float* thp, hipStream_t s);
 bool band_supported(int W, int B);
+void band_phase_fold(int W, const float2* Ab, int H, int nb, int NCA, int ncc0, int ncc1, const float* theta,
+                     float* out, const float2* pre, const float2* ptw, hipStream_t s);
 void band_phase(int W, int B, bool ref, const float2* Ab, int H, int nb, int NCA, int ncc0, int ncc1,
                 const float* theta, float* out, const float2* pre, const float2* ptw, hipStream_t s);
 // column-0 prefix of the residue-free unwrap (kernels_unwrap.hip)

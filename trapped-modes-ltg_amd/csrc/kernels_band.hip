@@ -304,23 +304,32 @@ __global__ __launch_bounds__((BPCfg<W, B>::THREADS), FCD_BAND_WAVES) void k_band
 #define FCD_BAND_RES_TAB512 1  // 512-bin window: pass twiddles from LDS (register twiddles spill at 4 waves per SIMD)
 #endif
 
-template <int W, int B, int ROWS>
+#ifndef FCD_FOLD_ROWS
+#define FCD_FOLD_ROWS 4  // rows per item of the folded 4096-point band kernel (4 waves each)
+#endif
+#ifndef FCD_FOLD_PREF
+#define FCD_FOLD_PREF 0  // its pre-twiddles as factors ([RL] + [L][16]: 4 KB instead of 32 KB)
+#endif
+
+template <int W, int B, int ROWS, int FOLD = 1>
 struct BRCfg {
+    static_assert(FOLD == 1 || FOLD == 2, "staged band of B or 2 B bins");
     static constexpr int G = B / 16, L = W / B, RL = W / 16;
+    static constexpr int SB = FOLD * B;     // staged band bins (FOLD = 2: two B-bin halves folded per group)
     static_assert(RL == 64 || RL == 128 || RL == 256, "one, two or four waves per row");
     static_assert(BTILE % ROWS == 0, "items cover whole or half Ab tiles");
     static constexpr int THREADS = ROWS * RL;
     static constexpr int SR = ROWS + 1;     // staged row pitch (complex)
     static constexpr int REGION = GSched<B>::REGION;
-    static constexpr int STAGE = B * SR;    // float2 per staging buffer
-    static constexpr int TN = B * ROWS;     // staged slots per item tile
+    static constexpr int STAGE = SB * SR;   // float2 per staging buffer
+    static constexpr int TN = SB * ROWS;    // staged slots per item tile
     static constexpr int SPT = (TN + THREADS - 1) / THREADS;
     static constexpr int NBUF = 2;  // staging buffers
     static constexpr bool TAB = B > 256 && FCD_BAND_RES_TAB512;  // pass twiddles from an LDS table (GroupFFTTab::run_half)
     // pre-twiddles exp(2 pi i (t + G q) g / W): the [16][RL] table, or at 4096-point rows its
     // factors exp(2 pi i t g / W) (per lane, in registers) and exp(2 pi i G q g / W) ([L][16]),
     // the same product k_phase_rows_wide's REF mode forms for the reference angles
-    static constexpr bool PREF = W == 4096 && FCD_BAND_RES_PREF;
+    static constexpr bool PREF = W == 4096 && (B == 512 ? FCD_BAND_RES_PREF : FCD_FOLD_PREF);
     static constexpr int PRE = PREF ? RL + L * 16 : RL * 16;
     static constexpr size_t XOFF = (size_t)(NBUF * STAGE + PRE) * 8;  // exchange regions (bytes)
     static constexpr size_t TOFF = XOFF + (size_t)ROWS * L * REGION * 4;  // twiddle table (bytes, TAB)
@@ -328,11 +337,11 @@ struct BRCfg {
     static_assert(TOFF % 8 == 0, "table alignment");
 };
 
-template <int W, int B, int ROWS>
-__global__ __launch_bounds__((BRCfg<W, B, ROWS>::THREADS), 1) void k_band_phase_res(
+template <int W, int B, int ROWS, int FOLD = 1>
+__global__ __launch_bounds__((BRCfg<W, B, ROWS, FOLD>::THREADS), 1) void k_band_phase_res(
     const float2* __restrict__ Ab, int H, int nb, int NCA, int ncc0, int ncc1, const float* __restrict__ theta,
     float* __restrict__ out, const float2* __restrict__ pre, const float2* __restrict__ ptw, int slices) {
-    using C = BRCfg<W, B, ROWS>;
+    using C = BRCfg<W, B, ROWS, FOLD>;
     constexpr int G = C::G, L = C::L, RL = C::RL, E = 16, SPT = C::SPT, TN = C::TN, SR = C::SR;
     constexpr int HALVES = BTILE / ROWS;  // item tiles per Ab tile
     extern __shared__ __attribute__((aligned(16))) float2 lds_b[];
@@ -347,6 +356,14 @@ __global__ __launch_bounds__((BRCfg<W, B, ROWS>::THREADS), 1) void k_band_phase_
         for (int i = threadIdx.x; i < GSched<B>::TABLE; i += C::THREADS) btab[i] = ptw[i];
     } else {
         fft.load(ptw, t);
+    }
+    // FOLD = 2: group g's input is A[j] + w_g A[j + B] (times the pre-twiddle of j), w_g =
+    // exp(2 pi i B g / W), the 2 B-bin band folded onto one B-point transform per group
+    float2 om = make_float2(1.f, 0.f);
+    if constexpr (FOLD == 2) {
+        double sn, cs;
+        sincospi(2.0 * (double)g * B / W, &sn, &cs);
+        om = make_float2((float)cs, (float)sn);
     }
     float2 pb = make_float2(1.f, 0.f);
     if constexpr (C::PREF) {  // pre[l][q]: q = 0 gives exp(2 pi i t g / W), t = 0 the G q g factor
@@ -400,8 +417,11 @@ __global__ __launch_bounds__((BRCfg<W, B, ROWS>::THREADS), 1) void k_band_phase_
     auto row_step = [&](const float2* st, const float (&th)[E], int c, int row, int f) {
         float2 x[E];
 #pragma unroll
-        for (int q = 0; q < E; ++q)
-            x[q] = cmul(st[(t + G * q) * SR + rl], C::PREF ? cmul(pb, ptl[RL + g * 16 + q]) : ptl[q * RL + l]);
+        for (int q = 0; q < E; ++q) {
+            float2 a = st[(t + G * q) * SR + rl];
+            if constexpr (FOLD == 2) a = cadd(a, cmul(om, st[(t + G * q + B) * SR + rl]));
+            x[q] = cmul(a, C::PREF ? cmul(pb, ptl[RL + g * 16 + q]) : ptl[q * RL + l]);
+        }
         if constexpr (C::TAB)
             GroupFFTTab<B>::template run_half<true>(x, s, t, btab);
         else
@@ -664,6 +684,26 @@ static void band_dispatch_b(int B, bool ref, const float2* Ab, int H, int nb, in
     }
     throw std::runtime_error("band_phase: unsupported band window " + std::to_string(B) + " for row length " +
                              std::to_string(W));
+}
+
+// 4096-point rows with a band of up to 512 bins: the theta-resident kernel at B = 256 with the
+// two 256-bin halves folded per group (16 groups of 256-point transforms, one exchange each,
+// float4 stores), pre / ptw the B = 256 tables, theta in the B = 256 lane order
+void band_phase_fold(int W, const float2* Ab, int H, int nb, int NCA, int ncc0, int ncc1, const float* theta,
+                     float* out, const float2* pre, const float2* ptw, hipStream_t s) {
+    if (W != 4096 || ncc0 > 512 || ncc1 > 512 || H % BTILE != 0)
+        throw std::runtime_error("band_phase_fold: 4096-point rows, bands of up to 512 bins");
+    constexpr int ROWS = FCD_FOLD_ROWS;
+    using R = BRCfg<4096, 256, ROWS, 2>;
+    static_assert(R::LDS <= 160 * 1024, "folded band kernel LDS");
+    const int slices = band_res_slices(H, nb, ROWS);
+    const int items = 2 * (H / ROWS) * slices;
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_band_phase_res<4096, 256, ROWS, 2>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)R::LDS);
+    hipLaunchKernelGGL((k_band_phase_res<4096, 256, ROWS, 2>), dim3(band_grid(items, (int)((160 * 1024) / R::LDS))),
+                       dim3(R::THREADS), R::LDS, s, Ab, H, nb, NCA, ncc0, ncc1, theta, out, pre, ptw, slices);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) throw std::runtime_error(std::string("band_phase_fold launch: ") + hipGetErrorString(e));
 }
 
 bool band_supported(int W, int B) { return B >= 16 && B <= 256 && 2 * B <= W && (B & (B - 1)) == 0; }
