@@ -2011,7 +2011,17 @@ int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int f
             hipEvent_t cen0 = nullptr, cen1 = nullptr;
             if (early && last) {
                 if (!c->cstream) {
-                    HIPCHK(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
+                    // the readback stream at the highest priority: the runtime gives it a hardware
+                    // queue of its own, so its copy does not wait behind the other streams'
+                    // integration kernels (with GPU_MAX_HW_QUEUES = 4 a default-priority stream
+                    // shared the second half's queue: the census came back after its c2r,
+                    // r06 trace, ~58 us of idle chip per call)
+                    int lo = 0, hi = 0;
+                    HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+                    if (fcd_env_int("FCD_CSTREAM_PRIO", 1))
+                        HIPCHK(hipStreamCreateWithPriority(&c->cstream, hipStreamNonBlocking, hi));
+                    else
+                        HIPCHK(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
                     for (auto& e : c->ev_cen) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
                 }
                 cen0 = c->ev_cen[0];
