@@ -236,10 +236,7 @@ struct fcd_ctx {
     int fused_B = 0;                 // band window of the fused kernel (= band_B, or 512 at 4096-point rows)
     DevBuf band_pre, band_ptw, theta_b;  // its pre-twiddles, pass twiddles, reference angle of the band
     DevBuf theta_p;                      // theta_b in the phase kernels' lane-contiguous order
-    // 4096-point rows: the folded band kernel's tables (B = 256) and theta_b in its lane
-    // order, built at its first use after each reference (band_phase_fold)
-    DevBuf fold_pre, fold_ptw, theta_f;
-    bool theta_f_ok = false;
+    int band_T = 0;                      // their group transform length (band_B, or 256 folded at 4096)
     bool fused_ok = false;           // k_phase_rows applies (height-only calls)
     bool force_unfused = false;      // FCD_UNFUSED=1: take the unfused chain (A/B measurement)
     int nstreams = 2;                // FCD_STREAMS: device-path chunks split over 1 or 2 streams
@@ -959,24 +956,18 @@ void build_demod_tables(fcd_ctx* c, hipStream_t s) {
     // 512-bin window the unfused band kernel does not (that path keeps k_demod_phase)
     c->fused_B = (c->band_B || W == 4096) && fcdk::phase_rows_supported(W, B, H) ? B : 0;
     std::vector<float2> pre, ptw;
+    // the group transforms' length: the window, or at 4096-point rows its halves folded
+    // per group (kernels_phase_rows_wide.hip / kernels_band.hip FOLD)
+    c->band_T = c->band_B ? c->band_B : (c->fused_B ? fcdk::phase_rows_wide_bt(W) : 0);
     if (c->band_B || c->fused_B) {
-        pre = band_pretwiddles(W, B);
-        ptw = group_twiddles(B);
+        pre = band_pretwiddles(W, c->band_T);
+        ptw = group_twiddles(c->band_T);
         c->band_pre.ensure(pre.size() * sizeof(float2));
         c->band_ptw.ensure(ptw.size() * sizeof(float2));
         upload(c->band_pre.p, pre.data(), pre.size() * sizeof(float2), s);
         upload(c->band_ptw.p, ptw.data(), ptw.size() * sizeof(float2), s);
         c->theta_b.ensure(2 * (size_t)c->hw() * sizeof(float));
         c->theta_p.ensure(2 * (size_t)c->hw() * sizeof(float));
-    }
-    c->theta_f_ok = false;
-    if (!c->band_B && c->fused_B == 512) {
-        const std::vector<float2> fp = band_pretwiddles(W, 256), ft = group_twiddles(256);
-        c->fold_pre.ensure(fp.size() * sizeof(float2));
-        c->fold_ptw.ensure(ft.size() * sizeof(float2));
-        upload(c->fold_pre.p, fp.data(), fp.size() * sizeof(float2), s);
-        upload(c->fold_ptw.p, ft.data(), ft.size() * sizeof(float2), s);
-        HIPCHK(hipStreamSynchronize(s));  // fp / ft die here
     }
     c->fused_ok = c->fused_B != 0;
     std::vector<float2> ztw;
@@ -1034,17 +1025,14 @@ void fast_demod(fcd_ctx* c, const float* frames, int nb, hipStream_t s, int fo =
     fcdk::demod_rows(c->W, frames, c->H, nb, T, Xb, c->twp_row.as<float2>(), s);
     fcdk::demod_cols(c->H, Xb, nb, T, Ab, c->NCA, dc_tw(c), s);
     // band-pruned inverse: band_B up to 2048-point rows; at 4096-point rows the fused
-    // kernel's 512-bin window (its REF mode made theta_b), as two 256-bin halves folded per
-    // group (FCD_WIDE_BAND 2, band_phase_fold) or as 512-point groups (1)
-    const int wide = fcd_env_int("FCD_WIDE_BAND", 2);
-    const int bB = c->band_B ? c->band_B : (c->W == 4096 && wide ? c->fused_B : 0);
-    if (!c->band_B && bB == 512 && wide == 2) {
-        if (!c->theta_f_ok) throw std::runtime_error("fast_demod: folded band angles missing");
-        fcdk::band_phase_fold(c->W, Ab, c->H, nb, c->NCA, c->NCc[0], c->NCc[1], c->theta_f.as<float>(), wrapped,
-                              c->fold_pre.as<float2>(), c->fold_ptw.as<float2>(), s);
-    } else if (bB)
-        fcdk::band_phase(c->W, bB, false, Ab, c->H, nb, c->NCA, c->NCc[0], c->NCc[1], c->theta_p.as<float>(), wrapped,
-                         c->band_pre.as<float2>(), c->band_ptw.as<float2>(), s);
+    // kernel's 512-bin window (its REF mode made theta_b) as two 256-bin halves folded per
+    // group (band_phase_fold)
+    if (c->band_B)
+        fcdk::band_phase(c->W, c->band_B, false, Ab, c->H, nb, c->NCA, c->NCc[0], c->NCc[1], c->theta_p.as<float>(),
+                         wrapped, c->band_pre.as<float2>(), c->band_ptw.as<float2>(), s);
+    else if (c->fused_B == 512 && c->band_T == 256 && fcd_env_int("FCD_WIDE_BAND", 1))
+        fcdk::band_phase_fold(c->W, Ab, c->H, nb, c->NCA, c->NCc[0], c->NCc[1], c->theta_p.as<float>(), wrapped,
+                              c->band_pre.as<float2>(), c->band_ptw.as<float2>(), s);
     else
         fcdk::demod_phase(c->W, Ab, c->H, nb, c->NCA, T, c->theta.as<float>(), wrapped, c->twp_row.as<float2>(), s);
 }
@@ -1062,19 +1050,7 @@ void band_reference(fcd_ctx* c, const float* dref, hipStream_t s) {
     else  // 4096-point rows: the fused kernel's own band transform in its REF mode
         fcdk::phase_rows_wide_ref(c->W, c->Ab.as<float2>(), c->H, c->NCA, c->NCc[0], c->NCc[1],
                                   c->band_pre.as<float2>(), c->band_ptw.as<float2>(), c->theta_b.as<float>(), s);
-    fcdk::band_theta_lanes(c->W, c->band_B ? c->band_B : c->fused_B, c->theta_b.as<float>(), 2 * c->H,
-                           c->theta_p.as<float>(), s);
-    c->theta_f_ok = false;
-}
-
-// theta_b in the folded band kernel's lane order (4096-point rows, fast_demod), from the
-// final theta_b of the reference (reference_state's last step)
-void fold_reference(fcd_ctx* c, hipStream_t s) {
-    c->theta_f_ok = false;
-    if (c->band_B || c->fused_B != 512) return;
-    c->theta_f.ensure(2 * (size_t)c->hw() * sizeof(float));
-    fcdk::band_theta_lanes(c->W, 256, c->theta_b.as<float>(), 2 * c->H, c->theta_f.as<float>(), s);
-    c->theta_f_ok = true;
+    fcdk::band_theta_lanes(c->W, c->band_T, c->theta_b.as<float>(), 2 * c->H, c->theta_p.as<float>(), s);
 }
 
 // Everything the per-frame path needs from the reference once c->info and
@@ -1128,7 +1104,6 @@ void reference_state(fcd_ctx* c, const float* dref0, const float* dref1, hipStre
             }
         }
     }
-    fold_reference(c, s);
     HIPCHK(hipStreamSynchronize(s));
 }
 

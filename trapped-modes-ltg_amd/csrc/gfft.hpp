@@ -195,10 +195,6 @@ struct GroupFFT {
 // LDS: GSched<B>::TABLE entries, pass-major as GroupFFT::load expects) instead
 // of per-lane registers: for long transforms whose register twiddles would
 // cost too many VGPRs (B = 1024: 27 complex per lane).
-#ifndef FCD_XA512
-#define FCD_XA512 2  // exchange addressing of the 512-point table-twiddle half transform (GroupFFTTab::xa)
-#endif
-
 template <int B>
 struct GroupFFTTab {
     using S = GSched<B>;
@@ -250,25 +246,8 @@ struct GroupFFTTab {
         }
     }
 
-    // float-half exchange (GroupFFT::run_half) with the table twiddles: the 512-point
-    // band transform of the theta-resident band kernel, whose register twiddles
-    // (23 complex per lane) would spill at four waves per SIMD
-    // float index of element n in the exchange region.  pad() leaves the 512-point
-    // transform's strided reads (t + 32 q, a half wave = one 32-bank b32 lane group) 2-way
-    // on one bank (t + t/16 spans 33 banks).  FCD_XA512 = 1: an XOR swizzle of each
-    // 32-float row, conflict-free for the reads and both passes' writes (16 t + r;
-    // 256 h + u + 16 r) but one address register per element; 2: n + n / 32
-    __device__ __forceinline__ static int xa(int n) {
-        if constexpr (B == 512 && FCD_XA512 == 1) {
-            const int row = n >> 5;
-            return (n & ~31) | ((n & 31) ^ ((row & 15) ^ ((row & 8) << 1)));
-        } else if constexpr (B == 512 && FCD_XA512 == 2) {
-            return n + (n >> 5);  // reads and the first pass's writes conflict-free, the second's 2-way on 8 banks
-        } else {
-            return pad(n);
-        }
-    }
-
+    // float-half exchange (GroupFFT::run_half) with the table twiddles: the folded 256-point
+    // band transforms of the 4096-point fused kernel, one carrier at a time
     template <bool INV>
     __device__ __forceinline__ static void run_half(float2 (&x)[E], float* s, int t, const float2* tab) {
         pass_half<0, INV>(x, s, t, tab);
@@ -305,12 +284,12 @@ struct GroupFFTTab {
                     const int k = j & (L - 1);
                     const int base = (j - k) * R + k;
 #pragma unroll
-                    for (int r = 0; r < R; ++r) s[xa(base + r * L)] = h ? a[b][r].y : a[b][r].x;
+                    for (int r = 0; r < R; ++r) s[pad(base + r * L)] = h ? a[b][r].y : a[b][r].x;
                 }
                 wave_sync();
 #pragma unroll
                 for (int q = 0; q < E; ++q) {
-                    const float v = s[xa(t + G * q)];
+                    const float v = s[pad(t + G * q)];
                     if (h) x[q].y = v; else x[q].x = v;
                 }
             }

@@ -230,6 +230,7 @@ void phase_rows_wide(int W, bool unwrap, const float2* Ab, int H, int nb, int NC
 void phase_rows_wide_seam(int W, int H, int nb, const float2* seam, int* flags, hipStream_t s);
 void phase_rows_wide_ref(int W, const float2* Ab, int H, int NCA, int ncc0, int ncc1, const float2* pre,
                          const float2* ptw, float* theta_b, hipStream_t s);
+int phase_rows_wide_bt(int W);  // its band group transform length (the window, or half of it folded)
 
 // ---- unwrap ----
 // counts[m] = residues of map m; any_only: counts[m] > 0 iff map m has residues (blocks of

@@ -288,22 +288,9 @@ __global__ __launch_bounds__((BPCfg<W, B>::THREADS), FCD_BAND_WAVES) void k_band
 #define FCD_BAND_RES_ROWS 16  // rows per item (waves per workgroup): 16 = one Ab tile; 8 = half a tile, two workgroups per CU (same speed, kbench r02ap)
 #endif
 
-#ifndef FCD_BAND_RES_ROWS_4096
-#define FCD_BAND_RES_ROWS_4096 4  // rows per item at 4096-point rows (4 waves each): 4 = 1024 threads (2: two 512-thread workgroups per CU, 1-3% slower, r06 wb4)
-#endif
-#ifndef FCD_BAND_RES_PREF
-#define FCD_BAND_RES_PREF 0  // 1: at 4096-point rows the pre-twiddles as the factors k_phase_rows_wide uses ([RL] + [L][16]; one more cmul, 2% slower)
-#endif
-#ifndef FCD_BAND_RES_PAIR
-#define FCD_BAND_RES_PAIR 1  // 512-bin window: the half-wave groups' neighbouring pixels paired into float2 stores
-#endif
 #ifndef FCD_BAND_QUAD
 #define FCD_BAND_QUAD 1  // 256-bin window: the quarter-wave groups' neighbouring pixels transposed into float4 stores
 #endif
-#ifndef FCD_BAND_RES_TAB512
-#define FCD_BAND_RES_TAB512 1  // 512-bin window: pass twiddles from LDS (register twiddles spill at 4 waves per SIMD)
-#endif
-
 #ifndef FCD_FOLD_ROWS
 #define FCD_FOLD_ROWS 4  // rows per item of the folded 4096-point band kernel (4 waves each)
 #endif
@@ -325,16 +312,13 @@ struct BRCfg {
     static constexpr int TN = SB * ROWS;    // staged slots per item tile
     static constexpr int SPT = (TN + THREADS - 1) / THREADS;
     static constexpr int NBUF = 2;  // staging buffers
-    static constexpr bool TAB = B > 256 && FCD_BAND_RES_TAB512;  // pass twiddles from an LDS table (GroupFFTTab::run_half)
     // pre-twiddles exp(2 pi i (t + G q) g / W): the [16][RL] table, or at 4096-point rows its
     // factors exp(2 pi i t g / W) (per lane, in registers) and exp(2 pi i G q g / W) ([L][16]),
     // the same product k_phase_rows_wide's REF mode forms for the reference angles
-    static constexpr bool PREF = W == 4096 && (B == 512 ? FCD_BAND_RES_PREF : FCD_FOLD_PREF);
+    static constexpr bool PREF = W == 4096 && FCD_FOLD_PREF;
     static constexpr int PRE = PREF ? RL + L * 16 : RL * 16;
     static constexpr size_t XOFF = (size_t)(NBUF * STAGE + PRE) * 8;  // exchange regions (bytes)
-    static constexpr size_t TOFF = XOFF + (size_t)ROWS * L * REGION * 4;  // twiddle table (bytes, TAB)
-    static constexpr size_t LDS = TOFF + (TAB ? (size_t)GSched<B>::TABLE * 8 : 0);
-    static_assert(TOFF % 8 == 0, "table alignment");
+    static constexpr size_t LDS = XOFF + (size_t)ROWS * L * REGION * 4;
 };
 
 template <int W, int B, int ROWS, int FOLD = 1>
@@ -350,13 +334,8 @@ __global__ __launch_bounds__((BRCfg<W, B, ROWS, FOLD>::THREADS), 1) void k_band_
     const int rl = threadIdx.x / RL;             // this wave's (or wave pair's) row of the tile
     const int l = threadIdx.x % RL, g = l / G, t = l % G;
     float* const s = reinterpret_cast<float*>(lds_b) + C::XOFF / 4 + (size_t)(rl * L + g) * C::REGION;
-    float2* const btab = reinterpret_cast<float2*>(reinterpret_cast<char*>(lds_b) + C::TOFF);
     GroupFFT<B> fft;
-    if constexpr (C::TAB) {
-        for (int i = threadIdx.x; i < GSched<B>::TABLE; i += C::THREADS) btab[i] = ptw[i];
-    } else {
-        fft.load(ptw, t);
-    }
+    fft.load(ptw, t);
     // FOLD = 2: group g's input is A[j] + w_g A[j + B] (times the pre-twiddle of j), w_g =
     // exp(2 pi i B g / W), the 2 B-bin band folded onto one B-point transform per group
     float2 om = make_float2(1.f, 0.f);
@@ -422,10 +401,7 @@ __global__ __launch_bounds__((BRCfg<W, B, ROWS, FOLD>::THREADS), 1) void k_band_
             if constexpr (FOLD == 2) a = cadd(a, cmul(om, st[(t + G * q + B) * SR + rl]));
             x[q] = cmul(a, C::PREF ? cmul(pb, ptl[RL + g * 16 + q]) : ptl[q * RL + l]);
         }
-        if constexpr (C::TAB)
-            GroupFFTTab<B>::template run_half<true>(x, s, t, btab);
-        else
-            fft.template run_half<true>(x, s, t);
+        fft.template run_half<true>(x, s, t);
         float* o = out + (((long)f * 2 + c) * H + row) * W;
 #pragma unroll
         for (int q0 = 0; q0 < E; q0 += 2 * FCD_ATAN_N) {
@@ -468,16 +444,7 @@ __global__ __launch_bounds__((BRCfg<W, B, ROWS, FOLD>::THREADS), 1) void k_band_
             for (int k = 0; k < FCD_ATAN_N; ++k) {
                 const int n = g + L * t + RL * (q0 + 2 * k);
                 constexpr bool NT = FCD_BAND_RES_STORE == 1 || (FCD_BAND_RES_STORE == 0 && RL == 64);
-                if constexpr (G == 32 && FCD_BAND_RES_PAIR) {
-                    // 512-bin groups are half waves: group g (lanes 0-31) and g + 1 (32-63)
-                    // hold neighbouring pixels.  One half exchange gives the lower lanes both
-                    // pixels of slot q, the upper lanes both of q + 1: float2 stores
-                    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(wq[k].x), __float_as_uint(wq[k].y),
-                                                                    false, false);
-                    const float2 v = make_float2(__uint_as_float(r[0]), __uint_as_float(r[1]));
-                    if (!FCD_BAND_NOSTORE || v.x == 1234.5f)
-                        *reinterpret_cast<float2*>(o + (g & ~1) + L * t + RL * (q0 + 2 * k + (g & 1))) = v;
-                } else if constexpr (FCD_BAND_NOSTORE) {
+                if constexpr (FCD_BAND_NOSTORE) {
                     if (wq[k].x == 1234.5f) o[n] = wq[k].y;
                 } else if constexpr (NT) {
                     st_stream(o + n, wq[k].x);
@@ -610,25 +577,6 @@ static int band_grid(long items, int per_cu) {
 template <int W, int B>
 static void launch_band(bool ref, const float2* Ab, int H, int nb, int NCA, int ncc0, int ncc1, const float* theta,
                         float* out, const float2* pre, const float2* ptw, hipStream_t s) {
-    if constexpr (B > 256) {
-        // 4096-point rows, 512-bin window: the theta-resident form only (the reference
-        // angles come from k_phase_rows_wide's REF mode, the same decomposition)
-        static_assert(W == 4096 && B == 512, "512-bin window: 4096-point rows");
-        if (ref) throw std::runtime_error("band_phase: no REF mode at a 512-bin window (phase_rows_wide_ref)");
-        constexpr int ROWS = FCD_BAND_RES_ROWS_4096;
-        using R = BRCfg<W, B, ROWS>;
-        static_assert(R::LDS <= 160 * 1024, "resident band kernel LDS");
-        const int slices = band_res_slices(H, nb, ROWS);
-        const int items = 2 * (H / ROWS) * slices;
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_band_phase_res<W, B, ROWS>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)R::LDS);
-        hipLaunchKernelGGL((k_band_phase_res<W, B, ROWS>), dim3(band_grid(items, (int)((160 * 1024) / R::LDS))),
-                           dim3(R::THREADS), R::LDS, s, Ab, H,
-                           nb, NCA, ncc0, ncc1, theta, out, pre, ptw, slices);
-        const hipError_t e = hipGetLastError();
-        if (e != hipSuccess) throw std::runtime_error(std::string("band_phase_res launch: ") + hipGetErrorString(e));
-        return;
-    } else {
     using C = BPCfg<W, B>;
     const size_t lds = C::LDS;
     const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(8, (160 * 1024) / lds));
@@ -667,7 +615,6 @@ static void launch_band(bool ref, const float2* Ab, int H, int nb, int NCA, int 
     }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) throw std::runtime_error(std::string("band_phase launch: ") + hipGetErrorString(e));
-    }
 }
 
 template <int W>
@@ -679,7 +626,6 @@ static void band_dispatch_b(int B, bool ref, const float2* Ab, int H, int nb, in
         case 64: if constexpr (W >= 128) { launch_band<W, 64>(ref, Ab, H, nb, NCA, ncc0, ncc1, theta, out, pre, ptw, s); return; } break;
         case 128: if constexpr (W >= 256) { launch_band<W, 128>(ref, Ab, H, nb, NCA, ncc0, ncc1, theta, out, pre, ptw, s); return; } break;
         case 256: if constexpr (W >= 512) { launch_band<W, 256>(ref, Ab, H, nb, NCA, ncc0, ncc1, theta, out, pre, ptw, s); return; } break;
-        case 512: if constexpr (W == 4096) { launch_band<W, 512>(ref, Ab, H, nb, NCA, ncc0, ncc1, theta, out, pre, ptw, s); return; } break;
         default: break;
     }
     throw std::runtime_error("band_phase: unsupported band window " + std::to_string(B) + " for row length " +

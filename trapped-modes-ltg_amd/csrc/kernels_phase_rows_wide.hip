@@ -42,15 +42,26 @@ namespace fcdk {
 
 namespace {
 
+#ifndef FCD_WIDE_FOLD
+#define FCD_WIDE_FOLD 1  // 4096: the 512-bin band as 16 folded 256-point groups (0: 8 groups of 512)
+#endif
+#ifndef FCD_WIDE_LOCKSTEP
+#define FCD_WIDE_LOCKSTEP 1  // 4096: both carriers' band transforms in lockstep (GroupFFTTab2, as at 2048); 0: one after the other (c5 3.70 k vs 3.76 k, r06 wl)
+#endif
+
 template <int W>
 struct WideCfg {
     static_assert(W == 2048 || W == 4096, "2048- or 4096-point rows");
-    static constexpr int B = W / 8;                 // band window
+    static constexpr int B = W / 8;                 // band window (staged bins per carrier)
+    // transform length: B, or at 4096 (FCD_WIDE_FOLD) B / 2 with the band's two halves folded
+    // per group (kernels_band.hip FOLD): 16 groups of 256 points, one exchange each
+    static constexpr int BF = W == 4096 && FCD_WIDE_FOLD ? B / 2 : B;
+    static constexpr int FOLD = B / BF;
     static constexpr int NWR = W / 1024;            // waves per row
     static constexpr int RL = W / 16;               // lanes per row
     static constexpr int ROWS = W == 2048 ? 4 : 2;  // rows per tile
     static constexpr int THREADS = ROWS * RL;       // 512
-    static constexpr int G = B / 16, L = W / B;
+    static constexpr int G = BF / 16, L = W / BF;
     static constexpr int ZT = zt_layout(W);         // Zt layout tile height (kernels.hpp)
     static constexpr int SLOT = padded_len(W) + 2;  // row slot (float2), 16-byte multiple
     static constexpr int HALF = padded_len(1024);   // one wave's 1024-point region; pad(k + 1024 h) = pad(k) + h HALF
@@ -61,19 +72,19 @@ struct WideCfg {
     // exp(2 pi i (t + G q) g / W) = exp(2 pi i t g / W) exp(2 pi i G q g / W): [RL] + [L][16]
     static constexpr bool PRE_LDS = W == 2048;
     static constexpr bool CTW_LDS = W == 2048;      // join twiddles in LDS (else read from L2)
-    static constexpr bool SEQ = B > 256;            // the carriers' band transforms one after the other
+    static constexpr bool SEQ = W == 4096 && !FCD_WIDE_LOCKSTEP;  // the carriers' band transforms one after the other
     // LDS carve (float2 units)
     static constexpr int OFF_STAGE = 0;                                      // [2][B][SROW]
     static constexpr int OFF_PRE = OFF_STAGE + 2 * B * SROW;
     static constexpr int OFF_ZTAB = OFF_PRE + (PRE_LDS ? 16 * RL : RL + L * 16);
     static constexpr int OFF_CTW = OFF_ZTAB + ZTAB;
     static constexpr int OFF_BTAB = OFF_CTW + (CTW_LDS ? NCTW : 0);
-    static constexpr int OFF_SLOT = (OFF_BTAB + GSched<B>::TABLE + 1) & ~1;
+    static constexpr int OFF_SLOT = (OFF_BTAB + GSched<BF>::TABLE + 1) & ~1;
     static constexpr int OFF_PREV = OFF_SLOT + ROWS * SLOT;  // the last row's second slot
     static constexpr int OFF_CARRY = OFF_PREV + SLOT;        // [ROWS + 1][NWR] wave scan totals (int)
     static constexpr size_t LDS = (size_t)OFF_CARRY * 8 + (size_t)(ROWS + 1) * NWR * 4;
     static_assert(SLOT % 2 == 0 && LDS <= 160 * 1024, "fused wide kernel LDS");
-    static_assert(2 * L * GSched<B>::REGION <= 2 * SLOT, "paired float-half band exchange fits the slot");
+    static_assert(2 * L * GSched<BF>::REGION <= 2 * SLOT, "paired float-half band exchange fits the slot");
     static_assert(NWR * HALF <= SLOT, "NWR 1024-point exchange regions per slot");
     static_assert(ZT % ROWS == 0 && 2 * B * ROWS % THREADS == 0, "tile shapes");
 };
@@ -98,7 +109,7 @@ __global__ __launch_bounds__(WideCfg<W>::THREADS, 1) void k_phase_rows_wide(
     float* __restrict__ col0, int* __restrict__ flags, float2* __restrict__ Zt, float2* __restrict__ seam, int per,
     float* __restrict__ theta_out) {
     using C = WideCfg<W>;
-    constexpr int B = C::B, NWR = C::NWR, RL = C::RL, ROWS = C::ROWS, G = C::G, L = C::L, SROW = C::SROW;
+    constexpr int B = C::B, BF = C::BF, NWR = C::NWR, RL = C::RL, ROWS = C::ROWS, G = C::G, L = C::L, SROW = C::SROW;
     extern __shared__ __attribute__((aligned(16))) float2 lds_w[];
     float2* const stage = lds_w + C::OFF_STAGE;
     float2* const ptl = lds_w + C::OFF_PRE;
@@ -109,6 +120,18 @@ __global__ __launch_bounds__(WideCfg<W>::THREADS, 1) void k_phase_rows_wide(
     const int row = threadIdx.x / RL, l = threadIdx.x % RL;  // tile row; lane in the row's waves
     const int wv = l >> 6, lane = threadIdx.x & 63;          // wave of the row
     const int g = l / G, t = l % G;                          // band group / lane in group
+    // FOLD: group g's input is A[j] + w_g A[j + BF], w_g = exp(2 pi i BF g / W)
+    float2 om = make_float2(1.f, 0.f);
+    if constexpr (C::FOLD == 2) {
+        double sn, cs;
+        sincospi(2.0 * (double)g * BF / W, &sn, &cs);
+        om = make_float2((float)cs, (float)sn);
+    }
+    auto band_in = [&](int c, int q, int row_) {  // carrier c's (folded) band value t + G q of tile row row_
+        float2 a = stage[(c * B + t + G * q) * SROW + row_];
+        if constexpr (C::FOLD == 2) a = cadd(a, cmul(om, stage[(c * B + t + G * q + BF) * SROW + row_]));
+        return a;
+    };
     // the last row alternates between two slots, so the previous tile's last
     // unwrapped row survives for the census against this tile's first row
     auto slot_idx = [&](int w, int k) { return w == ROWS - 1 && k ? ROWS : w; };
@@ -119,7 +142,7 @@ __global__ __launch_bounds__(WideCfg<W>::THREADS, 1) void k_phase_rows_wide(
         for (int i = 0; i < h; ++i) a += unbias_total(carry[slot_idx(w, k) * NWR + i]);
         return a * kTwoPiW;
     };
-    for (int i = threadIdx.x; i < GSched<B>::TABLE; i += C::THREADS) btab[i] = ptw[i];
+    for (int i = threadIdx.x; i < GSched<C::BF>::TABLE; i += C::THREADS) btab[i] = ptw[i];
     if constexpr (C::PRE_LDS) {
         for (int i = threadIdx.x; i < 16 * RL; i += C::THREADS) ptl[(i % 16) * RL + i / 16] = pre[i];
     } else {  // pre[l][q]: lane l = g G + t; q = 0 gives exp(2 pi i t g / W), t = 0 the G q g factor
@@ -177,8 +200,12 @@ __global__ __launch_bounds__(WideCfg<W>::THREADS, 1) void k_phase_rows_wide(
                 for (int c = 0; c < 2; ++c) {
                     float2 x[16];
 #pragma unroll
-                    for (int q = 0; q < 16; ++q) x[q] = cmul(stage[(c * B + t + G * q) * SROW + row], pretw(q));
-                    GroupFFTTab<B>::template run<true>(x, slot + g * GSched<B>::REGION, t, btab);
+                    for (int q = 0; q < 16; ++q) x[q] = cmul(band_in(c, q, row), pretw(q));
+                    if constexpr (C::FOLD == 2)
+                        GroupFFTTab<BF>::template run_half<true>(x, reinterpret_cast<float*>(slot) + g * GSched<BF>::REGION,
+                                                                 t, btab);
+                    else
+                        GroupFFTTab<BF>::template run<true>(x, slot + g * GSched<BF>::REGION, t, btab);
                     if constexpr (REF) {  // the reference's angles, natural layout
                         float* o = theta_out + ((long)c * H + r) * W;
 #pragma unroll
@@ -224,11 +251,11 @@ __global__ __launch_bounds__(WideCfg<W>::THREADS, 1) void k_phase_rows_wide(
 #pragma unroll
                 for (int q = 0; q < 16; ++q) {
                     const float2 p = pretw(q);
-                    x0[q] = cmul(stage[(t + G * q) * SROW + row], p);
-                    x1[q] = cmul(stage[(B + t + G * q) * SROW + row], p);
+                    x0[q] = cmul(band_in(0, q, row), p);
+                    x1[q] = cmul(band_in(1, q, row), p);
                 }
                 float* const sx = reinterpret_cast<float*>(slot);
-                GroupFFTTab2<B>::template run_half<true>(x0, x1, sx + g * GSched<B>::REGION, sx + (L + g) * GSched<B>::REGION,
+                GroupFFTTab2<BF>::template run_half<true>(x0, x1, sx + g * GSched<BF>::REGION, sx + (L + g) * GSched<BF>::REGION,
                                                          t, btab);
                 if constexpr (REF) {  // the reference's angles, natural layout
 #pragma unroll
@@ -558,6 +585,8 @@ void phase_rows_wide_ref(int W, const float2* Ab, int H, int NCA, int ncc0, int 
     phase_rows_wide_t<4096>(2, Ab, H, 1, NCA, ncc0, ncc1, nullptr, pre, ptw, nullptr, nullptr, nullptr, nullptr,
                             nullptr, theta_b, s);
 }
+
+int phase_rows_wide_bt(int W) { return W == 2048 ? WideCfg<2048>::BF : WideCfg<4096>::BF; }
 
 size_t phase_rows_wide_lds(int W) { return W == 2048 ? WideCfg<2048>::LDS : WideCfg<4096>::LDS; }
 
