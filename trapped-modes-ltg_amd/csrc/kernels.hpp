@@ -11,6 +11,9 @@
 
 namespace fcdk {
 
+// the current device's CU count, cached once per process (kernels_fast.hip)
+int device_cu_count();
+
 // Row-FFT input / output modes.
 // ROW_IN_Z (mr_rows only): z = (w0 + 2 pi k0) + i (w1 + 2 pi k1) of the two maps' rows, in =
 // wrapped [nb][2][H][W], PhaseOut::kin the k-fields (null: none), as make_z

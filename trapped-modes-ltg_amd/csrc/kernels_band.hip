@@ -523,13 +523,7 @@ __global__ __launch_bounds__((BRCfg<W, B, ROWS, FOLD>::THREADS), 1) void k_band_
 }
 
 static int band_res_slices(int H, int nb, int rows) {
-    static int ncu = 0;
-    if (!ncu) {
-        int dev = 0;
-        hipDeviceProp_t p;
-        if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&p, dev) == hipSuccess) ncu = p.multiProcessorCount;
-        if (!ncu) ncu = 256;
-    }
+    const int ncu = device_cu_count();  // (atomic cache: launchers run from two host threads)
     const int tiles = 2 * (H / rows);
     const int want = (FCD_BAND_RES_ITEMS * ncu + tiles - 1) / tiles;
     return std::max(1, std::min(nb, want));
@@ -563,13 +557,7 @@ void band_theta_lanes(int W, int B, const float* theta, int rows, float* thp, hi
 
 // ------------------------------------------------------------------ launchers
 static int band_grid(long items, int per_cu) {
-    static int ncu = 0;
-    if (!ncu) {
-        int dev = 0;
-        hipDeviceProp_t p;
-        if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&p, dev) == hipSuccess) ncu = p.multiProcessorCount;
-        if (!ncu) ncu = 256;
-    }
+    const int ncu = device_cu_count();  // (atomic cache: launchers run from two host threads)
     const long cap = (long)ncu * per_cu;
     return (int)(items < cap ? (items > 0 ? items : 1) : cap);
 }

@@ -692,7 +692,7 @@ __global__ __launch_bounds__(C2RCfg<W>::THREADS) void k_int_c2r(const float2* __
 // ------------------------------------------------------------------ launchers
 // (atomic: the exact-first chain's two halves launch from two host threads)
 static std::atomic<int> g_num_cu{0};
-static int grid_for(long work_items, int per_cu) {
+int device_cu_count() {
     int ncu = g_num_cu.load(std::memory_order_relaxed);
     if (!ncu) {
         int dev = 0;
@@ -702,6 +702,10 @@ static int grid_for(long work_items, int per_cu) {
         if (!ncu) ncu = 256;
         g_num_cu.store(ncu, std::memory_order_relaxed);
     }
+    return ncu;
+}
+static int grid_for(long work_items, int per_cu) {
+    const int ncu = device_cu_count();
     const long cap = (long)ncu * per_cu;
     return (int)(work_items < cap ? (work_items > 0 ? work_items : 1) : cap);
 }

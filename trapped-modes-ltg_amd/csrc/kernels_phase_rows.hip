@@ -471,13 +471,7 @@ int phase_rows_tile(int W) { return W == 2048 ? 4 : (W == 4096 ? 2 : PR_ROWS); }
 // Blocks of k_phase_rows at 1024-point rows: the tiles split evenly over the blocks (one
 // block per CU), each a contiguous range of `per` consecutive 8-row tiles.
 static void pr_layout(int H, int nb, int& grid, int& per) {
-    static int ncu = 0;
-    if (!ncu) {
-        int dev = 0;
-        hipDeviceProp_t p;
-        if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&p, dev) == hipSuccess) ncu = p.multiProcessorCount;
-        if (!ncu) ncu = 256;
-    }
+    const int ncu = device_cu_count();  // (atomic cache: launchers run from two host threads)
     const long items = (long)nb * (H / PR_ROWS);
     const int per_cu = std::max<int>(1, std::min<int>(160 * 1024 / (int)PR_LDS, 16 / PR_WAVES));
     const int slots = (int)std::min<long>(items, (long)ncu * per_cu);

@@ -486,13 +486,7 @@ __global__ __launch_bounds__(256) void k_seam_check_wide(const float2* __restric
 namespace {
 
 int num_cus() {
-    static int ncu = 0;
-    if (!ncu) {
-        int dev = 0;
-        hipDeviceProp_t p;
-        if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&p, dev) == hipSuccess) ncu = p.multiProcessorCount;
-        if (!ncu) ncu = 256;
-    }
+    const int ncu = device_cu_count();  // (atomic cache: launchers run from two host threads)
     return ncu;
 }
 
