@@ -42,6 +42,15 @@ namespace fcdk {
 
 namespace {
 
+#ifndef FCD_WIDE_NOTHETA
+#define FCD_WIDE_NOTHETA 0  // diagnostic ablation only (wrong results): no reference-angle loads
+#endif
+#if FCD_WIDE_NOTHETA && !defined(FCD_DIAGNOSTIC)
+#error "FCD_WIDE_NOTHETA is diagnostic-only: build with -DFCD_DIAGNOSTIC"
+#endif
+#ifndef FCD_WIDE_ZT_NT
+#define FCD_WIDE_ZT_NT 1  // streaming Zt stores at 4096 too (fused 133.6 -> 131.4 us/frame, c5 +0.6 %, r06 te; 0: plain)
+#endif
 #ifndef FCD_WIDE_FOLD
 #define FCD_WIDE_FOLD 1  // 4096: the 512-bin band as 16 folded 256-point groups (0: 8 groups of 512)
 #endif
@@ -273,13 +282,15 @@ __global__ __launch_bounds__(WideCfg<W>::THREADS, 1) void k_phase_rows_wide(
                     __syncthreads();  // the slots' exchange regions before the next tile
                     continue;
                 }
-                // reference angles of this lane's 16 pixels (lane-contiguous copy, band_theta_lanes)
+                // reference angles of this lane's 16 pixels (lane-contiguous copy, band_theta_lanes).
+                // (Issued ahead of the band transforms with a counted wait, as the 1024 kernel
+                // does: 7 VGPRs spilled at 2048 and 4096, fused 4096 133.6 -> 141 us/frame, r06 te.)
                 float4 th4[2][4];
 #pragma unroll
                 for (int c = 0; c < 2; ++c) {
                     const float4* tp = reinterpret_cast<const float4*>(theta + ((long)c * H + r) * W) + l * 4;
 #pragma unroll
-                    for (int k = 0; k < 4; ++k) th4[c][k] = tp[k];
+                    for (int k = 0; k < 4; ++k) th4[c][k] = FCD_WIDE_NOTHETA ? make_float4(0.f, 0.f, 0.f, 0.f) : tp[k];
                 }
 #pragma unroll
                 for (int q0 = 0; q0 < 16; q0 += 4) {  // two pixel pairs of each carrier per interleaved group
@@ -425,8 +436,9 @@ __global__ __launch_bounds__(WideCfg<W>::THREADS, 1) void k_phase_rows_wide(
                 // Zt).  With 4-row runs plain stores let the L2 join it with the next tile's
                 // half (3.09k -> 3.15k frames/s, r04j); with 16-row runs (eight tiles per
                 // line) plain stores cost a read of every line (r04q: reads 206 -> 279 MB),
-                // so those stay streaming
-                if constexpr (C::ROWS * 8 >= 32 || C::ZT != 2 * C::ROWS) st_stream(p, v);
+                // so those stay streaming.  Round 6 (folded band): streaming at 4-row runs
+                // too, the half lines no longer crowding the reference angles out of L2
+                if constexpr (C::ROWS * 8 >= 32 || C::ZT != 2 * C::ROWS || FCD_WIDE_ZT_NT) st_stream(p, v);
                 else *p = v;
             };
 #pragma unroll JU
