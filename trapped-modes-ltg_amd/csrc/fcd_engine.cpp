@@ -242,12 +242,14 @@ struct fcd_ctx {
     int nstreams = 2;                // FCD_STREAMS: device-path chunks split over 1 or 2 streams
     int fused_split = 2;             // ... for the fused chain (default: 2 up to 1024-wide rows, 1 above)
     bool early_census = true;        // FCD_EARLY_CENSUS: device calls read the census back before the integration
-    hipStream_t cstream = nullptr;   // its copy stream and the two halves' "census complete" events
+    // the two halves' "census copied" events: each half copies its flags to `census` on its
+    // own stream as soon as they are final (first_pass_chunk)
     hipEvent_t ev_cen[2] = {nullptr, nullptr};
     hipEvent_t ev_done = nullptr;    // end of the last device call's work on its (caller's) stream
     hipStream_t done_stream = nullptr;  // that stream, while the work may still be running
     bool done_pending = false;
-    hipStream_t aux = nullptr;       // the second stream and its fork / join events
+    hipStream_t aux = nullptr;       // the second stream of the fused chain's halves, and the fork / join events
+    hipStream_t aux_x = nullptr;     // the exact-first chain's second stream (get_aux)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     DevBuf ir_seam;                  // k_int_rows2's seam rows (tile-range edges), one region per stream
     DevBuf ztw, col0, seam;          // its 1024-point group-FFT twiddles; column-0 wrapped values [f][2][H];
@@ -1014,6 +1016,20 @@ fcdk::DemodTables demod_tables(fcd_ctx* c) {
     return t;
 }
 
+// The second stream of a two-halves chain (exact: the exact-first chain's, its own so the
+// two chains' orders never mix) and the fork / join events, created on first use.  (The
+// exact chain's at the highest priority measured 8.1-8.5 k against 10.3-10.5 k camera
+// frames/s in the bench's context, r06 ax: its half then ran ahead of the caller's.)
+hipStream_t get_aux(fcd_ctx* c, bool exact) {
+    if (!c->ev_fork) {
+        HIPCHK(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
+    }
+    hipStream_t& st = exact ? c->aux_x : c->aux;
+    if (!st) HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    return st;
+}
+
 // Fast path for nb frames (device pointer): band-pruned demod -> wrapped (c->wrapped).
 // fo: first workspace frame (as first_pass_chunk).
 void fast_demod(fcd_ctx* c, const float* frames, int nb, hipStream_t s, int fo = 0) {
@@ -1328,15 +1344,15 @@ FCD_API int fcd_destroy(fcd_ctx* ctx) {
         if (ctx->ev_done) (void)hipEventSynchronize(ctx->ev_done);
         (void)hipStreamSynchronize(ctx->own);
         (void)hipStreamDestroy(ctx->own);
-        if (ctx->cstream) {
-            (void)hipStreamSynchronize(ctx->cstream);
-            (void)hipStreamDestroy(ctx->cstream);
-            for (hipEvent_t e : ctx->ev_cen) (void)hipEventDestroy(e);
-        }
+        for (hipEvent_t e : ctx->ev_cen)
+            if (e) (void)hipEventDestroy(e);
         if (ctx->ev_done) (void)hipEventDestroy(ctx->ev_done);
-        if (ctx->aux) {
-            (void)hipStreamSynchronize(ctx->aux);
-            (void)hipStreamDestroy(ctx->aux);
+        for (hipStream_t st : {ctx->aux, ctx->aux_x})
+            if (st) {
+                (void)hipStreamSynchronize(st);
+                (void)hipStreamDestroy(st);
+            }
+        if (ctx->ev_fork) {
             (void)hipEventDestroy(ctx->ev_fork);
             (void)hipEventDestroy(ctx->ev_join);
         }
@@ -1500,7 +1516,8 @@ namespace {
 // kernel + tile-range census, which then runs right after it), before the integration.
 void first_pass_chunk(fcd_ctx* c, const float* fr, int nb, bool unwrap, bool fused, int* res, float* hdst,
                       int32_t* kdst, const fcdk::IntegCoef& coef, hipStream_t s, int fo = 0,
-                      hipEvent_t census_ev = nullptr) {
+                      hipEvent_t census_ev = nullptr, const int* census_src = nullptr, int* census_host = nullptr,
+                      size_t census_n = 0) {
     if (fused) {
         // height only: band transforms, phase, unwrap and the z-row FFT in one
         // pass (kernels_phase_rows.hip); colk lands in the spectra's DC bins
@@ -1521,6 +1538,11 @@ void first_pass_chunk(fcd_ctx* c, const float* fr, int nb, bool unwrap, bool fus
         fcdk::phase_rows(c->W, unwrap, Ab, c->H, nb, c->NCA, c->NCc[0], c->NCc[1], c->theta_p.as<float>(),
                          c->band_pre.as<float2>(), c->band_ptw.as<float2>(), c->ztw.as<float2>(), col0, res, Zt, seam,
                          s, defer);
+        // early census: the flags go to the page-locked readback buffer on this stream as soon
+        // as they are final (a copy on a stream of its own waited behind whatever shared its
+        // hardware queue), and the event marks their arrival
+        if (census_ev && census_n)
+            HIPCHK(hipMemcpyAsync(census_host, census_src, census_n * sizeof(int), hipMemcpyDeviceToHost, s));
         if (census_ev) HIPCHK(hipEventRecord(census_ev, s));
         if (unwrap) fcdk::unwrap_colk_compact(col0, 2 * nb, c->H, colk, s);
         if (c->profiling) HIPCHK(hipEventRecord(c->next_event(), s));
@@ -1896,18 +1918,14 @@ int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int f
                 // and small graph-round kernels overlap the other half's kernels, instead of
                 // leaving the chip idle (the camera frames' exact chain, r04ap trace).
                 const int nb0 = (nb + 1) / 2;
-                if (!c->aux) {
-                    HIPCHK(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
-                    HIPCHK(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
-                    HIPCHK(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
-                }
+                hipStream_t const ax = get_aux(c, true);
                 HIPCHK(hipEventRecord(c->ev_fork, s));
-                HIPCHK(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
+                HIPCHK(hipStreamWaitEvent(ax, c->ev_fork, 0));
                 std::exception_ptr err1;
                 std::thread t1([&] {
                     try {
                         HIPCHK(hipSetDevice(c->device));
-                        half(1, nb0, nb - nb0, c->aux);
+                        half(1, nb0, nb - nb0, ax);
                     } catch (...) {
                         err1 = std::current_exception();
                     }
@@ -1919,7 +1937,7 @@ int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int f
                     err0 = std::current_exception();
                 }
                 t1.join();
-                HIPCHK(hipEventRecord(c->ev_join, c->aux));
+                HIPCHK(hipEventRecord(c->ev_join, ax));
                 HIPCHK(hipStreamWaitEvent(s, c->ev_join, 0));
                 if (err0) std::rethrow_exception(err0);
                 if (err1) std::rethrow_exception(err1);
@@ -1985,20 +2003,9 @@ int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int f
             const bool last = f0 + nb >= n_frames;
             hipEvent_t cen0 = nullptr, cen1 = nullptr;
             if (early && last) {
-                if (!c->cstream) {
-                    // the readback stream at the highest priority: the runtime gives it a hardware
-                    // queue of its own, so its copy does not wait behind the other streams'
-                    // integration kernels (with GPU_MAX_HW_QUEUES = 4 a default-priority stream
-                    // shared the second half's queue: the census came back after its c2r,
-                    // r06 trace, ~58 us of idle chip per call)
-                    int lo = 0, hi = 0;
-                    HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-                    if (fcd_env_int("FCD_CSTREAM_PRIO", 1))
-                        HIPCHK(hipStreamCreateWithPriority(&c->cstream, hipStreamNonBlocking, hi));
-                    else
-                        HIPCHK(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
+                if (!c->ev_cen[0])
                     for (auto& e : c->ev_cen) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-                }
+                c->census.ensure((size_t)n_frames * 2 * sizeof(int));
                 cen0 = c->ev_cen[0];
                 cen1 = nsplit == 2 ? c->ev_cen[1] : nullptr;
                 cen_halves = nsplit;
@@ -2007,23 +2014,25 @@ int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int f
                 // two halves of the chunk on two streams: kernels bound by different
                 // resources (HBM-bound c2r / demod_rows, latency-bound phase_rows /
                 // int_cols) overlap instead of running back to back
-                if (!c->aux) {
-                    HIPCHK(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
-                    HIPCHK(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
-                    HIPCHK(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
-                }
+                hipStream_t const ax = get_aux(c, false);
                 const int na = (nb + 1) / 2, nb2 = nb - na;
                 // (r01bh/bi, 1024^2 x 256: 74.5k -> 75.7-76.3k frames/s; starting the
                 // second half after the first half's demod kernels instead: no gain)
                 HIPCHK(hipEventRecord(c->ev_fork, s));
-                HIPCHK(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
-                first_pass_chunk(c, fr, na, unwrap != 0, fused, rs, hdst, nullptr, coef, s, 0, cen0);
+                HIPCHK(hipStreamWaitEvent(ax, c->ev_fork, 0));
+                // early census: half 0 reads back every earlier frame's flags too (the earlier
+                // chunks' halves joined this stream), half 1 its own
+                int* const ch = cen0 ? static_cast<int*>(c->census.p) : nullptr;
+                first_pass_chunk(c, fr, na, unwrap != 0, fused, rs, hdst, nullptr, coef, s, 0, cen0, res, ch,
+                                 cen0 ? 2 * ((size_t)f0 + na) : 0);
                 first_pass_chunk(c, fr + (size_t)na * hw, nb2, unwrap != 0, fused, rs ? rs + 2 * na : nullptr,
-                                 hdst + (size_t)na * hw, nullptr, coef, c->aux, na, cen1);
-                HIPCHK(hipEventRecord(c->ev_join, c->aux));
+                                 hdst + (size_t)na * hw, nullptr, coef, ax, na, cen1, rs ? rs + 2 * na : nullptr,
+                                 ch ? ch + 2 * ((size_t)f0 + na) : nullptr, cen1 ? 2 * (size_t)nb2 : 0);
+                HIPCHK(hipEventRecord(c->ev_join, ax));
                 HIPCHK(hipStreamWaitEvent(s, c->ev_join, 0));
             } else {
-                first_pass_chunk(c, fr, nb, unwrap != 0, fused, rs, hdst, kdst, coef, s, 0, cen0);
+                first_pass_chunk(c, fr, nb, unwrap != 0, fused, rs, hdst, kdst, coef, s, 0, cen0, res,
+                                 cen0 ? static_cast<int*>(c->census.p) : nullptr, cen0 ? 2 * ((size_t)f0 + nb) : 0);
             }
             if (height_out && !dev)
                 HIPCHK(hipMemcpyAsync(height_out + (size_t)f0 * hw, hdst, (size_t)nb * hw * 4, out_kind, s));
@@ -2054,12 +2063,17 @@ int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int f
     std::vector<int> counts((size_t)n_frames * 2);
     c->census.ensure(counts.size() * sizeof(int));
     int* cdst = static_cast<int*>(c->census.p);
-    hipStream_t qs = s;  // the stream the readback runs on (and the poll below queries)
-    if (cen_halves > 0) {
-        qs = c->cstream;
-        for (int h = 0; h < cen_halves; ++h) HIPCHK(hipStreamWaitEvent(qs, c->ev_cen[h], 0));
-    }
-    HIPCHK(hipMemcpyAsync(cdst, res, counts.size() * sizeof(int), hipMemcpyDeviceToHost, qs));
+    // early census: the halves copied their flags on their own streams and marked them
+    // (first_pass_chunk); otherwise one copy on the caller's stream after everything
+    if (cen_halves == 0) HIPCHK(hipMemcpyAsync(cdst, res, counts.size() * sizeof(int), hipMemcpyDeviceToHost, s));
+    auto ready = [&]() {
+        if (cen_halves == 0) return hipStreamQuery(s);
+        for (int h = 0; h < cen_halves; ++h) {
+            const hipError_t e = hipEventQuery(c->ev_cen[h]);
+            if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
+    };
     // polled rather than a blocking wait: the caller's next batch is enqueued as soon
     // as this one's census is back (a blocking wait's wake-up sat in every bench step,
     // ~17 us per 256-frame step at 1024^2).  The poll yields the core between queries
@@ -2069,10 +2083,17 @@ int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int f
     hipError_t qe = hipErrorNotReady;
     {
         const auto t_end = std::chrono::steady_clock::now() + std::chrono::microseconds(spin_us);
-        while ((qe = hipStreamQuery(qs)) == hipErrorNotReady && std::chrono::steady_clock::now() < t_end)
+        while ((qe = ready()) == hipErrorNotReady && std::chrono::steady_clock::now() < t_end)
             std::this_thread::yield();
     }
-    if (qe == hipErrorNotReady) qe = hipStreamSynchronize(qs);
+    if (qe == hipErrorNotReady) {
+        if (cen_halves == 0) {
+            qe = hipStreamSynchronize(s);
+        } else {
+            qe = hipSuccess;
+            for (int h = 0; h < cen_halves && qe == hipSuccess; ++h) qe = hipEventSynchronize(c->ev_cen[h]);
+        }
+    }
     HIPCHK(qe);
     std::memcpy(counts.data(), cdst, counts.size() * sizeof(int));
     std::vector<int> redo;
