@@ -270,3 +270,22 @@ def test_single_call_device_memory_is_bounded(fresh):
     assert (4096, 4096) not in [k[0] for k in mine]
     _lib._engines.clear()
     gc.collect()
+
+
+def test_4096_folded_band_demod_equals_full_length(large, fresh, monkeypatch):
+    """The phases chain at 4096 (fcd.compute_height_map's, fcd.py:63, 118): the folded
+    band-pruned inverse (16 groups of 256 points per row, the 512-bin window's halves summed
+    per group, kernels_band.hip FOLD) against the full-length inverse row transform
+    (`FCD_WIDE_BAND=0`, k_demod_phase<4096>) on the same frame: the same wrapped phases up to
+    float32 rounding, and the same residue-free heights."""
+    from pyfcd import _lib
+    ref, frame = case_frames(large, "s4096")
+    eng = _lib.Engine(ref.shape)
+    eng.set_reference(ref, 0.001)
+    h1, w1, _ = eng.process(frame[None], 1.0, unwrap=True, want_phases=True)
+    monkeypatch.setenv("FCD_WIDE_BAND", "0")
+    h0, w0, _ = eng.process(frame[None], 1.0, unwrap=True, want_phases=True)
+    d = wrap_diff(w1[0], w0[0])
+    assert d.max() < 2e-4 and float(np.median(d)) < 2e-6, (d.max(), float(np.median(d)))
+    assert rel_l2(h1[0], h0[0]) < 1e-5
+    eng.close()
