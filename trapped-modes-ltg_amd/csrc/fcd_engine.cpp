@@ -994,7 +994,11 @@ void build_demod_tables(fcd_ctx* c, hipStream_t s) {
     // 50.5k / 63.5k / 68.1k / 68.9k frames/s.  16 GiB of workspace by default
     // (of 288 GB HBM): 256 frames at 1024^2, 128 at 2048^2, 32 at 4096^2 (8 GiB, 16 frames
     // at 4096^2: c5 3.40 k -> 3.49 k; 24 GiB measured 3.43 k, r05zd / r05ze).
-    const long budget = (long)fcd_env_int("FCD_CHUNK_MB", 16384) << 20;
+    // (round 6, 4096-point rows: 32 GiB, 64 frames per launch: c5 3.75 k -> 3.90 k frames/s,
+    // fused stage 130 -> 122 us/frame; 16 frames 3.82 k, 47 frames 3.79 k, r06 ck / ck2.  At
+    // 2048^2 256 frames per launch gave +2 % frames/s but the demod group's roofline 0.32 ->
+    // 0.31, so 2048-point rows keep 16 GiB)
+    const long budget = (long)fcd_env_int("FCD_CHUNK_MB", W >= 4096 ? 32768 : 16384) << 20;
     c->fchunk = (int)std::max(1L, std::min((long)fcd_env_int("FCD_CHUNK_MAX", 256), budget / per_frame));
     // the workspace itself is allocated per call, for the frames the call launches at once
     // (ensure_fast_ws): the reference's own setup below needs one frame's
