@@ -329,7 +329,7 @@ __global__ __launch_bounds__((BRCfg<W, B, ROWS, FOLD>::THREADS), 1) void k_band_
     constexpr int G = C::G, L = C::L, RL = C::RL, E = 16, SPT = C::SPT, TN = C::TN, SR = C::SR;
     constexpr int HALVES = BTILE / ROWS;  // item tiles per Ab tile
     extern __shared__ __attribute__((aligned(16))) float2 lds_b[];
-    float2* const stage0 = lds_b;                // [NBUF][B][SR]
+    float2* const stage0 = lds_b;                // [NBUF][SB][SR]
     float2* const ptl = lds_b + C::NBUF * C::STAGE;  // pre-twiddles [q][RL] (PREF: [RL] + [L][16])
     const int rl = threadIdx.x / RL;             // this wave's (or wave pair's) row of the tile
     const int l = threadIdx.x % RL, g = l / G, t = l % G;
