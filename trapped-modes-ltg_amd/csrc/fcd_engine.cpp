@@ -248,9 +248,8 @@ struct fcd_ctx {
     hipEvent_t ev_done = nullptr;    // end of the last device call's work on its (caller's) stream
     hipStream_t done_stream = nullptr;  // that stream, while the work may still be running
     bool done_pending = false;
-    hipStream_t aux = nullptr;       // the second stream of the fused chain's halves, and the fork / join events
-    hipStream_t aux_x = nullptr;     // the exact-first chain's second stream (get_aux)
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    hipStream_t aux = nullptr;       // the second stream of the two-halves chains and its fork / join events (get_aux)
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_join0 = nullptr;
     DevBuf ir_seam;                  // k_int_rows2's seam rows (tile-range edges), one region per stream
     DevBuf ztw, col0, seam;          // its 1024-point group-FFT twiddles; column-0 wrapped values [f][2][H];
                                      // first/last unwrapped rows of every tile [f][H/tile][2][W]
@@ -1020,18 +1019,20 @@ fcdk::DemodTables demod_tables(fcd_ctx* c) {
     return t;
 }
 
-// The second stream of a two-halves chain (exact: the exact-first chain's, its own so the
-// two chains' orders never mix) and the fork / join events, created on first use.  (The
-// exact chain's at the highest priority measured 8.1-8.5 k against 10.3-10.5 k camera
-// frames/s in the bench's context, r06 ax: its half then ran ahead of the caller's.)
-hipStream_t get_aux(fcd_ctx* c, bool exact) {
-    if (!c->ev_fork) {
+// The second stream of the two-halves chains (fused and exact-first) and the fork / join
+// events, created on first use.  One stream for both: every stream a context adds shifts the
+// runtime's round-robin dealing of default-priority streams over GPU_MAX_HW_QUEUES (4)
+// hardware queues, and a second stream that lands on the caller's queue serialises the
+// halves (a separate exact-chain stream did so under tools/fixup_bench.py: 10.5 k -> 8.6 k
+// camera frames/s, r06z; at the highest priority its half ran ahead of the caller's, r06 ax).
+hipStream_t get_aux(fcd_ctx* c) {
+    if (!c->aux) {
+        HIPCHK(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
         HIPCHK(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&c->ev_join0, hipEventDisableTiming));
     }
-    hipStream_t& st = exact ? c->aux_x : c->aux;
-    if (!st) HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-    return st;
+    return c->aux;
 }
 
 // Fast path for nb frames (device pointer): band-pruned demod -> wrapped (c->wrapped).
@@ -1297,6 +1298,7 @@ FCD_API int fcd_create(int device, int rows, int cols, fcd_ctx** out) {
             if (gsb) c->mr_gs.ensure(gsb);
         }
         HIPCHK(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking));
+        get_aux(c.get());  // right after `own`: the two get different hardware queues (process_impl)
         // plain tables exp(-2 pi i m / n) (power-of-two LDS kernels), or the mixed-radix plans'
         // tables (with Bluestein's chirp and convolution spectra)
         const std::vector<float2> tr = c->generic ? fcdk::mr_tables(c->mr_row) : twiddles(cols),
@@ -1351,14 +1353,12 @@ FCD_API int fcd_destroy(fcd_ctx* ctx) {
         for (hipEvent_t e : ctx->ev_cen)
             if (e) (void)hipEventDestroy(e);
         if (ctx->ev_done) (void)hipEventDestroy(ctx->ev_done);
-        for (hipStream_t st : {ctx->aux, ctx->aux_x})
-            if (st) {
-                (void)hipStreamSynchronize(st);
-                (void)hipStreamDestroy(st);
-            }
-        if (ctx->ev_fork) {
+        if (ctx->aux) {
+            (void)hipStreamSynchronize(ctx->aux);
+            (void)hipStreamDestroy(ctx->aux);
             (void)hipEventDestroy(ctx->ev_fork);
             (void)hipEventDestroy(ctx->ev_join);
+            (void)hipEventDestroy(ctx->ev_join0);
         }
         delete ctx;
     })
@@ -1921,9 +1921,17 @@ int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int f
                 // and MST workspace: one half's census read-back, graph-round convergence checks
                 // and small graph-round kernels overlap the other half's kernels, instead of
                 // leaving the chip idle (the camera frames' exact chain, r04ap trace).
+                // Both halves on the context's own two streams (created one after the other at
+                // fcd_create, so the runtime deals them different hardware queues), the caller's
+                // stream only forking and joining them: with the caller's stream as the first
+                // half's, whether the halves overlapped depended on how many streams the process
+                // had created before the second (camera frames 9.86 k / 10.4 k frames/s in two
+                // process layouts, r06)
                 const int nb0 = (nb + 1) / 2;
-                hipStream_t const ax = get_aux(c, true);
+                hipStream_t const ax = get_aux(c);
+                hipStream_t const h0 = c->own;
                 HIPCHK(hipEventRecord(c->ev_fork, s));
+                if (h0 != s) HIPCHK(hipStreamWaitEvent(h0, c->ev_fork, 0));
                 HIPCHK(hipStreamWaitEvent(ax, c->ev_fork, 0));
                 std::exception_ptr err1;
                 std::thread t1([&] {
@@ -1936,13 +1944,17 @@ int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int f
                 });
                 std::exception_ptr err0;
                 try {
-                    half(0, 0, nb0, s);
+                    half(0, 0, nb0, h0);
                 } catch (...) {
                     err0 = std::current_exception();
                 }
                 t1.join();
                 HIPCHK(hipEventRecord(c->ev_join, ax));
                 HIPCHK(hipStreamWaitEvent(s, c->ev_join, 0));
+                if (h0 != s) {
+                    HIPCHK(hipEventRecord(c->ev_join0, h0));
+                    HIPCHK(hipStreamWaitEvent(s, c->ev_join0, 0));
+                }
                 if (err0) std::rethrow_exception(err0);
                 if (err1) std::rethrow_exception(err1);
             }
@@ -2018,7 +2030,7 @@ int process_impl(fcd_ctx* c, const void* frames, int format, int n_frames, int f
                 // two halves of the chunk on two streams: kernels bound by different
                 // resources (HBM-bound c2r / demod_rows, latency-bound phase_rows /
                 // int_cols) overlap instead of running back to back
-                hipStream_t const ax = get_aux(c, false);
+                hipStream_t const ax = get_aux(c);
                 const int na = (nb + 1) / 2, nb2 = nb - na;
                 // (r01bh/bi, 1024^2 x 256: 74.5k -> 75.7-76.3k frames/s; starting the
                 // second half after the first half's demod kernels instead: no gain)
