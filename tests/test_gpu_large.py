@@ -289,3 +289,31 @@ def test_4096_folded_band_demod_equals_full_length(large, fresh, monkeypatch):
     assert d.max() < 2e-4 and float(np.median(d)) < 2e-6, (d.max(), float(np.median(d)))
     assert rel_l2(h1[0], h0[0]) < 1e-5
     eng.close()
+
+
+def test_rectangular_4096_wide_frames_match_oracle(fresh):
+    """4096-point rows on a short frame (256 x 4096): the folded band demod of the phases
+    chain, the folded fused kernel of the height-only chain and its reference angles against
+    the CPU oracle's chain (oracle/fcd_oracle.py, fcd.py:13-35): carriers, wrapped phases
+    (2e-4 rad), the unwrap up to the anchor, heights (1e-5)."""
+    from bench_data import make_residue_frame
+    from oracle import fcd_oracle as O
+    from pyfcd import _lib
+    rows, cols = 256, 4096
+    ref, frame = make_residue_frame(rows, [], seed=5, rotate_deg=5.0, quantum=4096, cols=cols)
+    eng = _lib.Engine(ref.shape)
+    info = eng.set_reference(ref, 0.001)
+    (cars, cf) = O.compute_carriers(ref, 0.001)
+    assert info.calibration_factor == cf
+    assert sorted(tuple(info.peaks[i]) for i in range(2)) == sorted(tuple(int(v) for v in c.pixels) for c in cars)
+    h, w, k = eng.process(frame[None], 1.0, unwrap=True, want_phases=True)
+    hf, _, _ = eng.process(frame[None], 1.0, unwrap=True, want_phases=False)
+    ho, _, _, ex = O.compute_height_map(ref, frame, 0.001, height=1.0)
+    for m in range(2):
+        assert wrap_diff(w[0][m], ex["wrapped"][m]).max() < 2e-4, m
+        _, ko = O.unwrap(w[0][m])
+        d = k[0][m].astype(np.int64) - ko
+        assert np.all(d == d.flat[0]), m
+    assert rel_l2(h[0], ho) < 1e-5, rel_l2(h[0], ho)
+    assert rel_l2(hf[0], ho) < 1e-5, rel_l2(hf[0], ho)
+    eng.close()
