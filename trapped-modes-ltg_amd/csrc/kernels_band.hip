@@ -275,7 +275,7 @@ __global__ __launch_bounds__((BPCfg<W, B>::THREADS), FCD_BAND_WAVES) void k_band
 #define FCD_BAND_RESIDENT 1  // 0: k_band_phase for every launch
 #endif
 #ifndef FCD_BAND_RES_ITEMS
-#define FCD_BAND_RES_ITEMS 4  // target items per CU (frame slices = items * CUs / (2 * row tiles))
+#define FCD_BAND_RES_ITEMS 1  // target items per CU (frame slices = items * CUs / (2 * row tiles)); 1: c2 demod group 1101-1115 -> 1081-1093 us, c3 -1.5 % (4 before, r06 it2)
 #endif
 // Phase stores of the theta-resident kernel: streaming (nt) or plain.  With two waves per
 // row (2048) a wave's store covers 16-byte pieces of every 32-byte sector (groups 0-3 of
